@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""PCApply throughput of the MI355X circulant FFT preconditioner.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--grid 256]
+
+One "step" = one PCApply x = (1/N) IDFT3(DFT3(b) ./ Diag) over one synthetic
+256^3 complex-double grid (BASELINE.json metric "PCApply/s on 256^3 complex
+grid").  Inputs are generated on the device (SplitMix64
+U[-1,1) complex, seed 20251017) and are resident in HBM before timing starts.
+
+N = 1: the single-GPU plan (5 kernel launches per apply).  N > 1 (launched by
+torch.distributed.run, one rank per GPU): the same grid slab-decomposed along
+z over N GPUs with two RCCL all-to-all transposes per apply (strong scaling;
+value = whole-job PCApply/s).
+
+Also reported: the roofline of the dominant kernel (algorithmic
+bytes / its mean duration from HIP events on the launch stream, vs 8 TB/s), the
+apply-level roofline on B_alg = 208 N bytes, and a CPU baseline (the oracle's C
+restatement, OpenMP over the host cores, bounded sample) timed on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
+LAM = (0.6, 0.15, 0.02)  # lambda set A, testFftSolver_3D.py:85-91
+SEED = 20251017
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def kernel_alg_bytes(mode: str, N: int, n_axis: int) -> int:
+    """Algorithmic HBM bytes of one axis-pass launch (SURVEY.md §8d per-unit figure x units)."""
+    b = 32 * N  # read N c128 + write N c128
+    if mode == "fused_diag":
+        b += 16 * N  # + read Diag
+    elif mode == "fused_sep":
+        b += 16 * (N // n_axis + n_axis)  # per-column + per-point symbol tables
+    return b
+
+
+def cpu_baseline(grid, budget_s: float = 20.0):
+    """The oracle's C restatement (test infrastructure; the checker, never the product)."""
+    import numpy as np
+    from oracle import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    O.set_threads(threads)
+    n = tuple(grid)
+    N = int(np.prod(n))
+    b = O.c_fill_uniform(N, SEED)
+    d = O.c_build_diag_transport(n, LAM)
+    t0 = time.perf_counter()
+    O.c_solve_3d(d, b, n)  # warm-up (page faults, thread pool)
+    first = time.perf_counter() - t0
+    reps = max(1, min(5, int(budget_s / max(first, 1e-3))))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        O.c_solve_3d(d, b, n)
+    dt = (time.perf_counter() - t0) / reps
+    return {"value": round(1.0 / dt, 4), "unit": "PCApply/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} timed applies (+1 warm-up) of the full {n[0]}x{n[1]}x{n[2]} grid, "
+                      f"oracle/cfp_oracle.c restatement of solve_3D, OpenMP {threads} threads, "
+                      f"{dt * 1e3:.0f} ms/apply"}
+
+
+def load_traffic(grid, kernel_name: str):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        data = json.load(open(path))
+    except Exception:
+        return None, None
+    key = f"{grid[0]}x{grid[1]}x{grid[2]}"
+    ent = data.get(key, {}).get(kernel_name)
+    if not ent:
+        return None, None
+    return ent.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--grid", type=int, nargs="+", default=[256])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    args = ap.parse_args()
+    grid = args.grid * 3 if len(args.grid) == 1 else args.grid
+    if len(grid) != 3:
+        raise SystemExit("--grid takes 1 or 3 integers")
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import circulantpreconditioner_amd as cp
+
+    nx, ny, nz = grid
+    N = nx * ny * nz
+    stream = torch.cuda.current_stream()
+    roof = None
+    roof_apply = None
+    passes_info = None
+    if world == 1:
+        b = torch.empty(N, dtype=torch.complex128, device=dev)
+        x = torch.empty_like(b)
+        cp.fill_uniform(b, SEED)
+        plan = cp.CirculantPlan(grid, device=local_rank)
+        plan.set_transport_symbol(LAM)
+        run = lambda: plan.apply(b, out=x)  # noqa: E731
+        parallelism = "single GPU"
+    else:
+        from circulantpreconditioner_amd.distributed import SlabPlan
+        plan = SlabPlan(grid, rank=rank, world=world, device=local_rank)
+        plan.set_transport_symbol(LAM)
+        b = torch.empty(plan.local_size, dtype=torch.complex128, device=dev)
+        x = torch.empty_like(b)
+        cp.fill_uniform(b, SEED, offset=plan.local_offset)
+        run = lambda: plan.apply(b, out=x)  # noqa: E731
+        parallelism = f"z-slab x{world}, RCCL all-to-all over xGMI"
+
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = args.steps / elapsed  # whole-job PCApply/s (one grid per step)
+
+    # per-launch timing of the dominant kernel (HIP events on the launch stream)
+    if world == 1:
+        passes_info = plan.passes()
+        ms = plan.time_passes(b, x, iters=max(10, min(50, args.steps)))
+        for p, m in zip(passes_info, ms):
+            p["ms"] = round(m, 5)
+        k = max(range(len(ms)), key=lambda i: ms[i])
+        dom = passes_info[k]
+        alg = kernel_alg_bytes(dom["mode"], N, dom["n"])
+        achieved = alg / (ms[k] * 1e-3) / 1e9
+        kname = f"pass{k}_{dom['axis']}_{dom['mode']}"
+        traffic, tsrc = load_traffic(grid, kname)
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": kname, "alg_bytes_per_launch": alg, "mean_ms": round(ms[k], 5)}
+        if tsrc:
+            roof["traffic_source"] = tsrc
+        b_alg = 208 * N
+        ach_apply = b_alg / (ms_per_step * 1e-3) / 1e9
+        roof_apply = {"B_alg_bytes": b_alg, "achieved": round(ach_apply, 1), "peak": HBM_PEAK_GBS,
+                      "unit": "GB/s", "frac": round(ach_apply / HBM_PEAK_GBS, 4),
+                      "note": "SURVEY §8d: B_alg = 208 N (13 c128 sweeps) / wall time per apply"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(grid, args.cpu_budget)
+        except Exception as e:  # report, never fake
+            log(f"cpu baseline failed: {e}")
+
+    if rank == 0:
+        out = {
+            "metric": "PCApply/s on 256^3 complex grid" if grid == [256, 256, 256] else
+                      f"PCApply/s on {nx}x{ny}x{nz} complex grid",
+            "value": round(value, 3),
+            "unit": "PCApply/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "c128 (f64 complex)",
+            "data": f"synthetic: SplitMix64 U[-1,1) complex b, seed {SEED}, generated in HBM",
+            "config": {"workload": f"{nx}x{ny}x{nz} c128 circulant PCApply, transport symbol lambda={LAM}",
+                       "grid": grid, "global_batch": 1, "parallelism": parallelism},
+            "roofline": roof,
+            "roofline_apply": roof_apply,
+            "cpu_baseline": cpu,
+        }
+        if passes_info is not None:
+            out["passes"] = passes_info
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

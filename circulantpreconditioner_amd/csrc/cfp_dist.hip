@@ -1,0 +1,420 @@
+// cfp_dist.hip -- z-slab decomposition of the circulant apply over P GPUs.
+//
+// Replaces the FFTW-MPI slab transposes that PETSc's MATFFTW performs inside MatMult /
+// MatMultTranspose when size > 1 (src/FftLinearSolver_3D.c:170,180).
+// The y passes read/write the exchange chunks directly (no pack/unpack kernels): the
+// forward y pass writes point ky of a column to chunk ky / nyl, the inverse y pass reads
+// it back from there, so an all-to-all is a set of contiguous peer messages.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <complex>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <vector>
+
+#include "../../include/circulant_fft.h"
+#include "../../include/circulant_fft_dist.h"
+#include "cfp_host.h"
+#include "cfp_internal.h"
+
+using namespace cfp;
+
+#define HIPCHK(expr)                                        \
+  do {                                                      \
+    hipError_t _e = (expr);                                 \
+    if (_e != hipSuccess) return cfp::hip_error(_e, #expr); \
+  } while (0)
+#define NCCLCHK(expr)                                                                            \
+  do {                                                                                           \
+    ncclResult_t _r = (expr);                                                                    \
+    if (_r != ncclSuccess) return cfp::set_error(CFP_ERR_LIB, "%s: %s", #expr, ncclGetErrorString(_r)); \
+  } while (0)
+
+namespace {
+
+struct SlabLayout {
+  i64 nx, ny, nz;
+  int P, r;
+  i64 nzl, nyl, z0, y0, local, chunk, offset;
+};
+
+int make_layout(i64 nx, i64 ny, i64 nz, int P, int r, SlabLayout* L) {
+  if (nx < 1 || ny < 1 || nz < 1) return set_error(CFP_ERR_ARG_OUTOFRANGE, "grid sizes must be >= 1");
+  if (P < 1 || r < 0 || r >= P) return set_error(CFP_ERR_ARG_OUTOFRANGE, "rank %d of %d", r, P);
+  if (nz % P || ny % P)
+    return set_error(CFP_ERR_ARG_SIZ, "slab decomposition needs nranks | nz and nranks | ny (nz=%lld ny=%lld P=%d)",
+                     (long long)nz, (long long)ny, P);
+  if (nx > 4096 || ny > 4096 || nz > 4096) return set_error(CFP_ERR_SUP, "axis lengths above 4096 unsupported");
+  L->nx = nx; L->ny = ny; L->nz = nz; L->P = P; L->r = r;
+  L->nzl = nz / P; L->nyl = ny / P;
+  L->z0 = r * L->nzl; L->y0 = r * L->nyl;
+  L->local = L->nzl * ny * nx;
+  L->chunk = L->nzl * L->nyl * nx;
+  L->offset = L->z0 * ny * nx;
+  return CFP_SUCCESS;
+}
+
+Side side(i64 inner_stride, i64 outer_stride, i64 pt_stride, i64 seg_len, i64 seg_stride) {
+  Side s;
+  s.inner_stride = inner_stride;
+  s.outer_stride = outer_stride;
+  s.pt_stride = pt_stride;
+  s.seg_len = (int)seg_len;
+  s.seg_shift = ilog2_exact(seg_len);
+  s.seg_stride = seg_stride;
+  return s;
+}
+
+enum Buf { B_IN = 0, B_X = 1, B_W = 2 };
+
+struct Step {
+  bool exchange;
+  PassDesc pass;  // kernel steps
+  int src, dst;   // buffer ids
+  int fused;      // 1 if this is the symbol pass
+};
+
+std::vector<Step> slab_steps(const SlabLayout& L) {
+  std::vector<Step> st;
+  const i64 nx = L.nx, ny = L.ny, nz = L.nz, nzl = L.nzl, nyl = L.nyl;
+  auto kern = [&](int n, i64 ncols, i64 inner_n, Side in, Side out, int mode, int src, int dst, int fused) {
+    Step s;
+    s.exchange = false;
+    s.pass.n = n; s.pass.ncols = ncols; s.pass.inner_n = inner_n;
+    s.pass.in = in; s.pass.out = out; s.pass.mode = mode; s.pass.scale = 1.0;
+    s.pass.colsym = s.pass.axsym = s.pass.diag = nullptr;
+    s.src = src; s.dst = dst; s.fused = fused;
+    st.push_back(s);
+  };
+  auto exch = [&](int src, int dst) {
+    Step s;
+    std::memset(&s, 0, sizeof(s));
+    s.exchange = true; s.src = src; s.dst = dst;
+    st.push_back(s);
+  };
+  const Side xs = side(0, nx, 1, nx, 0);                    // x rows of the local slab
+  const Side ynat = side(1, nx * ny, nx, ny, 0);            // y columns, natural [nzl][ny][nx]
+  const Side ysplit = side(1, nyl * nx, nx, nyl, L.chunk);  // y columns in per-peer chunks
+  const Side zs = side(1, 0, nx * nyl, nz, 0);              // z columns of [nz][nyl][nx]
+  int cur = B_IN;
+  if (nx > 1) { kern((int)nx, nzl * ny, 1, xs, xs, PASS_FWD, B_IN, B_X, 0); cur = B_X; }
+  kern((int)ny, nx * nzl, nx, ynat, ysplit, PASS_FWD, cur, B_W, 0);
+  exch(B_W, B_X);
+  kern((int)nz, nx * nyl, nx * nyl, zs, zs, PASS_FUSED_SEP, B_X, B_X, 1);
+  exch(B_X, B_W);
+  kern((int)ny, nx * nzl, nx, ysplit, ynat, PASS_INV, B_W, B_X, 0);
+  if (nx > 1) kern((int)nx, nzl * ny, 1, xs, xs, PASS_INV, B_X, B_X, 0);
+  // 1/N on the last launch
+  for (int i = (int)st.size() - 1; i >= 0; --i)
+    if (!st[i].exchange) { st[i].pass.scale = 1.0 / (double)(nx * ny * nz); break; }
+  return st;
+}
+
+// Per-rank device state shared by both executors.
+struct SlabRank {
+  SlabLayout L;
+  int device = 0;
+  std::map<int, cd*> tw;
+  cd* colsym = nullptr;
+  cd* axsym = nullptr;
+  cd* work = nullptr;
+  bool sym = false;
+  std::vector<Step> steps;
+
+  int init(const SlabLayout& lay, int dev) {
+    L = lay;
+    device = dev;
+    steps = slab_steps(L);
+    for (const Step& s : steps) {
+      if (s.exchange || tw.count(s.pass.n)) continue;
+      std::vector<cd> h = host_twiddles(s.pass.n, -1);
+      cd* d = nullptr;
+      HIPCHK(hipMalloc(&d, sizeof(cd) * h.size()));
+      HIPCHK(hipMemcpy(d, h.data(), sizeof(cd) * h.size(), hipMemcpyHostToDevice));
+      tw[s.pass.n] = d;
+    }
+    HIPCHK(hipMalloc(&work, sizeof(cd) * (size_t)L.local));
+    return CFP_SUCCESS;
+  }
+  void release() {
+    for (auto& kv : tw) hipFree(kv.second);
+    tw.clear();
+    if (colsym) hipFree(colsym);
+    if (axsym) hipFree(axsym);
+    if (work) hipFree(work);
+    colsym = axsym = work = nullptr;
+  }
+  // colsym over the z-pass columns g = ix + nx*iyl (global ky = y0 + iyl); axsym over kz
+  int set_transport(const double lam[6]) {
+    std::vector<cd> hat[3] = {host_transport_symbol(L.nx), host_transport_symbol(L.ny), host_transport_symbol(L.nz)};
+    std::vector<cd> s[3];
+    for (int a = 0; a < 3; ++a) {
+      const double lr = lam[2 * a], li = lam[2 * a + 1];
+      s[a].resize(hat[a].size());
+      for (size_t k = 0; k < hat[a].size(); ++k) {
+        const double cr = hat[a][k].x, ci = hat[a][k].y;
+        s[a][k] = make_cd(cr * lr - ci * li, cr * li + ci * lr);
+      }
+    }
+    const i64 ncols = L.nx * L.nyl;
+    std::vector<cd> col((size_t)ncols);
+    for (i64 g = 0; g < ncols; ++g) {
+      const i64 ix = g % L.nx, ky = L.y0 + g / L.nx;
+      col[(size_t)g] = make_cd(s[0][ix].x + s[1][ky].x, s[0][ix].y + s[1][ky].y);
+    }
+    if (!colsym) HIPCHK(hipMalloc(&colsym, sizeof(cd) * (size_t)ncols));
+    if (!axsym) HIPCHK(hipMalloc(&axsym, sizeof(cd) * (size_t)L.nz));
+    HIPCHK(hipMemcpy(colsym, col.data(), sizeof(cd) * (size_t)ncols, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(axsym, s[2].data(), sizeof(cd) * (size_t)L.nz, hipMemcpyHostToDevice));
+    sym = true;
+    return CFP_SUCCESS;
+  }
+  cd* buf(int id, const cd* b, cd* x) const { return id == B_IN ? (cd*)b : (id == B_X ? x : work); }
+  int launch(const Step& s, const cd* b, cd* x, hipStream_t st) const {
+    PassDesc p = s.pass;
+    if (s.fused) { p.colsym = colsym; p.axsym = axsym; }
+    hipError_t e = launch_axis_pass(p, buf(s.src, b, x), buf(s.dst, b, x), tw.at(p.n), st);
+    return e == hipSuccess ? CFP_SUCCESS : hip_error(e, "slab axis pass");
+  }
+};
+
+}  // namespace
+
+struct cfp_dist_plan_s {
+  SlabRank R;
+  ncclComm_t comm = nullptr;
+};
+
+struct cfp_group_s {
+  std::vector<SlabRank> R;
+  std::vector<hipStream_t> streams;
+};
+
+extern "C" int cfp_slab_layout(int64_t nx, int64_t ny, int64_t nz, int P, int r, int64_t* out) {
+  if (!out) return set_error(CFP_ERR_ARG_NULL, "out is NULL");
+  SlabLayout L;
+  int rc = make_layout(nx, ny, nz, P, r, &L);
+  if (rc) return rc;
+  const int64_t v[8] = {L.nzl, L.nyl, L.z0, L.y0, L.local, L.chunk, L.offset, (int64_t)P};
+  std::memcpy(out, v, sizeof(v));
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_dist_unique_id_bytes(void) { return (int)sizeof(ncclUniqueId); }
+
+extern "C" int cfp_dist_get_unique_id(char* id_out) {
+  if (!id_out) return set_error(CFP_ERR_ARG_NULL, "id_out is NULL");
+  ncclUniqueId id;
+  NCCLCHK(ncclGetUniqueId(&id));
+  std::memcpy(id_out, &id, sizeof(id));
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_dist_plan_create(cfp_dist_plan_t* plan, int64_t nx, int64_t ny, int64_t nz, int P, int r,
+                                    const char* uid, int device) {
+  if (!plan || !uid) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  *plan = nullptr;
+  SlabLayout L;
+  int rc = make_layout(nx, ny, nz, P, r, &L);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(device));
+  std::unique_ptr<cfp_dist_plan_s> p(new cfp_dist_plan_s);
+  rc = p->R.init(L, device);
+  if (rc) { p->R.release(); return rc; }
+  ncclUniqueId id;
+  std::memcpy(&id, uid, sizeof(id));
+  ncclResult_t nr = ncclCommInitRank(&p->comm, P, id, r);
+  if (nr != ncclSuccess) {
+    p->R.release();
+    return set_error(CFP_ERR_LIB, "ncclCommInitRank: %s", ncclGetErrorString(nr));
+  }
+  *plan = p.release();
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_dist_plan_destroy(cfp_dist_plan_t p) {
+  if (!p) return CFP_SUCCESS;
+  hipSetDevice(p->R.device);
+  if (p->comm) ncclCommDestroy(p->comm);
+  p->R.release();
+  delete p;
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_dist_plan_set_symbol_transport(cfp_dist_plan_t p, const double lam[6]) {
+  if (!p || !lam) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  HIPCHK(hipSetDevice(p->R.device));
+  return p->R.set_transport(lam);
+}
+
+extern "C" int cfp_dist_plan_local_size(cfp_dist_plan_t p, int64_t* n) {
+  if (!p || !n) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  *n = p->R.L.local;
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_dist_plan_num_phases(cfp_dist_plan_t p, int* n) {
+  if (!p || !n) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  *n = (int)p->R.steps.size();
+  return CFP_SUCCESS;
+}
+
+static int rccl_exchange(cfp_dist_plan_s* p, const cd* src, cd* dst, hipStream_t s) {
+  const SlabLayout& L = p->R.L;
+  const size_t cnt = (size_t)L.chunk * 2;  // doubles per peer message
+  HIPCHK(hipMemcpyAsync(dst + L.r * L.chunk, src + L.r * L.chunk, sizeof(cd) * (size_t)L.chunk,
+                        hipMemcpyDeviceToDevice, s));
+  if (L.P == 1) return CFP_SUCCESS;
+  NCCLCHK(ncclGroupStart());
+  for (int q = 0; q < L.P; ++q) {
+    if (q == L.r) continue;
+    NCCLCHK(ncclSend(src + q * L.chunk, cnt, ncclDouble, q, p->comm, s));
+    NCCLCHK(ncclRecv(dst + q * L.chunk, cnt, ncclDouble, q, p->comm, s));
+  }
+  NCCLCHK(ncclGroupEnd());
+  return CFP_SUCCESS;
+}
+
+static int dist_apply(cfp_dist_plan_s* p, const cd* b, cd* x, hipStream_t s, std::vector<hipEvent_t>* ev) {
+  if (!p->R.sym) return set_error(CFP_ERR_ARG_WRONGSTATE, "no symbol set on the slab plan");
+  for (size_t i = 0; i < p->R.steps.size(); ++i) {
+    const Step& st = p->R.steps[i];
+    if (ev) HIPCHK(hipEventRecord((*ev)[i], s));
+    int rc;
+    if (st.exchange) rc = rccl_exchange(p, p->R.buf(st.src, b, x), p->R.buf(st.dst, b, x), s);
+    else rc = p->R.launch(st, b, x, s);
+    if (rc) return rc;
+  }
+  if (ev) HIPCHK(hipEventRecord((*ev)[p->R.steps.size()], s));
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_dist_plan_apply(cfp_dist_plan_t p, const double* b, double* x, void* stream) {
+  if (!p || !b || !x) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  HIPCHK(hipSetDevice(p->R.device));
+  return dist_apply(p, (const cd*)b, (cd*)x, (hipStream_t)stream, nullptr);
+}
+
+extern "C" int cfp_dist_plan_time_phases(cfp_dist_plan_t p, const double* b, double* x, int iters, double* ms_out,
+                                         void* stream) {
+  if (!p || !b || !x || !ms_out) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  if (iters < 1) return set_error(CFP_ERR_ARG_OUTOFRANGE, "iters must be >= 1");
+  HIPCHK(hipSetDevice(p->R.device));
+  const size_t np = p->R.steps.size();
+  std::vector<hipEvent_t> ev(np + 1);
+  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  std::vector<double> acc(np, 0.0);
+  int rc = CFP_SUCCESS;
+  for (int it = 0; it < iters && !rc; ++it) {
+    rc = dist_apply(p, (const cd*)b, (cd*)x, (hipStream_t)stream, &ev);
+    if (rc) break;
+    if (hipEventSynchronize(ev[np]) != hipSuccess) { rc = set_error(CFP_ERR_LIB, "event sync"); break; }
+    for (size_t i = 0; i < np; ++i) {
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+      acc[i] += ms;
+    }
+  }
+  for (auto& e : ev) hipEventDestroy(e);
+  if (rc) return rc;
+  for (size_t i = 0; i < np; ++i) ms_out[i] = acc[i] / iters;
+  return CFP_SUCCESS;
+}
+
+// ------------------------------------------------------------------ single-process group
+extern "C" int cfp_group_create(cfp_group_t* group, int64_t nx, int64_t ny, int64_t nz, int P, const int* devices) {
+  if (!group || !devices) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  *group = nullptr;
+  std::unique_ptr<cfp_group_s> g(new cfp_group_s);
+  g->R.resize((size_t)P);
+  g->streams.resize((size_t)P, nullptr);
+  for (int r = 0; r < P; ++r) {
+    SlabLayout L;
+    int rc = make_layout(nx, ny, nz, P, r, &L);
+    if (!rc) {
+      hipError_t e = hipSetDevice(devices[r]);
+      if (e != hipSuccess) rc = hip_error(e, "hipSetDevice");
+    }
+    if (!rc) rc = g->R[r].init(L, devices[r]);
+    if (!rc) {
+      hipError_t e = hipStreamCreateWithFlags(&g->streams[r], hipStreamNonBlocking);
+      if (e != hipSuccess) rc = hip_error(e, "hipStreamCreate");
+    }
+    if (rc) {
+      for (int q = 0; q <= r; ++q) {
+        g->R[q].release();
+        if (g->streams[q]) hipStreamDestroy(g->streams[q]);
+      }
+      return rc;
+    }
+  }
+  *group = g.release();
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_group_destroy(cfp_group_t g) {
+  if (!g) return CFP_SUCCESS;
+  for (size_t r = 0; r < g->R.size(); ++r) {
+    hipSetDevice(g->R[r].device);
+    g->R[r].release();
+    if (g->streams[r]) hipStreamDestroy(g->streams[r]);
+  }
+  delete g;
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_group_set_symbol_transport(cfp_group_t g, const double lam[6]) {
+  if (!g || !lam) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  for (auto& R : g->R) {
+    HIPCHK(hipSetDevice(R.device));
+    int rc = R.set_transport(lam);
+    if (rc) return rc;
+  }
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_group_apply(cfp_group_t g, const double* const* b, double* const* x) {
+  if (!g || !b || !x) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  const int P = (int)g->R.size();
+  for (auto& R : g->R)
+    if (!R.sym) return set_error(CFP_ERR_ARG_WRONGSTATE, "no symbol set on the group");
+  const size_t nsteps = g->R[0].steps.size();
+  for (size_t i = 0; i < nsteps; ++i) {
+    const Step& st = g->R[0].steps[i];
+    if (!st.exchange) {
+      for (int r = 0; r < P; ++r) {
+        HIPCHK(hipSetDevice(g->R[r].device));
+        int rc = g->R[r].launch(g->R[r].steps[i], (const cd*)b[r], (cd*)x[r], g->streams[r]);
+        if (rc) return rc;
+      }
+    } else {
+      for (int r = 0; r < P; ++r) {
+        HIPCHK(hipSetDevice(g->R[r].device));
+        HIPCHK(hipStreamSynchronize(g->streams[r]));
+      }
+      // rank r's chunk q goes to rank q's chunk r
+      for (int r = 0; r < P; ++r) {
+        const SlabRank& S = g->R[r];
+        HIPCHK(hipSetDevice(S.device));
+        const cd* src = S.buf(st.src, (const cd*)b[r], (cd*)x[r]);
+        for (int q = 0; q < P; ++q) {
+          const SlabRank& D = g->R[q];
+          cd* dst = D.buf(st.dst, (const cd*)b[q], (cd*)x[q]);
+          HIPCHK(hipMemcpyAsync(dst + r * D.L.chunk, src + q * S.L.chunk, sizeof(cd) * (size_t)S.L.chunk,
+                                hipMemcpyDefault, g->streams[r]));
+        }
+      }
+      for (int r = 0; r < P; ++r) {
+        HIPCHK(hipSetDevice(g->R[r].device));
+        HIPCHK(hipStreamSynchronize(g->streams[r]));
+      }
+    }
+  }
+  for (int r = 0; r < P; ++r) {
+    HIPCHK(hipSetDevice(g->R[r].device));
+    HIPCHK(hipStreamSynchronize(g->streams[r]));
+  }
+  return CFP_SUCCESS;
+}

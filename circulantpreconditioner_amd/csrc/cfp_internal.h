@@ -1,0 +1,63 @@
+// cfp_internal.h -- shared device/host definitions of the MI355X circulant FFT library.
+//
+// Data model: complex double, interleaved (re, im) = double2,
+// grid index i = ix + nx*(iy + ny*iz) (x fastest), i.e. row-major {nz, ny, nx} as the
+// reference's MatCreateFFT(..., dims={nz,ny,nx}) (src/PCSHELLFft_3D.cxx:34-35).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cfp {
+
+typedef double2 cd;
+typedef long long i64;
+
+// How the points of one FFT column are addressed on one side (input or output) of an
+// axis pass.  Column g (0 <= g < ncols) starts at
+//     base(g) = (g % inner_n) * inner_stride + (g / inner_n) * outer_stride
+// and point k (0 <= k < n) of that column sits at
+//     base(g) + (k >> seg_shift) * seg_stride + (k & seg_mask) * pt_stride.
+// An unsplit axis has seg_len = n (seg_shift large).  A split axis is what the slab
+// transposes of the multi-GPU path produce: the y axis cut into P segments of n/P points,
+// each segment in its own peer chunk.
+struct Side {
+  i64 inner_stride;
+  i64 outer_stride;
+  i64 pt_stride;
+  i64 seg_stride;
+  int seg_shift;  // log2(seg_len) when seg_len is a power of two, else -1 (generic kernel only)
+  int seg_len;
+};
+
+enum PassMode : int {
+  PASS_FWD = 0,         // out = scale * DFT(in)             (forward, e^{-})
+  PASS_INV = 1,         // out = scale * IDFT(in)            (backward, e^{+}, unnormalised)
+  PASS_FUSED_SEP = 2,   // out = scale * IDFT( DFT(in) / (colsym[g] + axsym[k]) )
+  PASS_FUSED_DIAG = 3,  // out = scale * IDFT( DFT(in) / diag[same addressing as in] )
+};
+
+struct PassDesc {
+  int n;          // points per column (FFT length along the axis)
+  i64 ncols;      // number of columns
+  i64 inner_n;    // columns are enumerated inner-fastest: g = inner + inner_n * outer
+  Side in, out;
+  int mode;
+  double scale;
+  const cd* colsym;  // [ncols]   (PASS_FUSED_SEP)
+  const cd* axsym;   // [n]       (PASS_FUSED_SEP)
+  const cd* diag;    // addressed like `in` (PASS_FUSED_DIAG)
+};
+
+__host__ __device__ inline cd make_cd(double x, double y) { cd r; r.x = x; r.y = y; return r; }
+
+// Launchers (cfp_kernels.hip).  tw = forward twiddle table W_n[k] = exp(-2 pi i k / n), k < n.
+hipError_t launch_axis_pass(const PassDesc& p, const cd* in, cd* out, const cd* tw, hipStream_t s);
+bool fast_path_supported(const PassDesc& p);
+hipError_t launch_pointwise_divide(cd* w, const cd* x, const cd* y, i64 n, hipStream_t s);
+hipError_t launch_scale(cd* x, cd alpha, i64 n, hipStream_t s);
+hipError_t launch_fill_uniform(cd* x, i64 n, uint64_t seed, i64 offset, hipStream_t s);
+hipError_t launch_build_diag_separable(cd* diag, const cd* cx, const cd* cy, const cd* cz, i64 nx, i64 ny,
+                                       i64 nz, cd lx, cd ly, cd lz, hipStream_t s);
+hipError_t launch_sym_divide_inplace(cd* x, const cd* colsym, const cd* axsym, i64 n, hipStream_t s);
+
+}  // namespace cfp

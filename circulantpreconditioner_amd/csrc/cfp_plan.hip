@@ -1,0 +1,506 @@
+// cfp_plan.hip -- host side of the single-GPU plan: pass schedule, symbol tables, C ABI.
+//
+// A plan replaces the reference's persistent PCSHELL state (struct FFTPrecTransportContext,
+// src/PCSHELLFft_3D.hxx:8-21: FFT_MAT, Diag, b_hat, b_cartesien) with:
+//   * the axis-pass schedule of one apply (cfp_kernels.hip),
+//   * per-axis twiddle tables W_n (host long double -> device double),
+//   * the symbol: separable tables (colsym over the fused axis' columns, axsym over its
+//     points) generated once, or an explicit Diag vector for a general symbol.
+// An apply reads b, writes x, and needs no scratch (x is the work buffer).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/circulant_fft.h"
+#include "cfp_internal.h"
+#include "cfp_host.h"
+
+using namespace cfp;
+
+// ------------------------------------------------------------------ error plumbing
+static thread_local std::string g_err;
+
+namespace cfp {
+int set_error(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+int hip_error(hipError_t e, const char* what) {
+  return set_error(e == hipErrorOutOfMemory ? CFP_ERR_MEM : CFP_ERR_LIB, "%s: %s", what, hipGetErrorString(e));
+}
+}  // namespace cfp
+
+#define HIPCHK(expr)                                     \
+  do {                                                   \
+    hipError_t _e = (expr);                              \
+    if (_e != hipSuccess) return cfp::hip_error(_e, #expr); \
+  } while (0)
+
+extern "C" const char* cfp_last_error(void) { return g_err.c_str(); }
+extern "C" const char* cfp_version(void) { return "circulant_fft 0.1.0 (gfx950)"; }
+
+extern "C" int cfp_device_count(int* count) {
+  if (!count) return set_error(CFP_ERR_ARG_NULL, "count is NULL");
+  HIPCHK(hipGetDeviceCount(count));
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_stream_sync(void* stream) {
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return CFP_SUCCESS;
+}
+
+// ------------------------------------------------------------------ twiddles
+namespace cfp {
+
+std::vector<cd> host_twiddles(int n, int sign) {
+  std::vector<cd> t((size_t)n);
+  for (int k = 0; k < n; ++k) {
+    long double a = 2.0L * 3.14159265358979323846264338327950288L * (long double)k / (long double)n;
+    t[k] = make_cd((double)cosl(a), (double)(sign * sinl(a)));
+  }
+  return t;
+}
+
+// 1 - e^{-2 pi i k / n}: the 1-D DFT of the transport column (1, -1, 0, ...)
+std::vector<cd> host_transport_symbol(i64 n) {
+  std::vector<cd> s((size_t)n, make_cd(0.0, 0.0));
+  if (n <= 1) return s;
+  for (i64 k = 0; k < n; ++k) {
+    long double a = 2.0L * 3.14159265358979323846264338327950288L * (long double)k / (long double)n;
+    s[k] = make_cd((double)(1.0L - cosl(a)), (double)sinl(a));
+  }
+  return s;
+}
+
+int ilog2_exact(i64 v) {
+  if (v <= 0 || (v & (v - 1))) return -1;
+  int l = 0;
+  while ((1LL << l) < v) ++l;
+  return l;
+}
+
+Side natural_side(int axis, const i64 n[3]) {
+  Side s;
+  const i64 nx = n[0], ny = n[1];
+  s.seg_len = (int)n[axis];
+  s.seg_shift = ilog2_exact(n[axis]);
+  if (s.seg_shift < 0) s.seg_shift = 30;  // unused by the generic kernel
+  s.seg_stride = 0;
+  if (axis == 0) { s.inner_stride = 0; s.outer_stride = nx; s.pt_stride = 1; }
+  else if (axis == 1) { s.inner_stride = 1; s.outer_stride = nx * ny; s.pt_stride = nx; }
+  else { s.inner_stride = 1; s.outer_stride = 0; s.pt_stride = nx * ny; }
+  if (ilog2_exact(n[axis]) < 0) s.seg_shift = -1;
+  return s;
+}
+
+void natural_cols(int axis, const i64 n[3], i64* ncols, i64* inner_n) {
+  const i64 N = n[0] * n[1] * n[2];
+  *ncols = N / n[axis];
+  *inner_n = axis == 0 ? 1 : (axis == 1 ? n[0] : n[0] * n[1]);
+}
+
+}  // namespace cfp
+
+// ------------------------------------------------------------------ plan
+struct cfp_plan_s {
+  int device = 0;
+  i64 n[3] = {1, 1, 1};
+  i64 N = 1;
+  std::map<int, cd*> tw;  // device forward twiddles per axis length
+  int sym_kind = 0;       // 0 none, 1 separable, 2 explicit diag
+  cd* colsym = nullptr;   // separable: per column of the fused axis (sum over the other axes)
+  cd* axsym = nullptr;    //            per point of the fused axis
+  cd* diag = nullptr;     // explicit
+  cd* host_stage = nullptr;  // device staging buffers for cfp_plan_apply_host
+  std::vector<int> axes;     // non-trivial axes, x..z
+  int fused_axis = 0;
+  std::vector<cd> sym1d[3];  // separable: lambda_d * c_d_hat (host copies)
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    hipGetDevice(&prev);
+    if (prev != dev) hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur;
+    hipGetDevice(&cur);
+    if (prev >= 0 && cur != prev) hipSetDevice(prev);
+  }
+};
+
+int ensure_tw(cfp_plan_s* p, int n) {
+  if (p->tw.count(n)) return CFP_SUCCESS;
+  std::vector<cd> h = host_twiddles(n, -1);
+  cd* d = nullptr;
+  HIPCHK(hipMalloc(&d, sizeof(cd) * (size_t)n));
+  HIPCHK(hipMemcpy(d, h.data(), sizeof(cd) * (size_t)n, hipMemcpyHostToDevice));
+  p->tw[n] = d;
+  return CFP_SUCCESS;
+}
+
+// The apply schedule: forward passes over all non-trivial axes but the last, the fused
+// DFT/divide/IDFT pass over the last one, then the inverse passes in reverse order; the
+// 1/N scale rides on the final launch.
+struct Step {
+  int axis;
+  int mode;
+  bool from_b;
+  bool scale;
+};
+
+std::vector<Step> apply_steps(const cfp_plan_s* p) {
+  std::vector<Step> st;
+  const std::vector<int>& A = p->axes;
+  if (A.empty()) {
+    st.push_back({0, -1, true, true});  // N == 1: fused pass on a length-1 axis
+    return st;
+  }
+  for (size_t i = 0; i + 1 < A.size(); ++i) st.push_back({A[i], PASS_FWD, i == 0, false});
+  st.push_back({A.back(), -1, A.size() == 1, A.size() == 1});
+  for (int i = (int)A.size() - 2; i >= 0; --i) st.push_back({A[i], PASS_INV, false, i == 0});
+  return st;
+}
+
+PassDesc make_pass(const cfp_plan_s* p, int axis, int mode, double scale) {
+  PassDesc d;
+  d.n = (int)p->n[axis];
+  natural_cols(axis, p->n, &d.ncols, &d.inner_n);
+  d.in = natural_side(axis, p->n);
+  d.out = d.in;
+  d.mode = mode;
+  d.scale = scale;
+  d.colsym = p->colsym;
+  d.axsym = p->axsym;
+  d.diag = p->diag;
+  return d;
+}
+
+int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStream_t s, std::vector<hipEvent_t>* ev) {
+  if (!diag_override && p->sym_kind == 0)
+    return set_error(CFP_ERR_ARG_WRONGSTATE, "no symbol set on plan (call cfp_plan_set_symbol_* first)");
+  std::vector<Step> st = apply_steps(p);
+  const double invN = 1.0 / (double)p->N;
+  for (size_t i = 0; i < st.size(); ++i) {
+    const Step& q = st[i];
+    int mode = q.mode;
+    if (mode < 0) mode = (diag_override || p->sym_kind == 2) ? PASS_FUSED_DIAG : PASS_FUSED_SEP;
+    PassDesc d = make_pass(p, q.axis, mode, q.scale ? invN : 1.0);
+    if (diag_override) d.diag = diag_override;
+    int rc = ensure_tw(p, d.n);
+    if (rc) return rc;
+    if (ev) HIPCHK(hipEventRecord((*ev)[i], s));
+    hipError_t e = launch_axis_pass(d, q.from_b ? b : x, x, p->tw[d.n], s);
+    if (e != hipSuccess) return hip_error(e, "axis pass launch");
+  }
+  if (ev) HIPCHK(hipEventRecord((*ev)[st.size()], s));
+  return CFP_SUCCESS;
+}
+
+int run_transform(cfp_plan_s* p, bool inverse, const cd* in, cd* out, hipStream_t s) {
+  if (p->axes.empty()) {
+    if (in != out) HIPCHK(hipMemcpyAsync(out, in, sizeof(cd), hipMemcpyDeviceToDevice, s));
+    return CFP_SUCCESS;
+  }
+  bool first = true;
+  for (int ax : p->axes) {
+    PassDesc d = make_pass(p, ax, inverse ? PASS_INV : PASS_FWD, 1.0);
+    int rc = ensure_tw(p, d.n);
+    if (rc) return rc;
+    hipError_t e = launch_axis_pass(d, first ? in : out, out, p->tw[d.n], s);
+    if (e != hipSuccess) return hip_error(e, "axis pass launch");
+    first = false;
+  }
+  return CFP_SUCCESS;
+}
+
+void free_symbol(cfp_plan_s* p) {
+  if (p->colsym) hipFree(p->colsym);
+  if (p->axsym) hipFree(p->axsym);
+  if (p->diag) hipFree(p->diag);
+  p->colsym = p->axsym = p->diag = nullptr;
+  p->sym_kind = 0;
+}
+
+std::complex<double> lamc(const double lam[6], int a) { return {lam[2 * a], lam[2 * a + 1]}; }
+
+// Build colsym/axsym from per-axis host vectors s_d[k] = lambda_d * c_d_hat[k].
+int upload_separable(cfp_plan_s* p, const std::vector<cd> s[3]) {
+  const int f = p->fused_axis;
+  const i64 nf = p->n[f];
+  i64 ncols, inner_n;
+  natural_cols(f, p->n, &ncols, &inner_n);
+  std::vector<cd> col((size_t)ncols), ax((size_t)nf);
+  // column g of axis f -> the coordinates of the other two axes
+  for (i64 g = 0; g < ncols; ++g) {
+    i64 idx[3];
+    if (f == 0) { idx[0] = 0; idx[1] = g % p->n[1]; idx[2] = g / p->n[1]; }
+    else if (f == 1) { idx[0] = g % p->n[0]; idx[1] = 0; idx[2] = g / p->n[0]; }
+    else { idx[0] = g % p->n[0]; idx[1] = g / p->n[0]; idx[2] = 0; }
+    // reference summation order: ((x + y) + z) + 1 with the fused axis' term added last
+    double re = 0.0, im = 0.0;
+    for (int a = 0; a < 3; ++a) {
+      if (a == f) continue;
+      re += s[a][(size_t)idx[a]].x;
+      im += s[a][(size_t)idx[a]].y;
+    }
+    col[(size_t)g] = make_cd(re, im);
+  }
+  for (i64 k = 0; k < nf; ++k) ax[(size_t)k] = s[f][(size_t)k];
+  free_symbol(p);
+  HIPCHK(hipMalloc(&p->colsym, sizeof(cd) * (size_t)ncols));
+  HIPCHK(hipMalloc(&p->axsym, sizeof(cd) * (size_t)nf));
+  HIPCHK(hipMemcpy(p->colsym, col.data(), sizeof(cd) * (size_t)ncols, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(p->axsym, ax.data(), sizeof(cd) * (size_t)nf, hipMemcpyHostToDevice));
+  for (int a = 0; a < 3; ++a) p->sym1d[a] = s[a];
+  p->sym_kind = 1;
+  return CFP_SUCCESS;
+}
+
+int set_separable(cfp_plan_s* p, const std::vector<cd> hat[3], const double lam[6]) {
+  std::vector<cd> s[3];
+  for (int a = 0; a < 3; ++a) {
+    std::complex<double> l = lamc(lam, a);
+    s[a].resize(hat[a].size());
+    for (size_t k = 0; k < hat[a].size(); ++k) {
+      std::complex<double> c(hat[a][k].x, hat[a][k].y);
+      // c * lambda as in vec_kronecker_product_identity_* (src/FftLinearSolver_3D.c:100,122)
+      const double re = c.real() * l.real() - c.imag() * l.imag();
+      const double im = c.real() * l.imag() + c.imag() * l.real();
+      s[a][k] = make_cd(re, im);
+    }
+  }
+  return upload_separable(p, s);
+}
+
+}  // namespace
+
+extern "C" int cfp_plan_create(cfp_plan_t* plan, int64_t nx, int64_t ny, int64_t nz, int device) {
+  if (!plan) return set_error(CFP_ERR_ARG_NULL, "plan is NULL");
+  *plan = nullptr;
+  if (nx < 1 || ny < 1 || nz < 1) return set_error(CFP_ERR_ARG_OUTOFRANGE, "grid sizes must be >= 1");
+  if (nx > 4096 || ny > 4096 || nz > 4096)
+    return set_error(CFP_ERR_SUP, "axis lengths above 4096 are not supported");
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return set_error(CFP_ERR_ARG_OUTOFRANGE, "device %d out of range", device);
+  DeviceGuard dg(device);
+  std::unique_ptr<cfp_plan_s> p(new cfp_plan_s);
+  p->device = device;
+  p->n[0] = nx; p->n[1] = ny; p->n[2] = nz;
+  p->N = nx * ny * nz;
+  for (int a = 0; a < 3; ++a)
+    if (p->n[a] > 1) p->axes.push_back(a);
+  p->fused_axis = p->axes.empty() ? 0 : p->axes.back();
+  for (int a : p->axes) {
+    int rc = ensure_tw(p.get(), (int)p->n[a]);
+    if (rc) return rc;
+  }
+  if (p->axes.empty()) {
+    int rc = ensure_tw(p.get(), 1);
+    if (rc) return rc;
+  }
+  *plan = p.release();
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_plan_destroy(cfp_plan_t p) {
+  if (!p) return CFP_SUCCESS;
+  DeviceGuard dg(p->device);
+  free_symbol(p);
+  for (auto& kv : p->tw) hipFree(kv.second);
+  if (p->host_stage) hipFree(p->host_stage);
+  delete p;
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_plan_set_symbol_transport(cfp_plan_t p, const double lam[6]) {
+  if (!p || !lam) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  DeviceGuard dg(p->device);
+  std::vector<cd> hat[3];
+  for (int a = 0; a < 3; ++a) hat[a] = host_transport_symbol(p->n[a]);
+  return set_separable(p, hat, lam);
+}
+
+extern "C" int cfp_plan_set_symbol_separable(cfp_plan_t p, const double* cx, const double* cy, const double* cz,
+                                             const double lam[6]) {
+  if (!p || !cx || !cy || !cz || !lam) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  DeviceGuard dg(p->device);
+  std::vector<cd> hat[3];
+  const double* src[3] = {cx, cy, cz};
+  for (int a = 0; a < 3; ++a) {
+    hat[a].resize((size_t)p->n[a]);
+    std::memcpy(hat[a].data(), src[a], sizeof(cd) * (size_t)p->n[a]);
+  }
+  return set_separable(p, hat, lam);
+}
+
+extern "C" int cfp_plan_set_diag(cfp_plan_t p, const double* diag, int on_device) {
+  if (!p || !diag) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  DeviceGuard dg(p->device);
+  free_symbol(p);
+  HIPCHK(hipMalloc(&p->diag, sizeof(cd) * (size_t)p->N));
+  HIPCHK(hipMemcpy(p->diag, diag, sizeof(cd) * (size_t)p->N, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+  p->sym_kind = 2;
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_plan_get_diag(cfp_plan_t p, double* diag_dev, void* stream) {
+  if (!p || !diag_dev) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  DeviceGuard dg(p->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (p->sym_kind == 2) {
+    HIPCHK(hipMemcpyAsync(diag_dev, p->diag, sizeof(cd) * (size_t)p->N, hipMemcpyDeviceToDevice, s));
+    return CFP_SUCCESS;
+  }
+  if (p->sym_kind != 1) return set_error(CFP_ERR_ARG_WRONGSTATE, "no symbol set");
+  cd* tmp[3] = {nullptr, nullptr, nullptr};
+  for (int a = 0; a < 3; ++a) {
+    HIPCHK(hipMalloc(&tmp[a], sizeof(cd) * (size_t)p->n[a]));
+    HIPCHK(hipMemcpy(tmp[a], p->sym1d[a].data(), sizeof(cd) * (size_t)p->n[a], hipMemcpyHostToDevice));
+  }
+  const cd one = make_cd(1.0, 0.0);
+  hipError_t e = launch_build_diag_separable((cd*)diag_dev, tmp[0], tmp[1], tmp[2], p->n[0], p->n[1], p->n[2], one,
+                                             one, one, s);
+  hipStreamSynchronize(s);
+  for (int a = 0; a < 3; ++a) hipFree(tmp[a]);
+  if (e != hipSuccess) return hip_error(e, "build diag");
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_plan_apply(cfp_plan_t p, const double* b, double* x, void* stream) {
+  if (!p || !b || !x) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  DeviceGuard dg(p->device);
+  return run_apply(p, nullptr, (const cd*)b, (cd*)x, (hipStream_t)stream, nullptr);
+}
+
+extern "C" int cfp_plan_apply_with_diag(cfp_plan_t p, const double* diag, const double* b, double* x, void* stream) {
+  if (!p || !diag || !b || !x) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  DeviceGuard dg(p->device);
+  return run_apply(p, (const cd*)diag, (const cd*)b, (cd*)x, (hipStream_t)stream, nullptr);
+}
+
+extern "C" int cfp_plan_apply_host(cfp_plan_t p, const double* b, double* x) {
+  if (!p || !b || !x) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  DeviceGuard dg(p->device);
+  const size_t bytes = sizeof(cd) * (size_t)p->N;
+  if (!p->host_stage) HIPCHK(hipMalloc(&p->host_stage, bytes));
+  HIPCHK(hipMemcpy(p->host_stage, b, bytes, hipMemcpyHostToDevice));
+  int rc = run_apply(p, nullptr, p->host_stage, p->host_stage, nullptr, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipMemcpy(x, p->host_stage, bytes, hipMemcpyDeviceToHost));
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_plan_forward(cfp_plan_t p, const double* in, double* out, void* stream) {
+  if (!p || !in || !out) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  DeviceGuard dg(p->device);
+  return run_transform(p, false, (const cd*)in, (cd*)out, (hipStream_t)stream);
+}
+
+extern "C" int cfp_plan_backward(cfp_plan_t p, const double* in, double* out, void* stream) {
+  if (!p || !in || !out) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  DeviceGuard dg(p->device);
+  return run_transform(p, true, (const cd*)in, (cd*)out, (hipStream_t)stream);
+}
+
+extern "C" int cfp_plan_num_passes(cfp_plan_t p, int* passes) {
+  if (!p || !passes) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  *passes = (int)apply_steps(p).size();
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_plan_pass_info(cfp_plan_t p, int pass, int* axis, int* n, int64_t* ncols, int* mode, int* fast) {
+  if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
+  std::vector<Step> st = apply_steps(p);
+  if (pass < 0 || pass >= (int)st.size()) return set_error(CFP_ERR_ARG_OUTOFRANGE, "pass index");
+  int m = st[pass].mode;
+  if (m < 0) m = p->sym_kind == 2 ? PASS_FUSED_DIAG : PASS_FUSED_SEP;
+  PassDesc d = make_pass(p, st[pass].axis, m, 1.0);
+  if (axis) *axis = st[pass].axis;
+  if (n) *n = d.n;
+  if (ncols) *ncols = d.ncols;
+  if (mode) *mode = m;
+  if (fast) *fast = fast_path_supported(d) ? 1 : 0;
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_plan_time_passes(cfp_plan_t p, const double* b, double* x, int iters, double* ms_out, void* stream) {
+  if (!p || !b || !x || !ms_out) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  if (iters < 1) return set_error(CFP_ERR_ARG_OUTOFRANGE, "iters must be >= 1");
+  DeviceGuard dg(p->device);
+  hipStream_t s = (hipStream_t)stream;
+  const size_t np = apply_steps(p).size();
+  std::vector<double> acc(np, 0.0);
+  std::vector<hipEvent_t> ev(np + 1);
+  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  int rc = CFP_SUCCESS;
+  for (int it = 0; it < iters && rc == CFP_SUCCESS; ++it) {
+    rc = run_apply(p, nullptr, (const cd*)b, (cd*)x, s, &ev);
+    if (rc) break;
+    hipError_t e = hipEventSynchronize(ev[np]);
+    if (e != hipSuccess) { rc = hip_error(e, "event sync"); break; }
+    for (size_t i = 0; i < np; ++i) {
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+      acc[i] += ms;
+    }
+  }
+  for (auto& e : ev) hipEventDestroy(e);
+  if (rc) return rc;
+  for (size_t i = 0; i < np; ++i) ms_out[i] = acc[i] / iters;
+  return CFP_SUCCESS;
+}
+
+// ------------------------------------------------------------------ vector kernels
+extern "C" int cfp_pointwise_divide(double* w, const double* x, const double* y, int64_t n, void* stream) {
+  if (!w || !x || !y) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  hipError_t e = launch_pointwise_divide((cd*)w, (const cd*)x, (const cd*)y, n, (hipStream_t)stream);
+  return e == hipSuccess ? CFP_SUCCESS : hip_error(e, "pointwise divide");
+}
+
+extern "C" int cfp_scale(double* x, double re, double im, int64_t n, void* stream) {
+  if (!x) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  hipError_t e = launch_scale((cd*)x, make_cd(re, im), n, (hipStream_t)stream);
+  return e == hipSuccess ? CFP_SUCCESS : hip_error(e, "scale");
+}
+
+extern "C" int cfp_fill_uniform(double* x, int64_t n, uint64_t seed, int64_t offset, void* stream) {
+  if (!x) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  hipError_t e = launch_fill_uniform((cd*)x, n, seed, offset, (hipStream_t)stream);
+  return e == hipSuccess ? CFP_SUCCESS : hip_error(e, "fill uniform");
+}
+
+extern "C" int cfp_build_diag_3d(double* diag, const double* cx, const double* cy, const double* cz, int64_t nx,
+                                 int64_t ny, int64_t nz, const double lam[6], void* stream) {
+  if (!diag || !cx || !cy || !cz || !lam) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  hipError_t e = launch_build_diag_separable((cd*)diag, (const cd*)cx, (const cd*)cy, (const cd*)cz, nx, ny, nz,
+                                             make_cd(lam[0], lam[1]), make_cd(lam[2], lam[3]),
+                                             make_cd(lam[4], lam[5]), (hipStream_t)stream);
+  return e == hipSuccess ? CFP_SUCCESS : hip_error(e, "build diag");
+}
+
+extern "C" int cfp_transport_symbol_1d(int64_t n, double* out) {
+  if (!out) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  if (n < 1) return set_error(CFP_ERR_ARG_OUTOFRANGE, "n must be >= 1");
+  std::vector<cd> s = host_transport_symbol(n);
+  std::memcpy(out, s.data(), sizeof(cd) * (size_t)n);
+  return CFP_SUCCESS;
+}

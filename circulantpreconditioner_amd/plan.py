@@ -1,0 +1,219 @@
+"""Python host API over the HIP plan (``include/circulant_fft.h``).
+
+PyTorch only supplies device memory and streams here; every computation is a
+launch of the gfx950 kernels in ``libcirculant_fft.so``.
+
+    plan = CirculantPlan((nx, ny, nz), device=0)
+    plan.set_transport_symbol((lx, ly, lz))      # setupFFTPrec3D (src/PCSHELLFft_3D.cxx:26-84)
+    x = plan.apply(b)                            # solve_3D       (src/FftLinearSolver_3D.c:166-190)
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib
+
+
+def _stream_handle(stream=None) -> int:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return int(stream.cuda_stream)
+
+
+def _dev_ptr(t: torch.Tensor, n: int, name: str) -> int:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.dtype != torch.complex128:
+        raise TypeError(f"{name} must be complex128, got {t.dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device (HIP) tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if t.numel() != n:
+        raise ValueError(f"{name} has {t.numel()} elements, expected {n}")
+    return t.data_ptr()
+
+
+def _lam6(lam: Sequence) -> ctypes.Array:
+    vals = []
+    for v in lam:
+        c = complex(v)
+        vals += [c.real, c.imag]
+    if len(vals) != 6:
+        raise ValueError("lambda must have three entries (x, y, z)")
+    return (ctypes.c_double * 6)(*vals)
+
+
+PASS_MODES = {0: "fwd", 1: "inv", 2: "fused_sep", 3: "fused_diag"}
+
+
+class CirculantPlan:
+    """One (n_x, n_y, n_z) grid on one GPU: the reference's FFT_MAT + Diag (+ b_hat)."""
+
+    def __init__(self, dims: Sequence[int], device: int | None = None):
+        nx, ny, nz = (int(d) for d in dims)
+        if device is None:
+            device = torch.cuda.current_device()
+        self.dims = (nx, ny, nz)
+        self.N = nx * ny * nz
+        self.device = int(device)
+        h = ctypes.c_void_p()
+        check(lib().cfp_plan_create(ctypes.byref(h), nx, ny, nz, self.device))
+        self._h = h
+
+    # ---------------------------------------------------------------- symbol
+    def set_transport_symbol(self, lam: Sequence) -> "CirculantPlan":
+        """Diag = 1 + sum_d lambda_d (1 - e^{-2 pi i k_d/n_d}) (closed form)."""
+        check(lib().cfp_plan_set_symbol_transport(self._h, _lam6(lam)))
+        return self
+
+    def set_separable_symbol(self, cx_hat, cy_hat, cz_hat, lam: Sequence) -> "CirculantPlan":
+        """Diag = 1 + lx*tile(cx_hat) + ly*repeat(tile(cy_hat)) + lz*repeat(cz_hat)."""
+        arrs = [np.ascontiguousarray(np.asarray(a, dtype=np.complex128).reshape(-1)) for a in (cx_hat, cy_hat, cz_hat)]
+        for a, n in zip(arrs, self.dims):
+            if a.size != n:
+                raise ValueError("1-D symbol vector length does not match the grid")
+        check(lib().cfp_plan_set_symbol_separable(self._h, arrs[0].ctypes.data, arrs[1].ctypes.data,
+                                                  arrs[2].ctypes.data, _lam6(lam)))
+        return self
+
+    def set_diag(self, diag) -> "CirculantPlan":
+        """General symbol: explicit Diag vector (device tensor or host array)."""
+        if isinstance(diag, torch.Tensor) and diag.is_cuda:
+            check(lib().cfp_plan_set_diag(self._h, _dev_ptr(diag, self.N, "diag"), 1))
+            torch.cuda.synchronize(diag.device)
+        else:
+            d = np.ascontiguousarray(np.asarray(diag.cpu() if isinstance(diag, torch.Tensor) else diag,
+                                                dtype=np.complex128).reshape(-1))
+            if d.size != self.N:
+                raise ValueError("diag size mismatch")
+            check(lib().cfp_plan_set_diag(self._h, d.ctypes.data, 0))
+        return self
+
+    def get_diag(self) -> torch.Tensor:
+        out = torch.empty(self.N, dtype=torch.complex128, device=f"cuda:{self.device}")
+        check(lib().cfp_plan_get_diag(self._h, out.data_ptr(), _stream_handle()))
+        return out
+
+    # ---------------------------------------------------------------- apply
+    def apply(self, b: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+        """x = (1/N) IDFT(DFT(b) ./ Diag).  `out` may be `b` (in place)."""
+        bp = _dev_ptr(b, self.N, "b")
+        if out is None:
+            out = torch.empty_like(b)
+        xp = _dev_ptr(out, self.N, "out")
+        check(lib().cfp_plan_apply(self._h, bp, xp, _stream_handle(stream)))
+        return out
+
+    def apply_with_diag(self, diag: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
+                        stream=None) -> torch.Tensor:
+        bp = _dev_ptr(b, self.N, "b")
+        dp = _dev_ptr(diag, self.N, "diag")
+        if out is None:
+            out = torch.empty_like(b)
+        check(lib().cfp_plan_apply_with_diag(self._h, dp, bp, _dev_ptr(out, self.N, "out"), _stream_handle(stream)))
+        return out
+
+    def apply_host(self, b) -> np.ndarray:
+        """PCIe-inclusive variant: host numpy in, host numpy out (synchronous)."""
+        bb = np.ascontiguousarray(np.asarray(b, dtype=np.complex128).reshape(-1))
+        if bb.size != self.N:
+            raise ValueError("b size mismatch")
+        x = np.empty_like(bb)
+        check(lib().cfp_plan_apply_host(self._h, bb.ctypes.data, x.ctypes.data))
+        return x
+
+    def forward(self, x: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+        """Unnormalised 3-D DFT (MatMult on MATFFTW)."""
+        if out is None:
+            out = torch.empty_like(x)
+        check(lib().cfp_plan_forward(self._h, _dev_ptr(x, self.N, "x"), _dev_ptr(out, self.N, "out"),
+                                     _stream_handle(stream)))
+        return out
+
+    def backward(self, x: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+        """Unnormalised inverse 3-D DFT (MatMultTranspose on MATFFTW)."""
+        if out is None:
+            out = torch.empty_like(x)
+        check(lib().cfp_plan_backward(self._h, _dev_ptr(x, self.N, "x"), _dev_ptr(out, self.N, "out"),
+                                      _stream_handle(stream)))
+        return out
+
+    # ---------------------------------------------------------------- introspection
+    def passes(self) -> list:
+        n = ctypes.c_int()
+        check(lib().cfp_plan_num_passes(self._h, ctypes.byref(n)))
+        out = []
+        for i in range(n.value):
+            ax, nn, mode, fast = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+            nc = ctypes.c_int64()
+            check(lib().cfp_plan_pass_info(self._h, i, ctypes.byref(ax), ctypes.byref(nn), ctypes.byref(nc),
+                                           ctypes.byref(mode), ctypes.byref(fast)))
+            out.append({"axis": "xyz"[ax.value], "n": nn.value, "ncols": nc.value,
+                        "mode": PASS_MODES[mode.value], "fast": bool(fast.value)})
+        return out
+
+    def time_passes(self, b: torch.Tensor, x: torch.Tensor, iters: int = 20, stream=None) -> list:
+        """Mean device time (ms) of each launch of one apply, HIP events on `stream`."""
+        npass = len(self.passes())
+        ms = (ctypes.c_double * npass)()
+        check(lib().cfp_plan_time_passes(self._h, _dev_ptr(b, self.N, "b"), _dev_ptr(x, self.N, "x"), int(iters),
+                                         ms, _stream_handle(stream)))
+        return list(ms)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().cfp_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def fill_uniform(t: torch.Tensor, seed: int, offset: int = 0, stream=None) -> torch.Tensor:
+    """Counter-based synthetic input generated on the GPU."""
+    check(lib().cfp_fill_uniform(_dev_ptr(t, t.numel(), "t"), t.numel(), int(seed), int(offset),
+                                 _stream_handle(stream)))
+    return t
+
+
+def transport_symbol_1d(n: int) -> np.ndarray:
+    out = np.empty(int(n), dtype=np.complex128)
+    check(lib().cfp_transport_symbol_1d(int(n), out.ctypes.data))
+    return out
+
+
+def pointwise_divide(w: torch.Tensor, x: torch.Tensor, y: torch.Tensor, stream=None) -> torch.Tensor:
+    n = w.numel()
+    check(lib().cfp_pointwise_divide(_dev_ptr(w, n, "w"), _dev_ptr(x, n, "x"), _dev_ptr(y, n, "y"), n,
+                                     _stream_handle(stream)))
+    return w
+
+
+def scale(x: torch.Tensor, alpha: complex, stream=None) -> torch.Tensor:
+    a = complex(alpha)
+    check(lib().cfp_scale(_dev_ptr(x, x.numel(), "x"), a.real, a.imag, x.numel(), _stream_handle(stream)))
+    return x
+
+
+def build_diag_3d(diag: torch.Tensor, cx_hat: torch.Tensor, cy_hat: torch.Tensor, cz_hat: torch.Tensor,
+                  dims: Sequence[int], lam: Sequence, stream=None) -> torch.Tensor:
+    nx, ny, nz = (int(d) for d in dims)
+    check(lib().cfp_build_diag_3d(_dev_ptr(diag, nx * ny * nz, "diag"), _dev_ptr(cx_hat, nx, "cx_hat"),
+                                  _dev_ptr(cy_hat, ny, "cy_hat"), _dev_ptr(cz_hat, nz, "cz_hat"), nx, ny, nz,
+                                  _lam6(lam), _stream_handle(stream)))
+    return diag

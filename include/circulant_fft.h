@@ -1,0 +1,112 @@
+/*
+ * circulant_fft.h -- C ABI of the MI355X-native circulant FFT preconditioner (libcirculant_fft.so).
+ *
+ * This is the plan-level boundary.  Every pointer argument named `*_dev` is a device
+ * pointer (hipMalloc'd, HBM-resident); complex values are interleaved (re, im) doubles;
+ * grids are x-fastest, i = ix + nx*(iy + ny*iz) -- the row-major {nz, ny, nx} layout of the
+ * reference's MatCreateFFT(..., dims = {n_z, n_y, n_x}) (src/PCSHELLFft_3D.cxx:34-35).
+ * `stream` is a hipStream_t (NULL = default stream).  Calls that take a stream only
+ * enqueue work (stream-ordered, like any HIP library call); cfp_stream_sync() waits.
+ *
+ * Return values are error codes numerically equal to PETSc's (petscerror.h): 0 =
+ * PETSC_SUCCESS, so a PETSc caller may PetscCall() them directly.  cfp_last_error()
+ * returns a message for the calling thread's last failure.
+ *
+ * What each entry replaces in the reference (/root/reference):
+ *   cfp_plan_create + cfp_plan_set_symbol_*      setupFFTPrec3D            src/PCSHELLFft_3D.cxx:26-84
+ *                                                (MatCreateFFT + Diag build, src/FftLinearSolver_3D.c:136-164)
+ *   cfp_plan_apply                               solve_3D (complex build)  src/FftLinearSolver_3D.c:166-190
+ *                                                (the arithmetic of applyFFT3DPrecTransport, src/PCSHELLFft_3D.cxx:10-24)
+ *   cfp_plan_apply_with_diag                     solve_3D with a caller-owned Diag Vec  :166-190
+ *   cfp_plan_forward / cfp_plan_backward         MatMult / MatMultTranspose on MATFFTW (:170, :180)
+ *   cfp_pointwise_divide / cfp_scale             VecPointwiseDivide (:174) / VecScale (:184)
+ *   cfp_build_diag_3d                            build_diag_mat_vec_3D      :136-164
+ *   cfp_transport_symbol_1d                      build_transport_col + 1-D MatMult (:80-90, :235-249)
+ *   cfp_plan_destroy                             destroyFFTPrec3D           src/PCSHELLFft_3D.cxx:86-99
+ * The PETSc-typed PCSHELL callbacks themselves are declared in pcshell_fft3d.h.
+ */
+#ifndef CIRCULANT_FFT_H
+#define CIRCULANT_FFT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* error codes (values of petscerror.h) */
+#define CFP_SUCCESS 0
+#define CFP_ERR_MEM 55         /* PETSC_ERR_MEM */
+#define CFP_ERR_SUP 56         /* PETSC_ERR_SUP: unsupported size / layout */
+#define CFP_ERR_ARG_SIZ 60     /* PETSC_ERR_ARG_SIZ */
+#define CFP_ERR_ARG_WRONG 62   /* PETSC_ERR_ARG_WRONG */
+#define CFP_ERR_ARG_OUTOFRANGE 63 /* PETSC_ERR_ARG_OUTOFRANGE */
+#define CFP_ERR_ARG_WRONGSTATE 73 /* PETSC_ERR_ARG_WRONGSTATE (no symbol set yet) */
+#define CFP_ERR_LIB 76         /* PETSC_ERR_LIB: HIP / RCCL runtime failure */
+#define CFP_ERR_ARG_NULL 85    /* PETSC_ERR_ARG_NULL */
+
+typedef struct cfp_plan_s *cfp_plan_t;
+
+/* ---- version / diagnostics */
+const char *cfp_version(void);
+const char *cfp_last_error(void);
+int cfp_device_count(int *count);
+int cfp_stream_sync(void *stream);
+
+/* ---- single-GPU plan: n_x, n_y, n_z >= 1, each <= 4096; `device` = HIP ordinal. */
+int cfp_plan_create(cfp_plan_t *plan, int64_t nx, int64_t ny, int64_t nz, int device);
+int cfp_plan_destroy(cfp_plan_t plan);
+
+/* Transport symbol in closed form: Diag[k] = 1 + sum_d lambda_d (1 - e^{-2 pi i k_d / n_d}),
+ * lam = {lx.re, lx.im, ly.re, ly.im, lz.re, lz.im}.  Axes with n_d == 1 contribute 0
+ * (build_transport_col leaves a size-1 column zero, src/FftLinearSolver_3D.c:83). */
+int cfp_plan_set_symbol_transport(cfp_plan_t plan, const double lam[6]);
+/* Separable symbol from caller-given 1-D eigenvalue vectors (host arrays of n_x, n_y, n_z
+ * complex values, e.g. the 1-D DFTs of arbitrary circulant columns):
+ * Diag = 1 + lx*tile(cx_hat) + ly*repeat(tile(cy_hat)) + lz*repeat(cz_hat)   (:136-164). */
+int cfp_plan_set_symbol_separable(cfp_plan_t plan, const double *cx_hat, const double *cy_hat,
+                                  const double *cz_hat, const double lam[6]);
+/* General symbol: an explicit Diag vector of N complex values (copied into the plan).
+ * diag_is_device != 0 means `diag` is a device pointer. */
+int cfp_plan_set_diag(cfp_plan_t plan, const double *diag, int diag_is_device);
+/* Materialise the plan's current symbol as a full Diag vector (device). */
+int cfp_plan_get_diag(cfp_plan_t plan, double *diag_dev, void *stream);
+
+/* x = (1/N) * IDFT3( DFT3(b) ./ Diag ): one PCApply / one direct solve.
+ * b_dev may alias x_dev (the direct solver passes Un, Un). */
+int cfp_plan_apply(cfp_plan_t plan, const double *b_dev, double *x_dev, void *stream);
+/* Same with a caller-owned Diag vector (device), as solve_3D(FFT_MAT, X, Diag, b, b_hat, size). */
+int cfp_plan_apply_with_diag(cfp_plan_t plan, const double *diag_dev, const double *b_dev, double *x_dev,
+                             void *stream);
+/* Host-buffer variant (PCIe-inclusive): stages b through the plan's device buffers. Synchronous. */
+int cfp_plan_apply_host(cfp_plan_t plan, const double *b_host, double *x_host);
+
+/* Unnormalised 3-D transforms: forward (e^{-}, MatMult) and backward (e^{+}, MatMultTranspose). */
+int cfp_plan_forward(cfp_plan_t plan, const double *in_dev, double *out_dev, void *stream);
+int cfp_plan_backward(cfp_plan_t plan, const double *in_dev, double *out_dev, void *stream);
+
+/* Introspection: number of kernel launches of one apply, and per-launch timing.
+ * cfp_plan_time_passes runs `iters` applies and writes the mean duration (ms) of each of the
+ * apply's launches into ms_out[0..passes) (HIP events on `stream`). */
+int cfp_plan_num_passes(cfp_plan_t plan, int *passes);
+int cfp_plan_pass_info(cfp_plan_t plan, int pass, int *axis, int *n, int64_t *ncols, int *mode, int *fast);
+int cfp_plan_time_passes(cfp_plan_t plan, const double *b_dev, double *x_dev, int iters, double *ms_out,
+                         void *stream);
+
+/* ---- vector kernels (device arrays of n complex values) */
+int cfp_pointwise_divide(double *w_dev, const double *x_dev, const double *y_dev, int64_t n, void *stream);
+int cfp_scale(double *x_dev, double alpha_re, double alpha_im, int64_t n, void *stream);
+/* synthetic input of SURVEY.md §8d: element i gets U[-1,1)^2 from SplitMix64(seed ^ 2(i+offset)),
+ * SplitMix64(seed ^ 2(i+offset)+1) */
+int cfp_fill_uniform(double *x_dev, int64_t n, uint64_t seed, int64_t offset, void *stream);
+/* build_diag_mat_vec_3D on device from three device 1-D vectors */
+int cfp_build_diag_3d(double *diag_dev, const double *cx_hat_dev, const double *cy_hat_dev,
+                      const double *cz_hat_dev, int64_t nx, int64_t ny, int64_t nz, const double lam[6],
+                      void *stream);
+/* host: out[k] = DFT(1, -1, 0, ...)[k] = 1 - e^{-2 pi i k/n} (0 for n == 1), n complex values */
+int cfp_transport_symbol_1d(int64_t n, double *out_host);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CIRCULANT_FFT_H */

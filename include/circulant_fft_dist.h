@@ -1,0 +1,64 @@
+/*
+ * circulant_fft_dist.h -- slab-decomposed circulant FFT preconditioner over several GPUs.
+ *
+ * Layout: rank r of P owns the z-planes [r*nz/P, (r+1)*nz/P) of the
+ * x-fastest grid, i.e. the contiguous rows [r*N/P, (r+1)*N/P) -- exactly PETSc's
+ * PETSC_DECIDE distribution of VecCreateMPI (tests/TransportEquationFFT_..._mpi.cxx:66) and
+ * FFTW-MPI's local_n0 slabs of MATFFTW (src/PCSHELLFft_3D.cxx:34-35).  Requires P | nz and
+ * P | ny.
+ *
+ * One apply = x-fwd, y-fwd (written straight into per-peer send chunks), all-to-all,
+ * z: DFT ./Diag IDFT, all-to-all back, y-inv (read straight from the received chunks),
+ * x-inv * 1/N.  Two all-to-alls per apply (FFTW-MPI's non-transposed plans need four).
+ * Diag is generated per rank from lambda and global frequency indices (no communication).
+ *
+ * Two executors share the same pass schedule:
+ *   cfp_dist_plan_*   one process per GPU, RCCL (ncclSend/ncclRecv in a group) over xGMI;
+ *   cfp_group_*       one process driving P slabs (on one or several GPUs) with device
+ *                     copies as the exchange -- a single-process multi-GPU mode and the way
+ *                     the slab layouts are exercised on a one-GPU machine.
+ */
+#ifndef CIRCULANT_FFT_DIST_H
+#define CIRCULANT_FFT_DIST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct cfp_dist_plan_s *cfp_dist_plan_t;
+typedef struct cfp_group_s *cfp_group_t;
+
+/* host-only layout query: out[0..8) = {nz_local, ny_local, z0, y0, local_size,
+ * chunk (elements per peer message), local_offset (global index of the first local element),
+ * nranks} */
+int cfp_slab_layout(int64_t nx, int64_t ny, int64_t nz, int nranks, int rank, int64_t *out);
+
+/* RCCL unique id (128 bytes): created on rank 0, broadcast by the caller, passed to every rank */
+int cfp_dist_unique_id_bytes(void);
+int cfp_dist_get_unique_id(char *id_out);
+
+int cfp_dist_plan_create(cfp_dist_plan_t *plan, int64_t nx, int64_t ny, int64_t nz, int nranks, int rank,
+                         const char *unique_id, int device);
+int cfp_dist_plan_destroy(cfp_dist_plan_t plan);
+int cfp_dist_plan_set_symbol_transport(cfp_dist_plan_t plan, const double lam[6]);
+/* b_dev, x_dev: this rank's slab (local_size complex values); b may alias x */
+int cfp_dist_plan_apply(cfp_dist_plan_t plan, const double *b_dev, double *x_dev, void *stream);
+int cfp_dist_plan_local_size(cfp_dist_plan_t plan, int64_t *local_size);
+int cfp_dist_plan_num_phases(cfp_dist_plan_t plan, int *phases);
+/* mean ms of each phase (kernels and exchanges, in order) over `iters` applies */
+int cfp_dist_plan_time_phases(cfp_dist_plan_t plan, const double *b_dev, double *x_dev, int iters, double *ms_out,
+                              void *stream);
+
+/* single-process group of P slabs; devices[r] = HIP device of slab r (may repeat) */
+int cfp_group_create(cfp_group_t *group, int64_t nx, int64_t ny, int64_t nz, int nranks, const int *devices);
+int cfp_group_destroy(cfp_group_t group);
+int cfp_group_set_symbol_transport(cfp_group_t group, const double lam[6]);
+/* b_devs[r], x_devs[r]: slab r on devices[r]; synchronous */
+int cfp_group_apply(cfp_group_t group, const double *const *b_devs, double *const *x_devs);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CIRCULANT_FFT_DIST_H */

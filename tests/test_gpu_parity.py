@@ -1,0 +1,230 @@
+"""GPU parity: the HIP path (through the C ABI) vs the golden vectors and the CPU oracle.
+
+Tolerance (north_star): relative L2 error <= 1e-10 on the preconditioned vector.
+Full-size cases (256^3, 512^3) are checked through size-independent properties:
+the residual ||C x - b|| / ||b|| of the circulant operator, and the round trip
+backward(forward(b)) = N b.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+
+
+def _lam(case):
+    return tuple(complex(re, im) for re, im in case["lam"])
+
+
+@pytest.fixture(scope="module")
+def cp():
+    import circulantpreconditioner_amd as cp
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    return cp
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.complex128)).cuda()
+
+
+def _rel(a, b):
+    a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else a
+    b = b.detach().cpu().numpy() if isinstance(b, torch.Tensor) else b
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+def apply_C_torch(x, n, lam):
+    """y = C x on the device with torch.roll (test-side checker, not the product)."""
+    nx, ny, nz = n
+    u = x.reshape(nz, ny, nx)
+    y = u.clone()
+    for l, dim, nd in ((lam[0], 2, nx), (lam[1], 1, ny), (lam[2], 0, nz)):
+        if nd > 1 and l != 0:
+            y = y + l * (u - torch.roll(u, shifts=1, dims=dim))
+    return y.reshape(-1)
+
+
+GOLDEN = ["kat3d_4x3x2", "py3d_10x25x40", "kat1d_4", "py1d_8", "py2d_12x10", "py2d_50x200",
+          "rand16_A", "rand16_B", "odd6x5x7"]
+
+
+@pytest.mark.parametrize("name", GOLDEN)
+def test_golden_transport_symbol(cp, golden, name):
+    c = golden[name]
+    n = tuple(c["n"])
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(_lam(c))
+        x = plan.apply(_dev(c["b"]))
+        torch.cuda.synchronize()
+        assert _rel(x, c["x"]) < TOL
+        assert _rel(plan.get_diag(), c["diag"]) < 1e-14
+
+
+@pytest.mark.parametrize("name", GOLDEN)
+def test_golden_explicit_diag(cp, golden, name):
+    c = golden[name]
+    n = tuple(c["n"])
+    with cp.CirculantPlan(n) as plan:
+        plan.set_diag(_dev(c["diag"]))
+        x = plan.apply(_dev(c["b"]))
+        assert _rel(x, c["x"]) < TOL
+        # solve_3D with a caller-owned Diag vector
+        y = plan.apply_with_diag(_dev(c["diag"]), _dev(c["b"]))
+        assert _rel(y, c["x"]) < TOL
+
+
+def test_golden_rand32(cp, golden):
+    c = golden["rand32_A"]
+    n = tuple(c["n"])
+    b = torch.empty(32 ** 3, dtype=torch.complex128, device="cuda")
+    cp.fill_uniform(b, c["b_generator"]["seed"])
+    import hashlib
+    assert hashlib.sha256(b.cpu().numpy().tobytes()).hexdigest() == c["b_sha256"]
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(_lam(c))
+        assert _rel(plan.apply(b), c["x"]) < TOL
+
+
+def test_kat1d_published(cp, golden):
+    c = golden["kat1d_4"]
+    with cp.CirculantPlan((4, 1, 1)) as plan:
+        plan.set_transport_symbol((0.5, 0, 0))
+        x = plan.apply(_dev(c["b"])).cpu().numpy()
+    np.testing.assert_allclose(x.real, [6.7, 2.9, 6.3, 20.1], atol=1e-12)
+    assert np.abs(x.imag).max() < 1e-12
+
+
+SIZES = [(16, 16, 16), (32, 32, 32), (64, 64, 64), (128, 128, 128), (32, 64, 128), (256, 16, 8),
+         (8, 256, 16), (512, 4, 16), (16, 32, 512), (1024, 16, 16), (7, 9, 11), (20, 30, 40),
+         (64, 1, 1), (1, 64, 1), (1, 1, 64), (100, 1, 1), (1, 1, 1), (48, 64, 1), (2, 2, 2),
+         (1000, 3, 2), (3, 243, 5)]
+
+
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("lam", [(0.6, 0.15, 0.02), (55.6, 0.0, 0.0), (0.3 + 0.2j, -0.1j, 1.7)])
+def test_vs_oracle(cp, oracle, n, lam):
+    N = int(np.prod(n))
+    b = oracle.c_fill_uniform(N, 20251017)
+    d = oracle.c_build_diag_transport(n, lam)
+    ref = oracle.c_solve_3d(d, b, n)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam)
+        x = plan.apply(_dev(b))
+        assert _rel(x, ref) < TOL, plan.passes()
+
+
+@pytest.mark.parametrize("n", [(32, 32, 32), (64, 32, 16), (20, 30, 40), (128, 1, 1)])
+def test_forward_backward_vs_oracle(cp, oracle, n):
+    N = int(np.prod(n))
+    b = oracle.c_fill_uniform(N, 3)
+    with cp.CirculantPlan(n) as plan:
+        f = plan.forward(_dev(b))
+        assert _rel(f, oracle.c_fft3d(b, n, -1)) < 1e-13
+        g = plan.backward(_dev(b))
+        assert _rel(g, oracle.c_fft3d(b, n, +1)) < 1e-13
+
+
+def test_alias_in_place(cp, oracle):
+    n = (64, 64, 64)
+    lam = (0.6, 0.15, 0.02)
+    b = oracle.c_fill_uniform(int(np.prod(n)), 9)
+    ref = oracle.c_solve_3d(oracle.c_build_diag_transport(n, lam), b, n)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam)
+        t = _dev(b)
+        plan.apply(t, out=t)  # PetscFft3DTransportSolver(ctx, Un, Un)
+        assert _rel(t, ref) < TOL
+
+
+def test_b_not_modified(cp, oracle):
+    n = (64, 32, 128)
+    b = oracle.c_fill_uniform(int(np.prod(n)), 4)
+    tb = _dev(b)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol((0.6, 0.15, 0.02))
+        plan.apply(tb)
+    np.testing.assert_array_equal(tb.cpu().numpy(), b)
+
+
+def test_separable_symbol_custom_columns(cp, oracle):
+    # arbitrary 1-D circulant columns -> separable symbol (build_diag_mat_vec_3D with any c_hat)
+    n = (32, 16, 8)
+    rng = np.random.default_rng(5)
+    cols = [rng.standard_normal(k) * 0.1 for k in n]
+    hats = [np.fft.fft(c) for c in cols]
+    lam = (1.0, 0.5, 2.0)
+    d = oracle.c_build_diag_3d(*hats, n, lam)
+    b = oracle.c_fill_uniform(int(np.prod(n)), 8)
+    ref = oracle.c_solve_3d(d, b, n)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_separable_symbol(*hats, lam)
+        assert _rel(plan.apply(_dev(b)), ref) < TOL
+        assert _rel(plan.get_diag(), d) < 1e-14
+
+
+def test_build_diag_kernel(cp, oracle):
+    n = (12, 10, 6)
+    lam = (0.6, 0.15 + 0.1j, 0.02)
+    hats = [np.fft.fft(oracle.np_transport_col(k)) for k in n]
+    d = torch.empty(int(np.prod(n)), dtype=torch.complex128, device="cuda")
+    cp.build_diag_3d(d, *[_dev(h) for h in hats], n, lam)
+    assert _rel(d, oracle.c_build_diag_3d(*hats, n, lam)) < 1e-15
+
+
+def test_vector_kernels(cp):
+    x = torch.randn(1000, dtype=torch.complex128, device="cuda")
+    y = torch.randn(1000, dtype=torch.complex128, device="cuda") + 2
+    w = torch.empty_like(x)
+    cp.pointwise_divide(w, x, y)
+    assert _rel(w, x / y) < 1e-15
+    z = x.clone()
+    cp.scale(z, 0.25 - 0.5j)
+    assert _rel(z, x * (0.25 - 0.5j)) < 1e-15
+
+
+def test_fill_uniform_matches_oracle(cp, oracle):
+    t = torch.empty(12345, dtype=torch.complex128, device="cuda")
+    cp.fill_uniform(t, 42, offset=777)
+    np.testing.assert_array_equal(t.cpu().numpy(), oracle.c_fill_uniform(12345, 42, 777))
+
+
+def test_host_apply(cp, oracle):
+    n = (32, 16, 24)
+    lam = (0.6, 0.15, 0.02)
+    b = oracle.c_fill_uniform(int(np.prod(n)), 1)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam)
+        x = plan.apply_host(b)
+    assert oracle.rel_l2(x, oracle.c_solve_3d(oracle.c_build_diag_transport(n, lam), b, n)) < TOL
+
+
+@pytest.mark.parametrize("n", [(256, 256, 256), (512, 512, 512)])
+def test_full_size_residual(cp, n):
+    """Size-independent property at the bench sizes: ||C x - b|| / ||b|| and round trip."""
+    N = int(np.prod(n))
+    lam = (0.6, 0.15, 0.02)
+    b = torch.empty(N, dtype=torch.complex128, device="cuda")
+    cp.fill_uniform(b, 20251017)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam)
+        x = plan.apply(b)
+        r = apply_C_torch(x, n, lam) - b
+        assert float(torch.linalg.vector_norm(r) / torch.linalg.vector_norm(b)) < 1e-12
+        del r
+        f = plan.forward(b)
+        plan.backward(f, out=f)
+        f /= N
+        assert float(torch.linalg.vector_norm(f - b) / torch.linalg.vector_norm(b)) < 1e-13
+        assert all(p["fast"] for p in plan.passes())
+
+
+def test_errors(cp):
+    with pytest.raises(cp.CirculantError):
+        cp.CirculantPlan((0, 4, 4))
+    with pytest.raises(cp.CirculantError):
+        cp.CirculantPlan((8192, 1, 1))
+    with cp.CirculantPlan((8, 8, 8)) as plan:
+        b = torch.zeros(512, dtype=torch.complex128, device="cuda")
+        with pytest.raises(cp.CirculantError):
+            plan.apply(b)  # no symbol yet: PETSC_ERR_ARG_WRONGSTATE
