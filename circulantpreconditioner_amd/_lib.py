@@ -103,6 +103,6 @@ def _parse_decls(path: str) -> list:
     out = []
     for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][\w]*\s*\**\s*([A-Za-z_]\w*)\s*\([^;{]*\)\s*;", txt, flags=re.M):
         name = m.group(1)
-        if name not in ("if", "while", "return", "sizeof"):
+        if name not in ("if", "while", "return", "sizeof") and len(name) > 2:
             out.append(name)
     return out

@@ -5,11 +5,41 @@ from __future__ import annotations
 import ctypes
 
 
+class PetscScalar(ctypes.Structure):
+    """PetscScalar of a complex PETSc build (std::complex<double> / double _Complex)."""
+    _fields_ = [("re", ctypes.c_double), ("im", ctypes.c_double)]
+
+    @classmethod
+    def of(cls, v) -> "PetscScalar":
+        c = complex(v)
+        return cls(c.real, c.imag)
+
+    def __complex__(self):
+        return complex(self.re, self.im)
+
+
+class FFTPrecTransportContext(ctypes.Structure):
+    """struct FFTPrecTransportContext (src/PCSHELLFft_3D.hxx:8-21 + trailing plan)."""
+    _fields_ = [("spaceDim", ctypes.c_int64), ("n_x", ctypes.c_int64), ("n_y", ctypes.c_int64),
+                ("n_z", ctypes.c_int64), ("lambda_x", PetscScalar), ("lambda_y", PetscScalar),
+                ("lambda_z", PetscScalar), ("FFT_MAT", ctypes.c_void_p), ("intersectionMatrix", ctypes.c_void_p),
+                ("Diag", ctypes.c_void_p), ("b_hat", ctypes.c_void_p), ("b_cartesien", ctypes.c_void_p),
+                ("plan", ctypes.c_void_p)]
+
+
+class StructuredTransportContext(ctypes.Structure):
+    """struct StructuredTransportContext (src/FftLinearSolver_3D.h:7-19), passed by value."""
+    _fields_ = [("n_x", ctypes.c_int64), ("n_y", ctypes.c_int64), ("n_z", ctypes.c_int64),
+                ("a_x", PetscScalar), ("a_y", PetscScalar), ("a_z", PetscScalar), ("dt", PetscScalar),
+                ("delta_x", PetscScalar), ("delta_y", PetscScalar), ("delta_z", PetscScalar),
+                ("FFT_MAT", ctypes.c_void_p)]
+
+
 def declare(L) -> None:
-    i64, dp, vp, c_int, dbl = ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double
-    P = ctypes.POINTER
+    i64, dp, vp, c_int = ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int
+    S, P, cs = PetscScalar, ctypes.POINTER, ctypes.c_char_p
     sig = {
-        # slab-distributed plan over RCCL
+        # slab-distributed plan over RCCL + single-process group
         "cfp_dist_get_unique_id": ([ctypes.c_char_p], c_int),
         "cfp_dist_unique_id_bytes": ([], c_int),
         "cfp_slab_layout": ([i64, i64, i64, c_int, c_int, P(i64)], c_int),
@@ -20,16 +50,49 @@ def declare(L) -> None:
         "cfp_dist_plan_local_size": ([vp, P(i64)], c_int),
         "cfp_dist_plan_time_phases": ([vp, dp, dp, c_int, dp, vp], c_int),
         "cfp_dist_plan_num_phases": ([vp, P(c_int)], c_int),
-        # mini-PETSc objects + the reference-named callbacks
-        "VecCreateSeqHIPWithArray": ([vp, c_int, i64, dp, P(vp)], c_int),
-        "VecCreateSeqHIP": ([vp, i64, P(vp)], c_int),
-        "VecCreateSeq": ([vp, i64, P(vp)], c_int),
+        "cfp_group_create": ([P(vp), i64, i64, i64, c_int, P(c_int)], c_int),
+        "cfp_group_destroy": ([vp], c_int),
+        "cfp_group_set_symbol_transport": ([vp, dp], c_int),
+        "cfp_group_apply": ([vp, P(vp), P(vp)], c_int),
+        # PETSc stand-in
+        "PetscErrorLastMessage": ([], cs),
+        "VecMiniSetStream": ([vp], c_int),
+        "VecCreateSeq": ([c_int, i64, P(vp)], c_int),
+        "VecCreateSeqHIP": ([c_int, i64, P(vp)], c_int),
+        "VecCreateSeqHIPWithArray": ([c_int, i64, i64, vp, P(vp)], c_int),
+        "VecDuplicate": ([vp, P(vp)], c_int),
         "VecDestroy": ([P(vp)], c_int),
         "VecGetSize": ([vp, P(i64)], c_int),
-        "VecSetValuesHost": ([vp, i64, dp], c_int),
-        "VecGetValuesHost": ([vp, i64, dp], c_int),
-        "PCCreate": ([vp, P(vp)], c_int),
-        "PCSetType": ([vp, ctypes.c_char_p], c_int),
+        "VecGetArray": ([vp, P(vp)], c_int),
+        "VecRestoreArray": ([vp, P(vp)], c_int),
+        "VecGetArrayRead": ([vp, P(vp)], c_int),
+        "VecRestoreArrayRead": ([vp, P(vp)], c_int),
+        "VecHIPGetArray": ([vp, P(vp)], c_int),
+        "VecHIPRestoreArray": ([vp, P(vp)], c_int),
+        "VecSet": ([vp, S], c_int),
+        "VecSetValue": ([vp, i64, S, c_int], c_int),
+        "VecCopy": ([vp, vp], c_int),
+        "VecScale": ([vp, S], c_int),
+        "VecShift": ([vp, S], c_int),
+        "VecAXPY": ([vp, S, vp], c_int),
+        "VecAYPX": ([vp, S, vp], c_int),
+        "VecWAXPY": ([vp, S, vp, vp], c_int),
+        "VecPointwiseDivide": ([vp, vp, vp], c_int),
+        "VecPointwiseMult": ([vp, vp, vp], c_int),
+        "VecDot": ([vp, vp, P(S)], c_int),
+        "VecNorm": ([vp, c_int, P(ctypes.c_double)], c_int),
+        "MatCreateSeqAIJWithArrays": ([c_int, i64, i64, P(i64), P(i64), vp, P(vp)], c_int),
+        "MatCreateFFT": ([c_int, i64, P(i64), cs, P(vp)], c_int),
+        "MatCreateFFTHIP": ([c_int, i64, P(i64), P(vp)], c_int),
+        "MatFFTHIPGetPlan": ([vp, P(vp)], c_int),
+        "MatCreateVecsFFTW": ([vp, P(vp), P(vp), P(vp)], c_int),
+        "MatGetSize": ([vp, P(i64), P(i64)], c_int),
+        "MatMult": ([vp, vp, vp], c_int),
+        "MatMultTranspose": ([vp, vp, vp], c_int),
+        "MatShift": ([vp, S], c_int),
+        "MatDestroy": ([P(vp)], c_int),
+        "PCCreate": ([c_int, P(vp)], c_int),
+        "PCSetType": ([vp, cs], c_int),
         "PCShellSetContext": ([vp, vp], c_int),
         "PCShellGetContext": ([vp, P(vp)], c_int),
         "PCShellSetApply": ([vp, vp], c_int),
@@ -38,26 +101,21 @@ def declare(L) -> None:
         "PCSetUp": ([vp], c_int),
         "PCApply": ([vp, vp, vp], c_int),
         "PCDestroy": ([P(vp)], c_int),
-        "MatCreateFFT": ([vp, i64, P(i64), c_int, P(vp)], c_int),
-        "MatMult": ([vp, vp, vp], c_int),
-        "MatMultTranspose": ([vp, vp, vp], c_int),
-        "MatDestroy": ([P(vp)], c_int),
-        "VecPointwiseDivide": ([vp, vp, vp], c_int),
-        "VecScale": ([vp, dbl, dbl], c_int),
+        # the reference-named boundary
         "applyFFT3DPrecTransport": ([vp, vp, vp], c_int),
         "setupFFTPrec3D": ([vp], c_int),
         "destroyFFTPrec3D": ([vp], c_int),
-        "getFFTPrec3DContext": ([i64, dbl, i64, dbl, dbl, dbl, dbl, dbl, dbl, dbl, dbl, dbl, vp], c_int),
+        "getFFTPrec3DContext": ([i64, S, i64, S, S, S, S, S, S, S, S, S, P(FFTPrecTransportContext)], c_int),
         "FFTPrecTransportContextCreate": ([P(vp)], c_int),
         "FFTPrecTransportContextDestroy": ([P(vp)], c_int),
-        "FFTPrecTransportContextGetDims": ([vp, P(i64), dp], c_int),
         "solve_3D": ([vp, vp, vp, vp, vp, i64], c_int),
         "build_transport_col": ([vp, i64], c_int),
-        "build_diag_mat_vec_3D": ([vp, vp, vp, vp, i64, i64, i64, dbl, dbl, dbl], c_int),
-        "FftTransportSolver": ([i64, i64, i64, dbl, dbl, dbl, vp, vp, vp], c_int),
-        "Fft3DTransportSolver": ([i64, i64, i64, dbl, dbl, dbl, dbl, dbl, dbl, dbl, vp, vp, vp], c_int),
-        "Fft2DTransportSolver": ([i64, i64, dbl, dbl, dbl, dbl, dbl, vp, vp, vp], c_int),
-        "Fft1DTransportSolver": ([i64, dbl, dbl, dbl, vp, vp, vp], c_int),
+        "build_diag_mat_vec_3D": ([vp, vp, vp, vp, i64, i64, i64, S, S, S], c_int),
+        "FftTransportSolver": ([i64, i64, i64, S, S, S, vp, vp, vp], c_int),
+        "Fft3DTransportSolver": ([i64, i64, i64, S, S, S, S, S, S, S, vp, vp, vp], c_int),
+        "Fft2DTransportSolver": ([i64, i64, S, S, S, S, S, vp, vp, vp], c_int),
+        "Fft1DTransportSolver": ([i64, S, S, S, vp, vp, vp], c_int),
+        "PetscFft3DTransportSolver": ([StructuredTransportContext, vp, vp], c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name, None)

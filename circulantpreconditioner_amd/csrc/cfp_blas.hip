@@ -1,0 +1,229 @@
+// cfp_blas.hip -- device vector kernels (complex double) behind the PETSc-compatible Vec/Mat
+// layer: axpy-family updates, PETSc-convention dot / norms, CSR SpMV.  These carry the
+// GMRES harness, not the FFT hot path.
+#include "cfp_blas.h"
+
+namespace cfp {
+
+#define BLAS_THREADS 256
+#define RED_BLOCKS 1024
+
+__device__ __forceinline__ cd bcadd(cd a, cd b) { return make_cd(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ cd bcmul(cd a, cd b) { return make_cd(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+
+static unsigned nblocks(i64 n) {
+  i64 b = (n + BLAS_THREADS - 1) / BLAS_THREADS;
+  if (b > 16384) b = 16384;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+#define GRID_LOOP(i, n) for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += (i64)gridDim.x * blockDim.x)
+
+__global__ void k_set(cd* x, cd a, i64 n) { GRID_LOOP(i, n) x[i] = a; }
+__global__ void k_shift(cd* x, cd a, i64 n) { GRID_LOOP(i, n) x[i] = bcadd(x[i], a); }
+__global__ void k_copy(cd* y, const cd* x, i64 n) { GRID_LOOP(i, n) y[i] = x[i]; }
+// y = y + a x
+__global__ void k_axpy(cd* y, cd a, const cd* x, i64 n) { GRID_LOOP(i, n) y[i] = bcadd(y[i], bcmul(a, x[i])); }
+// y = x + b y
+__global__ void k_aypx(cd* y, cd b, const cd* x, i64 n) { GRID_LOOP(i, n) y[i] = bcadd(x[i], bcmul(b, y[i])); }
+// w = a x + y
+__global__ void k_waxpy(cd* w, cd a, const cd* x, const cd* y, i64 n) {
+  GRID_LOOP(i, n) w[i] = bcadd(bcmul(a, x[i]), y[i]);
+}
+__global__ void k_pmult(cd* w, const cd* x, const cd* y, i64 n) { GRID_LOOP(i, n) w[i] = bcmul(x[i], y[i]); }
+// y += sum_j a_j x_j  (the GMRES basis update, k vectors at once)
+__global__ void k_maxpy(cd* y, int k, const cd* a, const cd* const* xs, i64 n) {
+  GRID_LOOP(i, n) {
+    cd acc = y[i];
+    for (int j = 0; j < k; ++j) acc = bcadd(acc, bcmul(a[j], xs[j][i]));
+    y[i] = acc;
+  }
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// kind: 0 = dot y^H x (re, im), 1 = sum |x|^2, 2 = sum |re|+|im|, 3 = max |x|
+__global__ void k_reduce(const cd* x, const cd* y, i64 n, int kind, double* partial) {
+  __shared__ double s0[BLAS_THREADS / 64], s1[BLAS_THREADS / 64];
+  double a = 0.0, b = 0.0;
+  GRID_LOOP(i, n) {
+    const cd u = x[i];
+    if (kind == 0) {
+      const cd v = y[i];  // u * conj(v)
+      a += u.x * v.x + u.y * v.y;
+      b += u.y * v.x - u.x * v.y;
+    } else if (kind == 1) {
+      a += u.x * u.x + u.y * u.y;
+    } else if (kind == 2) {
+      a += fabs(u.x) + fabs(u.y);
+    } else {
+      a = fmax(a, hypot(u.x, u.y));
+    }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (kind == 3) a = wave_max(a);
+  else { a = wave_sum(a); b = wave_sum(b); }
+  if (lane == 0) { s0[w] = a; s1[w] = b; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double ta = s0[0], tb = s1[0];
+    for (int k = 1; k < BLAS_THREADS / 64; ++k) {
+      if (kind == 3) ta = fmax(ta, s0[k]);
+      else { ta += s0[k]; tb += s1[k]; }
+    }
+    partial[2 * blockIdx.x] = ta;
+    partial[2 * blockIdx.x + 1] = tb;
+  }
+}
+
+// several dots against one vector: out[j] = x_j^H ... PETSc VecMDot(x, k, y[], val): val_j = y_j^H x
+__global__ void k_mdot(const cd* x, int k, const cd* const* ys, i64 n, double* partial) {
+  extern __shared__ double sm[];  // 2 * k * (BLAS_THREADS/64)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int j = 0; j < k; ++j) {
+    double a = 0.0, b = 0.0;
+    GRID_LOOP(i, n) {
+      const cd u = x[i], v = ys[j][i];
+      a += u.x * v.x + u.y * v.y;
+      b += u.y * v.x - u.x * v.y;
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if (lane == 0) { sm[(2 * j) * (BLAS_THREADS / 64) + w] = a; sm[(2 * j + 1) * (BLAS_THREADS / 64) + w] = b; }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 2 * k; t += blockDim.x) {
+    double s = 0.0;
+    for (int q = 0; q < BLAS_THREADS / 64; ++q) s += sm[t * (BLAS_THREADS / 64) + q];
+    partial[(size_t)blockIdx.x * 2 * k + t] = s;
+  }
+}
+
+// CSR y = A x, one thread per row
+__global__ void k_csr_spmv(i64 m, const i64* rowptr, const i64* col, const cd* val, const cd* x, cd* y) {
+  GRID_LOOP(r, m) {
+    cd acc = make_cd(0.0, 0.0);
+    for (i64 p = rowptr[r]; p < rowptr[r + 1]; ++p) acc = bcadd(acc, bcmul(val[p], x[col[p]]));
+    y[r] = acc;
+  }
+}
+
+hipError_t blas_set(cd* x, cd a, i64 n, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_set, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, x, a, n);
+  return hipGetLastError();
+}
+hipError_t blas_shift(cd* x, cd a, i64 n, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_shift, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, x, a, n);
+  return hipGetLastError();
+}
+hipError_t blas_copy(cd* y, const cd* x, i64 n, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_copy, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, y, x, n);
+  return hipGetLastError();
+}
+hipError_t blas_axpy(cd* y, cd a, const cd* x, i64 n, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_axpy, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, y, a, x, n);
+  return hipGetLastError();
+}
+hipError_t blas_aypx(cd* y, cd b, const cd* x, i64 n, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_aypx, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, y, b, x, n);
+  return hipGetLastError();
+}
+hipError_t blas_waxpy(cd* w, cd a, const cd* x, const cd* y, i64 n, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_waxpy, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, w, a, x, y, n);
+  return hipGetLastError();
+}
+hipError_t blas_pmult(cd* w, const cd* x, const cd* y, i64 n, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_pmult, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, w, x, y, n);
+  return hipGetLastError();
+}
+hipError_t blas_maxpy(cd* y, int k, const cd* a_dev, const cd* const* xs_dev, i64 n, hipStream_t s) {
+  if (n > 0 && k > 0) hipLaunchKernelGGL(k_maxpy, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, y, k, a_dev, xs_dev, n);
+  return hipGetLastError();
+}
+hipError_t blas_csr_spmv(i64 m, const i64* rowptr, const i64* col, const cd* val, const cd* x, cd* y, hipStream_t s) {
+  if (m > 0) hipLaunchKernelGGL(k_csr_spmv, dim3(nblocks(m)), dim3(BLAS_THREADS), 0, s, m, rowptr, col, val, x, y);
+  return hipGetLastError();
+}
+
+// Synchronous reductions (the result is needed on the host, as in PETSc).
+static hipError_t reduce(const cd* x, const cd* y, i64 n, int kind, double out[2], hipStream_t s) {
+  static thread_local double* partial = nullptr;
+  static thread_local double* hpart = nullptr;
+  if (!partial) {
+    hipError_t e = hipMalloc(&partial, sizeof(double) * 2 * RED_BLOCKS);
+    if (e != hipSuccess) return e;
+    e = hipHostMalloc(&hpart, sizeof(double) * 2 * RED_BLOCKS);
+    if (e != hipSuccess) return e;
+  }
+  unsigned nb = nblocks(n);
+  if (nb > RED_BLOCKS) nb = RED_BLOCKS;
+  hipLaunchKernelGGL(k_reduce, dim3(nb), dim3(BLAS_THREADS), 0, s, x, y, n, kind, partial);
+  hipError_t e = hipMemcpyAsync(hpart, partial, sizeof(double) * 2 * nb, hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) return e;
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return e;
+  double a = 0.0, b = 0.0;
+  for (unsigned k = 0; k < nb; ++k) {
+    if (kind == 3) a = fmax(a, hpart[2 * k]);
+    else { a += hpart[2 * k]; b += hpart[2 * k + 1]; }
+  }
+  out[0] = a;
+  out[1] = b;
+  return hipSuccess;
+}
+
+hipError_t blas_dot(const cd* x, const cd* y, i64 n, cd* val, hipStream_t s) {
+  double o[2];
+  hipError_t e = reduce(x, y, n, 0, o, s);
+  *val = make_cd(o[0], o[1]);
+  return e;
+}
+hipError_t blas_norm(const cd* x, i64 n, int type, double* val, hipStream_t s) {
+  double o[2];
+  const int kind = type == 1 ? 1 : (type == 0 ? 2 : (type == 3 ? 3 : 1));
+  hipError_t e = reduce(x, nullptr, n, kind, o, s);
+  *val = kind == 1 ? sqrt(o[0]) : o[0];
+  return e;
+}
+
+hipError_t blas_mdot(const cd* x, int k, const cd* const* ys_dev, i64 n, cd* vals, hipStream_t s) {
+  static thread_local double* partial = nullptr;
+  static thread_local double* hpart = nullptr;
+  static thread_local int cap = 0;
+  const int NB = 256;
+  if (cap < k) {
+    if (partial) hipFree(partial);
+    if (hpart) hipHostFree(hpart);
+    hipError_t e = hipMalloc(&partial, sizeof(double) * 2 * k * NB);
+    if (e != hipSuccess) return e;
+    e = hipHostMalloc(&hpart, sizeof(double) * 2 * k * NB);
+    if (e != hipSuccess) return e;
+    cap = k;
+  }
+  unsigned nb = nblocks(n);
+  if (nb > (unsigned)NB) nb = NB;
+  const size_t sm = sizeof(double) * 2 * k * (BLAS_THREADS / 64);
+  hipLaunchKernelGGL(k_mdot, dim3(nb), dim3(BLAS_THREADS), sm, s, x, k, ys_dev, n, partial);
+  hipError_t e = hipMemcpyAsync(hpart, partial, sizeof(double) * 2 * k * nb, hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) return e;
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return e;
+  for (int j = 0; j < k; ++j) {
+    double a = 0.0, b = 0.0;
+    for (unsigned q = 0; q < nb; ++q) {
+      a += hpart[(size_t)q * 2 * k + 2 * j];
+      b += hpart[(size_t)q * 2 * k + 2 * j + 1];
+    }
+    vals[j] = make_cd(a, b);
+  }
+  return hipSuccess;
+}
+
+}  // namespace cfp

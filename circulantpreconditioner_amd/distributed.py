@@ -1,0 +1,148 @@
+"""Slab-decomposed circulant apply over several GPUs (include/circulant_fft_dist.h).
+
+``SlabPlan``: one process per GPU (torch.distributed.run), RCCL all-to-all over
+xGMI between the y and z passes.  The 128-byte RCCL unique id is created by the
+library on rank 0 and broadcast through the caller's torch.distributed group.
+
+``SlabGroup``: one process driving P slabs (on one or several GPUs) with device
+copies as the exchange -- the same pass schedule, usable on a one-GPU machine.
+
+Layout: rank r holds z-planes [r nz/P, (r+1) nz/P), i.e. the
+contiguous elements [r N/P, (r+1) N/P) -- PETSc's PETSC_DECIDE Vec layout.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import torch
+
+from ._lib import check, lib
+from .plan import _dev_ptr, _lam6, _stream_handle
+
+
+def slab_layout(dims: Sequence[int], nranks: int, rank: int) -> dict:
+    """Host-only layout query (no GPU needed)."""
+    nx, ny, nz = (int(d) for d in dims)
+    out = (ctypes.c_int64 * 8)()
+    check(lib().cfp_slab_layout(nx, ny, nz, int(nranks), int(rank), out))
+    keys = ("nz_local", "ny_local", "z0", "y0", "local_size", "chunk", "local_offset", "nranks")
+    return dict(zip(keys, list(out)))
+
+
+class SlabPlan:
+    """This rank's part of a slab-distributed plan (RCCL)."""
+
+    def __init__(self, dims: Sequence[int], rank: int, world: int, device: int | None = None, group=None):
+        import torch.distributed as dist
+        nx, ny, nz = (int(d) for d in dims)
+        self.dims = (nx, ny, nz)
+        self.rank, self.world = int(rank), int(world)
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        nbytes = lib().cfp_dist_unique_id_bytes()
+        uid = ctypes.create_string_buffer(nbytes)
+        if self.rank == 0:
+            check(lib().cfp_dist_get_unique_id(uid))
+        on_dev = dist.get_backend(group) == "nccl"
+        t = torch.frombuffer(bytearray(uid.raw), dtype=torch.uint8)
+        t = t.to(f"cuda:{self.device}") if on_dev else t.clone()
+        dist.broadcast(t, src=0, group=group)
+        uid = ctypes.create_string_buffer(bytes(t.cpu().numpy().tobytes()), nbytes)
+        self.layout = slab_layout(self.dims, self.world, self.rank)
+        h = ctypes.c_void_p()
+        check(lib().cfp_dist_plan_create(ctypes.byref(h), nx, ny, nz, self.world, self.rank, uid, self.device))
+        self._h = h
+
+    @property
+    def local_size(self) -> int:
+        return self.layout["local_size"]
+
+    @property
+    def local_offset(self) -> int:
+        return self.layout["local_offset"]
+
+    def set_transport_symbol(self, lam) -> "SlabPlan":
+        check(lib().cfp_dist_plan_set_symbol_transport(self._h, _lam6(lam)))
+        return self
+
+    def apply(self, b: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+        if out is None:
+            out = torch.empty_like(b)
+        n = self.local_size
+        check(lib().cfp_dist_plan_apply(self._h, _dev_ptr(b, n, "b"), _dev_ptr(out, n, "out"),
+                                        _stream_handle(stream)))
+        return out
+
+    def time_phases(self, b: torch.Tensor, x: torch.Tensor, iters: int = 10, stream=None) -> list:
+        nph = ctypes.c_int()
+        check(lib().cfp_dist_plan_num_phases(self._h, ctypes.byref(nph)))
+        ms = (ctypes.c_double * nph.value)()
+        n = self.local_size
+        check(lib().cfp_dist_plan_time_phases(self._h, _dev_ptr(b, n, "b"), _dev_ptr(x, n, "x"), int(iters), ms,
+                                              _stream_handle(stream)))
+        return list(ms)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().cfp_dist_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class SlabGroup:
+    """P slabs driven from one process (exchange = device copies)."""
+
+    def __init__(self, dims: Sequence[int], nranks: int, devices: Sequence[int] | None = None):
+        nx, ny, nz = (int(d) for d in dims)
+        self.dims = (nx, ny, nz)
+        self.P = int(nranks)
+        devs = list(devices) if devices is not None else [torch.cuda.current_device()] * self.P
+        if len(devs) != self.P:
+            raise ValueError("one device per slab")
+        self.devices = devs
+        arr = (ctypes.c_int * self.P)(*devs)
+        h = ctypes.c_void_p()
+        check(lib().cfp_group_create(ctypes.byref(h), nx, ny, nz, self.P, arr))
+        self._h = h
+        self.layouts = [slab_layout(self.dims, self.P, r) for r in range(self.P)]
+
+    def set_transport_symbol(self, lam) -> "SlabGroup":
+        check(lib().cfp_group_set_symbol_transport(self._h, _lam6(lam)))
+        return self
+
+    def scatter(self, full: torch.Tensor) -> list:
+        out = []
+        for r, L in enumerate(self.layouts):
+            o, n = L["local_offset"], L["local_size"]
+            out.append(full[o:o + n].to(f"cuda:{self.devices[r]}").contiguous())
+        return out
+
+    def apply(self, bs: Sequence[torch.Tensor], xs: Sequence[torch.Tensor] | None = None) -> list:
+        if xs is None:
+            xs = [torch.empty_like(b) for b in bs]
+        bp = (ctypes.c_void_p * self.P)(*[_dev_ptr(b, L["local_size"], "b") for b, L in zip(bs, self.layouts)])
+        xp = (ctypes.c_void_p * self.P)(*[_dev_ptr(x, L["local_size"], "x") for x, L in zip(xs, self.layouts)])
+        check(lib().cfp_group_apply(self._h, bp, xp))
+        return list(xs)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().cfp_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

@@ -1,0 +1,318 @@
+"""Python mirror of the reference's PETSc-facing interface, over the C ABI.
+
+The objects are the library's PETSc stand-in (include/petsc_mini.h): ``Vec``
+(device VECSEQHIP wrapping a torch tensor's memory, or host VECSEQ), ``Mat``
+(FFT matrix, AIJ), ``PC`` (PCSHELL).  The functions carry the reference's names
+and argument order (src/PCSHELLFft_3D.hxx, src/FftLinearSolver_3D.h), so the
+parity tests read like the reference's own drivers:
+
+    ctx = getFFTPrec3DContext(3, dt, N, ax, ay, az, xmin, ymin, zmin, xmax, ymax, zmax)
+    pc = PC.shell(ctx)                        # PCSetType(PCSHELL) + PCShellSet*
+    pc.setup()                                # setupFFTPrec3D
+    pc.apply(b, x)                            # PCApply -> applyFFT3DPrecTransport
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import numpy as np
+import torch
+
+from ._lib import CirculantError, lib
+from ._lib_ext import FFTPrecTransportContext, PetscScalar, StructuredTransportContext
+
+PETSC_COMM_WORLD = 0
+PETSC_COMM_SELF = 1
+INSERT_VALUES, ADD_VALUES = 1, 2
+NORM_1, NORM_2, NORM_INFINITY = 0, 1, 3
+
+
+class PetscError(CirculantError):
+    pass
+
+
+def PetscCall(rc: int) -> None:
+    if rc != 0:
+        msg = lib().PetscErrorLastMessage().decode(errors="replace")
+        cfp = lib().cfp_last_error().decode(errors="replace")
+        raise PetscError(rc, f"{msg} {('| ' + cfp) if cfp else ''}".strip())
+
+
+def _S(v) -> PetscScalar:
+    return PetscScalar.of(v)
+
+
+class Vec:
+    """A PETSc Vec of the stand-in.  ``Vec.from_tensor`` wraps device memory without a copy."""
+
+    def __init__(self, handle, keep=None, owned: bool = True):
+        self.h = handle if isinstance(handle, ctypes.c_void_p) else ctypes.c_void_p(handle)
+        self._keep = keep  # keeps a wrapped tensor alive
+        self.owned = owned
+
+    @classmethod
+    def borrow(cls, handle) -> "Vec":
+        """Non-owning view of a Vec created elsewhere (e.g. ctx.Diag made by setupFFTPrec3D)."""
+        return cls(handle, owned=False)
+
+    @classmethod
+    def from_tensor(cls, t: torch.Tensor) -> "Vec":
+        if t.dtype != torch.complex128 or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("need a contiguous complex128 device tensor")
+        h = ctypes.c_void_p()
+        PetscCall(lib().VecCreateSeqHIPWithArray(PETSC_COMM_SELF, 1, t.numel(), t.data_ptr(), ctypes.byref(h)))
+        return cls(h, keep=t)
+
+    @classmethod
+    def seq_hip(cls, n: int) -> "Vec":
+        h = ctypes.c_void_p()
+        PetscCall(lib().VecCreateSeqHIP(PETSC_COMM_SELF, int(n), ctypes.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def seq(cls, n: int) -> "Vec":
+        """Host-only VECSEQ (exercises the PCIe staging path)."""
+        h = ctypes.c_void_p()
+        PetscCall(lib().VecCreateSeq(PETSC_COMM_SELF, int(n), ctypes.byref(h)))
+        return cls(h)
+
+    @property
+    def size(self) -> int:
+        n = ctypes.c_int64()
+        PetscCall(lib().VecGetSize(self.h, ctypes.byref(n)))
+        return n.value
+
+    def set_array(self, a) -> "Vec":
+        a = np.ascontiguousarray(np.asarray(a, dtype=np.complex128).reshape(-1))
+        if a.size != self.size:
+            raise ValueError("size mismatch")
+        p = ctypes.c_void_p()
+        PetscCall(lib().VecGetArray(self.h, ctypes.byref(p)))
+        ctypes.memmove(p, a.ctypes.data, a.nbytes)
+        PetscCall(lib().VecRestoreArray(self.h, ctypes.byref(p)))
+        return self
+
+    def array(self) -> np.ndarray:
+        n = self.size
+        p = ctypes.c_void_p()
+        PetscCall(lib().VecGetArrayRead(self.h, ctypes.byref(p)))
+        out = np.empty(n, dtype=np.complex128)
+        ctypes.memmove(out.ctypes.data, p, out.nbytes)
+        PetscCall(lib().VecRestoreArrayRead(self.h, ctypes.byref(p)))
+        return out
+
+    def set(self, alpha) -> "Vec":
+        PetscCall(lib().VecSet(self.h, _S(alpha)))
+        return self
+
+    def norm(self, kind: int = NORM_2) -> float:
+        v = ctypes.c_double()
+        PetscCall(lib().VecNorm(self.h, kind, ctypes.byref(v)))
+        return v.value
+
+    def dot(self, other: "Vec") -> complex:
+        s = PetscScalar()
+        PetscCall(lib().VecDot(self.h, other.h, ctypes.byref(s)))
+        return complex(s)
+
+    def axpy(self, alpha, x: "Vec") -> "Vec":
+        PetscCall(lib().VecAXPY(self.h, _S(alpha), x.h))
+        return self
+
+    def destroy(self) -> None:
+        if self.owned and self.h is not None and self.h.value:
+            PetscCall(lib().VecDestroy(ctypes.byref(self.h)))
+        self.h = None
+        self._keep = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+class Mat:
+    def __init__(self, handle: ctypes.c_void_p, owned: bool = True):
+        self.h = handle
+        self.owned = owned
+
+    @classmethod
+    def create_fft(cls, dims: Sequence[int]) -> "Mat":
+        """MatCreateFFT(comm, ndim, dims = {n_z, n_y, n_x}, MATFFTW, &A)."""
+        d = (ctypes.c_int64 * len(dims))(*[int(v) for v in dims])
+        h = ctypes.c_void_p()
+        PetscCall(lib().MatCreateFFT(PETSC_COMM_WORLD, len(dims), d, b"fftw", ctypes.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def aij(cls, rowptr, col, val, shape) -> "Mat":
+        m, n = shape
+        rp = np.ascontiguousarray(rowptr, dtype=np.int64)
+        cj = np.ascontiguousarray(col, dtype=np.int64)
+        va = np.ascontiguousarray(val, dtype=np.complex128)
+        h = ctypes.c_void_p()
+        PetscCall(lib().MatCreateSeqAIJWithArrays(PETSC_COMM_SELF, m, n,
+                                                  rp.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                                  cj.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                                  va.ctypes.data, ctypes.byref(h)))
+        return cls(h)
+
+    def create_vecs(self, nvec: int = 1) -> list:
+        hs = [ctypes.c_void_p() for _ in range(3)]
+        refs = [ctypes.byref(hs[i]) if i < nvec else None for i in range(3)]
+        PetscCall(lib().MatCreateVecsFFTW(self.h, *refs))
+        return [Vec(hs[i]) for i in range(nvec)]
+
+    def mult(self, x: Vec, y: Vec) -> Vec:
+        PetscCall(lib().MatMult(self.h, x.h, y.h))
+        return y
+
+    def mult_transpose(self, x: Vec, y: Vec) -> Vec:
+        PetscCall(lib().MatMultTranspose(self.h, x.h, y.h))
+        return y
+
+    def shift(self, a) -> "Mat":
+        PetscCall(lib().MatShift(self.h, _S(a)))
+        return self
+
+    def destroy(self) -> None:
+        if self.owned and self.h is not None and self.h.value:
+            PetscCall(lib().MatDestroy(ctypes.byref(self.h)))
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+def _fn(name: str) -> int:
+    return ctypes.cast(getattr(lib(), name), ctypes.c_void_p).value
+
+
+class PC:
+    def __init__(self):
+        self.h = ctypes.c_void_p()
+        PetscCall(lib().PCCreate(PETSC_COMM_WORLD, ctypes.byref(self.h)))
+        self.ctx = None
+
+    @classmethod
+    def shell(cls, ctx: FFTPrecTransportContext) -> "PC":
+        """PCSetType(pc, PCSHELL); PCShellSetContext; PCShellSetSetUp/Apply/Destroy with the
+        reference's callbacks (the registration the reference never does, ToDo.md:1)."""
+        pc = cls()
+        PetscCall(lib().PCSetType(pc.h, b"shell"))
+        pc.ctx = ctx
+        PetscCall(lib().PCShellSetContext(pc.h, ctypes.addressof(ctx)))
+        PetscCall(lib().PCShellSetSetUp(pc.h, _fn("setupFFTPrec3D")))
+        PetscCall(lib().PCShellSetApply(pc.h, _fn("applyFFT3DPrecTransport")))
+        PetscCall(lib().PCShellSetDestroy(pc.h, _fn("destroyFFTPrec3D")))
+        return pc
+
+    @classmethod
+    def none(cls) -> "PC":
+        pc = cls()
+        PetscCall(lib().PCSetType(pc.h, b"none"))
+        return pc
+
+    def setup(self) -> "PC":
+        PetscCall(lib().PCSetUp(self.h))
+        return self
+
+    def apply(self, b: Vec, x: Vec) -> Vec:
+        PetscCall(lib().PCApply(self.h, b.h, x.h))
+        return x
+
+    def destroy(self) -> None:
+        if self.h is not None and self.h.value:
+            PetscCall(lib().PCDestroy(ctypes.byref(self.h)))
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+# ------------------------------------------------------------- reference-named functions
+def getFFTPrec3DContext(ndim, dt, nbCells, a_x, a_y, a_z, Xmin, Ymin, Zmin, Xmax, Ymax, Zmax
+                        ) -> FFTPrecTransportContext:
+    """src/PCSHELLFft_3D.cxx:101-151 (returns the filled context)."""
+    ctx = FFTPrecTransportContext()
+    PetscCall(lib().getFFTPrec3DContext(int(ndim), _S(dt), int(nbCells), _S(a_x), _S(a_y), _S(a_z), _S(Xmin),
+                                        _S(Ymin), _S(Zmin), _S(Xmax), _S(Ymax), _S(Zmax), ctypes.byref(ctx)))
+    return ctx
+
+
+def make_context(dims: Sequence[int], lam: Sequence, space_dim: int = 3) -> FFTPrecTransportContext:
+    """Context with explicit n and lambda (the reference struct filled by hand)."""
+    ctx = FFTPrecTransportContext()
+    ctx.spaceDim = space_dim
+    ctx.n_x, ctx.n_y, ctx.n_z = (int(d) for d in dims)
+    ctx.lambda_x, ctx.lambda_y, ctx.lambda_z = (PetscScalar.of(v) for v in lam)
+    return ctx
+
+
+def applyFFT3DPrecTransport(pc: PC, b: Vec, x: Vec) -> None:
+    PetscCall(lib().applyFFT3DPrecTransport(pc.h, b.h, x.h))
+
+
+def setupFFTPrec3D(pc: PC) -> None:
+    PetscCall(lib().setupFFTPrec3D(pc.h))
+
+
+def destroyFFTPrec3D(pc: PC) -> None:
+    PetscCall(lib().destroyFFTPrec3D(pc.h))
+
+
+def solve_3D(FFT_MAT: Mat, X: Vec, Diag: Vec, b: Vec, b_hat: Vec | None, size: int) -> None:
+    PetscCall(lib().solve_3D(FFT_MAT.h, X.h, Diag.h, b.h, b_hat.h if b_hat is not None else None, int(size)))
+
+
+def build_transport_col(c: Vec, size: int) -> None:
+    PetscCall(lib().build_transport_col(c.h, int(size)))
+
+
+def build_diag_mat_vec_3D(Diag: Vec, c_x_hat: Vec, c_y_hat: Vec, c_z_hat: Vec, n_x, n_y, n_z, lambda_x, lambda_y,
+                          lambda_z) -> None:
+    PetscCall(lib().build_diag_mat_vec_3D(Diag.h, c_x_hat.h, c_y_hat.h, c_z_hat.h, int(n_x), int(n_y), int(n_z),
+                                          _S(lambda_x), _S(lambda_y), _S(lambda_z)))
+
+
+def FftTransportSolver(n_x, n_y, n_z, lambda_x, lambda_y, lambda_z, X: Vec, b: Vec, FFT_MAT: Mat) -> None:
+    PetscCall(lib().FftTransportSolver(int(n_x), int(n_y), int(n_z), _S(lambda_x), _S(lambda_y), _S(lambda_z),
+                                       X.h, b.h, FFT_MAT.h))
+
+
+def Fft3DTransportSolver(n_x, n_y, n_z, a_x, a_y, a_z, dt, delta_x, delta_y, delta_z, X: Vec, b: Vec,
+                         FFT_MAT: Mat) -> None:
+    PetscCall(lib().Fft3DTransportSolver(int(n_x), int(n_y), int(n_z), _S(a_x), _S(a_y), _S(a_z), _S(dt),
+                                         _S(delta_x), _S(delta_y), _S(delta_z), X.h, b.h, FFT_MAT.h))
+
+
+def Fft2DTransportSolver(n_x, n_y, a_x, a_y, dt, delta_x, delta_y, X: Vec, b: Vec, FFT_MAT: Mat) -> None:
+    PetscCall(lib().Fft2DTransportSolver(int(n_x), int(n_y), _S(a_x), _S(a_y), _S(dt), _S(delta_x), _S(delta_y),
+                                         X.h, b.h, FFT_MAT.h))
+
+
+def Fft1DTransportSolver(n_x, a_x, dt, delta_x, X: Vec, b: Vec, FFT_MAT: Mat) -> None:
+    PetscCall(lib().Fft1DTransportSolver(int(n_x), _S(a_x), _S(dt), _S(delta_x), X.h, b.h, FFT_MAT.h))
+
+
+def StructuredContext(n_x, n_y, n_z, a_x, a_y, a_z, dt, delta_x, delta_y, delta_z, FFT_MAT: Mat
+                      ) -> StructuredTransportContext:
+    c = StructuredTransportContext()
+    c.n_x, c.n_y, c.n_z = int(n_x), int(n_y), int(n_z)
+    for name, v in (("a_x", a_x), ("a_y", a_y), ("a_z", a_z), ("dt", dt), ("delta_x", delta_x),
+                    ("delta_y", delta_y), ("delta_z", delta_z)):
+        setattr(c, name, PetscScalar.of(v))
+    c.FFT_MAT = FFT_MAT.h
+    return c
+
+
+def PetscFft3DTransportSolver(customCtx: StructuredTransportContext, b: Vec, x: Vec) -> None:
+    PetscCall(lib().PetscFft3DTransportSolver(customCtx, b.h, x.h))

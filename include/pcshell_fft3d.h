@@ -1,0 +1,106 @@
+/*
+ * pcshell_fft3d.h -- the reference's PETSc-facing interface of the circulant FFT
+ * preconditioner, re-implemented on the MI355X plan (libcirculant_fft.so).
+ *
+ * Same names, argument order and meaning as the reference headers:
+ *   src/PCSHELLFft_3D.hxx:8-45    FFTPrecTransportContext, applyFFT3DPrecTransport,
+ *                                 setupFFTPrec3D, destroyFFTPrec3D, getFFTPrec3DContext
+ *   src/FftLinearSolver_3D.h:7-43 StructuredTransportContext, Fft{3,2,1}DTransportSolver,
+ *                                 PetscFft3DTransportSolver, FftTransportSolver, solve_3D,
+ *                                 build_diag_mat_vec_3D, build_transport_col
+ * Registration by the caller, unchanged from PETSc practice:
+ *   PCSetType(pc, PCSHELL); PCShellSetContext(pc, &ctx);
+ *   PCShellSetSetUp(pc, setupFFTPrec3D); PCShellSetApply(pc, applyFFT3DPrecTransport);
+ *   PCShellSetDestroy(pc, destroyFFTPrec3D);
+ *
+ * Documented differences (each fixes a reference defect):
+ *   - getFFTPrec3DContext's last argument is the context to fill (the reference takes a
+ *     SOLVERLAB `Mesh` by value and writes through an uninitialised pointer, item 2);
+ *   - the callbacks fetch the context with PCShellGetContext(pc, &ctx) (item 2);
+ *   - a NULL intersectionMatrix means the identity (Cartesian mesh; the reference never
+ *     creates it, item 2);
+ *   - FftTransportSolver/Fft3DSolver do not destroy the caller's FFT_MAT (item 6) and cache
+ *     the symbol between calls with equal lambdas (item 9);
+ *   - FFTPrecTransportContext has one extra trailing member (`plan`, owned by setup/destroy).
+ */
+#ifndef CFP_PCSHELL_FFT3D_H
+#define CFP_PCSHELL_FFT3D_H
+
+#include "petsc_mini.h"
+#include "circulant_fft.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+struct FFTPrecTransportContext {
+  PetscInt spaceDim;
+  PetscInt n_x;
+  PetscInt n_y;
+  PetscInt n_z;
+  PetscScalar lambda_x;
+  PetscScalar lambda_y;
+  PetscScalar lambda_z;
+  Mat FFT_MAT;
+  Mat intersectionMatrix;
+  Vec Diag;
+  Vec b_hat;
+  Vec b_cartesien;
+  cfp_plan_t plan; /* extra: the HIP plan behind FFT_MAT (set up by setupFFTPrec3D) */
+};
+typedef struct FFTPrecTransportContext FFTPrecTransportContext;
+
+struct StructuredTransportContext {
+  PetscInt n_x;
+  PetscInt n_y;
+  PetscInt n_z;
+  PetscScalar a_x;
+  PetscScalar a_y;
+  PetscScalar a_z;
+  PetscScalar dt;
+  PetscScalar delta_x;
+  PetscScalar delta_y;
+  PetscScalar delta_z;
+  Mat FFT_MAT;
+};
+
+/* ---- PCSHELL callbacks (src/PCSHELLFft_3D.hxx:23-25) */
+PetscErrorCode applyFFT3DPrecTransport(PC pc, Vec b, Vec x);
+PetscErrorCode setupFFTPrec3D(PC pc);
+PetscErrorCode destroyFFTPrec3D(PC pc);
+/* src/PCSHELLFft_3D.hxx:27-41 (Mesh srcMesh -> FFTPrecTransportContext *ctx, see above):
+ * n_d = floor(cbrt(nbCells)) (3-D), floor(sqrt) (2-D), nbCells (1-D);
+ * lambda_d = a_d * dt * (max_d - min_d) / n_d (src/PCSHELLFft_3D.cxx:146-148, kept as is) */
+PetscErrorCode getFFTPrec3DContext(PetscInt ndim, PetscScalar dt, PetscInt nbCells, PetscScalar a_x, PetscScalar a_y,
+                                   PetscScalar a_z, PetscScalar Xmin, PetscScalar Ymin, PetscScalar Zmin,
+                                   PetscScalar Xmax, PetscScalar Ymax, PetscScalar Zmax,
+                                   FFTPrecTransportContext *ctx);
+
+/* ---- direct solver (src/FftLinearSolver_3D.h:21-43) */
+PetscErrorCode Fft3DTransportSolver(PetscInt n_x, PetscInt n_y, PetscInt n_z, PetscScalar a_x, PetscScalar a_y,
+                                    PetscScalar a_z, PetscScalar dt, PetscScalar delta_x, PetscScalar delta_y,
+                                    PetscScalar delta_z, Vec X, Vec b, Mat FFT_MAT);
+PetscErrorCode Fft2DTransportSolver(PetscInt n_x, PetscInt n_y, PetscScalar a_x, PetscScalar a_y, PetscScalar dt,
+                                    PetscScalar delta_x, PetscScalar delta_y, Vec X, Vec b, Mat FFT_MAT);
+PetscErrorCode Fft1DTransportSolver(PetscInt n_x, PetscScalar a_x, PetscScalar dt, PetscScalar delta_x, Vec X, Vec b,
+                                    Mat FFT_MAT);
+PetscErrorCode PetscFft3DTransportSolver(struct StructuredTransportContext customCtx, Vec b, Vec x);
+PetscErrorCode FftTransportSolver(PetscInt n_x, PetscInt n_y, PetscInt n_z, PetscScalar lambda_x,
+                                  PetscScalar lambda_y, PetscScalar lambda_z, Vec X, Vec b, Mat FFT_MAT);
+PetscErrorCode solve_3D(Mat FFT_MAT, Vec X, Vec Diag, Vec b, Vec b_hat, PetscInt size);
+PetscErrorCode build_diag_mat_vec_3D(Vec Diag, Vec c_x_hat, Vec c_y_hat, Vec c_z_hat, PetscInt n_x, PetscInt n_y,
+                                     PetscInt n_z, PetscScalar lambda_x, PetscScalar lambda_y, PetscScalar lambda_z);
+PetscErrorCode build_transport_col(Vec c, PetscInt size);
+
+/* ---- helpers that are not in the reference */
+/* FFT matrix backed by the HIP plan (what MatCreateFFT(.., MATFFTW, ..) returns here) */
+PetscErrorCode MatCreateFFTHIP(MPI_Comm comm, PetscInt ndim, const PetscInt dims[], Mat *A);
+/* the plan behind an FFT matrix made by MatCreateFFT/MatCreateFFTHIP (NULL otherwise) */
+PetscErrorCode MatFFTHIPGetPlan(Mat A, cfp_plan_t *plan);
+PetscErrorCode FFTPrecTransportContextCreate(FFTPrecTransportContext **ctx);
+PetscErrorCode FFTPrecTransportContextDestroy(FFTPrecTransportContext **ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFP_PCSHELL_FFT3D_H */

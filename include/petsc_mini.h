@@ -1,0 +1,187 @@
+/*
+ * petsc_mini.h -- the subset of the PETSc C API that the circulant preconditioner boundary
+ * uses, implemented by libcirculant_fft.so when real PETSc is absent (it is absent in this
+ * image and on the GPU box: SURVEY.md §8c).
+ *
+ * Names, argument order and semantics follow PETSc >= 3.19 (complex scalars, VECHIP
+ * offload model).  Compiling with -DCFP_WITH_PETSC replaces this whole header by the real
+ * <petscksp.h>; pcshell_fft3d.cpp only calls functions that exist there.  Deliberate
+ * differences of the stand-in:
+ *   - PetscInt is 64-bit (as a PETSc built --with-64-bit-indices);
+ *   - MPI_Comm is an int tag (no MPI inside; only PETSC_COMM_SELF/WORLD of size 1);
+ *   - Vec is either host-only (VECSEQ) or device-resident with a host mirror (VECSEQHIP),
+ *     with PETSc's offload mask semantics for the Get/Restore pairs;
+ *   - Mat supports MATSHELL (user operations), MATSEQAIJ (CSR, device SpMV) and the FFT
+ *     shell made by MatCreateFFT / MatCreateFFTHIP.
+ */
+#ifndef CFP_PETSC_MINI_H
+#define CFP_PETSC_MINI_H
+
+#ifdef CFP_WITH_PETSC
+#include <petscksp.h>
+#else
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+#include <complex>
+typedef std::complex<double> PetscScalar;
+extern "C" {
+#else
+#include <complex.h>
+typedef double _Complex PetscScalar;
+#endif
+
+typedef int PetscErrorCode;
+typedef int64_t PetscInt;
+typedef double PetscReal;
+typedef double PetscLogDouble;
+typedef int PetscMPIInt;
+typedef enum { PETSC_FALSE = 0, PETSC_TRUE = 1 } PetscBool;
+typedef int MPI_Comm;
+#define PETSC_COMM_WORLD ((MPI_Comm)0)
+#define PETSC_COMM_SELF ((MPI_Comm)1)
+#define PETSC_DECIDE (-1)
+#define PETSC_DETERMINE (-1)
+#define PETSC_DEFAULT (-2)
+
+/* error codes (petscerror.h) */
+#define PETSC_SUCCESS 0
+#define PETSC_ERR_MEM 55
+#define PETSC_ERR_SUP 56
+#define PETSC_ERR_ARG_SIZ 60
+#define PETSC_ERR_ARG_IDN 61
+#define PETSC_ERR_ARG_WRONG 62
+#define PETSC_ERR_ARG_OUTOFRANGE 63
+#define PETSC_ERR_ARG_WRONGSTATE 73
+#define PETSC_ERR_LIB 76
+#define PETSC_ERR_PLIB 77
+#define PETSC_ERR_ARG_NULL 85
+#define PETSC_ERR_CONV_FAILED 91
+
+typedef enum { PETSC_MEMTYPE_HOST = 0, PETSC_MEMTYPE_DEVICE = 1, PETSC_MEMTYPE_HIP = 3 } PetscMemType;
+typedef enum { NORM_1 = 0, NORM_2 = 1, NORM_FROBENIUS = 2, NORM_INFINITY = 3 } NormType;
+typedef enum { INSERT_VALUES = 1, ADD_VALUES = 2 } InsertMode;
+
+typedef struct _p_Vec *Vec;
+typedef struct _p_Mat *Mat;
+typedef struct _p_PC *PC;
+typedef const char *MatType;
+typedef const char *PCType;
+typedef const char *VecType;
+#define VECSEQ "seq"
+#define VECSEQHIP "seqhip"
+#define MATSHELL "shell"
+#define MATSEQAIJ "seqaij"
+#define MATFFTW "fftw"
+#define PCSHELL "shell"
+#define PCNONE "none"
+
+typedef enum {
+  MATOP_MULT = 3,
+  MATOP_MULT_TRANSPOSE = 5,
+  MATOP_DESTROY = 26
+} MatOperation;
+
+/* error reporting (PetscCall/PetscCheck in the PETSc style) */
+PetscErrorCode PetscErrorSet(PetscErrorCode code, const char *func, const char *msg);
+const char *PetscErrorLastMessage(void);
+#define PetscFunctionBeginUser do { } while (0)
+#define PetscFunctionReturn(x) return (x)
+#define PetscCall(expr)                                   \
+  do {                                                    \
+    PetscErrorCode ierr__ = (expr);                       \
+    if (ierr__) return ierr__;                            \
+  } while (0)
+#define PetscCheck(cond, comm, code, msg)                  \
+  do {                                                    \
+    if (!(cond)) return PetscErrorSet((code), __func__, (msg)); \
+  } while (0)
+PetscErrorCode PetscTime(PetscLogDouble *t);
+
+/* ---- Vec */
+PetscErrorCode VecCreateSeq(MPI_Comm comm, PetscInt n, Vec *v);
+PetscErrorCode VecCreateSeqHIP(MPI_Comm comm, PetscInt n, Vec *v);
+PetscErrorCode VecCreateSeqHIPWithArray(MPI_Comm comm, PetscInt bs, PetscInt n, const PetscScalar *gpuarray, Vec *v);
+PetscErrorCode VecCreateMPI(MPI_Comm comm, PetscInt nlocal, PetscInt N, Vec *v);
+PetscErrorCode VecDuplicate(Vec v, Vec *newv);
+PetscErrorCode VecDestroy(Vec *v);
+PetscErrorCode VecGetType(Vec v, VecType *type);
+PetscErrorCode VecGetSize(Vec v, PetscInt *n);
+PetscErrorCode VecGetLocalSize(Vec v, PetscInt *n);
+PetscErrorCode VecGetOwnershipRange(Vec v, PetscInt *lo, PetscInt *hi);
+PetscErrorCode VecGetArray(Vec v, PetscScalar **a);
+PetscErrorCode VecRestoreArray(Vec v, PetscScalar **a);
+PetscErrorCode VecGetArrayRead(Vec v, const PetscScalar **a);
+PetscErrorCode VecRestoreArrayRead(Vec v, const PetscScalar **a);
+PetscErrorCode VecGetArrayWrite(Vec v, PetscScalar **a);
+PetscErrorCode VecRestoreArrayWrite(Vec v, PetscScalar **a);
+PetscErrorCode VecGetArrayReadAndMemType(Vec v, const PetscScalar **a, PetscMemType *mtype);
+PetscErrorCode VecRestoreArrayReadAndMemType(Vec v, const PetscScalar **a);
+PetscErrorCode VecGetArrayWriteAndMemType(Vec v, PetscScalar **a, PetscMemType *mtype);
+PetscErrorCode VecRestoreArrayWriteAndMemType(Vec v, PetscScalar **a);
+PetscErrorCode VecGetArrayAndMemType(Vec v, PetscScalar **a, PetscMemType *mtype);
+PetscErrorCode VecRestoreArrayAndMemType(Vec v, PetscScalar **a);
+PetscErrorCode VecHIPGetArray(Vec v, PetscScalar **a);
+PetscErrorCode VecHIPRestoreArray(Vec v, PetscScalar **a);
+PetscErrorCode VecHIPGetArrayRead(Vec v, const PetscScalar **a);
+PetscErrorCode VecHIPRestoreArrayRead(Vec v, const PetscScalar **a);
+PetscErrorCode VecHIPGetArrayWrite(Vec v, PetscScalar **a);
+PetscErrorCode VecHIPRestoreArrayWrite(Vec v, PetscScalar **a);
+PetscErrorCode VecSet(Vec v, PetscScalar alpha);
+PetscErrorCode VecSetValue(Vec v, PetscInt i, PetscScalar value, InsertMode mode);
+PetscErrorCode VecSetValues(Vec v, PetscInt n, const PetscInt *idx, const PetscScalar *y, InsertMode mode);
+PetscErrorCode VecGetValues(Vec v, PetscInt n, const PetscInt *idx, PetscScalar *y);
+PetscErrorCode VecAssemblyBegin(Vec v);
+PetscErrorCode VecAssemblyEnd(Vec v);
+PetscErrorCode VecCopy(Vec x, Vec y);
+PetscErrorCode VecScale(Vec x, PetscScalar alpha);
+PetscErrorCode VecShift(Vec x, PetscScalar alpha);
+PetscErrorCode VecAXPY(Vec y, PetscScalar alpha, Vec x);
+PetscErrorCode VecAYPX(Vec y, PetscScalar beta, Vec x);
+PetscErrorCode VecWAXPY(Vec w, PetscScalar alpha, Vec x, Vec y);
+PetscErrorCode VecPointwiseDivide(Vec w, Vec x, Vec y);
+PetscErrorCode VecPointwiseMult(Vec w, Vec x, Vec y);
+PetscErrorCode VecDot(Vec x, Vec y, PetscScalar *val);
+PetscErrorCode VecNorm(Vec x, NormType type, PetscReal *val);
+/* stream the Vec kernels are enqueued on (hipStream_t, NULL = default); not in PETSc */
+PetscErrorCode VecMiniSetStream(void *stream);
+
+/* ---- Mat */
+PetscErrorCode MatCreateShell(MPI_Comm comm, PetscInt m, PetscInt n, PetscInt M, PetscInt N, void *ctx, Mat *A);
+PetscErrorCode MatShellSetOperation(Mat A, MatOperation op, void (*f)(void));
+PetscErrorCode MatShellGetContext(Mat A, void *ctx);
+PetscErrorCode MatCreateSeqAIJWithArrays(MPI_Comm comm, PetscInt m, PetscInt n, PetscInt *i, PetscInt *j,
+                                         PetscScalar *a, Mat *A);
+PetscErrorCode MatGetType(Mat A, MatType *type);
+PetscErrorCode MatGetSize(Mat A, PetscInt *m, PetscInt *n);
+PetscErrorCode MatMult(Mat A, Vec x, Vec y);
+PetscErrorCode MatMultTranspose(Mat A, Vec x, Vec y);
+PetscErrorCode MatShift(Mat A, PetscScalar a);
+PetscErrorCode MatDestroy(Mat *A);
+/* the FFT matrix: a MATSHELL around a cfp plan; dims = {n_z, n_y, n_x} for ndim = 3
+ * (row-major, x fastest), {n_y, n_x} for 2, {n_x} for 1.  MatCreateFFT accepts only
+ * MATFFTW as type and returns the HIP implementation. */
+PetscErrorCode MatCreateFFT(MPI_Comm comm, PetscInt ndim, const PetscInt dims[], MatType type, Mat *A);
+PetscErrorCode MatCreateVecsFFTW(Mat A, Vec *x, Vec *y, Vec *z);
+
+/* ---- PC */
+PetscErrorCode PCCreate(MPI_Comm comm, PC *pc);
+PetscErrorCode PCSetType(PC pc, PCType type);
+PetscErrorCode PCGetType(PC pc, PCType *type);
+PetscErrorCode PCShellSetContext(PC pc, void *ctx);
+PetscErrorCode PCShellGetContext(PC pc, void *ctx); /* ctx is a pointer to the user's pointer */
+PetscErrorCode PCShellSetApply(PC pc, PetscErrorCode (*apply)(PC, Vec, Vec));
+PetscErrorCode PCShellSetSetUp(PC pc, PetscErrorCode (*setup)(PC));
+PetscErrorCode PCShellSetDestroy(PC pc, PetscErrorCode (*destroy)(PC));
+PetscErrorCode PCShellSetName(PC pc, const char *name);
+PetscErrorCode PCSetUp(PC pc);
+PetscErrorCode PCApply(PC pc, Vec x, Vec y);
+PetscErrorCode PCDestroy(PC *pc);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFP_WITH_PETSC */
+#endif /* CFP_PETSC_MINI_H */

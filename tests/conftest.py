@@ -17,6 +17,7 @@ def pytest_configure(config):
 def oracle():
     from oracle import oracle as O
     O.lib()
+    O.set_threads(min(16, len(os.sched_getaffinity(0))))
     return O
 
 
