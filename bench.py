@@ -93,6 +93,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--grid", type=int, nargs="+", default=[256])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--chunk", type=int, default=None,
+                    help="z-planes per chunk of the Infinity-Cache-resident x/y schedule (0 = off; default: plan's)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
     grid = args.grid * 3 if len(args.grid) == 1 else args.grid
@@ -126,6 +128,8 @@ def main() -> int:
         cp.fill_uniform(b, SEED)
         plan = cp.CirculantPlan(grid, device=local_rank)
         plan.set_transport_symbol(LAM)
+        if args.chunk is not None:
+            plan.set_chunking(args.chunk)
         run = lambda: plan.apply(b, out=x)  # noqa: E731
         parallelism = "single GPU"
     else:

@@ -1,0 +1,287 @@
+// cfp_fft_device.h -- device code of the fast axis-pass FFT (gfx950).  Included by
+// cfp_kernels.hip (product dispatch) and by tools/kexp (variant timing harness).
+//
+// Stockham autosort FFT of length N = R0 * PTS^(S-1) per column.  TPC = N/PTS threads own
+// one column; thread tpc keeps register slot m = point tpc + m*TPC on input and on output,
+// so a forward transform's output feeds an inverse transform straight from registers.
+// Stage s (radix r, Ns = product of earlier radices) maps butterfly j:
+//   in : data[j + t*N/r] * W_{Ns r}^{(j mod Ns) t}      out: data[(j/Ns)*Ns*r + (j mod Ns) + t*Ns]
+// Inter-stage exchanges go through LDS; every other step is in VGPRs.
+#pragma once
+#include "cfp_internal.h"
+
+namespace cfp {
+
+// -------------------------------------------------------------- variant flags
+enum : int {
+  F_SPLIT_LDS = 1,  // exchange real and imaginary parts separately (half the LDS footprint)
+  F_TW_GLOBAL = 2,  // twiddles from the global table (L1/L2) instead of an LDS copy
+  F_NT = 4,         // non-temporal global loads and stores
+  F_REV = 8,        // walk the tiles in reverse block order
+  F_NT_LD = 16,     // non-temporal global loads only
+  F_NT_ST = 32,     // non-temporal global stores only
+};
+
+// ------------------------------------------------------------------ complex helpers
+__device__ __forceinline__ cd cadd(cd a, cd b) { return make_cd(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ cd csub(cd a, cd b) { return make_cd(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ cd cmul(cd a, cd b) {
+  return make_cd(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ cd cconj(cd a) { return make_cd(a.x, -a.y); }
+// a / b = (a * conj(b)) / |b|^2, the complex VecPointwiseDivide of the reference
+// (src/FftLinearSolver_3D.c:174)
+__device__ __forceinline__ cd cdiv(cd a, cd b) {
+  double den = 1.0 / fma(b.x, b.x, b.y * b.y);
+  return make_cd(fma(a.x, b.x, a.y * b.y) * den, fma(a.y, b.x, -a.x * b.y) * den);
+}
+
+#define CFP_C1 0.92387953251128675613  // cos(pi/8)
+#define CFP_S1 0.38268343236508977173  // sin(pi/8)
+#define CFP_H 0.70710678118654752440   // sqrt(1/2)
+
+// v * W_R^k with W_R = exp(-2 pi i / R), R in {2,4,8,16}.  R and k are compile-time
+// constants after unrolling, so every branch folds and trivial factors cost nothing.
+template <int R>
+__device__ __forceinline__ cd twr(cd v, int k) {
+  const int e = (k * (16 / R)) & 15;  // exponent in units of 2 pi / 16
+  const double x = v.x, y = v.y;
+  switch (e) {
+    case 0: return v;
+    case 4: return make_cd(y, -x);                       // -i
+    case 8: return make_cd(-x, -y);                      // -1
+    case 12: return make_cd(-y, x);                      // +i
+    case 2: return make_cd((x + y) * CFP_H, (y - x) * CFP_H);
+    case 6: return make_cd((y - x) * CFP_H, -(x + y) * CFP_H);
+    case 10: return make_cd(-(x + y) * CFP_H, (x - y) * CFP_H);
+    case 14: return make_cd((x - y) * CFP_H, (x + y) * CFP_H);
+    // odd multiples of pi/8: (x + iy)(c + i s), c = cos(2 pi e/16), s = -sin(2 pi e/16)
+    case 1: return make_cd(fma(x, CFP_C1, y * CFP_S1), fma(y, CFP_C1, -x * CFP_S1));
+    case 3: return make_cd(fma(x, CFP_S1, y * CFP_C1), fma(y, CFP_S1, -x * CFP_C1));
+    case 5: return make_cd(fma(-x, CFP_S1, y * CFP_C1), fma(-y, CFP_S1, -x * CFP_C1));
+    case 7: return make_cd(fma(-x, CFP_C1, y * CFP_S1), fma(-y, CFP_C1, -x * CFP_S1));
+    case 9: return make_cd(fma(-x, CFP_C1, -y * CFP_S1), fma(-y, CFP_C1, x * CFP_S1));
+    case 11: return make_cd(fma(-x, CFP_S1, -y * CFP_C1), fma(-y, CFP_S1, x * CFP_C1));
+    case 13: return make_cd(fma(x, CFP_S1, -y * CFP_C1), fma(y, CFP_S1, x * CFP_C1));
+    default: return make_cd(fma(x, CFP_C1, -y * CFP_S1), fma(y, CFP_C1, x * CFP_S1));  // 15
+  }
+}
+
+__host__ __device__ constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v >> 1); }
+__host__ __device__ constexpr int bitrev(int i, int bits) {
+  return bits == 0 ? 0 : (((i & 1) << (bits - 1)) | bitrev(i >> 1, bits - 1));
+}
+
+// In-register forward DFT of R points, natural order in and out (radix-2 DIT, unrolled).
+template <int R>
+__device__ __forceinline__ void dft_reg(cd* v) {
+  constexpr int LB = ilog2(R);
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int j = bitrev(i, LB);
+    if (i < j) { cd t = v[i]; v[i] = v[j]; v[j] = t; }
+  }
+#pragma unroll
+  for (int len = 2; len <= R; len <<= 1) {
+    const int half = len >> 1;
+#pragma unroll
+    for (int i = 0; i < R; i += len) {
+#pragma unroll
+      for (int k = 0; k < half; ++k) {
+        cd u = v[i + k];
+        cd t = twr<R>(v[i + k + half], k * (R / len));
+        v[i + k] = cadd(u, t);
+        v[i + k + half] = csub(u, t);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ i64 pt_off(const Side& s, int k) {
+  return (i64)(k >> s.seg_shift) * s.seg_stride + (i64)(k & (s.seg_len - 1)) * s.pt_stride;
+}
+__device__ __forceinline__ i64 col_base(const Side& s, i64 g, i64 inner_n) {
+  return (g % inner_n) * s.inner_stride + (g / inner_n) * s.outer_stride;
+}
+
+typedef double dv2 __attribute__((ext_vector_type(2)));
+template <int FLAGS>
+__device__ __forceinline__ cd gload(const cd* p) {
+  if (FLAGS & (F_NT | F_NT_LD)) {
+    dv2 v = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(p));
+    return make_cd(v.x, v.y);
+  }
+  return *p;
+}
+template <int FLAGS>
+__device__ __forceinline__ void gstore(cd* p, cd v) {
+  if (FLAGS & (F_NT | F_NT_ST)) {
+    dv2 w;
+    w.x = v.x;
+    w.y = v.y;
+    __builtin_nontemporal_store(w, reinterpret_cast<dv2*>(p));
+  } else {
+    *p = v;
+  }
+}
+
+struct KArgs {
+  Side in, out;
+  i64 inner_n;
+  double scale;
+  const cd* tw;
+  const cd* colsym;
+  const cd* axsym;
+  const cd* diag;
+};
+
+template <int N, int PTS, int R0>
+struct Shape {
+  static constexpr int TPC = N / PTS;
+  static constexpr int QQ = PTS / R0;
+  static constexpr int S = 1 + (ilog2(N / R0) / ilog2(PTS));
+  static_assert(R0 * (1 << (ilog2(PTS) * (S - 1))) == N, "N must be R0 * PTS^k");
+};
+
+// LDS index of element idx of the workgroup's column c (row mode pads every 16 elements)
+template <int N, bool ROW, int T>
+__device__ __forceinline__ int lds_idx(int c, int idx) {
+  constexpr int RS = N + N / 16;
+  return ROW ? c * RS + idx + (idx >> 4) : idx * T + c;
+}
+
+// One LDS exchange: every thread writes its K values to positions wpos(k), then reads its
+// PTS values from positions rpos(t).  `first` skips the barrier that protects the previous
+// exchange's reads.  With F_SPLIT_LDS the real and imaginary halves go through a
+// double-typed buffer one after the other.
+template <int N, bool ROW, int T, int FLAGS, int K, int PTS, class WP, class RP>
+__device__ __forceinline__ void exchange(void* ldsv, cd* vals, WP wpos, cd* dst, RP rpos, int c, bool first) {
+  // vals may alias dst: all writes of a half complete (barrier) before its reads
+  if (!first) __syncthreads();
+  if (FLAGS & F_SPLIT_LDS) {
+    double* lds = (double*)ldsv;
+#pragma unroll
+    for (int k = 0; k < K; ++k) lds[lds_idx<N, ROW, T>(c, wpos(k))] = vals[k].x;
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < PTS; ++t) dst[t].x = lds[lds_idx<N, ROW, T>(c, rpos(t))];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) lds[lds_idx<N, ROW, T>(c, wpos(k))] = vals[k].y;
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < PTS; ++t) dst[t].y = lds[lds_idx<N, ROW, T>(c, rpos(t))];
+  } else {
+    cd* lds = (cd*)ldsv;
+#pragma unroll
+    for (int k = 0; k < K; ++k) lds[lds_idx<N, ROW, T>(c, wpos(k))] = vals[k];
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < PTS; ++t) dst[t] = lds[lds_idx<N, ROW, T>(c, rpos(t))];
+  }
+}
+
+// All stages of one forward column FFT (registers in, registers out, natural order).
+// `first` = no earlier LDS exchange in this kernel (skips one barrier).
+template <int N, int PTS, int R0, bool ROW, int T, int FLAGS>
+__device__ __forceinline__ void fft_stages(cd* v, void* lds, const cd* tws, int c, int tpc, bool first) {
+  typedef Shape<N, PTS, R0> SH;
+  constexpr int TPC = SH::TPC, QQ = SH::QQ, S = SH::S;
+  if constexpr (S == 1) {
+    dft_reg<R0>(v);
+    return;
+  } else {
+    // stage 0 (radix R0, Ns = 1, no twiddles): butterfly q works in place on slots
+    // {q + t*QQ}; butterfly j = tpc + q*TPC writes data[j*R0 + t] from slot q + t*QQ
+#pragma unroll
+    for (int q = 0; q < QQ; ++q) {
+      cd u[R0];
+#pragma unroll
+      for (int t = 0; t < R0; ++t) u[t] = v[q + t * QQ];
+      dft_reg<R0>(u);
+#pragma unroll
+      for (int t = 0; t < R0; ++t) v[q + t * QQ] = u[t];
+    }
+    exchange<N, ROW, T, FLAGS, PTS, PTS>(
+        lds, v, [&](int k) { return (tpc + (k % QQ) * TPC) * R0 + (k / QQ); }, v,
+        [&](int t) { return tpc + t * TPC; }, c, first);
+    int Ns = R0;
+#pragma unroll
+    for (int s = 1; s < S; ++s) {
+      const int jm = tpc & (Ns - 1);
+      const int step = N / (Ns * PTS);
+#pragma unroll
+      for (int t = 1; t < PTS; ++t) v[t] = cmul(v[t], tws[jm * t * step]);
+      dft_reg<PTS>(v);
+      if (s < S - 1) {
+        const int o = (tpc / Ns) * Ns * PTS + jm;
+        const int NsC = Ns;
+        exchange<N, ROW, T, FLAGS, PTS, PTS>(
+            lds, v, [&](int t) { return o + t * NsC; }, v, [&](int t) { return tpc + t * TPC; }, c, false);
+      }
+      Ns *= PTS;
+    }
+  }
+}
+
+template <int N, int PTS, int R0, bool ROW, int T, int MODE, int FLAGS>
+__global__ void __launch_bounds__(T*(N / PTS)) k_axis_fast(const cd* in, cd* out, KArgs a) {
+  typedef Shape<N, PTS, R0> SH;
+  constexpr int TPC = SH::TPC;
+  constexpr int NT = T * TPC;
+  constexpr int LDS_N = ROW ? T * (N + N / 16) : T * N;
+  constexpr bool NEED_LDS = SH::S > 1;
+  constexpr bool TW_LDS = NEED_LDS && !(FLAGS & F_TW_GLOBAL);
+  __shared__ __attribute__((aligned(16))) double lds_raw[NEED_LDS ? ((FLAGS & F_SPLIT_LDS) ? LDS_N : 2 * LDS_N) : 2];
+  __shared__ cd tws_lds[TW_LDS ? N : 1];
+
+  const int tid = threadIdx.x;
+  int c, tpc;
+  if (ROW) { tpc = tid % TPC; c = tid / TPC; }
+  else { c = tid % T; tpc = tid / T; }
+  const unsigned blk = (FLAGS & F_REV) ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;
+  const i64 g = (i64)blk * T + c;
+  const i64 bin = col_base(a.in, g, a.inner_n);
+  const i64 bout = col_base(a.out, g, a.inner_n);
+
+  const cd* tws = a.tw;
+  if constexpr (TW_LDS) {
+    for (int i = tid; i < N; i += NT) tws_lds[i] = a.tw[i];
+    tws = tws_lds;
+  }
+
+  cd v[PTS];
+#pragma unroll
+  for (int m = 0; m < PTS; ++m) v[m] = gload<FLAGS>(in + bin + pt_off(a.in, tpc + m * TPC));
+  if (MODE == PASS_INV) {
+#pragma unroll
+    for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
+  }
+  // the twiddle table copy is published by the first exchange's barrier
+  fft_stages<N, PTS, R0, ROW, T, FLAGS>(v, lds_raw, tws, c, tpc, true);
+
+  if (MODE == PASS_FUSED_SEP || MODE == PASS_FUSED_DIAG) {
+    cd cs = make_cd(0.0, 0.0);
+    if (MODE == PASS_FUSED_SEP) cs = a.colsym[g];
+#pragma unroll
+    for (int m = 0; m < PTS; ++m) {
+      const int k = tpc + m * TPC;
+      cd d;
+      if (MODE == PASS_FUSED_SEP) {
+        d = cadd(cadd(cs, a.axsym[k]), make_cd(1.0, 0.0));
+      } else {
+        d = a.diag[bin + pt_off(a.in, k)];
+      }
+      v[m] = cconj(cdiv(v[m], d));
+    }
+    fft_stages<N, PTS, R0, ROW, T, FLAGS>(v, lds_raw, tws, c, tpc, false);
+  }
+  const bool conj_out = (MODE != PASS_FWD);
+  const double sc = a.scale;
+  const double sy = conj_out ? -sc : sc;
+#pragma unroll
+  for (int m = 0; m < PTS; ++m)
+    gstore<FLAGS>(out + bout + pt_off(a.out, tpc + m * TPC), make_cd(v[m].x * sc, v[m].y * sy));
+}
+
+}  // namespace cfp

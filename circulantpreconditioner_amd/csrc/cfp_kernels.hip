@@ -21,248 +21,96 @@
 // each workgroup whole rows.
 // Generic path (any n <= 4096, incl. primes): LDS-resident mixed-radix Stockham with
 // direct O(r) sums per output, used for sizes the fast path does not instantiate.
-#include "cfp_internal.h"
+#include "cfp_fft_device.h"
 
 namespace cfp {
 
-// ------------------------------------------------------------------ complex helpers
-__device__ __forceinline__ cd cadd(cd a, cd b) { return make_cd(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ cd csub(cd a, cd b) { return make_cd(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ cd cmul(cd a, cd b) {
-  return make_cd(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
-}
-__device__ __forceinline__ cd cconj(cd a) { return make_cd(a.x, -a.y); }
-// a / b = (a * conj(b)) / |b|^2, the complex VecPointwiseDivide of the reference (:174)
-__device__ __forceinline__ cd cdiv(cd a, cd b) {
-  double den = 1.0 / fma(b.x, b.x, b.y * b.y);
-  return make_cd(fma(a.x, b.x, a.y * b.y) * den, fma(a.y, b.x, -a.x * b.y) * den);
-}
+// Per-(N, layout, role) configuration of the fast kernel: points per thread (PTS), first
+// stage radix (R0), columns (column mode) or rows (row mode) per workgroup (T) and variant
+// FLAGS (cfp_fft_device.h).  Roles: 0 = forward pass, 1 = inverse pass, 2 = fused middle
+// pass.  Shapes are the winners of isolated-kernel timing (tools/kexp/run_kexp.py); the
+// load/store cache policy per role is the winner of an exhaustive whole-apply sweep
+// (tools/kexp/run_sweep.py: every pass reads the previous pass's output, as in an apply),
+// profiles/r01_kexp_sweep.txt: non-temporal loads where a pass reads data that is cold in
+// the caches (the first pass reads b), non-temporal stores on the inverse passes.
+template <int N, bool ROW, int ROLE> struct Cfg;
+#define CFP_CFG(NN, ROWV, ROLE, P, R, TT, F)                               \
+  template <> struct Cfg<NN, ROWV, ROLE> {                                 \
+    static constexpr int PTS = P, R0 = R, T = TT, FLAGS = F, TPC = NN / P; \
+  };
+#define LD F_NT_LD
+#define ST F_NT_ST
+#define SPL F_SPLIT_LDS
+// role:     fwd=0 inv=1 fused=2
+//      N     row  role PTS R0  T   FLAGS
+CFP_CFG(16, false, 0, 4, 4, 16, 0)
+CFP_CFG(16, false, 1, 4, 4, 16, ST)
+CFP_CFG(16, false, 2, 4, 4, 16, LD)
+CFP_CFG(16, true, 0, 4, 4, 64, LD)
+CFP_CFG(16, true, 1, 4, 4, 64, ST)
+CFP_CFG(16, true, 2, 4, 4, 64, LD)
+CFP_CFG(32, false, 0, 8, 4, 16, 0)
+CFP_CFG(32, false, 1, 8, 4, 16, ST)
+CFP_CFG(32, false, 2, 8, 4, 16, LD)
+CFP_CFG(32, true, 0, 8, 4, 64, LD)
+CFP_CFG(32, true, 1, 8, 4, 64, ST)
+CFP_CFG(32, true, 2, 8, 4, 64, LD)
+CFP_CFG(64, false, 0, 8, 8, 16, 0)
+CFP_CFG(64, false, 1, 8, 8, 16, ST)
+CFP_CFG(64, false, 2, 8, 8, 16, LD)
+CFP_CFG(64, true, 0, 8, 8, 32, LD)
+CFP_CFG(64, true, 1, 8, 8, 32, ST)
+CFP_CFG(64, true, 2, 8, 8, 32, LD)
+CFP_CFG(128, false, 0, 8, 2, 16, 0)
+CFP_CFG(128, false, 1, 8, 2, 16, ST)
+CFP_CFG(128, false, 2, 8, 2, 16, LD)
+CFP_CFG(128, true, 0, 16, 8, 32, LD)
+CFP_CFG(128, true, 1, 16, 8, 32, ST)
+CFP_CFG(128, true, 2, 16, 8, 32, LD)
+CFP_CFG(256, false, 0, 8, 4, 16, 0)
+CFP_CFG(256, false, 1, 8, 4, 16, ST)
+CFP_CFG(256, false, 2, 16, 16, 16, SPL | LD)
+CFP_CFG(256, true, 0, 8, 4, 8, LD)
+CFP_CFG(256, true, 1, 8, 4, 8, ST)
+CFP_CFG(256, true, 2, 8, 4, 8, LD)
+CFP_CFG(512, false, 0, 16, 2, 16, SPL | LD)
+CFP_CFG(512, false, 1, 16, 2, 16, SPL | ST)
+CFP_CFG(512, false, 2, 8, 8, 8, LD)
+CFP_CFG(512, true, 0, 16, 2, 8, LD)
+CFP_CFG(512, true, 1, 16, 2, 8, ST)
+CFP_CFG(512, true, 2, 16, 2, 8, LD)
+CFP_CFG(1024, false, 0, 16, 4, 8, SPL | LD)
+CFP_CFG(1024, false, 1, 16, 4, 8, SPL | ST)
+CFP_CFG(1024, false, 2, 16, 4, 8, SPL | LD)
+CFP_CFG(1024, true, 0, 16, 4, 4, LD)
+CFP_CFG(1024, true, 1, 16, 4, 4, ST)
+CFP_CFG(1024, true, 2, 16, 4, 4, LD)
+#undef SPL
+#undef ST
+#undef LD
+#undef CFP_CFG
 
-#define CFP_C1 0.92387953251128675613  // cos(pi/8)
-#define CFP_S1 0.38268343236508977173  // sin(pi/8)
-#define CFP_H 0.70710678118654752440   // sqrt(1/2)
-
-// v * W_R^k with W_R = exp(-2 pi i / R), R in {2,4,8,16}.  R and k are compile-time
-// constants after unrolling, so every branch folds and trivial factors cost nothing.
-template <int R>
-__device__ __forceinline__ cd twr(cd v, int k) {
-  const int e = (k * (16 / R)) & 15;  // exponent in units of 2 pi / 16
-  const double x = v.x, y = v.y;
-  switch (e) {
-    case 0: return v;
-    case 4: return make_cd(y, -x);                       // -i
-    case 8: return make_cd(-x, -y);                      // -1
-    case 12: return make_cd(-y, x);                      // +i
-    case 2: return make_cd((x + y) * CFP_H, (y - x) * CFP_H);
-    case 6: return make_cd((y - x) * CFP_H, -(x + y) * CFP_H);
-    case 10: return make_cd(-(x + y) * CFP_H, (x - y) * CFP_H);
-    case 14: return make_cd((x - y) * CFP_H, (x + y) * CFP_H);
-    // odd multiples of pi/8: (x + iy)(c + i s), c = cos(2 pi e/16), s = -sin(2 pi e/16)
-    case 1: return make_cd(fma(x, CFP_C1, y * CFP_S1), fma(y, CFP_C1, -x * CFP_S1));
-    case 3: return make_cd(fma(x, CFP_S1, y * CFP_C1), fma(y, CFP_S1, -x * CFP_C1));
-    case 5: return make_cd(fma(-x, CFP_S1, y * CFP_C1), fma(-y, CFP_S1, -x * CFP_C1));
-    case 7: return make_cd(fma(-x, CFP_C1, y * CFP_S1), fma(-y, CFP_C1, -x * CFP_S1));
-    case 9: return make_cd(fma(-x, CFP_C1, -y * CFP_S1), fma(-y, CFP_C1, x * CFP_S1));
-    case 11: return make_cd(fma(-x, CFP_S1, -y * CFP_C1), fma(-y, CFP_S1, x * CFP_C1));
-    case 13: return make_cd(fma(x, CFP_S1, -y * CFP_C1), fma(y, CFP_S1, x * CFP_C1));
-    default: return make_cd(fma(x, CFP_C1, -y * CFP_S1), fma(y, CFP_C1, x * CFP_S1));  // 15
-  }
-}
-
-__host__ __device__ constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v >> 1); }
-__host__ __device__ constexpr int bitrev(int i, int bits) {
-  return bits == 0 ? 0 : (((i & 1) << (bits - 1)) | bitrev(i >> 1, bits - 1));
-}
-
-// In-register forward DFT of R points, natural order in and out (radix-2 DIT, unrolled).
-template <int R>
-__device__ __forceinline__ void dft_reg(cd* v) {
-  constexpr int LB = ilog2(R);
-#pragma unroll
-  for (int i = 0; i < R; ++i) {
-    const int j = bitrev(i, LB);
-    if (i < j) { cd t = v[i]; v[i] = v[j]; v[j] = t; }
-  }
-#pragma unroll
-  for (int len = 2; len <= R; len <<= 1) {
-    const int half = len >> 1;
-#pragma unroll
-    for (int i = 0; i < R; i += len) {
-#pragma unroll
-      for (int k = 0; k < half; ++k) {
-        cd u = v[i + k];
-        cd t = twr<R>(v[i + k + half], k * (R / len));
-        v[i + k] = cadd(u, t);
-        v[i + k + half] = csub(u, t);
-      }
-    }
-  }
-}
-
-__device__ __forceinline__ i64 pt_off(const Side& s, int k) {
-  return (i64)(k >> s.seg_shift) * s.seg_stride + (i64)(k & (s.seg_len - 1)) * s.pt_stride;
-}
-__device__ __forceinline__ i64 col_base(const Side& s, i64 g, i64 inner_n) {
-  return (g % inner_n) * s.inner_stride + (g / inner_n) * s.outer_stride;
-}
-
-struct KArgs {
-  Side in, out;
-  i64 inner_n;
-  double scale;
-  const cd* tw;
-  const cd* colsym;
-  const cd* axsym;
-  const cd* diag;
-};
-
-// ----------------------------------------------------------------- fast path
-// Shape of one column FFT: N = R0 * PTS^(S-1); TPC = N/PTS threads per column, each
-// holding PTS points.  Register slot m of thread tpc always holds point tpc + m*TPC on
-// input and output (natural order), so a forward transform's output can feed an inverse
-// transform straight from registers (the fused middle pass).
-template <int N, int PTS, int R0>
-struct Shape {
-  static constexpr int TPC = N / PTS;
-  static constexpr int QQ = PTS / R0;
-  static constexpr int S = 1 + (ilog2(N / R0) / ilog2(PTS));
-  static_assert(R0 * (1 << (ilog2(PTS) * (S - 1))) == N, "N must be R0 * PTS^k");
-};
-
-// Stockham stages.  Stage s (radix r, Ns = product of earlier radices) maps butterfly j:
-//   in  : data[j + t*N/r] * W_{Ns r}^{(j mod Ns) t}
-//   out : data[(j/Ns)*Ns*r + (j mod Ns) + t*Ns]
-template <int N, int PTS, int R0, bool ROW, int T>
-__device__ __forceinline__ void fft_stages(cd* v, cd* lds, const cd* tws, int c, int tpc, bool sync_first) {
-  typedef Shape<N, PTS, R0> SH;
-  constexpr int TPC = SH::TPC, QQ = SH::QQ, S = SH::S;
-  constexpr int RS = N + N / 16;  // padded row stride (row mode)
-  auto L = [&](int idx) -> int { return ROW ? c * RS + idx + (idx >> 4) : idx * T + c; };
-  if constexpr (S == 1) {
-    dft_reg<R0>(v);
-    return;
-  } else {
-    if (sync_first) __syncthreads();
-#pragma unroll
-    for (int q = 0; q < QQ; ++q) {
-      cd u[R0];
-#pragma unroll
-      for (int t = 0; t < R0; ++t) u[t] = v[q + t * QQ];
-      dft_reg<R0>(u);
-      const int j = tpc + q * TPC;
-#pragma unroll
-      for (int t = 0; t < R0; ++t) lds[L(j * R0 + t)] = u[t];
-    }
-    __syncthreads();
-    int Ns = R0;
-#pragma unroll
-    for (int s = 1; s < S; ++s) {
-      cd u[PTS];
-#pragma unroll
-      for (int t = 0; t < PTS; ++t) u[t] = lds[L(tpc + t * TPC)];
-      const int jm = tpc & (Ns - 1);
-      const int step = N / (Ns * PTS);
-#pragma unroll
-      for (int t = 1; t < PTS; ++t) u[t] = cmul(u[t], tws[jm * t * step]);
-      dft_reg<PTS>(u);
-      if (s == S - 1) {
-#pragma unroll
-        for (int t = 0; t < PTS; ++t) v[t] = u[t];
-      } else {
-        __syncthreads();
-        const int o = (tpc / Ns) * Ns * PTS + jm;
-#pragma unroll
-        for (int t = 0; t < PTS; ++t) lds[L(o + t * Ns)] = u[t];
-        __syncthreads();
-      }
-      Ns *= PTS;
-    }
-  }
-}
-
-template <int N, int PTS, int R0, bool ROW, int T, int MODE>
-__global__ void __launch_bounds__(T*(N / PTS)) k_axis_fast(const cd* in, cd* out, KArgs a) {
-  typedef Shape<N, PTS, R0> SH;
-  constexpr int TPC = SH::TPC;
-  constexpr int NT = T * TPC;
-  constexpr int LDS_N = ROW ? T * (N + N / 16) : T * N;
-  __shared__ cd lds[SH::S > 1 ? LDS_N : 1];
-  __shared__ cd tws[SH::S > 1 ? N : 1];
-
-  const int tid = threadIdx.x;
-  int c, tpc;
-  if (ROW) { tpc = tid % TPC; c = tid / TPC; }
-  else { c = tid % T; tpc = tid / T; }
-  const i64 g = (i64)blockIdx.x * T + c;
-  const i64 bin = col_base(a.in, g, a.inner_n);
-  const i64 bout = col_base(a.out, g, a.inner_n);
-
-  if constexpr (SH::S > 1) {
-    for (int i = tid; i < N; i += NT) tws[i] = a.tw[i];
-  }
-
-  cd v[PTS];
-#pragma unroll
-  for (int m = 0; m < PTS; ++m) v[m] = in[bin + pt_off(a.in, tpc + m * TPC)];
-  if (MODE == PASS_INV) {
-#pragma unroll
-    for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
-  }
-  fft_stages<N, PTS, R0, ROW, T>(v, lds, tws, c, tpc, false);
-
-  if (MODE == PASS_FUSED_SEP || MODE == PASS_FUSED_DIAG) {
-    cd cs = make_cd(0.0, 0.0);
-    if (MODE == PASS_FUSED_SEP) cs = a.colsym[g];
-#pragma unroll
-    for (int m = 0; m < PTS; ++m) {
-      const int k = tpc + m * TPC;
-      cd d;
-      if (MODE == PASS_FUSED_SEP) {
-        d = cadd(cadd(cs, a.axsym[k]), make_cd(1.0, 0.0));
-      } else {
-        d = a.diag[bin + pt_off(a.in, k)];
-      }
-      v[m] = cconj(cdiv(v[m], d));
-    }
-    fft_stages<N, PTS, R0, ROW, T>(v, lds, tws, c, tpc, true);
-  }
-  const bool conj_out = (MODE != PASS_FWD);
-  const double sc = a.scale;
-  const double sy = conj_out ? -sc : sc;
-#pragma unroll
-  for (int m = 0; m < PTS; ++m) {
-    out[bout + pt_off(a.out, tpc + m * TPC)] = make_cd(v[m].x * sc, v[m].y * sy);
-  }
-}
-
-// Per-N configuration: (PTS, R0, T_col).  Row mode packs 256 threads' worth of rows.
-template <int N> struct Cfg;
-template <> struct Cfg<16> { static constexpr int PTS = 4, R0 = 4, TCOL = 16; };
-template <> struct Cfg<32> { static constexpr int PTS = 8, R0 = 4, TCOL = 16; };
-template <> struct Cfg<64> { static constexpr int PTS = 8, R0 = 8, TCOL = 16; };
-template <> struct Cfg<128> { static constexpr int PTS = 16, R0 = 8, TCOL = 16; };
-template <> struct Cfg<256> { static constexpr int PTS = 16, R0 = 16, TCOL = 16; };
-template <> struct Cfg<512> { static constexpr int PTS = 16, R0 = 2, TCOL = 8; };
-template <> struct Cfg<1024> { static constexpr int PTS = 16, R0 = 4, TCOL = 4; };
-
-template <int N>
-struct FastCfg {
-  static constexpr int PTS = Cfg<N>::PTS, R0 = Cfg<N>::R0, TCOL = Cfg<N>::TCOL;
-  static constexpr int TPC = N / PTS;
-  static constexpr int TROW = (256 / TPC) > 0 ? (256 / TPC) : 1;
-};
+constexpr int role_of(int mode) { return mode == PASS_FWD ? 0 : (mode == PASS_INV ? 1 : 2); }
 
 static bool is_pow2(i64 v) { return v > 0 && (v & (v - 1)) == 0; }
 
+// row mode = the transform axis is contiguous (x); columns may be any 2-D set of rows
 static bool row_mode(const PassDesc& p) {
-  return p.inner_n == 1 && p.in.pt_stride == 1 && p.out.pt_stride == 1 && p.in.seg_len == p.n &&
-         p.out.seg_len == p.n;
+  return p.in.pt_stride == 1 && p.out.pt_stride == 1 && p.in.seg_len == p.n && p.out.seg_len == p.n;
+}
+
+template <int NN>
+static int tile_of(bool r, int role) {
+  if (r) return role == 0 ? Cfg<NN, true, 0>::T : (role == 1 ? Cfg<NN, true, 1>::T : Cfg<NN, true, 2>::T);
+  return role == 0 ? Cfg<NN, false, 0>::T : (role == 1 ? Cfg<NN, false, 1>::T : Cfg<NN, false, 2>::T);
 }
 
 static int fast_tile(const PassDesc& p) {
+  const bool r = row_mode(p);
+  const int role = role_of(p.mode);
   switch (p.n) {
 #define CFP_TILE(NN) \
-  case NN: return row_mode(p) ? FastCfg<NN>::TROW : FastCfg<NN>::TCOL;
+  case NN: return tile_of<NN>(r, role);
     CFP_TILE(16) CFP_TILE(32) CFP_TILE(64) CFP_TILE(128) CFP_TILE(256) CFP_TILE(512) CFP_TILE(1024)
 #undef CFP_TILE
     default: return 0;
@@ -284,11 +132,10 @@ bool fast_path_supported(const PassDesc& p) {
 
 template <int N, bool ROW, int MODE>
 static hipError_t launch_fast_t(const PassDesc& p, const cd* in, cd* out, const KArgs& a, hipStream_t s) {
-  typedef FastCfg<N> C;
-  constexpr int T = ROW ? C::TROW : C::TCOL;
-  const unsigned blocks = (unsigned)(p.ncols / T);
-  hipLaunchKernelGGL((k_axis_fast<N, C::PTS, C::R0, ROW, T, MODE>), dim3(blocks), dim3(T * C::TPC), 0, s, in,
-                     out, a);
+  typedef Cfg<N, ROW, role_of(MODE)> C;
+  const unsigned blocks = (unsigned)(p.ncols / C::T);
+  hipLaunchKernelGGL((k_axis_fast<N, C::PTS, C::R0, ROW, C::T, MODE, C::FLAGS>), dim3(blocks), dim3(C::T * C::TPC),
+                     0, s, in, out, a);
   return hipGetLastError();
 }
 

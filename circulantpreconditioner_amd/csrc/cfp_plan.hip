@@ -129,6 +129,7 @@ struct cfp_plan_s {
   std::vector<int> axes;     // non-trivial axes, x..z
   int fused_axis = 0;
   std::vector<cd> sym1d[3];  // separable: lambda_d * c_d_hat (host copies)
+  i64 chunk_planes = 0;      // > 0: chunked x/y schedule (see apply_steps)
 };
 
 namespace {
@@ -156,41 +157,73 @@ int ensure_tw(cfp_plan_s* p, int n) {
   return CFP_SUCCESS;
 }
 
-// The apply schedule: forward passes over all non-trivial axes but the last, the fused
-// DFT/divide/IDFT pass over the last one, then the inverse passes in reverse order; the
-// 1/N scale rides on the final launch.
 struct Step {
   int axis;
-  int mode;
+  int mode;    // PASS_* or -1 for the fused symbol pass
   bool from_b;
   bool scale;
+  i64 z0, z1;  // z-plane range of an x or y pass (z1 < 0: whole grid)
 };
 
+// The apply schedule: forward passes over all non-trivial axes but the last, the fused
+// DFT/divide/IDFT pass over the last one, then the inverse passes in reverse order; the
+// 1/N scale rides on the final launch.  With chunking (3-D grids), the x and y passes run
+// alternately over blocks of `chunk` z-planes, so the y pass reads planes the x pass has
+// just written while they are still resident in the 256 MiB Infinity Cache (and the
+// inverse pair likewise).
 std::vector<Step> apply_steps(const cfp_plan_s* p) {
   std::vector<Step> st;
   const std::vector<int>& A = p->axes;
   if (A.empty()) {
-    st.push_back({0, -1, true, true});  // N == 1: fused pass on a length-1 axis
+    st.push_back({0, -1, true, true, 0, -1});  // N == 1: fused pass on a length-1 axis
     return st;
   }
-  for (size_t i = 0; i + 1 < A.size(); ++i) st.push_back({A[i], PASS_FWD, i == 0, false});
-  st.push_back({A.back(), -1, A.size() == 1, A.size() == 1});
-  for (int i = (int)A.size() - 2; i >= 0; --i) st.push_back({A[i], PASS_INV, false, i == 0});
+  const bool chunked = p->chunk_planes > 0 && A.size() == 3 && p->chunk_planes < p->n[2];
+  if (chunked) {
+    const i64 C = p->chunk_planes, nz = p->n[2];
+    for (i64 z = 0; z < nz; z += C) {
+      const i64 z1 = z + C < nz ? z + C : nz;
+      st.push_back({0, PASS_FWD, true, false, z, z1});
+      st.push_back({1, PASS_FWD, false, false, z, z1});
+    }
+    st.push_back({2, -1, false, false, 0, -1});
+    for (i64 z = 0; z < nz; z += C) {
+      const i64 z1 = z + C < nz ? z + C : nz;
+      st.push_back({1, PASS_INV, false, false, z, z1});
+      st.push_back({0, PASS_INV, false, true, z, z1});
+    }
+    return st;
+  }
+  for (size_t i = 0; i + 1 < A.size(); ++i) st.push_back({A[i], PASS_FWD, i == 0, false, 0, -1});
+  st.push_back({A.back(), -1, A.size() == 1, A.size() == 1, 0, -1});
+  for (int i = (int)A.size() - 2; i >= 0; --i) st.push_back({A[i], PASS_INV, false, i == 0, 0, -1});
   return st;
 }
 
-PassDesc make_pass(const cfp_plan_s* p, int axis, int mode, double scale) {
+// pass descriptor of a step; *offset = element offset of the step's first z-plane
+PassDesc make_pass(const cfp_plan_s* p, const Step& q, int mode, double scale, i64* offset) {
   PassDesc d;
-  d.n = (int)p->n[axis];
-  natural_cols(axis, p->n, &d.ncols, &d.inner_n);
-  d.in = natural_side(axis, p->n);
+  d.n = (int)p->n[q.axis];
+  natural_cols(q.axis, p->n, &d.ncols, &d.inner_n);
+  d.in = natural_side(q.axis, p->n);
   d.out = d.in;
   d.mode = mode;
   d.scale = scale;
   d.colsym = p->colsym;
   d.axsym = p->axsym;
   d.diag = p->diag;
+  *offset = 0;
+  if (q.z1 >= 0 && q.axis < 2) {
+    const i64 planes = q.z1 - q.z0;
+    d.ncols = planes * (q.axis == 0 ? p->n[1] : p->n[0]);
+    *offset = q.z0 * p->n[0] * p->n[1];
+  }
   return d;
+}
+
+int step_mode(const cfp_plan_s* p, const Step& q, bool diag_override) {
+  if (q.mode >= 0) return q.mode;
+  return (diag_override || p->sym_kind == 2) ? PASS_FUSED_DIAG : PASS_FUSED_SEP;
 }
 
 int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStream_t s, std::vector<hipEvent_t>* ev) {
@@ -200,14 +233,13 @@ int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStr
   const double invN = 1.0 / (double)p->N;
   for (size_t i = 0; i < st.size(); ++i) {
     const Step& q = st[i];
-    int mode = q.mode;
-    if (mode < 0) mode = (diag_override || p->sym_kind == 2) ? PASS_FUSED_DIAG : PASS_FUSED_SEP;
-    PassDesc d = make_pass(p, q.axis, mode, q.scale ? invN : 1.0);
+    i64 off = 0;
+    PassDesc d = make_pass(p, q, step_mode(p, q, diag_override != nullptr), q.scale ? invN : 1.0, &off);
     if (diag_override) d.diag = diag_override;
     int rc = ensure_tw(p, d.n);
     if (rc) return rc;
     if (ev) HIPCHK(hipEventRecord((*ev)[i], s));
-    hipError_t e = launch_axis_pass(d, q.from_b ? b : x, x, p->tw[d.n], s);
+    hipError_t e = launch_axis_pass(d, (q.from_b ? b : x) + off, x + off, p->tw[d.n], s);
     if (e != hipSuccess) return hip_error(e, "axis pass launch");
   }
   if (ev) HIPCHK(hipEventRecord((*ev)[st.size()], s));
@@ -221,7 +253,9 @@ int run_transform(cfp_plan_s* p, bool inverse, const cd* in, cd* out, hipStream_
   }
   bool first = true;
   for (int ax : p->axes) {
-    PassDesc d = make_pass(p, ax, inverse ? PASS_INV : PASS_FWD, 1.0);
+    i64 off = 0;
+    PassDesc d = make_pass(p, Step{ax, inverse ? PASS_INV : PASS_FWD, first, false, 0, -1},
+                           inverse ? PASS_INV : PASS_FWD, 1.0, &off);
     int rc = ensure_tw(p, d.n);
     if (rc) return rc;
     hipError_t e = launch_axis_pass(d, first ? in : out, out, p->tw[d.n], s);
@@ -421,6 +455,13 @@ extern "C" int cfp_plan_backward(cfp_plan_t p, const double* in, double* out, vo
   return run_transform(p, true, (const cd*)in, (cd*)out, (hipStream_t)stream);
 }
 
+extern "C" int cfp_plan_set_chunking(cfp_plan_t p, int64_t chunk_planes) {
+  if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
+  if (chunk_planes < 0) return set_error(CFP_ERR_ARG_OUTOFRANGE, "chunk_planes must be >= 0");
+  p->chunk_planes = chunk_planes;
+  return CFP_SUCCESS;
+}
+
 extern "C" int cfp_plan_num_passes(cfp_plan_t p, int* passes) {
   if (!p || !passes) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
   *passes = (int)apply_steps(p).size();
@@ -431,9 +472,9 @@ extern "C" int cfp_plan_pass_info(cfp_plan_t p, int pass, int* axis, int* n, int
   if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
   std::vector<Step> st = apply_steps(p);
   if (pass < 0 || pass >= (int)st.size()) return set_error(CFP_ERR_ARG_OUTOFRANGE, "pass index");
-  int m = st[pass].mode;
-  if (m < 0) m = p->sym_kind == 2 ? PASS_FUSED_DIAG : PASS_FUSED_SEP;
-  PassDesc d = make_pass(p, st[pass].axis, m, 1.0);
+  const int m = step_mode(p, st[pass], false);
+  i64 off = 0;
+  PassDesc d = make_pass(p, st[pass], m, 1.0, &off);
   if (axis) *axis = st[pass].axis;
   if (n) *n = d.n;
   if (ncols) *ncols = d.ncols;

@@ -144,6 +144,11 @@ class CirculantPlan:
                                       _stream_handle(stream)))
         return out
 
+    def set_chunking(self, chunk_planes: int) -> "CirculantPlan":
+        """x/y passes alternate over blocks of `chunk_planes` z-planes (0 = off)."""
+        check(lib().cfp_plan_set_chunking(self._h, int(chunk_planes)))
+        return self
+
     # ---------------------------------------------------------------- introspection
     def passes(self) -> list:
         n = ctypes.c_int()

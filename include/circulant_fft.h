@@ -85,6 +85,11 @@ int cfp_plan_apply_host(cfp_plan_t plan, const double *b_host, double *x_host);
 int cfp_plan_forward(cfp_plan_t plan, const double *in_dev, double *out_dev, void *stream);
 int cfp_plan_backward(cfp_plan_t plan, const double *in_dev, double *out_dev, void *stream);
 
+/* Schedule option: > 0 runs the x and y passes of 3-D grids alternately over blocks of
+ * `chunk_planes` z-planes (Infinity-Cache-resident hand-off between the two passes);
+ * 0 (default) = one launch per axis pass. */
+int cfp_plan_set_chunking(cfp_plan_t plan, int64_t chunk_planes);
+
 /* Introspection: number of kernel launches of one apply, and per-launch timing.
  * cfp_plan_time_passes runs `iters` applies and writes the mean duration (ms) of each of the
  * apply's launches into ms_out[0..passes) (HIP events on `stream`). */

@@ -228,3 +228,21 @@ def test_errors(cp):
         b = torch.zeros(512, dtype=torch.complex128, device="cuda")
         with pytest.raises(cp.CirculantError):
             plan.apply(b)  # no symbol yet: PETSC_ERR_ARG_WRONGSTATE
+
+
+@pytest.mark.parametrize("n,chunk", [((64, 32, 48), 16), ((64, 32, 48), 20), ((32, 32, 32), 1), ((20, 12, 9), 4),
+                                     ((128, 128, 128), 32)])
+def test_chunked_schedule_vs_oracle(cp, oracle, n, chunk):
+    lam = (0.6, 0.15, 0.02 + 0.01j)
+    N = int(np.prod(n))
+    b = oracle.c_fill_uniform(N, 31)
+    ref = oracle.c_solve_3d(oracle.c_build_diag_transport(n, lam), b, n)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam).set_chunking(chunk)
+        nch = -(-n[2] // chunk)
+        assert len(plan.passes()) == 4 * nch + 1
+        x = plan.apply(_dev(b))
+        assert _rel(x, ref) < TOL
+        t = _dev(b)
+        plan.apply(t, out=t)
+        assert _rel(t, ref) < TOL

@@ -32,7 +32,7 @@ def load(d, counter):
 
 
 def pass_name(kname: str):
-    m = re.search(r"k_axis_fast<(\d+), (\d+), (\d+), (true|false), (\d+), (\d+)>", kname)
+    m = re.search(r"k_axis_fast<(\d+), (\d+), (\d+), (true|false), (\d+), (\d+)(?:, \d+)?>", kname)
     if not m:
         return None
     row, mode = m.group(4) == "true", int(m.group(6))
