@@ -109,6 +109,8 @@ def main() -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if os.environ.get("CFP_BENCH_SHARE_DEVICE"):  # rehearsal of N > 1 on a one-GPU box
+        local_rank = local_rank % torch.cuda.device_count()
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
@@ -134,13 +136,26 @@ def main() -> int:
         parallelism = "single GPU"
     else:
         from circulantpreconditioner_amd.distributed import SlabPlan
-        plan = SlabPlan(grid, rank=rank, world=world, device=local_rank)
+        exchange = os.environ.get("CFP_EXCHANGE", "rccl")
+        plan, err = None, None
+        try:
+            plan = SlabPlan(grid, rank=rank, world=world, device=local_rank, exchange=exchange)
+        except Exception as e:  # the library's own RCCL communicator failed on this rank
+            err = e
+        ok = torch.tensor([0 if plan is None else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            log(f"rank {rank}: {exchange} exchange unavailable ({err}); using torch.distributed all_to_all_single")
+            if plan is not None:
+                plan.close()
+            exchange = "torch"
+            plan = SlabPlan(grid, rank=rank, world=world, device=local_rank, exchange="torch")
         plan.set_transport_symbol(LAM)
         b = torch.empty(plan.local_size, dtype=torch.complex128, device=dev)
         x = torch.empty_like(b)
         cp.fill_uniform(b, SEED, offset=plan.local_offset)
         run = lambda: plan.apply(b, out=x)  # noqa: E731
-        parallelism = f"z-slab x{world}, RCCL all-to-all over xGMI"
+        parallelism = f"z-slab x{world}, all-to-all over xGMI ({exchange})"
 
     for _ in range(args.warmup):
         run()
@@ -185,6 +200,30 @@ def main() -> int:
         roof_apply = {"B_alg_bytes": b_alg, "achieved": round(ach_apply, 1), "peak": HBM_PEAK_GBS,
                       "unit": "GB/s", "frac": round(ach_apply / HBM_PEAK_GBS, 4),
                       "note": "SURVEY §8d: B_alg = 208 N (13 c128 sweeps) / wall time per apply"}
+    else:
+        # every rank takes part (the exchanges are collectives); rank 0 reports its own phases
+        passes_info = plan.phases()
+        ms = plan.time_phases(b, x, iters=max(5, min(20, args.steps)))
+        for p, m in zip(passes_info, ms):
+            p["ms"] = round(m, 5)
+        nloc = plan.local_size
+        kern = [i for i, p in enumerate(passes_info) if p["kind"] == "pass"]
+        k = max(kern, key=lambda i: ms[i])
+        dom = passes_info[k]
+        alg = kernel_alg_bytes(dom["mode"], nloc, dom["n"])
+        achieved = alg / (ms[k] * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": f"phase{k}_{dom['axis']}_{dom['mode']} (rank 0 slab)", "alg_bytes_per_launch": alg,
+                "mean_ms": round(ms[k], 5)}
+        ex = [ms[i] for i, p in enumerate(passes_info) if p["kind"] == "all-to-all"]
+        sent = 16 * nloc * (world - 1) / world  # bytes leaving this GPU per all-to-all
+        roof_apply = {"B_alg_bytes_per_gpu": 208 * nloc,
+                      "achieved_per_gpu": round(208 * nloc / (ms_per_step * 1e-3) / 1e9, 1),
+                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": round(208 * nloc / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                      "alltoall_ms": [round(e, 5) for e in ex],
+                      "alltoall_GBps_out_per_gpu": [round(sent / (e * 1e-3) / 1e9, 1) for e in ex]}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

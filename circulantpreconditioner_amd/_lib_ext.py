@@ -35,6 +35,31 @@ class StructuredTransportContext(ctypes.Structure):
                 ("FFT_MAT", ctypes.c_void_p)]
 
 
+class TransportConfig(ctypes.Structure):
+    """cfp_transport_config (include/transport_equation.h)."""
+    _fields_ = [("nx", ctypes.c_int64), ("ny", ctypes.c_int64), ("nz", ctypes.c_int64),
+                ("xmin", ctypes.c_double * 3), ("xmax", ctypes.c_double * 3), ("a", ctypes.c_double * 3),
+                ("cfl", ctypes.c_double), ("tmax", ctypes.c_double), ("ntmax", ctypes.c_int64),
+                ("precision", ctypes.c_double), ("max_its", ctypes.c_int64), ("restart", ctypes.c_int64),
+                ("pc", ctypes.c_int), ("sign_mode", ctypes.c_int), ("lambda_mode", ctypes.c_int),
+                ("pc_side", ctypes.c_int), ("on_device", ctypes.c_int)]
+
+
+class TransportResult(ctypes.Structure):
+    """cfp_transport_result (include/transport_equation.h)."""
+    _fields_ = [("steps", ctypes.c_int64), ("dt", ctypes.c_double), ("time", ctypes.c_double),
+                ("total_its", ctypes.c_int64), ("max_step_its", ctypes.c_int64), ("min_step_its", ctypes.c_int64),
+                ("last_reason", ctypes.c_int), ("all_converged", ctypes.c_int), ("last_residual", ctypes.c_double),
+                ("last_norm_dU", ctypes.c_double), ("solve_seconds", ctypes.c_double),
+                ("pc_seconds", ctypes.c_double), ("pc_calls", ctypes.c_int64), ("setup_seconds", ctypes.c_double),
+                ("lambda_", ctypes.c_double * 3)]
+
+    def as_dict(self) -> dict:
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "lambda_"}
+        d["lambda"] = list(self.lambda_)
+        return d
+
+
 def declare(L) -> None:
     i64, dp, vp, c_int = ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int
     S, P, cs = PetscScalar, ctypes.POINTER, ctypes.c_char_p
@@ -45,11 +70,16 @@ def declare(L) -> None:
         "cfp_slab_layout": ([i64, i64, i64, c_int, c_int, P(i64)], c_int),
         "cfp_dist_plan_create": ([P(vp), i64, i64, i64, c_int, c_int, ctypes.c_char_p, c_int], c_int),
         "cfp_dist_plan_destroy": ([vp], c_int),
+        "cfp_dist_plan_create_external": ([P(vp), i64, i64, i64, c_int, c_int, c_int], c_int),
+        "cfp_dist_plan_work_buffer": ([vp, P(ctypes.c_void_p)], c_int),
+        "cfp_dist_plan_run_segment": ([vp, c_int, dp, dp, vp], c_int),
+        "cfp_dist_plan_set_work_buffer": ([vp, dp], c_int),
         "cfp_dist_plan_set_symbol_transport": ([vp, dp], c_int),
         "cfp_dist_plan_apply": ([vp, dp, dp, vp], c_int),
         "cfp_dist_plan_local_size": ([vp, P(i64)], c_int),
         "cfp_dist_plan_time_phases": ([vp, dp, dp, c_int, dp, vp], c_int),
         "cfp_dist_plan_num_phases": ([vp, P(c_int)], c_int),
+        "cfp_dist_plan_phase_info": ([vp, c_int, P(c_int), P(c_int), P(c_int), P(c_int)], c_int),
         "cfp_group_create": ([P(vp), i64, i64, i64, c_int, P(c_int)], c_int),
         "cfp_group_destroy": ([vp], c_int),
         "cfp_group_set_symbol_transport": ([vp, dp], c_int),
@@ -101,6 +131,32 @@ def declare(L) -> None:
         "PCSetUp": ([vp], c_int),
         "PCApply": ([vp, vp, vp], c_int),
         "PCDestroy": ([P(vp)], c_int),
+        "VecMDot": ([vp, i64, P(vp), P(S)], c_int),
+        "VecMAXPY": ([vp, i64, P(S), P(vp)], c_int),
+        "KSPCreate": ([c_int, P(vp)], c_int),
+        "KSPSetType": ([vp, cs], c_int),
+        "KSPSetTolerances": ([vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, i64], c_int),
+        "KSPGMRESSetRestart": ([vp, i64], c_int),
+        "KSPSetPCSide": ([vp, c_int], c_int),
+        "KSPSetInitialGuessNonzero": ([vp, c_int], c_int),
+        "KSPGetPC": ([vp, P(vp)], c_int),
+        "KSPSetOperators": ([vp, vp, vp], c_int),
+        "KSPSetUp": ([vp], c_int),
+        "KSPSolve": ([vp, vp, vp], c_int),
+        "KSPGetConvergedReason": ([vp, P(c_int)], c_int),
+        "KSPGetIterationNumber": ([vp, P(i64)], c_int),
+        "KSPGetResidualNorm": ([vp, P(ctypes.c_double)], c_int),
+        "KSPMiniGetPCApplyStats": ([vp, P(i64), P(ctypes.c_double)], c_int),
+        "KSPDestroy": ([P(vp)], c_int),
+        # transport operator + GMRES time loop (include/transport_equation.h)
+        "cfp_transport_csr": ([i64, i64, i64, P(ctypes.c_double), ctypes.c_double, P(ctypes.c_double), c_int,
+                               ctypes.c_double, P(i64), P(i64), P(ctypes.c_double), P(i64)], c_int),
+        "cfp_cartesian_min_ratio_vol_surf": ([c_int, P(ctypes.c_double)], ctypes.c_double),
+        "computeDivergenceMatrixCartesian": ([i64, i64, i64, P(ctypes.c_double), ctypes.c_double,
+                                              P(ctypes.c_double), i64, P(vp)], c_int),
+        "initial_conditions_shock_cartesian": ([i64, i64, i64, P(ctypes.c_double), P(ctypes.c_double), vp], c_int),
+        "cfp_transport_config_default": ([P(TransportConfig), i64], None),
+        "TransportEquationGMRES": ([P(TransportConfig), P(TransportResult), P(ctypes.c_double)], c_int),
         # the reference-named boundary
         "applyFFT3DPrecTransport": ([vp, vp, vp], c_int),
         "setupFFTPrec3D": ([vp], c_int),

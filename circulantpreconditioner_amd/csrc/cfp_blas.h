@@ -3,6 +3,9 @@
 #include "cfp_internal.h"
 
 namespace cfp {
+#define MV_MAX 32
+struct MVPtrs { const cd* p[MV_MAX]; };
+struct MVCoef { cd a[MV_MAX]; };
 hipError_t blas_set(cd* x, cd a, i64 n, hipStream_t s);
 hipError_t blas_shift(cd* x, cd a, i64 n, hipStream_t s);
 hipError_t blas_copy(cd* y, const cd* x, i64 n, hipStream_t s);
@@ -10,11 +13,13 @@ hipError_t blas_axpy(cd* y, cd a, const cd* x, i64 n, hipStream_t s);    // y +=
 hipError_t blas_aypx(cd* y, cd b, const cd* x, i64 n, hipStream_t s);    // y = x + b y
 hipError_t blas_waxpy(cd* w, cd a, const cd* x, const cd* y, i64 n, hipStream_t s);  // w = a x + y
 hipError_t blas_pmult(cd* w, const cd* x, const cd* y, i64 n, hipStream_t s);
-hipError_t blas_maxpy(cd* y, int k, const cd* a_dev, const cd* const* xs_dev, i64 n, hipStream_t s);
+// y += sum_j a[j] xs[j]   (a, xs: host arrays of k coefficients / device pointers)
+hipError_t blas_maxpy(cd* y, int k, const cd* a, const cd* const* xs, i64 n, hipStream_t s);
 hipError_t blas_csr_spmv(i64 m, const i64* rowptr, const i64* col, const cd* val, const cd* x, cd* y, hipStream_t s);
 // synchronous reductions, PETSc conventions: dot = y^H x; norm type 0 = NORM_1 (sum |re|+|im|),
 // 1 = NORM_2, 3 = NORM_INFINITY (max modulus)
 hipError_t blas_dot(const cd* x, const cd* y, i64 n, cd* val, hipStream_t s);
 hipError_t blas_norm(const cd* x, i64 n, int type, double* val, hipStream_t s);
-hipError_t blas_mdot(const cd* x, int k, const cd* const* ys_dev, i64 n, cd* vals, hipStream_t s);
+// vals[j] = ys[j]^H x  (ys: host array of k device pointers)
+hipError_t blas_mdot(const cd* x, int k, const cd* const* ys, i64 n, cd* vals, hipStream_t s);
 }  // namespace cfp

@@ -31,11 +31,11 @@ __global__ void k_waxpy(cd* w, cd a, const cd* x, const cd* y, i64 n) {
   GRID_LOOP(i, n) w[i] = bcadd(bcmul(a, x[i]), y[i]);
 }
 __global__ void k_pmult(cd* w, const cd* x, const cd* y, i64 n) { GRID_LOOP(i, n) w[i] = bcmul(x[i], y[i]); }
-// y += sum_j a_j x_j  (the GMRES basis update, k vectors at once)
-__global__ void k_maxpy(cd* y, int k, const cd* a, const cd* const* xs, i64 n) {
+// y += sum_j a_j x_j  (the GMRES basis update, up to MV_MAX vectors per launch)
+__global__ void k_maxpy(cd* y, int k, MVCoef a, MVPtrs xs, i64 n) {
   GRID_LOOP(i, n) {
     cd acc = y[i];
-    for (int j = 0; j < k; ++j) acc = bcadd(acc, bcmul(a[j], xs[j][i]));
+    for (int j = 0; j < k; ++j) acc = bcadd(acc, bcmul(a.a[j], xs.p[j][i]));
     y[i] = acc;
   }
 }
@@ -83,26 +83,36 @@ __global__ void k_reduce(const cd* x, const cd* y, i64 n, int kind, double* part
   }
 }
 
-// several dots against one vector: out[j] = x_j^H ... PETSc VecMDot(x, k, y[], val): val_j = y_j^H x
-__global__ void k_mdot(const cd* x, int k, const cd* const* ys, i64 n, double* partial) {
-  extern __shared__ double sm[];  // 2 * k * (BLAS_THREADS/64)
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int j = 0; j < k; ++j) {
-    double a = 0.0, b = 0.0;
-    GRID_LOOP(i, n) {
-      const cd u = x[i], v = ys[j][i];
-      a += u.x * v.x + u.y * v.y;
-      b += u.y * v.x - u.x * v.y;
+// several dots against one vector, PETSc VecMDot(x, k, y[], val): val_j = y_j^H x.
+// One sweep of x per launch; up to MDOT_K accumulators per thread.
+#define MDOT_K 8
+__global__ void k_mdot(const cd* x, int k, MVPtrs ys, i64 n, double* partial) {
+  __shared__ double sm[2 * MDOT_K][BLAS_THREADS / 64];
+  double a[MDOT_K], b[MDOT_K];
+#pragma unroll
+  for (int j = 0; j < MDOT_K; ++j) { a[j] = 0.0; b[j] = 0.0; }
+  GRID_LOOP(i, n) {
+    const cd u = x[i];
+#pragma unroll
+    for (int j = 0; j < MDOT_K; ++j) {
+      if (j < k) {
+        const cd v = ys.p[j][i];
+        a[j] += u.x * v.x + u.y * v.y;
+        b[j] += u.y * v.x - u.x * v.y;
+      }
     }
-    a = wave_sum(a);
-    b = wave_sum(b);
-    if (lane == 0) { sm[(2 * j) * (BLAS_THREADS / 64) + w] = a; sm[(2 * j + 1) * (BLAS_THREADS / 64) + w] = b; }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < MDOT_K; ++j) {
+    const double ra = wave_sum(a[j]), rb = wave_sum(b[j]);
+    if (lane == 0) { sm[2 * j][w] = ra; sm[2 * j + 1][w] = rb; }
   }
   __syncthreads();
   for (int t = threadIdx.x; t < 2 * k; t += blockDim.x) {
     double s = 0.0;
-    for (int q = 0; q < BLAS_THREADS / 64; ++q) s += sm[t * (BLAS_THREADS / 64) + q];
-    partial[(size_t)blockIdx.x * 2 * k + t] = s;
+    for (int q = 0; q < BLAS_THREADS / 64; ++q) s += sm[t][q];
+    partial[(size_t)blockIdx.x * 2 * MDOT_K + t] = s;
   }
 }
 
@@ -143,8 +153,14 @@ hipError_t blas_pmult(cd* w, const cd* x, const cd* y, i64 n, hipStream_t s) {
   if (n > 0) hipLaunchKernelGGL(k_pmult, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, w, x, y, n);
   return hipGetLastError();
 }
-hipError_t blas_maxpy(cd* y, int k, const cd* a_dev, const cd* const* xs_dev, i64 n, hipStream_t s) {
-  if (n > 0 && k > 0) hipLaunchKernelGGL(k_maxpy, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, y, k, a_dev, xs_dev, n);
+hipError_t blas_maxpy(cd* y, int k, const cd* a, const cd* const* xs, i64 n, hipStream_t s) {
+  for (int j0 = 0; j0 < k; j0 += MV_MAX) {
+    const int kk = k - j0 < MV_MAX ? k - j0 : MV_MAX;
+    MVCoef c;
+    MVPtrs p;
+    for (int j = 0; j < kk; ++j) { c.a[j] = a[j0 + j]; p.p[j] = xs[j0 + j]; }
+    if (n > 0) hipLaunchKernelGGL(k_maxpy, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, y, kk, c, p, n);
+  }
   return hipGetLastError();
 }
 hipError_t blas_csr_spmv(i64 m, const i64* rowptr, const i64* col, const cd* val, const cd* x, cd* y, hipStream_t s) {
@@ -193,35 +209,35 @@ hipError_t blas_norm(const cd* x, i64 n, int type, double* val, hipStream_t s) {
   return e;
 }
 
-hipError_t blas_mdot(const cd* x, int k, const cd* const* ys_dev, i64 n, cd* vals, hipStream_t s) {
+hipError_t blas_mdot(const cd* x, int k, const cd* const* ys, i64 n, cd* vals, hipStream_t s) {
   static thread_local double* partial = nullptr;
   static thread_local double* hpart = nullptr;
-  static thread_local int cap = 0;
-  const int NB = 256;
-  if (cap < k) {
-    if (partial) hipFree(partial);
-    if (hpart) hipHostFree(hpart);
-    hipError_t e = hipMalloc(&partial, sizeof(double) * 2 * k * NB);
+  const int NB = 512;
+  if (!partial) {
+    hipError_t e = hipMalloc(&partial, sizeof(double) * 2 * MDOT_K * NB);
     if (e != hipSuccess) return e;
-    e = hipHostMalloc(&hpart, sizeof(double) * 2 * k * NB);
+    e = hipHostMalloc(&hpart, sizeof(double) * 2 * MDOT_K * NB);
     if (e != hipSuccess) return e;
-    cap = k;
   }
-  unsigned nb = nblocks(n);
-  if (nb > (unsigned)NB) nb = NB;
-  const size_t sm = sizeof(double) * 2 * k * (BLAS_THREADS / 64);
-  hipLaunchKernelGGL(k_mdot, dim3(nb), dim3(BLAS_THREADS), sm, s, x, k, ys_dev, n, partial);
-  hipError_t e = hipMemcpyAsync(hpart, partial, sizeof(double) * 2 * k * nb, hipMemcpyDeviceToHost, s);
-  if (e != hipSuccess) return e;
-  e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return e;
-  for (int j = 0; j < k; ++j) {
-    double a = 0.0, b = 0.0;
-    for (unsigned q = 0; q < nb; ++q) {
-      a += hpart[(size_t)q * 2 * k + 2 * j];
-      b += hpart[(size_t)q * 2 * k + 2 * j + 1];
+  for (int j0 = 0; j0 < k; j0 += MDOT_K) {
+    const int kk = k - j0 < MDOT_K ? k - j0 : MDOT_K;
+    MVPtrs p;
+    for (int j = 0; j < kk; ++j) p.p[j] = ys[j0 + j];
+    unsigned nb = nblocks(n);
+    if (nb > (unsigned)NB) nb = NB;
+    hipLaunchKernelGGL(k_mdot, dim3(nb), dim3(BLAS_THREADS), 0, s, x, kk, p, n, partial);
+    hipError_t e = hipMemcpyAsync(hpart, partial, sizeof(double) * 2 * MDOT_K * nb, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return e;
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    for (int j = 0; j < kk; ++j) {
+      double ra = 0.0, rb = 0.0;
+      for (unsigned q = 0; q < nb; ++q) {
+        ra += hpart[(size_t)q * 2 * MDOT_K + 2 * j];
+        rb += hpart[(size_t)q * 2 * MDOT_K + 2 * j + 1];
+      }
+      vals[j0 + j] = make_cd(ra, rb);
     }
-    vals[j] = make_cd(a, b);
   }
   return hipSuccess;
 }

@@ -74,14 +74,17 @@ struct Step {
   PassDesc pass;  // kernel steps
   int src, dst;   // buffer ids
   int fused;      // 1 if this is the symbol pass
+  int axis;       // 0, 1, 2 (kernel steps)
 };
 
 std::vector<Step> slab_steps(const SlabLayout& L) {
   std::vector<Step> st;
   const i64 nx = L.nx, ny = L.ny, nz = L.nz, nzl = L.nzl, nyl = L.nyl;
-  auto kern = [&](int n, i64 ncols, i64 inner_n, Side in, Side out, int mode, int src, int dst, int fused) {
+  auto kern = [&](int axis, int n, i64 ncols, i64 inner_n, Side in, Side out, int mode, int src, int dst,
+                  int fused) {
     Step s;
     s.exchange = false;
+    s.axis = axis;
     s.pass.n = n; s.pass.ncols = ncols; s.pass.inner_n = inner_n;
     s.pass.in = in; s.pass.out = out; s.pass.mode = mode; s.pass.scale = 1.0;
     s.pass.colsym = s.pass.axsym = s.pass.diag = nullptr;
@@ -99,13 +102,13 @@ std::vector<Step> slab_steps(const SlabLayout& L) {
   const Side ysplit = side(1, nyl * nx, nx, nyl, L.chunk);  // y columns in per-peer chunks
   const Side zs = side(1, 0, nx * nyl, nz, 0);              // z columns of [nz][nyl][nx]
   int cur = B_IN;
-  if (nx > 1) { kern((int)nx, nzl * ny, 1, xs, xs, PASS_FWD, B_IN, B_X, 0); cur = B_X; }
-  kern((int)ny, nx * nzl, nx, ynat, ysplit, PASS_FWD, cur, B_W, 0);
+  if (nx > 1) { kern(0, (int)nx, nzl * ny, 1, xs, xs, PASS_FWD, B_IN, B_X, 0); cur = B_X; }
+  kern(1, (int)ny, nx * nzl, nx, ynat, ysplit, PASS_FWD, cur, B_W, 0);
   exch(B_W, B_X);
-  kern((int)nz, nx * nyl, nx * nyl, zs, zs, PASS_FUSED_SEP, B_X, B_X, 1);
+  kern(2, (int)nz, nx * nyl, nx * nyl, zs, zs, PASS_FUSED_SEP, B_X, B_X, 1);
   exch(B_X, B_W);
-  kern((int)ny, nx * nzl, nx, ysplit, ynat, PASS_INV, B_W, B_X, 0);
-  if (nx > 1) kern((int)nx, nzl * ny, 1, xs, xs, PASS_INV, B_X, B_X, 0);
+  kern(1, (int)ny, nx * nzl, nx, ysplit, ynat, PASS_INV, B_W, B_X, 0);
+  if (nx > 1) kern(0, (int)nx, nzl * ny, 1, xs, xs, PASS_INV, B_X, B_X, 0);
   // 1/N on the last launch
   for (int i = (int)st.size() - 1; i >= 0; --i)
     if (!st[i].exchange) { st[i].pass.scale = 1.0 / (double)(nx * ny * nz); break; }
@@ -120,6 +123,7 @@ struct SlabRank {
   cd* colsym = nullptr;
   cd* axsym = nullptr;
   cd* work = nullptr;
+  bool own_work = true;
   bool sym = false;
   std::vector<Step> steps;
 
@@ -143,7 +147,7 @@ struct SlabRank {
     tw.clear();
     if (colsym) hipFree(colsym);
     if (axsym) hipFree(axsym);
-    if (work) hipFree(work);
+    if (work && own_work) hipFree(work);
     colsym = axsym = work = nullptr;
   }
   // colsym over the z-pass columns g = ix + nx*iyl (global ky = y0 + iyl); axsym over kz
@@ -234,6 +238,57 @@ extern "C" int cfp_dist_plan_create(cfp_dist_plan_t* plan, int64_t nx, int64_t n
   return CFP_SUCCESS;
 }
 
+// Plan without a communicator: the caller performs the two exchanges itself between the
+// three kernel segments (cfp_dist_plan_run_segment), e.g. with torch.distributed's RCCL.
+extern "C" int cfp_dist_plan_create_external(cfp_dist_plan_t* plan, int64_t nx, int64_t ny, int64_t nz, int P, int r,
+                                             int device) {
+  if (!plan) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  *plan = nullptr;
+  SlabLayout L;
+  int rc = make_layout(nx, ny, nz, P, r, &L);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(device));
+  std::unique_ptr<cfp_dist_plan_s> p(new cfp_dist_plan_s);
+  rc = p->R.init(L, device);
+  if (rc) { p->R.release(); return rc; }
+  *plan = p.release();
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_dist_plan_work_buffer(cfp_dist_plan_t p, double** work) {
+  if (!p || !work) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  *work = (double*)p->R.work;
+  return CFP_SUCCESS;
+}
+
+// use a caller-owned work buffer (local_size complex values) instead of the plan's own
+extern "C" int cfp_dist_plan_set_work_buffer(cfp_dist_plan_t p, double* work) {
+  if (!p || !work) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  HIPCHK(hipSetDevice(p->R.device));
+  if (p->R.work && p->R.own_work) hipFree(p->R.work);
+  p->R.work = (cd*)work;
+  p->R.own_work = false;
+  return CFP_SUCCESS;
+}
+
+// segment 0: kernels before the first exchange (which sends work -> receives into x);
+// segment 1: between the exchanges (the exchange after it sends x -> receives into work);
+// segment 2: kernels after the second exchange.
+extern "C" int cfp_dist_plan_run_segment(cfp_dist_plan_t p, int seg, const double* b, double* x, void* stream) {
+  if (!p || !b || !x) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  if (seg < 0 || seg > 2) return set_error(CFP_ERR_ARG_OUTOFRANGE, "segment must be 0, 1 or 2");
+  if (!p->R.sym) return set_error(CFP_ERR_ARG_WRONGSTATE, "no symbol set on the slab plan");
+  HIPCHK(hipSetDevice(p->R.device));
+  int cur = 0;
+  for (const Step& st : p->R.steps) {
+    if (st.exchange) { ++cur; continue; }
+    if (cur != seg) continue;
+    int rc = p->R.launch(st, (const cd*)b, (cd*)x, (hipStream_t)stream);
+    if (rc) return rc;
+  }
+  return CFP_SUCCESS;
+}
+
 extern "C" int cfp_dist_plan_destroy(cfp_dist_plan_t p) {
   if (!p) return CFP_SUCCESS;
   hipSetDevice(p->R.device);
@@ -261,9 +316,22 @@ extern "C" int cfp_dist_plan_num_phases(cfp_dist_plan_t p, int* n) {
   return CFP_SUCCESS;
 }
 
+extern "C" int cfp_dist_plan_phase_info(cfp_dist_plan_t p, int i, int* is_exchange, int* axis, int* n, int* mode) {
+  if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
+  if (i < 0 || i >= (int)p->R.steps.size()) return set_error(CFP_ERR_ARG_OUTOFRANGE, "phase index");
+  const Step& s = p->R.steps[i];
+  if (is_exchange) *is_exchange = s.exchange ? 1 : 0;
+  if (axis) *axis = s.exchange ? -1 : s.axis;
+  if (n) *n = s.exchange ? 0 : s.pass.n;
+  if (mode) *mode = s.exchange ? -1 : s.pass.mode;
+  return CFP_SUCCESS;
+}
+
 static int rccl_exchange(cfp_dist_plan_s* p, const cd* src, cd* dst, hipStream_t s) {
   const SlabLayout& L = p->R.L;
   const size_t cnt = (size_t)L.chunk * 2;  // doubles per peer message
+  if (L.P > 1 && !p->comm)
+    return set_error(CFP_ERR_ARG_WRONGSTATE, "plan made with cfp_dist_plan_create_external has no communicator");
   HIPCHK(hipMemcpyAsync(dst + L.r * L.chunk, src + L.r * L.chunk, sizeof(cd) * (size_t)L.chunk,
                         hipMemcpyDeviceToDevice, s));
   if (L.P == 1) return CFP_SUCCESS;

@@ -1,0 +1,292 @@
+// ksp_gmres.cpp -- KSPGMRES of the PETSc stand-in: the Krylov solver the reference's GMRES
+// drivers call (tests/TransportEquation_SphericalExplosion_impl_mpi.cxx:120-136,
+// KSPSetType(KSPGMRES), KSPSetTolerances(precision, precision, PETSC_DEFAULT, 1000)),
+// so the PCSHELL circulant preconditioner can run inside it.
+//
+// It restates PETSc's GMRES with PETSc's defaults: restart 30, left preconditioning,
+// classical Gram-Schmidt without refinement (one VecMDot + one VecMAXPY per iteration),
+// the preconditioned residual norm estimated from the rotated Hessenberg right-hand side,
+// KSPConvergedDefault (converged when ||r|| <= max(rtol ||r_0||, abstol), diverged when
+// ||r|| > dtol ||r_0||), the complex Givens rotations of KSPGMRESUpdateHessenberg, and the
+// true residual recomputed at every restart.  Every vector operation is a device kernel
+// (cfp_blas.hip); only the (restart+1) x restart Hessenberg lives on the host.
+//
+// Written against the PETSc API only; compiled out with -DCFP_WITH_PETSC (real PETSc has
+// its own KSP).
+#ifndef CFP_WITH_PETSC
+#include <sys/time.h>
+
+#include <cmath>
+#include <complex>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/petsc_mini.h"
+
+namespace {
+const int kKSPMagic = 0x4b535031;
+typedef std::complex<double> C;
+
+double now() {
+  struct timeval tv;
+  gettimeofday(&tv, nullptr);
+  return (double)tv.tv_sec + 1e-6 * (double)tv.tv_usec;
+}
+}  // namespace
+
+struct _p_KSP {
+  int magic = kKSPMagic;
+  std::string type = KSPGMRES;
+  PetscReal rtol = 1e-5, abstol = 1e-50, dtol = 1e5;
+  PetscInt maxits = 10000;
+  PetscInt restart = 30;
+  PCSide side = PC_LEFT;
+  bool guess_nonzero = false;
+  Mat A = nullptr, P = nullptr;
+  PC pc = nullptr;
+  KSPConvergedReason reason = KSP_CONVERGED_ITERATING;
+  PetscInt its = 0;
+  PetscReal rnorm = 0.0;
+  PetscInt pc_calls = 0;
+  double pc_seconds = 0.0;
+  // work space (sized for the current problem)
+  PetscInt n = -1, nvec = 0;
+  Vec* V = nullptr;  // restart + 1 basis vectors
+  Vec t = nullptr, t2 = nullptr, rhs = nullptr;
+};
+
+static PetscErrorCode kcheck(KSP k, const char* f) {
+  if (!k || k->magic != kKSPMagic) return PetscErrorSet(PETSC_ERR_ARG_NULL, f, "invalid KSP");
+  return PETSC_SUCCESS;
+}
+#define KCHK(k) PetscCall(kcheck((k), __func__))
+
+static void free_work(KSP k) {
+  if (k->V) VecDestroyVecs(k->nvec, &k->V);
+  VecDestroy(&k->t);
+  VecDestroy(&k->t2);
+  VecDestroy(&k->rhs);
+  k->n = -1;
+  k->nvec = 0;
+}
+
+extern "C" PetscErrorCode KSPCreate(MPI_Comm comm, KSP* ksp) {
+  if (!ksp) return PetscErrorSet(PETSC_ERR_ARG_NULL, __func__, "NULL output");
+  KSP k = new _p_KSP;
+  PetscErrorCode rc = PCCreate(comm, &k->pc);
+  if (rc) { delete k; return rc; }
+  *ksp = k;
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode KSPSetType(KSP k, KSPType type) {
+  KCHK(k);
+  if (!type || (std::strcmp(type, KSPGMRES) && std::strcmp(type, KSPPREONLY)))
+    return PetscErrorSet(PETSC_ERR_SUP, __func__, "stand-in KSP types: gmres, preonly");
+  k->type = type;
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode KSPSetTolerances(KSP k, PetscReal rtol, PetscReal abstol, PetscReal dtol, PetscInt maxits) {
+  KCHK(k);
+  if (rtol != PETSC_DEFAULT) k->rtol = rtol;
+  if (abstol != PETSC_DEFAULT) k->abstol = abstol;
+  if (dtol != PETSC_DEFAULT) k->dtol = dtol;
+  if (maxits != PETSC_DEFAULT) k->maxits = maxits;
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode KSPGMRESSetRestart(KSP k, PetscInt restart) {
+  KCHK(k);
+  if (restart < 1) return PetscErrorSet(PETSC_ERR_ARG_OUTOFRANGE, __func__, "restart must be >= 1");
+  if (restart != k->restart) free_work(k);
+  k->restart = restart;
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode KSPSetPCSide(KSP k, PCSide side) { KCHK(k); k->side = side; return PETSC_SUCCESS; }
+extern "C" PetscErrorCode KSPSetInitialGuessNonzero(KSP k, PetscBool f) {
+  KCHK(k);
+  k->guess_nonzero = f == PETSC_TRUE;
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode KSPGetPC(KSP k, PC* pc) { KCHK(k); *pc = k->pc; return PETSC_SUCCESS; }
+extern "C" PetscErrorCode KSPSetOperators(KSP k, Mat A, Mat P) { KCHK(k); k->A = A; k->P = P; return PETSC_SUCCESS; }
+extern "C" PetscErrorCode KSPSetUp(KSP k) {
+  KCHK(k);
+  return PCSetUp(k->pc);
+}
+extern "C" PetscErrorCode KSPGetConvergedReason(KSP k, KSPConvergedReason* r) { KCHK(k); *r = k->reason; return PETSC_SUCCESS; }
+extern "C" PetscErrorCode KSPGetIterationNumber(KSP k, PetscInt* its) { KCHK(k); *its = k->its; return PETSC_SUCCESS; }
+extern "C" PetscErrorCode KSPGetResidualNorm(KSP k, PetscReal* r) { KCHK(k); *r = k->rnorm; return PETSC_SUCCESS; }
+extern "C" PetscErrorCode KSPMiniGetPCApplyStats(KSP k, PetscInt* calls, PetscLogDouble* seconds) {
+  KCHK(k);
+  if (calls) *calls = k->pc_calls;
+  if (seconds) *seconds = k->pc_seconds;
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode KSPDestroy(KSP* pk) {
+  if (!pk || !*pk) return PETSC_SUCCESS;
+  KSP k = *pk;
+  KCHK(k);
+  free_work(k);
+  PetscErrorCode rc = PCDestroy(&k->pc);
+  k->magic = 0;
+  delete k;
+  *pk = nullptr;
+  return rc;
+}
+
+static PetscErrorCode pc_apply(KSP k, Vec x, Vec y) {
+  const double t0 = now();
+  PetscCall(PCApply(k->pc, x, y));
+  k->pc_seconds += now() - t0;
+  k->pc_calls += 1;
+  return PETSC_SUCCESS;
+}
+
+// KSPConvergedDefault
+static void converged(KSP k, PetscReal rnorm0) {
+  const PetscReal ttol = std::fmax(k->rtol * rnorm0, k->abstol);
+  if (std::isnan(rnorm0) || std::isnan(k->rnorm)) k->reason = KSP_DIVERGED_BREAKDOWN;
+  else if (k->rnorm <= ttol) k->reason = k->rnorm < k->abstol ? KSP_CONVERGED_ATOL : KSP_CONVERGED_RTOL;
+  else if (k->its > 0 && k->rnorm >= k->dtol * rnorm0) k->reason = KSP_DIVERGED_DTOL;
+}
+
+// preconditioned residual into z (left: z = B (b - A x); right: z = b - A x)
+static PetscErrorCode residual(KSP k, Vec b, Vec x, bool x_zero, Vec z) {
+  Vec r = k->side == PC_LEFT ? k->t : z;
+  if (x_zero) {
+    PetscCall(VecCopy(b, r));
+  } else {
+    PetscCall(MatMult(k->A, x, k->t2));
+    PetscCall(VecWAXPY(r, -1.0, k->t2, b));
+  }
+  if (k->side == PC_LEFT) PetscCall(pc_apply(k, r, z));
+  return PETSC_SUCCESS;
+}
+
+extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
+  KCHK(k);
+  if (!k->A) return PetscErrorSet(PETSC_ERR_ARG_WRONGSTATE, __func__, "KSPSetOperators has not been called");
+  PetscCall(PCSetUp(k->pc));
+  PetscInt n;
+  PetscCall(VecGetLocalSize(b, &n));
+  const PetscInt m = k->restart;
+  if (n != k->n || k->nvec != m + 1) {
+    free_work(k);
+    PetscCall(VecDuplicateVecs(b, m + 1, &k->V));
+    k->nvec = m + 1;
+    PetscCall(VecDuplicate(b, &k->t));
+    PetscCall(VecDuplicate(b, &k->t2));
+    PetscCall(VecDuplicate(b, &k->rhs));
+    k->n = n;
+  }
+  k->its = 0;
+  k->reason = KSP_CONVERGED_ITERATING;
+  k->pc_calls = 0;
+  k->pc_seconds = 0.0;
+  // KSPSolve(ksp, Un, Un): PETSc copies the right-hand side when b == x
+  if (b == x) {
+    PetscCall(VecCopy(b, k->rhs));
+    b = k->rhs;
+  }
+  if (k->type == KSPPREONLY) {
+    PetscCall(pc_apply(k, b, x));
+    k->its = 1;
+    k->reason = KSP_CONVERGED_ITS;
+    return PETSC_SUCCESS;
+  }
+  bool x_zero = !k->guess_nonzero;
+  if (x_zero) PetscCall(VecSet(x, 0.0));
+
+  std::vector<C> H((size_t)(m + 1) * m), cc((size_t)m), ss((size_t)m), rs((size_t)m + 1), y((size_t)m);
+  auto h = [&](PetscInt i, PetscInt j) -> C& { return H[(size_t)j * (m + 1) + i]; };
+  PetscReal rnorm0 = -1.0;
+  Vec* V = k->V;
+
+  while (true) {
+    PetscCall(residual(k, b, x, x_zero, V[0]));
+    x_zero = false;
+    PetscReal beta;
+    PetscCall(VecNorm(V[0], NORM_2, &beta));
+    k->rnorm = beta;
+    if (rnorm0 < 0) rnorm0 = beta;
+    converged(k, rnorm0);
+    if (k->reason != KSP_CONVERGED_ITERATING) break;
+    if (k->its >= k->maxits) { k->reason = KSP_DIVERGED_ITS; break; }
+    PetscCall(VecScale(V[0], 1.0 / beta));
+    std::fill(rs.begin(), rs.end(), C(0.0));
+    rs[0] = beta;
+    PetscInt j = 0;
+    bool happy = false;
+    for (; j < m && k->reason == KSP_CONVERGED_ITERATING && k->its < k->maxits; ++j) {
+      // w = B A v_j (left) or A B v_j (right), written into V[j+1]
+      if (k->side == PC_LEFT) {
+        PetscCall(MatMult(k->A, V[j], k->t));
+        PetscCall(pc_apply(k, k->t, V[j + 1]));
+      } else {
+        PetscCall(pc_apply(k, V[j], k->t));
+        PetscCall(MatMult(k->A, k->t, V[j + 1]));
+      }
+      // classical Gram-Schmidt: h_ij = v_i^H w, w -= sum h_ij v_i
+      std::vector<PetscScalar> hv((size_t)j + 1);
+      PetscCall(VecMDot(V[j + 1], j + 1, V, hv.data()));
+      std::vector<PetscScalar> neg((size_t)j + 1);
+      for (PetscInt i = 0; i <= j; ++i) {
+        h(i, j) = hv[(size_t)i];
+        neg[(size_t)i] = -hv[(size_t)i];
+      }
+      PetscCall(VecMAXPY(V[j + 1], j + 1, neg.data(), V));
+      PetscReal hn;
+      PetscCall(VecNorm(V[j + 1], NORM_2, &hn));
+      h(j + 1, j) = hn;
+      // happy breakdown test of KSPGMRESCycle: hn < min(hn / |rs_j|, haptol = 1e-30)
+      const double hapbnd = std::fmin(hn / std::abs(rs[(size_t)j]), 1e-30);
+      happy = hn < hapbnd;
+      if (!happy) PetscCall(VecScale(V[j + 1], 1.0 / hn));
+      // KSPGMRESUpdateHessenberg: previous rotations, then a new one
+      for (PetscInt i = 0; i < j; ++i) {
+        const C tt = h(i, j);
+        h(i, j) = std::conj(cc[(size_t)i]) * tt + ss[(size_t)i] * h(i + 1, j);
+        h(i + 1, j) = cc[(size_t)i] * h(i + 1, j) - ss[(size_t)i] * tt;
+      }
+      if (!happy) {
+        const double tt = std::sqrt(std::norm(h(j, j)) + std::norm(h(j + 1, j)));
+        if (tt == 0.0) { k->reason = KSP_DIVERGED_BREAKDOWN; break; }
+        cc[(size_t)j] = h(j, j) / tt;
+        ss[(size_t)j] = h(j + 1, j) / tt;
+        rs[(size_t)j + 1] = -(ss[(size_t)j] * rs[(size_t)j]);
+        rs[(size_t)j] = std::conj(cc[(size_t)j]) * rs[(size_t)j];
+        h(j, j) = std::conj(cc[(size_t)j]) * h(j, j) + ss[(size_t)j] * h(j + 1, j);
+        k->rnorm = std::abs(rs[(size_t)j + 1]);
+      } else {  // h(j+1,j) = 0: no new rotation, the residual estimate is exactly zero
+        rs[(size_t)j + 1] = 0.0;
+        k->rnorm = 0.0;
+      }
+      k->its += 1;
+      converged(k, rnorm0);
+      if (happy && k->reason == KSP_CONVERGED_ITERATING) k->reason = KSP_DIVERGED_BREAKDOWN;
+      if (k->reason == KSP_CONVERGED_ITERATING && k->its >= k->maxits) k->reason = KSP_DIVERGED_ITS;
+      if (k->reason != KSP_CONVERGED_ITERATING || happy) { ++j; break; }
+    }
+    // back substitution H(0:j, 0:j) y = rs(0:j), then x += V y (left) / x += B V y (right)
+    const PetscInt kk = j;
+    for (PetscInt i = kk - 1; i >= 0; --i) {
+      C s = rs[(size_t)i];
+      for (PetscInt q = i + 1; q < kk; ++q) s -= h(i, q) * y[(size_t)q];
+      y[(size_t)i] = s / h(i, i);
+    }
+    if (kk > 0) {
+      std::vector<PetscScalar> yy(y.begin(), y.begin() + kk);
+      if (k->side == PC_LEFT) {
+        PetscCall(VecMAXPY(x, kk, yy.data(), V));
+      } else {
+        PetscCall(VecSet(k->t2, 0.0));
+        PetscCall(VecMAXPY(k->t2, kk, yy.data(), V));
+        PetscCall(pc_apply(k, k->t2, k->t));
+        PetscCall(VecAXPY(x, 1.0, k->t));
+      }
+    }
+    if (k->reason != KSP_CONVERGED_ITERATING) break;
+  }
+  return PETSC_SUCCESS;
+}
+#endif  // CFP_WITH_PETSC

@@ -502,6 +502,78 @@ extern "C" PetscErrorCode VecNorm(Vec x, NormType t, PetscReal* val) {
   return PETSC_SUCCESS;
 }
 
+extern "C" PetscErrorCode VecMDot(Vec x, PetscInt nv, const Vec y[], PetscScalar val[]) {
+  VCHK(x);
+  if (nv <= 0) return PETSC_SUCCESS;
+  bool dev = x->hip;
+  for (PetscInt j = 0; j < nv; ++j) {
+    VCHK(y[j]);
+    PetscCall(same_size(x, y[j]));
+    dev = dev && y[j]->hip;
+  }
+  if (dev) {
+    const cd* xd;
+    PetscCall(dev_read(x, &xd));
+    std::vector<const cd*> ys((size_t)nv);
+    for (PetscInt j = 0; j < nv; ++j) PetscCall(dev_read(y[j], &ys[(size_t)j]));
+    std::vector<cd> r((size_t)nv);
+    HIPK(cfp::blas_mdot(xd, (int)nv, ys.data(), x->n, r.data(), g_stream));
+    for (PetscInt j = 0; j < nv; ++j) val[j] = PetscScalar(r[(size_t)j].x, r[(size_t)j].y);
+    return PETSC_SUCCESS;
+  }
+  for (PetscInt j = 0; j < nv; ++j) PetscCall(VecDot(x, y[j], &val[j]));
+  return PETSC_SUCCESS;
+}
+
+extern "C" PetscErrorCode VecMAXPY(Vec y, PetscInt nv, const PetscScalar alpha[], Vec x[]) {
+  VCHK(y);
+  if (nv <= 0) return PETSC_SUCCESS;
+  bool dev = y->hip;
+  for (PetscInt j = 0; j < nv; ++j) {
+    VCHK(x[j]);
+    PetscCall(same_size(y, x[j]));
+    dev = dev && x[j]->hip;
+  }
+  if (dev) {
+    std::vector<const cd*> xs((size_t)nv);
+    std::vector<cd> a((size_t)nv);
+    for (PetscInt j = 0; j < nv; ++j) {
+      PetscCall(dev_read(x[j], &xs[(size_t)j]));
+      a[(size_t)j] = tocd(alpha[j]);
+    }
+    cd* yd;
+    PetscCall(dev_rw(y, &yd));
+    HIPK(cfp::blas_maxpy(yd, (int)nv, a.data(), xs.data(), y->n, g_stream));
+    return PETSC_SUCCESS;
+  }
+  for (PetscInt j = 0; j < nv; ++j) PetscCall(VecAXPY(y, alpha[j], x[j]));
+  return PETSC_SUCCESS;
+}
+
+extern "C" PetscErrorCode VecDuplicateVecs(Vec v, PetscInt m, Vec* V[]) {
+  VCHK(v);
+  if (!V) return ERR(PETSC_ERR_ARG_NULL, "NULL output");
+  Vec* arr = (Vec*)calloc((size_t)(m > 0 ? m : 1), sizeof(Vec));
+  for (PetscInt j = 0; j < m; ++j) {
+    PetscErrorCode rc = VecDuplicate(v, &arr[j]);
+    if (rc) {
+      for (PetscInt q = 0; q < j; ++q) VecDestroy(&arr[q]);
+      free(arr);
+      return rc;
+    }
+  }
+  *V = arr;
+  return PETSC_SUCCESS;
+}
+
+extern "C" PetscErrorCode VecDestroyVecs(PetscInt m, Vec* V[]) {
+  if (!V || !*V) return PETSC_SUCCESS;
+  for (PetscInt j = 0; j < m; ++j) PetscCall(VecDestroy(&(*V)[j]));
+  free(*V);
+  *V = nullptr;
+  return PETSC_SUCCESS;
+}
+
 // ------------------------------------------------------------------ Mat
 static const int kMatMagic = 0x4d617431;
 typedef PetscErrorCode (*MatMultFn)(Mat, Vec, Vec);
@@ -563,18 +635,27 @@ extern "C" PetscErrorCode MatCreateSeqAIJWithArrays(MPI_Comm, PetscInt m, PetscI
   M->h_col.assign(j, j + nnz);
   M->h_val.resize((size_t)nnz);
   for (i64 k = 0; k < nnz; ++k) M->h_val[k] = tocd(a[k]);
-  hipError_t e = hipMalloc(&M->rowptr, sizeof(i64) * (size_t)(m + 1));
-  if (e == hipSuccess) e = hipMalloc(&M->col, sizeof(i64) * (size_t)(nnz > 0 ? nnz : 1));
-  if (e == hipSuccess) e = hipMalloc(&M->val, sizeof(cd) * (size_t)(nnz > 0 ? nnz : 1));
-  if (e == hipSuccess) e = hipMemcpy(M->rowptr, i, sizeof(i64) * (size_t)(m + 1), hipMemcpyHostToDevice);
-  if (e == hipSuccess && nnz) e = hipMemcpy(M->col, j, sizeof(i64) * (size_t)nnz, hipMemcpyHostToDevice);
-  if (e == hipSuccess && nnz) e = hipMemcpy(M->val, M->h_val.data(), sizeof(cd) * (size_t)nnz, hipMemcpyHostToDevice);
+  *A = M;  // the device copy is made by the first MatMult on HIP vectors
+  return PETSC_SUCCESS;
+}
+// mirror the host CSR into device memory (once; MatShift refreshes the values)
+static PetscErrorCode aij_upload(Mat M) {
+  if (M->rowptr) return PETSC_SUCCESS;
+  const size_t nnz = M->h_col.size();
+  hipError_t e = hipMalloc(&M->rowptr, sizeof(i64) * (size_t)(M->m + 1));
+  if (e == hipSuccess) e = hipMalloc(&M->col, sizeof(i64) * (nnz > 0 ? nnz : 1));
+  if (e == hipSuccess) e = hipMalloc(&M->val, sizeof(cd) * (nnz > 0 ? nnz : 1));
+  if (e == hipSuccess) e = hipMemcpy(M->rowptr, M->h_rowptr.data(), sizeof(i64) * (size_t)(M->m + 1), hipMemcpyHostToDevice);
+  if (e == hipSuccess && nnz) e = hipMemcpy(M->col, M->h_col.data(), sizeof(i64) * nnz, hipMemcpyHostToDevice);
+  if (e == hipSuccess && nnz) e = hipMemcpy(M->val, M->h_val.data(), sizeof(cd) * nnz, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
-    Mat tmp = M;
-    MatDestroy(&tmp);
+    if (M->rowptr) hipFree(M->rowptr);
+    if (M->col) hipFree(M->col);
+    if (M->val) hipFree(M->val);
+    M->rowptr = M->col = nullptr;
+    M->val = nullptr;
     return ERR(PETSC_ERR_MEM, hipGetErrorString(e));
   }
-  *A = M;
   return PETSC_SUCCESS;
 }
 extern "C" PetscErrorCode MatGetType(Mat A, MatType* t) {
@@ -592,6 +673,7 @@ static PetscErrorCode aij_mult(Mat A, Vec x, Vec y) {
   if (x->n != A->n || y->n != A->m) return ERR(PETSC_ERR_ARG_SIZ, "MatMult sizes");
   if (x == y) return ERR(PETSC_ERR_ARG_IDN, "x and y must be different vectors");
   if (x->hip && y->hip) {
+    PetscCall(aij_upload(A));
     const cd* xd;
     PetscCall(dev_read(x, &xd));
     cd* yd;
@@ -635,7 +717,8 @@ extern "C" PetscErrorCode MatShift(Mat A, PetscScalar a) {
       if (A->h_col[p] == r) { A->h_val[p] = D(C(A->h_val[p]) + a); found = true; }
     if (!found) return ERR(PETSC_ERR_ARG_WRONGSTATE, "MatShift needs an allocated diagonal");
   }
-  HCHK(hipMemcpy(A->val, A->h_val.data(), sizeof(cd) * A->h_val.size(), hipMemcpyHostToDevice));
+  if (A->val && !A->h_val.empty())
+    HCHK(hipMemcpy(A->val, A->h_val.data(), sizeof(cd) * A->h_val.size(), hipMemcpyHostToDevice));
   return PETSC_SUCCESS;
 }
 extern "C" PetscErrorCode MatDestroy(Mat* pA) {

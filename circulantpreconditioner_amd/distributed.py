@@ -31,26 +31,43 @@ def slab_layout(dims: Sequence[int], nranks: int, rank: int) -> dict:
 
 
 class SlabPlan:
-    """This rank's part of a slab-distributed plan (RCCL)."""
+    """This rank's part of a slab-distributed plan.
 
-    def __init__(self, dims: Sequence[int], rank: int, world: int, device: int | None = None, group=None):
+    exchange="rccl": the library's own RCCL communicator does both all-to-alls inside
+    cfp_dist_plan_apply.  exchange="torch": the library runs the three kernel segments and
+    the two all-to-alls go through torch.distributed.all_to_all_single on `group` (RCCL
+    under torch's "nccl" backend).  Both are one stream-ordered apply.
+    """
+
+    def __init__(self, dims: Sequence[int], rank: int, world: int, device: int | None = None, group=None,
+                 exchange: str = "rccl"):
         import torch.distributed as dist
         nx, ny, nz = (int(d) for d in dims)
         self.dims = (nx, ny, nz)
         self.rank, self.world = int(rank), int(world)
         self.device = torch.cuda.current_device() if device is None else int(device)
-        nbytes = lib().cfp_dist_unique_id_bytes()
-        uid = ctypes.create_string_buffer(nbytes)
-        if self.rank == 0:
-            check(lib().cfp_dist_get_unique_id(uid))
-        on_dev = dist.get_backend(group) == "nccl"
-        t = torch.frombuffer(bytearray(uid.raw), dtype=torch.uint8)
-        t = t.to(f"cuda:{self.device}") if on_dev else t.clone()
-        dist.broadcast(t, src=0, group=group)
-        uid = ctypes.create_string_buffer(bytes(t.cpu().numpy().tobytes()), nbytes)
+        self.group = group
+        self.exchange = exchange
         self.layout = slab_layout(self.dims, self.world, self.rank)
         h = ctypes.c_void_p()
-        check(lib().cfp_dist_plan_create(ctypes.byref(h), nx, ny, nz, self.world, self.rank, uid, self.device))
+        if exchange == "rccl":
+            nbytes = lib().cfp_dist_unique_id_bytes()
+            uid = ctypes.create_string_buffer(nbytes)
+            if self.rank == 0:
+                check(lib().cfp_dist_get_unique_id(uid))
+            on_dev = dist.get_backend(group) == "nccl"
+            t = torch.frombuffer(bytearray(uid.raw), dtype=torch.uint8)
+            t = t.to(f"cuda:{self.device}") if on_dev else t.clone()
+            dist.broadcast(t, src=0, group=group)
+            uid = ctypes.create_string_buffer(bytes(t.cpu().numpy().tobytes()), nbytes)
+            check(lib().cfp_dist_plan_create(ctypes.byref(h), nx, ny, nz, self.world, self.rank, uid, self.device))
+        elif exchange == "torch":
+            check(lib().cfp_dist_plan_create_external(ctypes.byref(h), nx, ny, nz, self.world, self.rank,
+                                                      self.device))
+            self.work = torch.empty(self.local_size, dtype=torch.complex128, device=f"cuda:{self.device}")
+            check(lib().cfp_dist_plan_set_work_buffer(h, self.work.data_ptr()))
+        else:
+            raise ValueError("exchange must be 'rccl' or 'torch'")
         self._h = h
 
     @property
@@ -69,11 +86,38 @@ class SlabPlan:
         if out is None:
             out = torch.empty_like(b)
         n = self.local_size
-        check(lib().cfp_dist_plan_apply(self._h, _dev_ptr(b, n, "b"), _dev_ptr(out, n, "out"),
-                                        _stream_handle(stream)))
+        bp, xp, sh = _dev_ptr(b, n, "b"), _dev_ptr(out, n, "out"), _stream_handle(stream)
+        if self.exchange == "rccl":
+            check(lib().cfp_dist_plan_apply(self._h, bp, xp, sh))
+            return out
+        import torch.distributed as dist
+        check(lib().cfp_dist_plan_run_segment(self._h, 0, bp, xp, sh))
+        dist.all_to_all_single(out, self.work, group=self.group)  # work chunks -> x chunks
+        check(lib().cfp_dist_plan_run_segment(self._h, 1, bp, xp, sh))
+        dist.all_to_all_single(self.work, out, group=self.group)  # x chunks -> work chunks
+        check(lib().cfp_dist_plan_run_segment(self._h, 2, bp, xp, sh))
+        return out
+
+    def phases(self) -> list:
+        """The apply's steps: axis passes and all-to-all exchanges, in order."""
+        nph = ctypes.c_int()
+        check(lib().cfp_dist_plan_num_phases(self._h, ctypes.byref(nph)))
+        out = []
+        for i in range(nph.value):
+            ex, ax, n, mode = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+            check(lib().cfp_dist_plan_phase_info(self._h, i, ctypes.byref(ex), ctypes.byref(ax), ctypes.byref(n),
+                                                 ctypes.byref(mode)))
+            if ex.value:
+                out.append({"kind": "all-to-all"})
+            else:
+                out.append({"kind": "pass", "axis": "xyz"[ax.value], "n": n.value,
+                            "mode": {0: "fwd", 1: "inv", 2: "fused_sep", 3: "fused_diag"}[mode.value]})
         return out
 
     def time_phases(self, b: torch.Tensor, x: torch.Tensor, iters: int = 10, stream=None) -> list:
+        """Mean ms of each phase (passes and exchanges, in order) over `iters` applies."""
+        if self.exchange == "torch":
+            return self._time_phases_torch(b, x, iters)
         nph = ctypes.c_int()
         check(lib().cfp_dist_plan_num_phases(self._h, ctypes.byref(nph)))
         ms = (ctypes.c_double * nph.value)()
@@ -81,6 +125,36 @@ class SlabPlan:
         check(lib().cfp_dist_plan_time_phases(self._h, _dev_ptr(b, n, "b"), _dev_ptr(x, n, "x"), int(iters), ms,
                                               _stream_handle(stream)))
         return list(ms)
+
+    def _time_phases_torch(self, b, x, iters):
+        import torch.distributed as dist
+        ph = self.phases()
+        n = self.local_size
+        bp, xp = _dev_ptr(b, n, "b"), _dev_ptr(x, n, "x")
+        sh = _stream_handle()
+        acc = [0.0] * len(ph)
+        for _ in range(iters):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(ph) + 1)]
+            seg = 0
+            for i, p in enumerate(ph):
+                ev[i].record()
+                if p["kind"] == "all-to-all":
+                    if seg == 1:
+                        dist.all_to_all_single(x, self.work, group=self.group)
+                    else:
+                        dist.all_to_all_single(self.work, x, group=self.group)
+                    continue
+                # run this single pass: segments hold consecutive passes, so time per segment
+                # once (the first pass of a segment carries the whole segment)
+                first_of_seg = i == 0 or ph[i - 1]["kind"] == "all-to-all"
+                if first_of_seg:
+                    check(lib().cfp_dist_plan_run_segment(self._h, seg, bp, xp, sh))
+                    seg += 1
+            ev[-1].record()
+            torch.cuda.synchronize()
+            for i in range(len(ph)):
+                acc[i] += ev[i].elapsed_time(ev[i + 1])
+        return [a / iters for a in acc]
 
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:

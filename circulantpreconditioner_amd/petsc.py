@@ -24,6 +24,7 @@ from ._lib_ext import FFTPrecTransportContext, PetscScalar, StructuredTransportC
 
 PETSC_COMM_WORLD = 0
 PETSC_COMM_SELF = 1
+PETSC_DEFAULT = -2
 INSERT_VALUES, ADD_VALUES = 1, 2
 NORM_1, NORM_2, NORM_INFINITY = 0, 1, 3
 
@@ -194,29 +195,36 @@ def _fn(name: str) -> int:
 
 
 class PC:
-    def __init__(self):
-        self.h = ctypes.c_void_p()
-        PetscCall(lib().PCCreate(PETSC_COMM_WORLD, ctypes.byref(self.h)))
+    def __init__(self, handle: ctypes.c_void_p | None = None, owned: bool = True):
+        if handle is None:
+            handle = ctypes.c_void_p()
+            PetscCall(lib().PCCreate(PETSC_COMM_WORLD, ctypes.byref(handle)))
+        self.h = handle
+        self.owned = owned
         self.ctx = None
 
     @classmethod
     def shell(cls, ctx: FFTPrecTransportContext) -> "PC":
         """PCSetType(pc, PCSHELL); PCShellSetContext; PCShellSetSetUp/Apply/Destroy with the
         reference's callbacks (the registration the reference never does, ToDo.md:1)."""
-        pc = cls()
-        PetscCall(lib().PCSetType(pc.h, b"shell"))
-        pc.ctx = ctx
-        PetscCall(lib().PCShellSetContext(pc.h, ctypes.addressof(ctx)))
-        PetscCall(lib().PCShellSetSetUp(pc.h, _fn("setupFFTPrec3D")))
-        PetscCall(lib().PCShellSetApply(pc.h, _fn("applyFFT3DPrecTransport")))
-        PetscCall(lib().PCShellSetDestroy(pc.h, _fn("destroyFFTPrec3D")))
-        return pc
+        return cls().set_shell(ctx)
+
+    def set_shell(self, ctx: FFTPrecTransportContext) -> "PC":
+        PetscCall(lib().PCSetType(self.h, b"shell"))
+        self.ctx = ctx
+        PetscCall(lib().PCShellSetContext(self.h, ctypes.addressof(ctx)))
+        PetscCall(lib().PCShellSetSetUp(self.h, _fn("setupFFTPrec3D")))
+        PetscCall(lib().PCShellSetApply(self.h, _fn("applyFFT3DPrecTransport")))
+        PetscCall(lib().PCShellSetDestroy(self.h, _fn("destroyFFTPrec3D")))
+        return self
 
     @classmethod
     def none(cls) -> "PC":
-        pc = cls()
-        PetscCall(lib().PCSetType(pc.h, b"none"))
-        return pc
+        return cls().set_none()
+
+    def set_none(self) -> "PC":
+        PetscCall(lib().PCSetType(self.h, b"none"))
+        return self
 
     def setup(self) -> "PC":
         PetscCall(lib().PCSetUp(self.h))
@@ -227,8 +235,102 @@ class PC:
         return x
 
     def destroy(self) -> None:
-        if self.h is not None and self.h.value:
+        if self.owned and self.h is not None and self.h.value:
             PetscCall(lib().PCDestroy(ctypes.byref(self.h)))
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+KSP_REASONS = {0: "ITERATING", 2: "CONVERGED_RTOL", 3: "CONVERGED_ATOL", 4: "CONVERGED_ITS",
+               7: "CONVERGED_HAPPY_BREAKDOWN", -3: "DIVERGED_ITS", -4: "DIVERGED_DTOL", -5: "DIVERGED_BREAKDOWN"}
+PC_LEFT, PC_RIGHT = 0, 1
+
+
+class KSP:
+    """KSPGMRES of the stand-in (csrc/ksp_gmres.cpp): restart 30, left preconditioning, CGS,
+    rtol 1e-5 / abstol 1e-50 / dtol 1e5 / maxits 10000 unless set, as PETSc's defaults."""
+
+    def __init__(self):
+        self.h = ctypes.c_void_p()
+        PetscCall(lib().KSPCreate(PETSC_COMM_WORLD, ctypes.byref(self.h)))
+        PetscCall(lib().KSPSetType(self.h, b"gmres"))
+        self._ops = None
+        self._pc = None
+
+    def set_type(self, t: str) -> "KSP":
+        PetscCall(lib().KSPSetType(self.h, t.encode()))
+        return self
+
+    def set_tolerances(self, rtol=PETSC_DEFAULT, abstol=PETSC_DEFAULT, dtol=PETSC_DEFAULT,
+                       maxits=PETSC_DEFAULT) -> "KSP":
+        PetscCall(lib().KSPSetTolerances(self.h, float(rtol), float(abstol), float(dtol), int(maxits)))
+        return self
+
+    def set_restart(self, m: int) -> "KSP":
+        PetscCall(lib().KSPGMRESSetRestart(self.h, int(m)))
+        return self
+
+    def set_pc_side(self, side: int) -> "KSP":
+        PetscCall(lib().KSPSetPCSide(self.h, int(side)))
+        return self
+
+    def set_initial_guess_nonzero(self, flag: bool = True) -> "KSP":
+        PetscCall(lib().KSPSetInitialGuessNonzero(self.h, 1 if flag else 0))
+        return self
+
+    def get_pc(self) -> PC:
+        if self._pc is None:
+            h = ctypes.c_void_p()
+            PetscCall(lib().KSPGetPC(self.h, ctypes.byref(h)))
+            self._pc = PC(h, owned=False)
+        return self._pc
+
+    def set_operators(self, A: Mat, P: Mat | None = None) -> "KSP":
+        self._ops = (A, P or A)
+        PetscCall(lib().KSPSetOperators(self.h, A.h, (P or A).h))
+        return self
+
+    def setup(self) -> "KSP":
+        PetscCall(lib().KSPSetUp(self.h))
+        return self
+
+    def solve(self, b: Vec, x: Vec) -> int:
+        PetscCall(lib().KSPSolve(self.h, b.h, x.h))
+        return self.reason
+
+    @property
+    def reason(self) -> int:
+        r = ctypes.c_int()
+        PetscCall(lib().KSPGetConvergedReason(self.h, ctypes.byref(r)))
+        return r.value
+
+    @property
+    def its(self) -> int:
+        n = ctypes.c_int64()
+        PetscCall(lib().KSPGetIterationNumber(self.h, ctypes.byref(n)))
+        return n.value
+
+    @property
+    def rnorm(self) -> float:
+        r = ctypes.c_double()
+        PetscCall(lib().KSPGetResidualNorm(self.h, ctypes.byref(r)))
+        return r.value
+
+    def pc_stats(self) -> tuple:
+        n, s = ctypes.c_int64(), ctypes.c_double()
+        PetscCall(lib().KSPMiniGetPCApplyStats(self.h, ctypes.byref(n), ctypes.byref(s)))
+        return n.value, s.value
+
+    def destroy(self) -> None:
+        if self.h is not None and self.h.value:
+            if self._pc is not None:
+                self._pc.h = None
+            PetscCall(lib().KSPDestroy(ctypes.byref(self.h)))
         self.h = None
 
     def __del__(self):

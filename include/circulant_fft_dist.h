@@ -42,11 +42,22 @@ int cfp_dist_get_unique_id(char *id_out);
 int cfp_dist_plan_create(cfp_dist_plan_t *plan, int64_t nx, int64_t ny, int64_t nz, int nranks, int rank,
                          const char *unique_id, int device);
 int cfp_dist_plan_destroy(cfp_dist_plan_t plan);
+/* Same plan without a communicator: the caller runs the three kernel segments and performs
+ * the two all-to-alls in between with its own collective library:
+ *   run_segment(0); alltoall(work -> x); run_segment(1); alltoall(x -> work); run_segment(2)
+ * (equal splits of `chunk` complex values per peer, peer order = rank order). */
+int cfp_dist_plan_create_external(cfp_dist_plan_t *plan, int64_t nx, int64_t ny, int64_t nz, int nranks, int rank,
+                                  int device);
+int cfp_dist_plan_work_buffer(cfp_dist_plan_t plan, double **work_dev);
+int cfp_dist_plan_set_work_buffer(cfp_dist_plan_t plan, double *work_dev); /* caller-owned, local_size values */
+int cfp_dist_plan_run_segment(cfp_dist_plan_t plan, int segment, const double *b_dev, double *x_dev, void *stream);
 int cfp_dist_plan_set_symbol_transport(cfp_dist_plan_t plan, const double lam[6]);
 /* b_dev, x_dev: this rank's slab (local_size complex values); b may alias x */
 int cfp_dist_plan_apply(cfp_dist_plan_t plan, const double *b_dev, double *x_dev, void *stream);
 int cfp_dist_plan_local_size(cfp_dist_plan_t plan, int64_t *local_size);
 int cfp_dist_plan_num_phases(cfp_dist_plan_t plan, int *phases);
+/* phase i: *is_exchange = 1 for an all-to-all, else 0 (axis pass); *axis, *n, *mode of a pass */
+int cfp_dist_plan_phase_info(cfp_dist_plan_t plan, int phase, int *is_exchange, int *axis, int *n, int *mode);
 /* mean ms of each phase (kernels and exchanges, in order) over `iters` applies */
 int cfp_dist_plan_time_phases(cfp_dist_plan_t plan, const double *b_dev, double *x_dev, int iters, double *ms_out,
                               void *stream);

@@ -145,6 +145,10 @@ PetscErrorCode VecPointwiseDivide(Vec w, Vec x, Vec y);
 PetscErrorCode VecPointwiseMult(Vec w, Vec x, Vec y);
 PetscErrorCode VecDot(Vec x, Vec y, PetscScalar *val);
 PetscErrorCode VecNorm(Vec x, NormType type, PetscReal *val);
+PetscErrorCode VecMDot(Vec x, PetscInt nv, const Vec y[], PetscScalar val[]); /* val_i = y_i^H x */
+PetscErrorCode VecMAXPY(Vec y, PetscInt nv, const PetscScalar alpha[], Vec x[]); /* y += sum alpha_i x_i */
+PetscErrorCode VecDuplicateVecs(Vec v, PetscInt m, Vec *V[]);
+PetscErrorCode VecDestroyVecs(PetscInt m, Vec *V[]);
 /* stream the Vec kernels are enqueued on (hipStream_t, NULL = default); not in PETSc */
 PetscErrorCode VecMiniSetStream(void *stream);
 
@@ -179,6 +183,41 @@ PetscErrorCode PCShellSetName(PC pc, const char *name);
 PetscErrorCode PCSetUp(PC pc);
 PetscErrorCode PCApply(PC pc, Vec x, Vec y);
 PetscErrorCode PCDestroy(PC *pc);
+
+/* ---- KSP: GMRES(restart) with PETSc's defaults (restart 30, left preconditioning,
+ * classical Gram-Schmidt without refinement, preconditioned residual norm, convergence when
+ * ||r_k|| <= max(rtol ||r_0||, abstol), divergence when ||r_k|| > dtol ||r_0||) */
+typedef struct _p_KSP *KSP;
+typedef const char *KSPType;
+#define KSPGMRES "gmres"
+#define KSPPREONLY "preonly"
+typedef enum { PC_LEFT = 0, PC_RIGHT = 1 } PCSide;
+typedef enum {
+  KSP_CONVERGED_ITERATING = 0,
+  KSP_CONVERGED_RTOL = 2,
+  KSP_CONVERGED_ATOL = 3,
+  KSP_CONVERGED_ITS = 4,
+  KSP_CONVERGED_HAPPY_BREAKDOWN = 7,
+  KSP_DIVERGED_ITS = -3,
+  KSP_DIVERGED_DTOL = -4,
+  KSP_DIVERGED_BREAKDOWN = -5
+} KSPConvergedReason;
+PetscErrorCode KSPCreate(MPI_Comm comm, KSP *ksp);
+PetscErrorCode KSPSetType(KSP ksp, KSPType type);
+PetscErrorCode KSPSetTolerances(KSP ksp, PetscReal rtol, PetscReal abstol, PetscReal dtol, PetscInt maxits);
+PetscErrorCode KSPGMRESSetRestart(KSP ksp, PetscInt restart);
+PetscErrorCode KSPSetPCSide(KSP ksp, PCSide side);
+PetscErrorCode KSPSetInitialGuessNonzero(KSP ksp, PetscBool flg);
+PetscErrorCode KSPGetPC(KSP ksp, PC *pc);
+PetscErrorCode KSPSetOperators(KSP ksp, Mat A, Mat P);
+PetscErrorCode KSPSetUp(KSP ksp);
+PetscErrorCode KSPSolve(KSP ksp, Vec b, Vec x);
+PetscErrorCode KSPGetConvergedReason(KSP ksp, KSPConvergedReason *reason);
+PetscErrorCode KSPGetIterationNumber(KSP ksp, PetscInt *its);
+PetscErrorCode KSPGetResidualNorm(KSP ksp, PetscReal *rnorm);
+PetscErrorCode KSPDestroy(KSP *ksp);
+/* not in PETSc: seconds spent inside PCApply during the last KSPSolve, and its call count */
+PetscErrorCode KSPMiniGetPCApplyStats(KSP ksp, PetscInt *calls, PetscLogDouble *seconds);
 
 #ifdef __cplusplus
 }
