@@ -60,6 +60,30 @@ class TransportResult(ctypes.Structure):
         return d
 
 
+class WaveConfig(ctypes.Structure):
+    """cfp_wave_config (include/wave_system.h)."""
+    _fields_ = [("nx", ctypes.c_int64), ("ny", ctypes.c_int64), ("nz", ctypes.c_int64),
+                ("xmin", ctypes.c_double * 3), ("xmax", ctypes.c_double * 3), ("c0", ctypes.c_double),
+                ("cfl", ctypes.c_double), ("tmax", ctypes.c_double), ("ntmax", ctypes.c_int64),
+                ("precision", ctypes.c_double), ("max_its", ctypes.c_int64), ("restart", ctypes.c_int64),
+                ("pc", ctypes.c_int), ("bc", ctypes.c_int), ("pc_side", ctypes.c_int), ("on_device", ctypes.c_int)]
+
+
+class WaveResult(ctypes.Structure):
+    """cfp_wave_result (include/wave_system.h)."""
+    _fields_ = [("steps", ctypes.c_int64), ("dt", ctypes.c_double), ("time", ctypes.c_double),
+                ("total_its", ctypes.c_int64), ("max_step_its", ctypes.c_int64), ("min_step_its", ctypes.c_int64),
+                ("last_reason", ctypes.c_int), ("all_converged", ctypes.c_int), ("last_residual", ctypes.c_double),
+                ("last_norm_dU", ctypes.c_double), ("solve_seconds", ctypes.c_double),
+                ("pc_seconds", ctypes.c_double), ("pc_calls", ctypes.c_int64), ("setup_seconds", ctypes.c_double),
+                ("kappa", ctypes.c_double * 3)]
+
+    def as_dict(self) -> dict:
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "kappa"}
+        d["kappa"] = list(self.kappa)
+        return d
+
+
 def declare(L) -> None:
     i64, dp, vp, c_int = ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int
     S, P, cs = PetscScalar, ctypes.POINTER, ctypes.c_char_p
@@ -147,6 +171,7 @@ def declare(L) -> None:
         "KSPGetIterationNumber": ([vp, P(i64)], c_int),
         "KSPGetResidualNorm": ([vp, P(ctypes.c_double)], c_int),
         "KSPMiniGetPCApplyStats": ([vp, P(i64), P(ctypes.c_double)], c_int),
+        "KSPMiniSetUpWork": ([vp, vp], c_int),
         "KSPDestroy": ([P(vp)], c_int),
         # transport operator + GMRES time loop (include/transport_equation.h)
         "cfp_transport_csr": ([i64, i64, i64, P(ctypes.c_double), ctypes.c_double, P(ctypes.c_double), c_int,
@@ -157,6 +182,25 @@ def declare(L) -> None:
         "initial_conditions_shock_cartesian": ([i64, i64, i64, P(ctypes.c_double), P(ctypes.c_double), vp], c_int),
         "cfp_transport_config_default": ([P(TransportConfig), i64], None),
         "TransportEquationGMRES": ([P(TransportConfig), P(TransportResult), P(ctypes.c_double)], c_int),
+        # wave system (include/wave_system.h)
+        "cfp_wave_plan_create": ([P(vp), i64, i64, i64, c_int], c_int),
+        "cfp_wave_plan_destroy": ([vp], c_int),
+        "cfp_wave_plan_set_symbol": ([vp, P(ctypes.c_double), ctypes.c_double], c_int),
+        "cfp_wave_plan_apply": ([vp, dp, dp, vp], c_int),
+        "cfp_wave_plan_forward": ([vp, dp, dp, vp], c_int),
+        "cfp_wave_plan_backward": ([vp, dp, dp, vp], c_int),
+        "cfp_wave_plan_num_passes": ([vp, P(c_int)], c_int),
+        "cfp_wave_plan_time_passes": ([vp, dp, dp, c_int, dp, vp], c_int),
+        "cfp_wave_csr": ([i64, i64, i64, P(ctypes.c_double), ctypes.c_double, ctypes.c_double, c_int,
+                          ctypes.c_double, P(i64), P(i64), P(ctypes.c_double), P(i64)], c_int),
+        "computeDivergenceMatrixWaveCartesian": ([i64, i64, i64, P(ctypes.c_double), ctypes.c_double,
+                                                  ctypes.c_double, i64, P(vp)], c_int),
+        "initial_conditions_shock_wave": ([i64, i64, i64, P(ctypes.c_double), P(ctypes.c_double), vp], c_int),
+        "applyFFT3DPrecWave": ([vp, vp, vp], c_int),
+        "setupFFTPrec3DWave": ([vp], c_int),
+        "destroyFFTPrec3DWave": ([vp], c_int),
+        "cfp_wave_config_default": ([P(WaveConfig), i64], None),
+        "WaveSystemGMRES": ([P(WaveConfig), P(WaveResult), P(ctypes.c_double)], c_int),
         # the reference-named boundary
         "applyFFT3DPrecTransport": ([vp, vp, vp], c_int),
         "setupFFTPrec3D": ([vp], c_int),

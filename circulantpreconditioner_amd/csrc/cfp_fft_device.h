@@ -133,7 +133,114 @@ struct KArgs {
   const cd* colsym;
   const cd* axsym;
   const cd* diag;
+  WaveSym wave;
 };
+
+// ------------------------------------------------------------ wave-system block symbol
+// The periodic version of the wave-system operator (src/WaveSystem.cxx:92-176, 4 unknowns
+// per cell: pressure, then the 3 momentum components) is block-circulant; its symbol at
+// frequency theta is the arrowhead matrix
+//   S = [ 1 + sum_d p_d    i c0^2 q_x   i c0^2 q_y   i c0^2 q_z ]
+//       [ i q_x            1 + p_x      0            0          ]
+//       [ i q_y            0            1 + p_y      0          ]
+//       [ i q_z            0            0            1 + p_z    ]
+// (p_d = kappa_d c0 (1 - cos theta_d), q_d = kappa_d sin theta_d, kappa_d = dt / h_d), so
+// S^-1 r is: eliminate the momentum rows, solve the pressure row, back-substitute.  The two
+// axes that are not transformed by the fused pass are constant along a column: their part is
+// folded once per column (WaveCol); per point one reciprocal remains (wave_point).
+struct WaveCol {
+  double den;     // 1 + sum_nf p_d + c0^2 sum_nf q_d^2 / (1 + p_d)   (nf: non-fused axes)
+  double w[3];    // q_d / (1 + p_d) for the non-fused axes, 0 for the fused one
+  double qm, iem; // this lane's momentum row (comp = 1 + dm): q_dm and 1 / (1 + p_dm)
+  bool mine_fused;
+};
+
+__device__ __forceinline__ WaveCol wave_col(const double2 pq[3], int fused, int comp, double c0sq) {
+  WaveCol wc;
+  wc.den = 1.0;
+  wc.qm = 0.0;
+  wc.iem = 1.0;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const double ie = 1.0 / (1.0 + pq[d].x);
+    const double w = pq[d].y * ie;
+    const bool nf = d != fused;
+    wc.w[d] = nf ? w : 0.0;
+    if (nf) wc.den += pq[d].x + c0sq * pq[d].y * w;
+    if (comp == 1 + d) { wc.qm = pq[d].y; wc.iem = ie; }
+  }
+  wc.mine_fused = comp == 1 + fused;
+  return wc;
+}
+
+// component `comp` of S^-1 r at one point; pk = (p, q) of the fused axis at that point
+__device__ __forceinline__ cd wave_point(const cd r[4], int comp, int f, const WaveCol& wc, double2 pk, double c0sq) {
+  const double ef = 1.0 + pk.x;
+  // den = den_nf + p_f + c0^2 q_f^2 / ef; with D2 = den * ef one reciprocal gives both 1/den
+  // and 1/ef:  inv = 1 / (ef * D2),  1/den = ef^2 inv,  1/ef = D2 inv
+  const double D2 = fma(wc.den + pk.x, ef, c0sq * pk.y * pk.y);
+  const double inv = 1.0 / (ef * D2);
+  const double id = ef * ef * inv, ief = D2 * inv;
+  const double wf = pk.y * ief;
+  cd t = make_cd(0.0, 0.0);
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {  // weights select on the (uniform) fused axis, r is not indexed
+    const double w = d == f ? wf : wc.w[d];
+    t.x = fma(w, r[d + 1].x, t.x);
+    t.y = fma(w, r[d + 1].y, t.y);
+  }
+  const cd x0 = make_cd(fma(c0sq, t.y, r[0].x) * id, fma(-c0sq, t.x, r[0].y) * id);
+  cd rc = r[1];
+#pragma unroll
+  for (int j = 2; j < 4; ++j)
+    if (comp == j) rc = r[j];
+  const double qc = wc.mine_fused ? pk.y : wc.qm, iec = wc.mine_fused ? ief : wc.iem;
+  const cd xm = make_cd(fma(qc, x0.y, rc.x) * iec, fma(-qc, x0.x, rc.y) * iec);
+  return comp == 0 ? x0 : xm;
+}
+
+// reference version (generic kernel): the same algebra without the per-column hoisting
+__device__ __forceinline__ cd wave_solve(const cd r[4], int comp, const double2 pq[3], double c0sq) {
+  double ie[3];
+  double den = 1.0 + pq[0].x + pq[1].x + pq[2].x;
+  cd t = make_cd(0.0, 0.0);
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    ie[d] = 1.0 / (1.0 + pq[d].x);
+    const double w = pq[d].y * ie[d];
+    den = fma(c0sq * pq[d].y, w, den);
+    t.x = fma(w, r[d + 1].x, t.x);
+    t.y = fma(w, r[d + 1].y, t.y);
+  }
+  const double id = 1.0 / den;
+  const cd x0 = make_cd(fma(c0sq, t.y, r[0].x) * id, fma(-c0sq, t.x, r[0].y) * id);
+  cd rc = r[1];
+  double qc = pq[0].y, iec = ie[0];
+#pragma unroll
+  for (int j = 2; j < 4; ++j)
+    if (comp == j) { rc = r[j]; qc = pq[j - 1].y; iec = ie[j - 1]; }
+  const cd xm = make_cd(fma(qc, x0.y, rc.x) * iec, fma(-qc, x0.x, rc.y) * iec);
+  return comp == 0 ? x0 : xm;
+}
+
+// lane J of each aligned quad of lanes, broadcast to the quad (DPP quad_perm, VALU only)
+template <int J>
+__device__ __forceinline__ double quad_bcast(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffll), J * 0x55, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), J * 0x55, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// (p, q) of the two non-fused axes for the cell of column group `cell`
+__device__ __forceinline__ void wave_cell_sym(const WaveSym& w, i64 cell, double2 pq[3]) {
+  i64 idx[3] = {0, 0, 0};
+  if (w.fused == 2) { idx[0] = cell % w.n[0]; idx[1] = cell / w.n[0]; }
+  else if (w.fused == 1) { idx[0] = cell % w.n[0]; idx[2] = cell / w.n[0]; }
+  else { idx[1] = cell % w.n[1]; idx[2] = cell / w.n[1]; }
+#pragma unroll
+  for (int d = 0; d < 3; ++d) pq[d] = d == w.fused ? make_double2(0.0, 0.0) : w.tab[d][idx[d]];
+}
 
 template <int N, int PTS, int R0>
 struct Shape {
@@ -260,6 +367,28 @@ __global__ void __launch_bounds__(T*(N / PTS)) k_axis_fast(const cd* in, cd* out
   // the twiddle table copy is published by the first exchange's barrier
   fft_stages<N, PTS, R0, ROW, T, FLAGS>(v, lds_raw, tws, c, tpc, true);
 
+  if constexpr (MODE == PASS_FUSED_WAVE) {
+    // the 4 components of a cell are columns 4j..4j+3: lanes of one quad (T % 4 == 0)
+    double2 pc[3];
+    wave_cell_sym(a.wave, g >> 2, pc);
+    const int comp = c & 3;
+    const double c0sq = a.wave.c0sq;
+    const WaveCol wc = wave_col(pc, a.wave.fused, comp, c0sq);
+    // the fused pass runs along the last non-trivial axis: z for 3-D grids
+    const int f = a.wave.fused;
+    const double2* tf = f == 0 ? a.wave.tab[0] : (f == 1 ? a.wave.tab[1] : a.wave.tab[2]);
+#pragma unroll
+    for (int m = 0; m < PTS; ++m) {
+      const double2 pk = tf[tpc + m * TPC];
+      cd r[4];
+      r[0] = make_cd(quad_bcast<0>(v[m].x), quad_bcast<0>(v[m].y));
+      r[1] = make_cd(quad_bcast<1>(v[m].x), quad_bcast<1>(v[m].y));
+      r[2] = make_cd(quad_bcast<2>(v[m].x), quad_bcast<2>(v[m].y));
+      r[3] = make_cd(quad_bcast<3>(v[m].x), quad_bcast<3>(v[m].y));
+      v[m] = cconj(wave_point(r, comp, f, wc, pk, c0sq));
+    }
+    fft_stages<N, PTS, R0, ROW, T, FLAGS>(v, lds_raw, tws, c, tpc, false);
+  }
   if (MODE == PASS_FUSED_SEP || MODE == PASS_FUSED_DIAG) {
     cd cs = make_cd(0.0, 0.0);
     if (MODE == PASS_FUSED_SEP) cs = a.colsym[g];

@@ -34,6 +34,17 @@ enum PassMode : int {
   PASS_INV = 1,         // out = scale * IDFT(in)            (backward, e^{+}, unnormalised)
   PASS_FUSED_SEP = 2,   // out = scale * IDFT( DFT(in) / (colsym[g] + axsym[k]) )
   PASS_FUSED_DIAG = 3,  // out = scale * IDFT( DFT(in) / diag[same addressing as in] )
+  PASS_FUSED_WAVE = 4,  // out = scale * IDFT( S(k)^-1 DFT(in) ), S = the 4x4 wave-system block
+                        // symbol; the 4 components of a cell are 4 consecutive columns
+};
+
+// Separable parts of the wave-system block symbol (cfp_wave.hip): for axis d and frequency
+// index k, p = kappa_d c0 (1 - cos theta), q = kappa_d sin theta, theta = 2 pi k / n_d.
+struct WaveSym {
+  const double2* tab[3];  // [n_d] (p, q) per axis
+  i64 n[3];               // grid sizes (cells)
+  double c0sq;            // c0^2
+  int fused;              // axis transformed by the fused pass
 };
 
 struct PassDesc {
@@ -46,6 +57,7 @@ struct PassDesc {
   const cd* colsym;  // [ncols]   (PASS_FUSED_SEP)
   const cd* axsym;   // [n]       (PASS_FUSED_SEP)
   const cd* diag;    // addressed like `in` (PASS_FUSED_DIAG)
+  WaveSym wave;      // PASS_FUSED_WAVE
 };
 
 __host__ __device__ inline cd make_cd(double x, double y) { cd r; r.x = x; r.y = y; return r; }

@@ -124,9 +124,13 @@ bool fast_path_supported(const PassDesc& p) {
   if (p.in.seg_shift < 0 || p.out.seg_shift < 0) return false;
   if (p.ncols % T != 0) return false;
   if (!row_mode(p)) {
-    if (p.inner_n % T != 0) return false;
+    // a tile of T columns covers whole inner groups or lies inside one
+    if (p.inner_n % T != 0 && T % p.inner_n != 0) return false;
     if (p.in.inner_stride != 1 || p.out.inner_stride != 1) return false;
+  } else if (p.mode == PASS_FUSED_WAVE) {
+    return false;
   }
+  if (p.mode == PASS_FUSED_WAVE && T % 4 != 0) return false;
   return true;
 }
 
@@ -147,10 +151,15 @@ static hipError_t launch_fast_n(const PassDesc& p, const cd* in, cd* out, const 
     case PASS_FWD: return launch_fast_t<N, ROWV, PASS_FWD>(p, in, out, a, s);     \
     case PASS_INV: return launch_fast_t<N, ROWV, PASS_INV>(p, in, out, a, s);     \
     case PASS_FUSED_SEP: return launch_fast_t<N, ROWV, PASS_FUSED_SEP>(p, in, out, a, s); \
-    default: return launch_fast_t<N, ROWV, PASS_FUSED_DIAG>(p, in, out, a, s);    \
+    case PASS_FUSED_DIAG: return launch_fast_t<N, ROWV, PASS_FUSED_DIAG>(p, in, out, a, s); \
+    default: break;                                                               \
   }
-  if (row) { CFP_M(true) } else { CFP_M(false) }
+  if (row) { CFP_M(true) } else {
+    CFP_M(false)
+    if (p.mode == PASS_FUSED_WAVE) return launch_fast_t<N, false, PASS_FUSED_WAVE>(p, in, out, a, s);
+  }
 #undef CFP_M
+  return hipErrorInvalidValue;
 }
 
 // ----------------------------------------------------------------- generic path
@@ -218,6 +227,24 @@ __global__ void __launch_bounds__(CFP_GEN_THREADS) k_axis_generic(const cd* in, 
   }
   __syncthreads();
   gen_fft(A, B, g, G);
+  if (mode == PASS_FUSED_WAVE) {
+    // columns 4j..4j+3 of the block are the 4 components of one cell (G % 4 == 0)
+    for (int i = threadIdx.x; i < G * n; i += blockDim.x) {
+      const int c = i / n, k = i - c * n;
+      const i64 gg = g0 + c;
+      if (gg >= g.ncols) continue;
+      double2 pq[3];
+      wave_cell_sym(g.k.wave, gg >> 2, pq);
+      pq[g.k.wave.fused] = g.k.wave.tab[g.k.wave.fused][k];
+      cd r[4];
+      const int c4 = c & ~3;
+      for (int j = 0; j < 4; ++j) r[j] = A[(c4 + j) * n + k];
+      B[i] = cconj(wave_solve(r, c & 3, pq, g.k.wave.c0sq));
+    }
+    __syncthreads();
+    cd* tmp = A; A = B; B = tmp;
+    gen_fft(A, B, g, G);
+  }
   if (mode == PASS_FUSED_SEP || mode == PASS_FUSED_DIAG) {
     for (int i = threadIdx.x; i < G * n; i += blockDim.x) {
       const int c = i / n, k = i - c * n;
@@ -266,6 +293,11 @@ static hipError_t launch_generic(const PassDesc& p, const cd* in, cd* out, const
   if (G < 1) G = 1;
   if (G > 64) G = 64;
   if ((i64)G > p.ncols) G = (int)p.ncols;
+  if (p.mode == PASS_FUSED_WAVE) {  // whole cells (4 columns) per block
+    if (G < 4) G = 4;
+    G &= ~3;
+    if (p.ncols % 4 != 0) return hipErrorInvalidValue;
+  }
   g.ncol_per_block = G;
   const size_t lds = (size_t)2 * G * p.n * sizeof(cd);
   if (lds > kGenericMaxLds) return hipErrorInvalidValue;
@@ -289,6 +321,7 @@ hipError_t launch_axis_pass(const PassDesc& p, const cd* in, cd* out, const cd* 
   a.colsym = p.colsym;
   a.axsym = p.axsym;
   a.diag = p.diag;
+  a.wave = p.wave;
   if (p.ncols <= 0) return hipSuccess;
   if (fast_path_supported(p)) {
     switch (p.n) {

@@ -134,6 +134,23 @@ extern "C" PetscErrorCode KSPDestroy(KSP* pk) {
   return rc;
 }
 
+extern "C" PetscErrorCode KSPMiniSetUpWork(KSP k, Vec v) {
+  KCHK(k);
+  PetscInt n;
+  PetscCall(VecGetLocalSize(v, &n));
+  const PetscInt m = k->restart;
+  if (n != k->n || k->nvec != m + 1) {
+    free_work(k);
+    PetscCall(VecDuplicateVecs(v, m + 1, &k->V));
+    k->nvec = m + 1;
+    PetscCall(VecDuplicate(v, &k->t));
+    PetscCall(VecDuplicate(v, &k->t2));
+    PetscCall(VecDuplicate(v, &k->rhs));
+    k->n = n;
+  }
+  return PETSC_SUCCESS;
+}
+
 static PetscErrorCode pc_apply(KSP k, Vec x, Vec y) {
   const double t0 = now();
   PetscCall(PCApply(k->pc, x, y));
@@ -167,18 +184,8 @@ extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
   KCHK(k);
   if (!k->A) return PetscErrorSet(PETSC_ERR_ARG_WRONGSTATE, __func__, "KSPSetOperators has not been called");
   PetscCall(PCSetUp(k->pc));
-  PetscInt n;
-  PetscCall(VecGetLocalSize(b, &n));
+  PetscCall(KSPMiniSetUpWork(k, b));
   const PetscInt m = k->restart;
-  if (n != k->n || k->nvec != m + 1) {
-    free_work(k);
-    PetscCall(VecDuplicateVecs(b, m + 1, &k->V));
-    k->nvec = m + 1;
-    PetscCall(VecDuplicate(b, &k->t));
-    PetscCall(VecDuplicate(b, &k->t2));
-    PetscCall(VecDuplicate(b, &k->rhs));
-    k->n = n;
-  }
   k->its = 0;
   k->reason = KSP_CONVERGED_ITERATING;
   k->pc_calls = 0;

@@ -1,0 +1,149 @@
+"""Wave-system block-circulant preconditioner and implicit GMRES loop (include/wave_system.h,
+SURVEY.md §8f row f2, BASELINE config 4).
+
+``WavePlan``: x = S^{-1} b for the periodic wave-system operator with 4 interleaved unknowns
+per cell (pressure, 3 momentum components; idx = cell*4 + comp as the reference's Un,
+tests/WaveSystem_SphericalExplosion_impl_seq.cxx:57-68), one HIP plan, 5 HBM sweeps.
+``wave_csr``: the reference operator (src/WaveSystem.cxx:92-176) on a Cartesian grid.
+``config``/``run``: WaveSystem_impl_seq's time loop with the block-circulant PCSHELL.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import numpy as np
+import torch
+
+from ._lib import check, lib
+from ._lib_ext import WaveConfig, WaveResult
+from .petsc import PetscCall
+from .plan import _dev_ptr, _stream_handle
+
+C0 = 700.0  # src/WaveSystem.hxx:17
+BC_WALL, BC_PERIODIC, BC_NEUMANN = 0, 1, 2
+_BC = {"wall": BC_WALL, "periodic": BC_PERIODIC, "neumann": BC_NEUMANN}
+PC_NONE, PC_FFT = 0, 1
+
+
+def _d3(v) -> ctypes.Array:
+    return (ctypes.c_double * 3)(*[float(x) for x in v])
+
+
+class WavePlan:
+    """Block-circulant inverse on an nx*ny*nz grid with 4 interleaved components."""
+
+    NCOMP = 4
+
+    def __init__(self, dims: Sequence[int], device: int | None = None):
+        nx, ny, nz = (int(d) for d in dims)
+        self.dims = (nx, ny, nz)
+        self.size = 4 * nx * ny * nz
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        h = ctypes.c_void_p()
+        check(lib().cfp_wave_plan_create(ctypes.byref(h), nx, ny, nz, self.device))
+        self._h = h
+
+    def set_symbol(self, kappa: Sequence[float], c0: float = C0) -> "WavePlan":
+        check(lib().cfp_wave_plan_set_symbol(self._h, _d3(kappa), float(c0)))
+        return self
+
+    def apply(self, b: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+        if out is None:
+            out = torch.empty_like(b)
+        check(lib().cfp_wave_plan_apply(self._h, _dev_ptr(b, self.size, "b"), _dev_ptr(out, self.size, "out"),
+                                        _stream_handle(stream)))
+        return out
+
+    def forward(self, x: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+        if out is None:
+            out = torch.empty_like(x)
+        check(lib().cfp_wave_plan_forward(self._h, _dev_ptr(x, self.size, "x"), _dev_ptr(out, self.size, "out"),
+                                          _stream_handle(stream)))
+        return out
+
+    def backward(self, x: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+        if out is None:
+            out = torch.empty_like(x)
+        check(lib().cfp_wave_plan_backward(self._h, _dev_ptr(x, self.size, "x"), _dev_ptr(out, self.size, "out"),
+                                           _stream_handle(stream)))
+        return out
+
+    def num_passes(self) -> int:
+        n = ctypes.c_int()
+        check(lib().cfp_wave_plan_num_passes(self._h, ctypes.byref(n)))
+        return n.value
+
+    def time_passes(self, b: torch.Tensor, x: torch.Tensor, iters: int = 10, stream=None) -> list:
+        np_ = self.num_passes()
+        ms = (ctypes.c_double * np_)()
+        check(lib().cfp_wave_plan_time_passes(self._h, _dev_ptr(b, self.size, "b"), _dev_ptr(x, self.size, "x"),
+                                              int(iters), ms, _stream_handle(stream)))
+        return list(ms)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().cfp_wave_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def wave_csr(dims: Sequence[int], h: Sequence[float], dt: float, c0: float = C0, bc: str | int = "wall",
+             shift: float = 0.0):
+    """(rowptr, col, val) of shift*I + computeDivergenceMatrix of the wave system (host)."""
+    nx, ny, nz = (int(v) for v in dims)
+    m = 4 * nx * ny * nz
+    rowptr = np.empty(m + 1, dtype=np.int64)
+    col = np.empty(28 * m, dtype=np.int64)
+    val = np.empty(28 * m, dtype=np.complex128)
+    nnz = ctypes.c_int64()
+    P64 = ctypes.POINTER(ctypes.c_int64)
+    b = _BC[bc] if isinstance(bc, str) else int(bc)
+    check(lib().cfp_wave_csr(nx, ny, nz, _d3(h), float(dt), float(c0), b, float(shift),
+                             rowptr.ctypes.data_as(P64), col.ctypes.data_as(P64),
+                             val.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(nnz)))
+    k = nnz.value
+    return rowptr, col[:k].copy(), val[:k].copy()
+
+
+def config(n: int | Sequence[int] = 32, **kw) -> WaveConfig:
+    """WaveSystem_impl_seq's defaults (c0 = 700, cfl = 1e3/3, tmax = 0.05, precision 1e-5,
+    1000 iterations, wall boundaries) with overrides: pc='none'|'fft', bc='wall'|'periodic'|
+    'neumann', steps=ntmax, device=True/False, or any WaveConfig field."""
+    cfg = WaveConfig()
+    dims = (int(n),) * 3 if np.isscalar(n) else tuple(int(v) for v in n)
+    lib().cfp_wave_config_default(ctypes.byref(cfg), dims[0])
+    cfg.nx, cfg.ny, cfg.nz = dims
+    for k, v in kw.items():
+        if k == "pc":
+            cfg.pc = {"none": PC_NONE, "fft": PC_FFT}[v] if isinstance(v, str) else int(v)
+        elif k == "bc":
+            cfg.bc = _BC[v] if isinstance(v, str) else int(v)
+        elif k == "steps":
+            cfg.ntmax = int(v)
+            cfg.tmax = 1e300
+        elif k == "device":
+            cfg.on_device = 1 if v else 0
+        elif k in ("xmin", "xmax"):
+            setattr(cfg, k, _d3(v))
+        else:
+            if not hasattr(cfg, k):
+                raise KeyError(k)
+            setattr(cfg, k, v)
+    return cfg
+
+
+def run(cfg: WaveConfig, return_field: bool = False):
+    """WaveSystemGMRES: the implicit time loop; result dict (and the final 4N field)."""
+    res = WaveResult()
+    m = int(4 * cfg.nx * cfg.ny * cfg.nz)
+    out = np.empty(m, dtype=np.complex128) if return_field else None
+    ptr = out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) if out is not None else None
+    PetscCall(lib().WaveSystemGMRES(ctypes.byref(cfg), ctypes.byref(res), ptr))
+    d = res.as_dict()
+    return (d, out) if return_field else d

@@ -218,6 +218,9 @@ PetscErrorCode KSPGetResidualNorm(KSP ksp, PetscReal *rnorm);
 PetscErrorCode KSPDestroy(KSP *ksp);
 /* not in PETSc: seconds spent inside PCApply during the last KSPSolve, and its call count */
 PetscErrorCode KSPMiniGetPCApplyStats(KSP ksp, PetscInt *calls, PetscLogDouble *seconds);
+/* not in PETSc: allocate the GMRES work vectors now (duplicates of v) instead of in the first
+ * KSPSolve, so a timed solve does not include their allocation */
+PetscErrorCode KSPMiniSetUpWork(KSP ksp, Vec v);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,115 @@
+/*
+ * wave_system.h -- the (d+1)-block-circulant preconditioner of the linear wave system and the
+ * implicit GMRES time loop it plugs into (BASELINE config 4).
+ *
+ * The reference assembles the implicit upwind wave-system matrix
+ *   src/WaveSystem.cxx:92-107   jacobianMatrices(normal, coeff) = (A(n) - |A(n)|) coeff / 2
+ *   src/WaveSystem.cxx:109-176  computeDivergenceMatrix(Mesh, Mat*, dt)  (wall / periodic /
+ *                               Neumann faces)
+ *   src/WaveSystem.cxx:25-76    initial_conditions_shock (pressure 155e5 inside r < 0.3, else
+ *                               70e5; velocity 0)
+ * and solves it with GMRES + ILU/BJACOBI (tests/WaveSystem_SphericalExplosion_impl_seq.cxx:
+ * 11-150, _impl_mpi.cxx).  It has no FFT preconditioner for it (ToDo.md:10 asks for one): the
+ * periodic operator is block-circulant with 4x4 blocks (d = 3: pressure, 3 momentum
+ * components, interleaved idx = cell*4 + comp as the reference's Un layout, :57-68), and this
+ * library inverts it exactly with 5 HBM sweeps, like the scalar plan.
+ *
+ * Symbol (theta_d = 2 pi k_d / n_d, kappa_d = dt / h_d, c0 = 700, src/WaveSystem.hxx:17):
+ *   S = I + sum_d kappa_d sum_{s=+-1} A^-(s e_d) (e^{i s theta_d} - 1),
+ *   A^-(n) = (A(n) - |A(n)|) / 2,  A(n) = [[0, c0^2 n^T], [n, 0]],  |A(n)| = diag(c0, c0 n n^T).
+ */
+#ifndef CFP_WAVE_SYSTEM_H
+#define CFP_WAVE_SYSTEM_H
+
+#include <stdint.h>
+
+#include "petsc_mini.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- the block-circulant plan (C ABI, device pointers, 4 interleaved components) */
+typedef struct cfp_wave_plan_s *cfp_wave_plan_t;
+int cfp_wave_plan_create(cfp_wave_plan_t *plan, int64_t nx, int64_t ny, int64_t nz, int device);
+int cfp_wave_plan_destroy(cfp_wave_plan_t plan);
+/* kappa[d] = dt / h_d, c0 = sound speed */
+int cfp_wave_plan_set_symbol(cfp_wave_plan_t plan, const double kappa[3], double c0);
+/* x = S^{-1} b on the periodic grid (b, x: 4*nx*ny*nz complex doubles; x may alias b) */
+int cfp_wave_plan_apply(cfp_wave_plan_t plan, const double *b, double *x, void *stream);
+/* unnormalised forward / backward 3-D DFT of each component (tests and tools) */
+int cfp_wave_plan_forward(cfp_wave_plan_t plan, const double *in, double *out, void *stream);
+int cfp_wave_plan_backward(cfp_wave_plan_t plan, const double *in, double *out, void *stream);
+int cfp_wave_plan_num_passes(cfp_wave_plan_t plan, int *passes);
+int cfp_wave_plan_time_passes(cfp_wave_plan_t plan, const double *b, double *x, int iters, double *ms_out,
+                              void *stream);
+
+/* ---- host assembly of the wave-system operator */
+enum { CFP_WAVE_BC_WALL = 0, CFP_WAVE_BC_PERIODIC = 1, CFP_WAVE_BC_NEUMANN = 2 };
+/* CSR of shift*I + computeDivergenceMatrix (src/WaveSystem.cxx:109-176) on an nx*ny*nz
+ * Cartesian grid, 4 unknowns per cell.  rowptr: 4n+1 entries; col/val room for 4n*28
+ * entries (val interleaved re,im).  Entries that are exactly zero are not stored; every row
+ * keeps its diagonal; columns ascend. */
+int cfp_wave_csr(int64_t nx, int64_t ny, int64_t nz, const double h[3], double dt, double c0, int bc, double shift,
+                 int64_t *rowptr, int64_t *col, double *val, int64_t *nnz);
+
+/* ---- PETSc-level entry points */
+PetscErrorCode computeDivergenceMatrixWaveCartesian(PetscInt nx, PetscInt ny, PetscInt nz, const PetscReal h[3],
+                                                    PetscReal dt, PetscReal c0, PetscInt bc, Mat *A);
+/* pressure 155e5 where |centre - domain centre| < 0.3 else 70e5, momentum 0 (U: 4N) */
+PetscErrorCode initial_conditions_shock_wave(PetscInt nx, PetscInt ny, PetscInt nz, const PetscReal xmin[3],
+                                             const PetscReal xmax[3], Vec U);
+
+/* PCSHELL of the block-circulant preconditioner (new capability; same registration pattern
+ * as applyFFT3DPrecTransport: PCShellSetContext(pc, &ctx), SetSetUp/SetApply/SetDestroy) */
+struct FFTPrecWaveContext {
+  PetscInt n_x, n_y, n_z;
+  PetscReal kappa_x, kappa_y, kappa_z; /* dt / h_d */
+  PetscReal c0;
+  cfp_wave_plan_t plan; /* created by setup, destroyed by destroy */
+};
+typedef struct FFTPrecWaveContext FFTPrecWaveContext;
+PetscErrorCode applyFFT3DPrecWave(PC pc, Vec b, Vec x);
+PetscErrorCode setupFFTPrec3DWave(PC pc);
+PetscErrorCode destroyFFTPrec3DWave(PC pc);
+
+/* ---- the implicit wave-system time loop (WaveSystem_impl_seq/mpi) */
+enum { CFP_WAVE_PC_NONE = 0, CFP_WAVE_PC_FFT = 1 };
+typedef struct {
+  int64_t nx, ny, nz;
+  double xmin[3], xmax[3];
+  double c0;          /* 700 (src/WaveSystem.hxx:17) */
+  double cfl;         /* reference main: 1e3 / dim */
+  double tmax;        /* 0.05 */
+  int64_t ntmax;
+  double precision;   /* rtol = abstol = stationarity threshold: 1e-5 (src/WaveSystem.hxx:19) */
+  int64_t max_its;    /* 1000 */
+  int64_t restart;    /* 30 */
+  int pc;             /* CFP_WAVE_PC_* */
+  int bc;             /* CFP_WAVE_BC_*: wall as the reference mains set up */
+  int pc_side;        /* PC_LEFT / PC_RIGHT */
+  int on_device;
+} cfp_wave_config;
+
+/* same layout as cfp_transport_result (transport_equation.h); lambda[] holds kappa */
+typedef struct {
+  int64_t steps;
+  double dt, time;
+  int64_t total_its, max_step_its, min_step_its;
+  int last_reason;
+  int all_converged;
+  double last_residual, last_norm_dU;
+  double solve_seconds, pc_seconds;
+  int64_t pc_calls;
+  double setup_seconds;
+  double kappa[3];
+} cfp_wave_result;
+
+void cfp_wave_config_default(cfp_wave_config *cfg, int64_t n);
+/* U_out: optional 4N complex (interleaved re,im) final field */
+PetscErrorCode WaveSystemGMRES(const cfp_wave_config *cfg, cfp_wave_result *res, double *U_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFP_WAVE_SYSTEM_H */

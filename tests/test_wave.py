@@ -1,0 +1,223 @@
+"""Row f2 (BASELINE config 4): wave-system operator, block-circulant
+preconditioner (HIP) and the implicit GMRES loop.
+
+Oracle: oracle/wave.py (reference assembly restated as a face loop, explicit 4x4 block symbol
+and numpy block-circulant solve, pinned to the assembly by the periodic round trip below)."""
+import ctypes
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import scipy.sparse.linalg as spla
+
+from circulantpreconditioner_amd import petsc as P
+from circulantpreconditioner_amd import wave as W
+
+from oracle import transport as OT
+from oracle import wave as OW
+
+
+def _csr(dims, h, dt, bc, shift=0.0, c0=700.0):
+    rp, col, val = W.wave_csr(dims, h, dt, c0, bc, shift)
+    m = 4 * int(np.prod(dims))
+    return sp.csr_matrix((val, col, rp), shape=(m, m))
+
+
+CASES = [((4, 3, 5), (0.25, 1 / 3, 0.2), 1e-3), ((6, 2, 1), (1 / 6, 0.5, 1.0), 2e-4), ((2, 2, 2), (0.5, 0.5, 0.5), 5e-4),
+         ((1, 1, 3), (1.0, 1.0, 1 / 3), 1e-4)]
+
+
+@pytest.mark.parametrize("bc", ["wall", "periodic", "neumann"])
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c[0])))
+def test_wave_csr_matches_face_loop(case, bc):
+    dims, h, dt = case
+    A = _csr(dims, h, dt, bc, shift=1.0)
+    R = OW.wave_matrix(dims, h, dt, bc=bc, shift=1.0)
+    scale = max(1.0, abs(R).max())
+    np.testing.assert_allclose(A.toarray(), R.toarray(), rtol=0, atol=1e-13 * scale)
+    assert A.has_sorted_indices
+    m = A.shape[0]
+    assert all(r in A.indices[A.indptr[r]:A.indptr[r + 1]] for r in range(m))
+
+
+def test_block_solve_inverts_periodic_assembly():
+    """Pin: the block-circulant inverse of the oracle undoes the reference's periodic assembly."""
+    dims, h = (4, 3, 5), (0.25, 1 / 3, 0.2)
+    dt = 3e-4
+    kappa = [dt / v for v in h]
+    A = OW.wave_matrix(dims, h, dt, bc="periodic", shift=1.0)
+    rng = np.random.default_rng(0)
+    b = rng.standard_normal(A.shape[0]) + 1j * rng.standard_normal(A.shape[0])
+    x = OW.block_solve(dims, kappa, b)
+    assert np.linalg.norm(A @ x - b) <= 1e-12 * np.linalg.norm(b)
+
+
+def test_arrowhead_closed_form_equals_block_symbol():
+    """The kernel's closed form (cfp_fft_device.h wave_solve) against the explicit symbol."""
+    dims, kappa, c0 = (5, 4, 3), (0.07, 0.03, 0.11), 700.0
+    S = OW.block_symbol(dims, kappa, c0)
+    nx, ny, nz = dims
+    kz, ky, kx = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    th = (2 * np.pi * kx / nx, 2 * np.pi * ky / ny, 2 * np.pi * kz / nz)
+    p = [kappa[d] * c0 * (1 - np.cos(th[d])) for d in range(3)]
+    q = [kappa[d] * np.sin(th[d]) for d in range(3)]
+    E = np.zeros_like(S)
+    E[..., 0, 0] = 1 + p[0] + p[1] + p[2]
+    for d in range(3):
+        E[..., 0, 1 + d] = 1j * c0 * c0 * q[d]
+        E[..., 1 + d, 0] = 1j * q[d]
+        E[..., 1 + d, 1 + d] = 1 + p[d]
+    np.testing.assert_allclose(S, E, rtol=0, atol=1e-9)
+
+
+def test_wave_initial_condition():
+    dims = (6, 5, 4)
+    v = P.Vec.seq(4 * int(np.prod(dims)))
+    lo, hi = (ctypes.c_double * 3)(-0.5, -0.5, -0.5), (ctypes.c_double * 3)(0.5, 0.5, 0.5)
+    P.PetscCall(P.lib().initial_conditions_shock_wave(*dims, lo, hi, v.h))
+    np.testing.assert_array_equal(v.array(), OW.initial_conditions_shock_wave(dims))
+
+
+def test_wave_csr_errors():
+    with pytest.raises(Exception):
+        W.wave_csr((0, 2, 2), (1, 1, 1), 1.0)
+    with pytest.raises(Exception):
+        W.wave_csr((2, 2, 2), (1, 1, 1), 1.0, bc=9)
+    with pytest.raises(Exception):
+        W.wave_csr((2, 2, 2), (1, 1, 1), 1.0, c0=0.0)
+
+
+def test_wave_driver_pcnone_host_matches_oracle():
+    dims = (6, 5, 4)
+    res, U = W.run(W.config(dims, pc="none", device=False), return_field=True)
+    dt, kappa, h = OW.dt_and_kappa(dims)
+    assert res["dt"] == pytest.approx(dt, rel=1e-15)
+    A = _csr(dims, h, dt, "wall", shift=1.0)  # the face-loop match is test_wave_csr_matches_face_loop
+    Uo = OW.initial_conditions_shock_wave(dims)
+    # the reference loop: while time <= tmax (0.05), time += dt
+    steps, t = 0, 0.0
+    while t <= 0.05:
+        t += dt
+        steps += 1
+    assert res["steps"] == steps
+    its, conv = 0, True
+    for _ in range(steps):
+        Uo, k, reason, _, _ = OT.gmres(A, Uo, rtol=1e-5, abstol=1e-5, maxits=1000)
+        its += k
+        conv = conv and reason in (2, 3)
+    # a stopping test that lands within rounding of the threshold may move by one iteration
+    assert abs(res["total_its"] - its) <= steps and res["all_converged"] == int(conv)
+    np.testing.assert_allclose(U, Uo, rtol=0, atol=1e-6 * np.abs(Uo).max())
+
+
+def test_wave_driver_fft_needs_device():
+    with pytest.raises(P.PetscError) as e:
+        W.run(W.config(4, pc="fft", device=False))
+    assert e.value.code == 56
+
+
+# --------------------------------------------------------------------------- GPU
+def _rand(m, seed):
+    rng = np.random.default_rng(seed)
+    return rng.standard_normal(m) + 1j * rng.standard_normal(m)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims", [(16, 16, 16), (32, 16, 8), (8, 8, 64), (64, 32, 16), (6, 5, 7), (12, 10, 3),
+                                  (16, 1, 1), (8, 4, 1), (1, 1, 1)],
+                         ids=lambda d: "x".join(map(str, d)))
+def test_wave_plan_matches_oracle(dims):
+    import torch
+    kappa = (0.079, 0.05, 0.11)
+    m = 4 * int(np.prod(dims))
+    b = _rand(m, 1)
+    plan = W.WavePlan(dims).set_symbol(kappa)
+    x = plan.apply(torch.from_numpy(b).cuda()).cpu().numpy()
+    xo = OW.block_solve(dims, kappa, b)
+    assert np.linalg.norm(x - xo) <= 1e-12 * np.linalg.norm(xo)
+
+
+@pytest.mark.gpu
+def test_wave_plan_aliasing_and_transforms():
+    import torch
+    dims = (16, 8, 32)
+    m = 4 * int(np.prod(dims))
+    b = _rand(m, 2)
+    plan = W.WavePlan(dims).set_symbol((0.08, 0.08, 0.08))
+    t = torch.from_numpy(b).cuda()
+    ref = plan.apply(t)
+    t2 = t.clone()
+    plan.apply(t2, out=t2)
+    assert torch.equal(ref, t2)
+    F = plan.forward(t).cpu().numpy().reshape(dims[2], dims[1], dims[0], 4)
+    Fo = np.fft.fftn(b.reshape(dims[2], dims[1], dims[0], 4), axes=(0, 1, 2))
+    assert np.linalg.norm(F - Fo) <= 1e-12 * np.linalg.norm(Fo)
+    Bk = plan.backward(torch.from_numpy(Fo.reshape(-1)).cuda()).cpu().numpy()
+    assert np.linalg.norm(Bk / np.prod(dims) - b) <= 1e-12 * np.linalg.norm(b)
+
+
+@pytest.mark.gpu
+def test_wave_plan_128_inverts_periodic_operator():
+    """Config 4 size, size-independent check: the periodic operator (reference assembly,
+    host SpMV) applied to the HIP solve returns b."""
+    import torch
+    dims = (128, 128, 128)
+    dt, kappa, h = OW.dt_and_kappa(dims)
+    m = 4 * 128 ** 3
+    b = _rand(m, 3)
+    x = W.WavePlan(dims).set_symbol(kappa).apply(torch.from_numpy(b).cuda()).cpu().numpy()
+    A = _csr(dims, h, dt, "periodic", shift=1.0)
+    assert np.linalg.norm(A @ x - b) <= 1e-11 * np.linalg.norm(b)
+
+
+@pytest.mark.gpu
+def test_wave_plan_errors():
+    import torch
+    plan = W.WavePlan((8, 8, 8))
+    x = torch.zeros(4 * 512, dtype=torch.complex128, device="cuda")
+    with pytest.raises(Exception):
+        plan.apply(x)  # no symbol
+    with pytest.raises(Exception):
+        plan.set_symbol((0.1, 0.1, 0.1), c0=-1.0)
+    plan.set_symbol((0.1, 0.1, 0.1))
+    with pytest.raises(ValueError):
+        plan.apply(torch.zeros(4 * 511, dtype=torch.complex128, device="cuda"))
+
+
+@pytest.mark.gpu
+def test_wave_driver_pcnone_device_equals_host():
+    dims = (8, 8, 8)
+    rh, Uh = W.run(W.config(dims, pc="none", device=False), return_field=True)
+    rd, Ud = W.run(W.config(dims, pc="none", device=True), return_field=True)
+    assert rd["total_its"] == rh["total_its"]
+    np.testing.assert_allclose(Ud, Uh, rtol=0, atol=1e-9 * np.abs(Uh).max())
+
+
+@pytest.mark.gpu
+def test_wave_driver_fft_pc_matches_oracle():
+    dims = (16, 16, 16)
+    res, U = W.run(W.config(dims, pc="fft", steps=2), return_field=True)
+    dt, kappa, h = OW.dt_and_kappa(dims)
+    assert res["kappa"] == pytest.approx(kappa, rel=1e-14)
+    A = OW.wave_matrix(dims, h, dt, bc="wall", shift=1.0)
+    U0 = OW.initial_conditions_shock_wave(dims)
+    M = lambda v: OW.block_solve(dims, kappa, v)  # noqa: E731
+    its = []
+    Uo = U0
+    for _ in range(2):
+        Uo, k, reason, _, _ = OT.gmres(A, Uo, M=M, rtol=1e-5, abstol=1e-5, maxits=1000)
+        its.append(k)
+    assert res["all_converged"] == 1
+    assert abs(res["total_its"] - sum(its)) <= max(1, sum(its) // 100)
+    Us = U0
+    for _ in range(2):
+        Us = spla.spsolve(A.tocsc(), Us)
+    assert np.linalg.norm(U - Us) <= 10 * np.linalg.norm(Uo - Us) + 1e-10 * np.linalg.norm(Us)
+
+
+@pytest.mark.gpu
+def test_wave_fft_pc_cuts_iterations():
+    r_none = W.run(W.config(32, pc="none"))
+    r_fft = W.run(W.config(32, pc="fft"))
+    assert r_fft["all_converged"] == 1
+    assert r_none["all_converged"] == 0 or r_fft["total_its"] * 3 <= r_none["total_its"]

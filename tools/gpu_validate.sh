@@ -1,4 +1,4 @@
-# GPU step: full gpu test suite, GMRES transport bench (configs 1/3), bench lines at 256^3 (with CPU baseline), 512^3, 128^3,
+# GPU step: full gpu test suite, GMRES bench (configs 1/3/4), bench lines at 256^3 (with CPU baseline), 512^3, 128^3,
 # rocprofv3 kernel stats and separate FETCH_SIZE / WRITE_SIZE PMC passes at 256^3.
 set -o pipefail
 mkdir -p gpurun_out
@@ -8,8 +8,8 @@ timeout -k 10 1200 python -m pytest tests -q -m gpu --maxfail=20 -p no:cacheprov
 rc=$?
 echo "pytest rc=$rc"; tail -4 gpurun_out/$TAG.tests.log
 if [ $rc -gt 1 ]; then exit $rc; fi
-timeout -k 10 600 python bench_transport.py --out gpurun_out/$TAG.transport.jsonl > gpurun_out/$TAG.transport.log 2>&1 || exit $?
-cat gpurun_out/$TAG.transport.jsonl
+timeout -k 10 600 python bench_gmres.py --out gpurun_out/$TAG.gmres.jsonl > gpurun_out/$TAG.gmres.log 2>&1 || exit $?
+cat gpurun_out/$TAG.gmres.jsonl
 timeout -k 10 300 python bench.py > gpurun_out/$TAG.bench256.json 2> gpurun_out/$TAG.bench256.err || exit $?
 cat gpurun_out/$TAG.bench256.json
 timeout -k 10 300 python bench.py --grid 512 --steps 30 --warmup 3 --no-cpu-baseline > gpurun_out/$TAG.bench512.json 2>/dev/null || exit $?
