@@ -190,7 +190,9 @@ def test_wave_driver_pcnone_device_equals_host():
     rh, Uh = W.run(W.config(dims, pc="none", device=False), return_field=True)
     rd, Ud = W.run(W.config(dims, pc="none", device=True), return_field=True)
     assert rd["total_its"] == rh["total_its"]
-    np.testing.assert_allclose(Ud, Uh, rtol=0, atol=1e-9 * np.abs(Uh).max())
+    # ten rtol = 1e-5 solves in a row (c0^2 = 4.9e5 couples pressure and momentum): the two
+    # rounding paths agree to the solver tolerance, not to rounding
+    np.testing.assert_allclose(Ud, Uh, rtol=0, atol=1e-5 * np.abs(Uh).max())
 
 
 @pytest.mark.gpu
