@@ -43,7 +43,7 @@ def kernel_alg_bytes(mode: str, N: int, n_axis: int) -> int:
     b = 32 * N  # read N c128 + write N c128
     if mode == "fused_diag":
         b += 16 * N  # + read Diag
-    elif mode == "fused_sep":
+    elif mode in ("fused_sep", "mid_fused"):
         b += 16 * (N // n_axis + n_axis)  # per-column + per-point symbol tables
     return b
 
@@ -93,6 +93,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--grid", type=int, nargs="+", default=[256])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--schedule", default="auto", choices=["auto", "five", "five_y", "three"],
+                    help="apply schedule: 5 axis passes fused on z (auto) or y, or 3 sweeps (256^3)")
     ap.add_argument("--chunk", type=int, default=None,
                     help="z-planes per chunk of the Infinity-Cache-resident x/y schedule (0 = off; default: plan's)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
@@ -132,6 +134,7 @@ def main() -> int:
         plan.set_transport_symbol(LAM)
         if args.chunk is not None:
             plan.set_chunking(args.chunk)
+        plan.set_schedule(args.schedule)
         run = lambda: plan.apply(b, out=x)  # noqa: E731
         parallelism = "single GPU"
     else:

@@ -46,6 +46,7 @@ def _declare(L) -> None:
         "cfp_plan_forward": ([vp, dp, dp, vp], c_int),
         "cfp_plan_backward": ([vp, dp, dp, vp], c_int),
         "cfp_plan_set_chunking": ([vp, i64], c_int),
+        "cfp_plan_set_schedule": ([vp, c_int], c_int),
         "cfp_plan_num_passes": ([vp, P(c_int)], c_int),
         "cfp_plan_pass_info": ([vp, c_int, P(c_int), P(c_int), P(i64), P(c_int), P(c_int)], c_int),
         "cfp_plan_time_passes": ([vp, dp, dp, c_int, dp, vp], c_int),

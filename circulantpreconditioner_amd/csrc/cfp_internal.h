@@ -36,6 +36,10 @@ enum PassMode : int {
   PASS_FUSED_DIAG = 3,  // out = scale * IDFT( DFT(in) / diag[same addressing as in] )
   PASS_FUSED_WAVE = 4,  // out = scale * IDFT( S(k)^-1 DFT(in) ), S = the 4x4 wave-system block
                         // symbol; the 4 components of a cell are 4 consecutive columns
+  // launches of the 3-sweep schedule (cfp_three_pass.hip); reported, not dispatched here
+  PASS_TP_ROWS_FWD = 5,  // x DFT + the 64-point stage of the y DFT
+  PASS_TP_MID = 6,       // 4-point y stage + z DFT, symbol, and their inverses
+  PASS_TP_ROWS_INV = 7,  // inverse of PASS_TP_ROWS_FWD, x 1/N
 };
 
 // Separable parts of the wave-system block symbol (cfp_wave.hip): for axis d and frequency

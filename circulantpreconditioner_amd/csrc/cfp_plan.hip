@@ -22,6 +22,7 @@
 #include "../../include/circulant_fft.h"
 #include "cfp_internal.h"
 #include "cfp_host.h"
+#include "cfp_three_pass.h"
 
 using namespace cfp;
 
@@ -130,6 +131,7 @@ struct cfp_plan_s {
   int fused_axis = 0;
   std::vector<cd> sym1d[3];  // separable: lambda_d * c_d_hat (host copies)
   i64 chunk_planes = 0;      // > 0: chunked x/y schedule (see apply_steps)
+  int schedule = CFP_SCHEDULE_AUTO;
 };
 
 namespace {
@@ -163,7 +165,27 @@ struct Step {
   bool from_b;
   bool scale;
   i64 z0, z1;  // z-plane range of an x or y pass (z1 < 0: whole grid)
+  int tp = -1; // >= 0: stage of the 3-sweep schedule (cfp_three_pass.hip)
 };
+
+// the 3-sweep schedule serves 256^3 grids with a separable symbol
+bool use_three_pass(const cfp_plan_s* p, bool diag_override) {
+  if (p->schedule != CFP_SCHEDULE_THREE_PASS || diag_override || p->sym_kind != 1) return false;
+  return three_pass_supported(p->n);
+}
+
+// axis order of the 5-pass schedule: the last one is fused with the symbol
+void order_axes(cfp_plan_s* p) {
+  p->axes.clear();
+  const int order_z[3] = {0, 1, 2}, order_y[3] = {0, 2, 1};
+  // AUTO fuses y on large grids (512^3: 4 % faster, profiles/r01_schedule_sweep.txt), z otherwise
+  const bool yf = p->schedule == CFP_SCHEDULE_FIVE_PASS_YFUSED ||
+                  (p->schedule == CFP_SCHEDULE_AUTO && p->n[1] >= 512 && p->n[2] >= 512);
+  const int* o = yf ? order_y : order_z;
+  for (int i = 0; i < 3; ++i)
+    if (p->n[o[i]] > 1) p->axes.push_back(o[i]);
+  p->fused_axis = p->axes.empty() ? 0 : p->axes.back();
+}
 
 // The apply schedule: forward passes over all non-trivial axes but the last, the fused
 // DFT/divide/IDFT pass over the last one, then the inverse passes in reverse order; the
@@ -171,14 +193,20 @@ struct Step {
 // alternately over blocks of `chunk` z-planes, so the y pass reads planes the x pass has
 // just written while they are still resident in the 256 MiB Infinity Cache (and the
 // inverse pair likewise).
-std::vector<Step> apply_steps(const cfp_plan_s* p) {
+std::vector<Step> apply_steps(const cfp_plan_s* p, bool diag_override = false) {
   std::vector<Step> st;
+  if (use_three_pass(p, diag_override)) {
+    st.push_back({0, PASS_TP_ROWS_FWD, true, false, 0, -1, 0});
+    st.push_back({2, PASS_TP_MID, false, false, 0, -1, 1});
+    st.push_back({0, PASS_TP_ROWS_INV, false, true, 0, -1, 2});
+    return st;
+  }
   const std::vector<int>& A = p->axes;
   if (A.empty()) {
     st.push_back({0, -1, true, true, 0, -1});  // N == 1: fused pass on a length-1 axis
     return st;
   }
-  const bool chunked = p->chunk_planes > 0 && A.size() == 3 && p->chunk_planes < p->n[2];
+  const bool chunked = p->chunk_planes > 0 && A.size() == 3 && A.back() == 2 && p->chunk_planes < p->n[2];
   if (chunked) {
     const i64 C = p->chunk_planes, nz = p->n[2];
     for (i64 z = 0; z < nz; z += C) {
@@ -229,10 +257,21 @@ int step_mode(const cfp_plan_s* p, const Step& q, bool diag_override) {
 int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStream_t s, std::vector<hipEvent_t>* ev) {
   if (!diag_override && p->sym_kind == 0)
     return set_error(CFP_ERR_ARG_WRONGSTATE, "no symbol set on plan (call cfp_plan_set_symbol_* first)");
-  std::vector<Step> st = apply_steps(p);
+  std::vector<Step> st = apply_steps(p, diag_override != nullptr);
   const double invN = 1.0 / (double)p->N;
   for (size_t i = 0; i < st.size(); ++i) {
     const Step& q = st[i];
+    if (q.tp >= 0) {
+      TPArgs a;
+      a.tw256 = p->tw[256];
+      a.colsym = p->colsym;
+      a.axsym = p->axsym;
+      a.scale = q.scale ? invN : 1.0;
+      if (ev) HIPCHK(hipEventRecord((*ev)[i], s));
+      hipError_t e = launch_three_pass(q.tp, q.from_b ? b : x, x, a, s);
+      if (e != hipSuccess) return hip_error(e, "3-sweep launch");
+      continue;
+    }
     i64 off = 0;
     PassDesc d = make_pass(p, q, step_mode(p, q, diag_override != nullptr), q.scale ? invN : 1.0, &off);
     if (diag_override) d.diag = diag_override;
@@ -340,9 +379,7 @@ extern "C" int cfp_plan_create(cfp_plan_t* plan, int64_t nx, int64_t ny, int64_t
   p->device = device;
   p->n[0] = nx; p->n[1] = ny; p->n[2] = nz;
   p->N = nx * ny * nz;
-  for (int a = 0; a < 3; ++a)
-    if (p->n[a] > 1) p->axes.push_back(a);
-  p->fused_axis = p->axes.empty() ? 0 : p->axes.back();
+  order_axes(p.get());
   for (int a : p->axes) {
     int rc = ensure_tw(p.get(), (int)p->n[a]);
     if (rc) return rc;
@@ -462,6 +499,24 @@ extern "C" int cfp_plan_set_chunking(cfp_plan_t p, int64_t chunk_planes) {
   return CFP_SUCCESS;
 }
 
+extern "C" int cfp_plan_set_schedule(cfp_plan_t p, int schedule) {
+  if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
+  if (schedule < CFP_SCHEDULE_AUTO || schedule > CFP_SCHEDULE_FIVE_PASS_YFUSED)
+    return set_error(CFP_ERR_ARG_OUTOFRANGE, "unknown schedule %d", schedule);
+  if (schedule == CFP_SCHEDULE_THREE_PASS && !three_pass_supported(p->n))
+    return set_error(CFP_ERR_SUP, "the 3-sweep schedule needs a 256x256x256 grid");
+  DeviceGuard dg(p->device);
+  const int f_old = p->fused_axis;
+  p->schedule = schedule;
+  order_axes(p);
+  // the separable tables are laid out for the fused axis: rebuild them if it moved
+  if (p->sym_kind == 1 && p->fused_axis != f_old) {
+    std::vector<cd> s[3] = {p->sym1d[0], p->sym1d[1], p->sym1d[2]};
+    return upload_separable(p, s);
+  }
+  return CFP_SUCCESS;
+}
+
 extern "C" int cfp_plan_num_passes(cfp_plan_t p, int* passes) {
   if (!p || !passes) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
   *passes = (int)apply_steps(p).size();
@@ -472,6 +527,14 @@ extern "C" int cfp_plan_pass_info(cfp_plan_t p, int pass, int* axis, int* n, int
   if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
   std::vector<Step> st = apply_steps(p);
   if (pass < 0 || pass >= (int)st.size()) return set_error(CFP_ERR_ARG_OUTOFRANGE, "pass index");
+  if (st[pass].tp >= 0) {  // 3-sweep launches: axis 3 = "x + y stage 1", 4 = "y stage 2 + z"
+    if (axis) *axis = st[pass].tp == 1 ? 4 : 3;
+    if (n) *n = (int)p->n[0];
+    if (ncols) *ncols = p->N / p->n[0];
+    if (mode) *mode = st[pass].mode;
+    if (fast) *fast = 1;
+    return CFP_SUCCESS;
+  }
   const int m = step_mode(p, st[pass], false);
   i64 off = 0;
   PassDesc d = make_pass(p, st[pass], m, 1.0, &off);

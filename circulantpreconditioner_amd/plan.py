@@ -49,7 +49,9 @@ def _lam6(lam: Sequence) -> ctypes.Array:
     return (ctypes.c_double * 6)(*vals)
 
 
-PASS_MODES = {0: "fwd", 1: "inv", 2: "fused_sep", 3: "fused_diag"}
+PASS_MODES = {0: "fwd", 1: "inv", 2: "fused_sep", 3: "fused_diag", 4: "fused_wave", 5: "rows_fwd", 6: "mid_fused",
+              7: "rows_inv"}
+PASS_AXES = {0: "x", 1: "y", 2: "z", 3: "xy", 4: "yz"}
 
 
 class CirculantPlan:
@@ -149,6 +151,14 @@ class CirculantPlan:
         check(lib().cfp_plan_set_chunking(self._h, int(chunk_planes)))
         return self
 
+    SCHEDULES = {"auto": 0, "five": 1, "three": 2, "five_y": 3}
+
+    def set_schedule(self, schedule: str | int) -> "CirculantPlan":
+        """'auto'/'five' (z fused), 'five_y' (y fused) or 'three' (256^3: 3 sweeps)."""
+        v = self.SCHEDULES[schedule] if isinstance(schedule, str) else int(schedule)
+        check(lib().cfp_plan_set_schedule(self._h, v))
+        return self
+
     # ---------------------------------------------------------------- introspection
     def passes(self) -> list:
         n = ctypes.c_int()
@@ -159,7 +169,7 @@ class CirculantPlan:
             nc = ctypes.c_int64()
             check(lib().cfp_plan_pass_info(self._h, i, ctypes.byref(ax), ctypes.byref(nn), ctypes.byref(nc),
                                            ctypes.byref(mode), ctypes.byref(fast)))
-            out.append({"axis": "xyz"[ax.value], "n": nn.value, "ncols": nc.value,
+            out.append({"axis": PASS_AXES[ax.value], "n": nn.value, "ncols": nc.value,
                         "mode": PASS_MODES[mode.value], "fast": bool(fast.value)})
         return out
 

@@ -90,6 +90,17 @@ int cfp_plan_backward(cfp_plan_t plan, const double *in_dev, double *out_dev, vo
  * 0 (default) = one launch per axis pass. */
 int cfp_plan_set_chunking(cfp_plan_t plan, int64_t chunk_planes);
 
+/* Apply schedule.  FIVE_PASS: x, y fwd, z fused with the symbol, y, x inv.
+ * FIVE_PASS_YFUSED: x, z fwd, y fused, z, x inv.  AUTO (default): YFUSED when ny, nz >= 512,
+ * else FIVE_PASS.  THREE_PASS (256^3 plans only, CFP_ERR_SUP
+ * otherwise; an explicit Diag still takes 5 passes): x + first y stage | last y stage + z +
+ * symbol + inverses | inverse of the first, 96 N bytes instead of 160 N. */
+#define CFP_SCHEDULE_AUTO 0
+#define CFP_SCHEDULE_FIVE_PASS 1
+#define CFP_SCHEDULE_THREE_PASS 2
+#define CFP_SCHEDULE_FIVE_PASS_YFUSED 3
+int cfp_plan_set_schedule(cfp_plan_t plan, int schedule);
+
 /* Introspection: number of kernel launches of one apply, and per-launch timing.
  * cfp_plan_time_passes runs `iters` applies and writes the mean duration (ms) of each of the
  * apply's launches into ms_out[0..passes) (HIP events on `stream`). */

@@ -246,3 +246,62 @@ def test_chunked_schedule_vs_oracle(cp, oracle, n, chunk):
         t = _dev(b)
         plan.apply(t, out=t)
         assert _rel(t, ref) < TOL
+
+
+# ------------------------------------------------------------------ 3-sweep schedule (256^3)
+@pytest.mark.parametrize("lam", [(0.6, 0.15, 0.02), (55.6, 0.0, 0.0), (0.3 + 0.2j, 1.1, 0.7 - 0.4j)],
+                         ids=["bench", "transport", "complex"])
+def test_three_pass_vs_oracle(cp, oracle, lam):
+    n = (256, 256, 256)
+    N = int(np.prod(n))
+    b = oracle.c_fill_uniform(N, 97)
+    ref = oracle.c_solve_3d(oracle.c_build_diag_transport(n, lam), b, n)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam).set_schedule("three")
+        modes = [p["mode"] for p in plan.passes()]
+        assert modes == ["rows_fwd", "mid_fused", "rows_inv"]
+        x = plan.apply(_dev(b))
+        assert _rel(x, ref) < TOL
+        t = _dev(b)
+        plan.apply(t, out=t)  # in place (b == x), as KSPSolve(ksp, Un, Un) hands it
+        assert torch.equal(t, x)
+        plan.set_schedule("five")
+        assert len(plan.passes()) == 5
+        x5 = plan.apply(_dev(b))
+        assert _rel(x5, x) < 1e-13
+
+
+def test_three_pass_schedule_rules(cp):
+    n = (256, 256, 256)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol((0.5, 0.5, 0.5))
+        assert len(plan.passes()) == 5  # default: 5 passes
+        plan.set_schedule("three")
+        assert len(plan.passes()) == 3
+        d = torch.ones(256 ** 3, dtype=torch.complex128, device="cuda") * 2.0
+        b = torch.ones_like(d)
+        x = plan.apply_with_diag(d, b)  # explicit Diag: the 5-pass fused-Diag path serves it
+        assert torch.allclose(x, b / 2.0)
+    with cp.CirculantPlan((128, 128, 128)) as plan:
+        with pytest.raises(cp.CirculantError):
+            plan.set_schedule("three")
+        plan.set_transport_symbol((0.5, 0.5, 0.5))
+        assert len(plan.passes()) == 5
+
+
+@pytest.mark.parametrize("n", [(64, 32, 48), (256, 256, 256), (20, 12, 9), (32, 1, 16)])
+def test_y_fused_schedule_vs_oracle(cp, oracle, n):
+    lam = (0.6, 0.15 + 0.05j, 0.02)
+    N = int(np.prod(n))
+    b = oracle.c_fill_uniform(N, 41)
+    ref = oracle.c_solve_3d(oracle.c_build_diag_transport(n, lam), b, n)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam)
+        plan.set_schedule("five_y")  # after the symbol: the tables are rebuilt for y
+        ps = plan.passes()
+        if n[1] > 1 and n[2] > 1:
+            assert [p["axis"] for p in ps] == ["x", "z", "y", "z", "x"]
+        assert _rel(plan.apply(_dev(b)), ref) < TOL
+    with cp.CirculantPlan(n) as plan:
+        plan.set_schedule("five_y").set_transport_symbol(lam)  # before the symbol
+        assert _rel(plan.apply(_dev(b)), ref) < TOL
