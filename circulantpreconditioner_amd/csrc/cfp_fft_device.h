@@ -20,7 +20,17 @@ enum : int {
   F_REV = 8,        // walk the tiles in reverse block order
   F_NT_LD = 16,     // non-temporal global loads only
   F_NT_ST = 32,     // non-temporal global stores only
+  F_LDS_SYNC = 64,  // exchange barriers wait for LDS only (global loads may stay in flight)
 };
+
+// Workgroup barrier that waits only for this wave's LDS accesses: global loads issued earlier
+// (a prefetch of the next work unit) stay in flight across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+template <int FLAGS>
+__device__ __forceinline__ void xbarrier() {
+  if (FLAGS & F_LDS_SYNC) lds_barrier();
+  else __syncthreads();
+}
 
 // ------------------------------------------------------------------ complex helpers
 __device__ __forceinline__ cd cadd(cd a, cd b) { return make_cd(a.x + b.x, a.y + b.y); }
@@ -264,25 +274,25 @@ __device__ __forceinline__ int lds_idx(int c, int idx) {
 template <int N, bool ROW, int T, int FLAGS, int K, int PTS, class WP, class RP>
 __device__ __forceinline__ void exchange(void* ldsv, cd* vals, WP wpos, cd* dst, RP rpos, int c, bool first) {
   // vals may alias dst: all writes of a half complete (barrier) before its reads
-  if (!first) __syncthreads();
+  if (!first) xbarrier<FLAGS>();
   if (FLAGS & F_SPLIT_LDS) {
     double* lds = (double*)ldsv;
 #pragma unroll
     for (int k = 0; k < K; ++k) lds[lds_idx<N, ROW, T>(c, wpos(k))] = vals[k].x;
-    __syncthreads();
+    xbarrier<FLAGS>();
 #pragma unroll
     for (int t = 0; t < PTS; ++t) dst[t].x = lds[lds_idx<N, ROW, T>(c, rpos(t))];
-    __syncthreads();
+    xbarrier<FLAGS>();
 #pragma unroll
     for (int k = 0; k < K; ++k) lds[lds_idx<N, ROW, T>(c, wpos(k))] = vals[k].y;
-    __syncthreads();
+    xbarrier<FLAGS>();
 #pragma unroll
     for (int t = 0; t < PTS; ++t) dst[t].y = lds[lds_idx<N, ROW, T>(c, rpos(t))];
   } else {
     cd* lds = (cd*)ldsv;
 #pragma unroll
     for (int k = 0; k < K; ++k) lds[lds_idx<N, ROW, T>(c, wpos(k))] = vals[k];
-    __syncthreads();
+    xbarrier<FLAGS>();
 #pragma unroll
     for (int t = 0; t < PTS; ++t) dst[t] = lds[lds_idx<N, ROW, T>(c, rpos(t))];
   }

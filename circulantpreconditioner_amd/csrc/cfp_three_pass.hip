@@ -41,50 +41,54 @@ __device__ __forceinline__ cd dft4_quad(cd v, int k) {
 }
 }  // namespace
 
+// Persistent: a workgroup walks units blockIdx.x, + gridDim.x, ... (one per CU).  Prefetching
+// the next unit into VGPRs across LDS-only barriers was tried and lost: at 1024 threads the
+// extra registers spill (profiles/r01_schedule_sweep.txt).
 template <bool INV, int FLAGS>
-__global__ void __launch_bounds__(1024) k_tp_rows(const cd* in, cd* out, TPArgs a) {
+__global__ void __launch_bounds__(1024) k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
+  constexpr int F = FLAGS | F_SPLIT_LDS | F_LDS_SYNC;
   __shared__ __attribute__((aligned(16))) double lds[TN1 * RS];  // 136 KB: both layouts fit
   __shared__ cd tw_l[TN + TN1];                                  // W_256, then W_64
   const int tid = threadIdx.x;
   for (int i = tid; i < TN; i += 1024) tw_l[i] = a.tw256[i];
   for (int i = tid; i < TN1; i += 1024) tw_l[TN + i] = a.tw256[4 * i];
-  const int z = blockIdx.x / TN2, y2 = blockIdx.x % TN2;
-  const i64 plane = (i64)z * TN * TN;
-
-  // phase A: 64-point DFT over y1 for every x (column mode, 256 columns x 4 threads)
-  const int x = tid & (TN - 1), ty = tid >> 8;
-  cd v[16];
-#pragma unroll
-  for (int m = 0; m < 16; ++m) {
-    const int y1 = ty + 4 * m;
-    v[m] = gload<FLAGS>(in + plane + x + (i64)TN * (y2 + TN2 * y1));
-    if (INV) v[m] = cconj(v[m]);
-  }
-  fft_stages<TN1, 16, 4, false, TN, FLAGS | F_SPLIT_LDS>(v, lds, tw_l + TN, x, ty, true);  // v[m]: k1 = ty + 4 m
-
-  // phase B: transpose to rows k1 (row-mode layout), thread (row r, tx) gets x = tx + 16 m
-  const int r = tid >> 4, tx = tid & 15;
-  __syncthreads();  // phase A's last LDS reads are done
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
-#pragma unroll
-    for (int m = 0; m < 16; ++m) lds[(ty + 4 * m) * RS + x + (x >> 4)] = half ? v[m].y : v[m].x;
-    __syncthreads();
+  const int x = tid & (TN - 1), ty = tid >> 8;  // phase A: column x, thread ty of 4
+  const int r = tid >> 4, tx = tid & 15;        // phase C: row r, thread tx of 16
+  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+    // unit u = (z, y2): rows y2 + 4 y1 of plane z
+    const i64 plane = (i64)(u / TN2) * TN * TN;
+    const int y2 = u % TN2;
+    cd v[16];
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
-      const int xx = tx + 16 * m;
-      const double val = lds[r * RS + xx + (xx >> 4)];
-      if (half) v[m].y = val; else v[m].x = val;
+      v[m] = gload<FLAGS>(in + plane + x + (i64)TN * (y2 + TN2 * (ty + 4 * m)));
+      if (INV) v[m] = cconj(v[m]);
     }
-    __syncthreads();
-  }
-
-  // phase C: 256-point DFT along row r (row mode, 64 rows x 16 threads)
-  fft_stages<TN, 16, 16, true, TN1, FLAGS | F_SPLIT_LDS>(v, lds, tw_l, r, tx, true);  // v[m]: kx = tx + 16 m
-  const double sc = a.scale, sy = INV ? -sc : sc;
+    // phase A: 64-point DFT over y1 for every x (column mode, 256 columns x 4 threads)
+    fft_stages<TN1, 16, 4, false, TN, F>(v, lds, tw_l + TN, x, ty, true);  // v[m]: k1 = ty + 4 m
+    // phase B: transpose to rows k1, thread (row r, tx) gets x = tx + 16 m
+    lds_barrier();  // phase A's last LDS reads are done
 #pragma unroll
-  for (int m = 0; m < 16; ++m)
-    gstore<FLAGS>(out + plane + (tx + 16 * m) + (i64)TN * (y2 + TN2 * r), make_cd(v[m].x * sc, v[m].y * sy));
+    for (int half = 0; half < 2; ++half) {
+#pragma unroll
+      for (int m = 0; m < 16; ++m) lds[(ty + 4 * m) * RS + x + (x >> 4)] = half ? v[m].y : v[m].x;
+      lds_barrier();
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const int xx = tx + 16 * m;
+        const double val = lds[r * RS + xx + (xx >> 4)];
+        if (half) v[m].y = val; else v[m].x = val;
+      }
+      lds_barrier();
+    }
+    // phase C: 256-point DFT along row r (row mode, 64 rows x 16 threads)
+    fft_stages<TN, 16, 16, true, TN1, F>(v, lds, tw_l, r, tx, true);  // v[m]: kx = tx + 16 m
+    const double sc = a.scale, sy = INV ? -sc : sc;
+    cd* dst = out + plane + (i64)TN * (y2 + TN2 * r) + tx;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) gstore<FLAGS>(dst + 16 * m, make_cd(v[m].x * sc, v[m].y * sy));
+    lds_barrier();  // the next unit's first exchange overwrites LDS
+  }
 }
 
 template <int FLAGS>
@@ -123,12 +127,24 @@ __global__ void __launch_bounds__(1024) k_tp_mid(cd* data, TPArgs a) {
 
 bool three_pass_supported(const i64 n[3]) { return n[0] == TN && n[1] == TN && n[2] == TN; }
 
+static int cu_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+      cus = 256;
+  }
+  return cus;
+}
+
 hipError_t launch_three_pass(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
-  const unsigned blocks = TN * TN2;  // P1/P3: z-planes x y2; P2: x-tiles x k1 (16 x 64)
+  const int units = TN * TN2;  // P1/P3: z-planes x y2; P2: x-tiles x k1 (16 x 64)
+  const unsigned pgrid = (unsigned)(units < cu_count() ? units : cu_count());
   switch (stage) {
-    case 0: hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD>), dim3(blocks), dim3(1024), 0, s, in, out, a); break;
+    case 0: hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD>), dim3(pgrid), dim3(1024), 0, s, in, out, a, units); break;
     case 1: hipLaunchKernelGGL((k_tp_mid<0>), dim3((TN / 16) * TN1), dim3(1024), 0, s, out, a); break;
-    default: hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST>), dim3(blocks), dim3(1024), 0, s, in, out, a); break;
+    default: hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST>), dim3(pgrid), dim3(1024), 0, s, in, out, a, units); break;
   }
   return hipGetLastError();
 }

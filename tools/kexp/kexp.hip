@@ -35,6 +35,11 @@ static const Var kVars[] = {
     V(128, 16, 8, true, 32, 0, 0) V(128, 16, 8, true, 32, 0, 16) V(128, 16, 8, true, 32, 0, 32)
     V(128, 8, 2, false, 16, 0, 0) V(128, 8, 2, false, 16, 0, 16) V(128, 8, 2, false, 16, 0, 32)
     V(128, 8, 2, false, 16, 2, 0) V(128, 8, 2, false, 16, 2, 16) V(128, 8, 2, false, 16, 2, 32)
+    // N = 256 fused-pass shapes (27..36): non-split / split, PTS 16 / 8 / 4, T 8 / 16 / 32, LDS twiddles or global
+    V(256, 16, 16, false, 8, 2, 16) V(256, 16, 16, false, 16, 2, 16) V(256, 8, 4, false, 16, 2, 16)
+    V(256, 8, 4, false, 16, 2, 17) V(256, 8, 4, false, 8, 2, 16) V(256, 16, 16, false, 32, 2, 17)
+    V(256, 16, 16, false, 16, 2, 19) V(256, 4, 4, false, 16, 2, 16) V(256, 8, 4, false, 32, 2, 17)
+    V(256, 16, 16, false, 8, 2, 17)
 };
 
 extern "C" int kexp_count() { return (int)(sizeof(kVars) / sizeof(kVars[0])); }
