@@ -47,6 +47,12 @@ def _declare(L) -> None:
         "cfp_plan_backward": ([vp, dp, dp, vp], c_int),
         "cfp_plan_set_chunking": ([vp, i64], c_int),
         "cfp_plan_set_schedule": ([vp, c_int], c_int),
+        "cfp_rplan_create": ([P(vp), i64, i64, i64, c_int], c_int),
+        "cfp_rplan_destroy": ([vp], c_int),
+        "cfp_rplan_set_symbol_transport": ([vp, P(ctypes.c_double)], c_int),
+        "cfp_rplan_apply": ([vp, vp, vp, vp], c_int),
+        "cfp_rplan_num_passes": ([vp, P(c_int)], c_int),
+        "cfp_rplan_time_passes": ([vp, vp, vp, c_int, P(ctypes.c_double), vp], c_int),
         "cfp_plan_num_passes": ([vp, P(c_int)], c_int),
         "cfp_plan_pass_info": ([vp, c_int, P(c_int), P(c_int), P(i64), P(c_int), P(c_int)], c_int),
         "cfp_plan_time_passes": ([vp, dp, dp, c_int, dp, vp], c_int),
@@ -91,7 +97,7 @@ def exported_symbols() -> list:
     """Names of every cfp_* / PETSc-boundary function the library must export."""
     names = []
     for hdr in ("circulant_fft.h", "circulant_fft_dist.h", "pcshell_fft3d.h", "petsc_mini.h",
-                "transport_equation.h", "wave_system.h"):
+                "transport_equation.h", "wave_system.h", "circulant_fft_real.h"):
         path = os.path.join(os.path.dirname(_HERE), "include", hdr)
         if os.path.exists(path):
             names += _parse_decls(path)

@@ -17,3 +17,6 @@ int ilog2_exact(i64 v);
 Side natural_side(int axis, const i64 n[3]);
 void natural_cols(int axis, const i64 n[3], i64* ncols, i64* inner_n);
 }  // namespace cfp
+
+// internal plan option used by the real (r2c) plan, cfp_plan.hip
+extern "C" int cfp_plan_set_external_x(struct cfp_plan_s* plan, int on);

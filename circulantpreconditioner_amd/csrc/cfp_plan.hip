@@ -132,6 +132,7 @@ struct cfp_plan_s {
   std::vector<cd> sym1d[3];  // separable: lambda_d * c_d_hat (host copies)
   i64 chunk_planes = 0;      // > 0: chunked x/y schedule (see apply_steps)
   int schedule = CFP_SCHEDULE_AUTO;
+  bool external_x = false;  // x transformed by the caller (real plan): y/z passes only, no 1/N
 };
 
 namespace {
@@ -170,7 +171,7 @@ struct Step {
 
 // the 3-sweep schedule serves 256^3 grids with a separable symbol
 bool use_three_pass(const cfp_plan_s* p, bool diag_override) {
-  if (p->schedule != CFP_SCHEDULE_THREE_PASS || diag_override || p->sym_kind != 1) return false;
+  if (p->schedule != CFP_SCHEDULE_THREE_PASS || diag_override || p->sym_kind != 1 || p->external_x) return false;
   return three_pass_supported(p->n);
 }
 
@@ -183,7 +184,7 @@ void order_axes(cfp_plan_s* p) {
                   (p->schedule == CFP_SCHEDULE_AUTO && p->n[1] >= 512 && p->n[2] >= 512);
   const int* o = yf ? order_y : order_z;
   for (int i = 0; i < 3; ++i)
-    if (p->n[o[i]] > 1) p->axes.push_back(o[i]);
+    if (p->n[o[i]] > 1 && !(p->external_x && o[i] == 0)) p->axes.push_back(o[i]);
   p->fused_axis = p->axes.empty() ? 0 : p->axes.back();
 }
 
@@ -258,7 +259,7 @@ int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStr
   if (!diag_override && p->sym_kind == 0)
     return set_error(CFP_ERR_ARG_WRONGSTATE, "no symbol set on plan (call cfp_plan_set_symbol_* first)");
   std::vector<Step> st = apply_steps(p, diag_override != nullptr);
-  const double invN = 1.0 / (double)p->N;
+  const double invN = p->external_x ? 1.0 : 1.0 / (double)p->N;
   for (size_t i = 0; i < st.size(); ++i) {
     const Step& q = st[i];
     if (q.tp >= 0) {
@@ -510,6 +511,22 @@ extern "C" int cfp_plan_set_schedule(cfp_plan_t p, int schedule) {
   p->schedule = schedule;
   order_axes(p);
   // the separable tables are laid out for the fused axis: rebuild them if it moved
+  if (p->sym_kind == 1 && p->fused_axis != f_old) {
+    std::vector<cd> s[3] = {p->sym1d[0], p->sym1d[1], p->sym1d[2]};
+    return upload_separable(p, s);
+  }
+  return CFP_SUCCESS;
+}
+
+// internal (cfp_host.h): the real plan transforms x itself (r2c / c2r rows) and runs this
+// plan's y/z passes over the half spectrum without the 1/N scale
+extern "C" int cfp_plan_set_external_x(cfp_plan_t p, int on) {
+  if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
+  DeviceGuard dg(p->device);
+  const int f_old = p->fused_axis;
+  p->external_x = on != 0;
+  order_axes(p);
+  if (p->axes.empty()) return set_error(CFP_ERR_SUP, "external x needs a non-trivial y or z axis");
   if (p->sym_kind == 1 && p->fused_axis != f_old) {
     std::vector<cd> s[3] = {p->sym1d[0], p->sym1d[1], p->sym1d[2]};
     return upload_separable(p, s);

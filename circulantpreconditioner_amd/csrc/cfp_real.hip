@@ -1,0 +1,308 @@
+// cfp_real.hip -- real-data circulant apply (include/circulant_fft_real.h, SURVEY.md §8f row
+// f4): the reference's real-scalar solve_3D (src/FftLinearSolver_3D.c:6-78, 166-190) as an
+// r2c / half-spectrum / c2r schedule.
+//
+// x pass, forward (k_rx<false>): a real row of nx = 2M values is read as M complex values
+// z[j] = (x[2j], x[2j+1]) (no repacking: the same bytes), Z = FFT_M(z) in registers/LDS, then
+//     E[k] = (Z[k] + conj Z[M-k]) / 2,  O[k] = (Z[k] - conj Z[M-k]) / 2i,
+//     X[k] = E[k] + W_2M^k O[k]  (k < M),   X[M] = E[0] - O[0]  (Nyquist),
+// with Z[M-k] taken from the partner lane of the same row (cross-lane shuffle).  X[0..M) goes
+// to the half-spectrum grid H (M x ny x nz), X[M] to the Nyquist grid Q (1 x ny x nz).
+// y/z: the complex plan's passes on H and on Q (z fused with the symbol, no 1/N).
+// x pass, inverse (k_rx<true>): the even/odd merge run backwards, then IFFT_M and 2/N.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <memory>
+#include <vector>
+
+#include "../../include/circulant_fft.h"
+#include "../../include/circulant_fft_real.h"
+#include "cfp_fft_device.h"
+#include "cfp_host.h"
+
+namespace cfp {
+
+__device__ __forceinline__ cd shfl_cd(cd v, int lane) { return make_cd(__shfl(v.x, lane), __shfl(v.y, lane)); }
+
+// M = nx/2 points per row FFT, PTS points per thread, first radix R0, T rows per workgroup
+template <int M, int PTS, int R0, int T, bool INV>
+__global__ void __launch_bounds__(T*(M / PTS)) k_rx(const double* in_r, cd* half, cd* nyq, double* out_r,
+                                                    const cd* twn, i64 rows, double scale) {
+  constexpr int TPC = M / PTS;
+  static_assert(64 % TPC == 0, "a row's threads must sit in one wavefront");
+  constexpr int NT = T * TPC;
+  constexpr int LDS_N = T * (M + M / 16);
+  constexpr bool NEED_LDS = Shape<M, PTS, R0>::S > 1;
+  constexpr int F = F_SPLIT_LDS;
+  __shared__ __attribute__((aligned(16))) double lds[NEED_LDS ? LDS_N : 2];
+  __shared__ cd tws[M];  // W_M[k] = W_2M[2k]
+  const int tid = threadIdx.x;
+  for (int i = tid; i < M; i += NT) tws[i] = twn[2 * i];
+  const int tpc = tid % TPC, c = tid / TPC;
+  const i64 row = (i64)blockIdx.x * T + c;
+  const bool live = row < rows;
+  const int lane = tid & 63;
+  const int pl = lane - tpc + ((TPC - tpc) & (TPC - 1));  // lane of the mirror partner
+  cd v[PTS];
+  if (!INV) {
+    const cd* in = reinterpret_cast<const cd*>(in_r) + row * M;
+#pragma unroll
+    for (int t = 0; t < PTS; ++t) v[t] = live ? in[tpc + t * TPC] : make_cd(0.0, 0.0);
+    fft_stages<M, PTS, R0, true, T, F>(v, lds, tws, c, tpc, true);  // v[t] = Z[tpc + t TPC]
+#pragma unroll
+    for (int t = 0; t < PTS; ++t) {
+      const int k = tpc + t * TPC;
+      const cd za = shfl_cd(v[(PTS - t) % PTS], pl), zb = shfl_cd(v[PTS - 1 - t], pl);
+      const cd zm = tpc == 0 ? za : zb;  // Z[M - k]
+      const cd e = make_cd(0.5 * (v[t].x + zm.x), 0.5 * (v[t].y - zm.y));
+      const cd d = make_cd(v[t].x - zm.x, v[t].y + zm.y);  // Z[k] - conj Z[M-k]
+      const cd o = make_cd(0.5 * d.y, -0.5 * d.x);          // d / 2i
+      if (live) {
+        half[row * M + k] = cadd(e, cmul(twn[k], o));
+        if (k == 0) nyq[row] = csub(e, o);
+      }
+    }
+  } else {
+    cd X[PTS];
+    const cd* h = half + row * M;
+#pragma unroll
+    for (int t = 0; t < PTS; ++t) X[t] = live ? h[tpc + t * TPC] : make_cd(0.0, 0.0);
+    const cd xn = (live && tpc == 0) ? nyq[row] : make_cd(0.0, 0.0);
+#pragma unroll
+    for (int t = 0; t < PTS; ++t) {
+      const int k = tpc + t * TPC;
+      const cd xa = shfl_cd(X[(PTS - t) % PTS], pl), xb = shfl_cd(X[PTS - 1 - t], pl);
+      const cd xm = tpc == 0 ? (t == 0 ? xn : xa) : xb;  // X[M - k]
+      const cd e = make_cd(0.5 * (X[t].x + xm.x), 0.5 * (X[t].y - xm.y));
+      const cd d = make_cd(0.5 * (X[t].x - xm.x), 0.5 * (X[t].y + xm.y));
+      const cd o = cmul(d, cconj(twn[k]));  // (X[k] - conj X[M-k]) W^-k / 2
+      const cd z = make_cd(e.x - o.y, e.y + o.x);  // E + i O
+      v[t] = cconj(z);  // inverse FFT by conjugation
+    }
+    fft_stages<M, PTS, R0, true, T, F>(v, lds, tws, c, tpc, true);
+    cd* out = reinterpret_cast<cd*>(out_r) + row * M;
+    if (live) {
+#pragma unroll
+      for (int t = 0; t < PTS; ++t) out[tpc + t * TPC] = make_cd(v[t].x * scale, -v[t].y * scale);
+    }
+  }
+}
+
+// row-pass shapes per M (TPC = M / PTS divides 64)
+template <int M> struct RCfg;
+template <> struct RCfg<16> { static constexpr int PTS = 4, R0 = 4, T = 64; };
+template <> struct RCfg<32> { static constexpr int PTS = 8, R0 = 4, T = 64; };
+template <> struct RCfg<64> { static constexpr int PTS = 8, R0 = 8, T = 32; };
+template <> struct RCfg<128> { static constexpr int PTS = 8, R0 = 2, T = 16; };
+template <> struct RCfg<256> { static constexpr int PTS = 8, R0 = 4, T = 8; };
+template <> struct RCfg<512> { static constexpr int PTS = 16, R0 = 2, T = 8; };
+
+template <int M, bool INV>
+static hipError_t launch_rx_m(const double* in, cd* half, cd* nyq, double* out, const cd* twn, i64 rows, double sc,
+                              hipStream_t s) {
+  typedef RCfg<M> C;
+  const unsigned blocks = (unsigned)((rows + C::T - 1) / C::T);
+  hipLaunchKernelGGL((k_rx<M, C::PTS, C::R0, C::T, INV>), dim3(blocks), dim3(C::T * (M / C::PTS)), 0, s, in, half, nyq,
+                     out, twn, rows, sc);
+  return hipGetLastError();
+}
+
+static hipError_t launch_rx(int M, bool inv, const double* in, cd* half, cd* nyq, double* out, const cd* twn, i64 rows,
+                            double sc, hipStream_t s) {
+#define CFP_RX(MM)                                                                       \
+  case MM:                                                                               \
+    return inv ? launch_rx_m<MM, true>(in, half, nyq, out, twn, rows, sc, s)             \
+               : launch_rx_m<MM, false>(in, half, nyq, out, twn, rows, sc, s);
+  switch (M) {
+    CFP_RX(16) CFP_RX(32) CFP_RX(64) CFP_RX(128) CFP_RX(256) CFP_RX(512)
+    default: return hipErrorInvalidValue;
+  }
+#undef CFP_RX
+}
+
+}  // namespace cfp
+
+using namespace cfp;
+
+#define HIPCHK(expr)                                        \
+  do {                                                      \
+    hipError_t _e = (expr);                                 \
+    if (_e != hipSuccess) return cfp::hip_error(_e, #expr); \
+  } while (0)
+#define CFPCHK(expr)              \
+  do {                            \
+    int _r = (expr);              \
+    if (_r != CFP_SUCCESS) return _r; \
+  } while (0)
+
+struct cfp_rplan_s {
+  int device = 0;
+  i64 n[3] = {1, 1, 1};
+  i64 M = 1;
+  cfp_plan_t main = nullptr;  // M x ny x nz half spectrum, y/z passes only
+  cfp_plan_t nyq = nullptr;   // 1 x ny x nz Nyquist column kx = nx/2
+  cd* H = nullptr;
+  cd* Q = nullptr;
+  cd* twn = nullptr;  // W_nx
+  bool has_sym = false;
+  hipStream_t side = nullptr;  // the Nyquist grid's passes overlap the half-spectrum passes
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
+namespace {
+struct RGuard {
+  int prev = -1;
+  explicit RGuard(int dev) {
+    hipGetDevice(&prev);
+    if (prev != dev) hipSetDevice(dev);
+  }
+  ~RGuard() {
+    int cur;
+    hipGetDevice(&cur);
+    if (prev >= 0 && cur != prev) hipSetDevice(prev);
+  }
+};
+
+void free_rplan(cfp_rplan_s* p) {
+  if (p->main) cfp_plan_destroy(p->main);
+  if (p->nyq) cfp_plan_destroy(p->nyq);
+  if (p->H) hipFree(p->H);
+  if (p->Q) hipFree(p->Q);
+  if (p->twn) hipFree(p->twn);
+  if (p->fork) hipEventDestroy(p->fork);
+  if (p->join) hipEventDestroy(p->join);
+  if (p->side) hipStreamDestroy(p->side);
+  delete p;
+}
+
+int run_real(cfp_rplan_s* p, const double* b, double* x, hipStream_t s, std::vector<hipEvent_t>* ev) {
+  if (!p->has_sym) return set_error(CFP_ERR_ARG_WRONGSTATE, "no symbol set (call cfp_rplan_set_symbol_transport)");
+  const i64 rows = p->n[1] * p->n[2];
+  const double sc = 2.0 / (double)(p->n[0] * p->n[1] * p->n[2]);
+  if (ev) HIPCHK(hipEventRecord((*ev)[0], s));
+  hipError_t e = launch_rx((int)p->M, false, b, p->H, p->Q, nullptr, p->twn, rows, 1.0, s);
+  if (e != hipSuccess) return hip_error(e, "r2c row pass");
+  // small grids: the cross-stream handshake costs more than the Nyquist passes it hides
+  const bool overlap = p->M * rows >= (i64(1) << 21);
+  if (ev || !overlap) {  // timed, or small: the stages one after the other
+    HIPCHK(hipEventRecord((*ev)[1], s));
+    CFPCHK(cfp_plan_apply(p->main, (const double*)p->H, (double*)p->H, s));
+    HIPCHK(hipEventRecord((*ev)[2], s));
+    CFPCHK(cfp_plan_apply(p->nyq, (const double*)p->Q, (double*)p->Q, s));
+    HIPCHK(hipEventRecord((*ev)[3], s));
+  } else {  // Nyquist grid on the side stream, concurrently with the half spectrum
+    HIPCHK(hipEventRecord(p->fork, s));
+    HIPCHK(hipStreamWaitEvent(p->side, p->fork, 0));
+    CFPCHK(cfp_plan_apply(p->nyq, (const double*)p->Q, (double*)p->Q, p->side));
+    HIPCHK(hipEventRecord(p->join, p->side));
+    CFPCHK(cfp_plan_apply(p->main, (const double*)p->H, (double*)p->H, s));
+    HIPCHK(hipStreamWaitEvent(s, p->join, 0));
+  }
+  e = launch_rx((int)p->M, true, nullptr, p->H, p->Q, x, p->twn, rows, sc, s);
+  if (e != hipSuccess) return hip_error(e, "c2r row pass");
+  if (ev) HIPCHK(hipEventRecord((*ev)[4], s));
+  return CFP_SUCCESS;
+}
+}  // namespace
+
+extern "C" int cfp_rplan_create(cfp_rplan_t* plan, int64_t nx, int64_t ny, int64_t nz, int device) {
+  if (!plan) return set_error(CFP_ERR_ARG_NULL, "plan is NULL");
+  *plan = nullptr;
+  if (nx < 1 || ny < 1 || nz < 1) return set_error(CFP_ERR_ARG_OUTOFRANGE, "grid sizes must be >= 1");
+  const i64 M = nx / 2;
+  if (nx % 2 || M < 16 || M > 512 || (M & (M - 1)))
+    return set_error(CFP_ERR_SUP, "real plan: nx/2 must be a power of two in [16, 512] (nx = %lld)", (long long)nx);
+  if (ny * nz < 2) return set_error(CFP_ERR_SUP, "real plan: needs ny * nz > 1");
+  cfp_rplan_s* p = new cfp_rplan_s;
+  p->device = device;
+  p->n[0] = nx;
+  p->n[1] = ny;
+  p->n[2] = nz;
+  p->M = M;
+  int rc = cfp_plan_create(&p->main, M, ny, nz, device);
+  if (rc == CFP_SUCCESS) rc = cfp_plan_set_external_x(p->main, 1);
+  if (rc == CFP_SUCCESS) rc = cfp_plan_create(&p->nyq, 1, ny, nz, device);
+  if (rc == CFP_SUCCESS) rc = cfp_plan_set_external_x(p->nyq, 1);
+  if (rc != CFP_SUCCESS) {
+    free_rplan(p);
+    return rc;
+  }
+  RGuard g(device);
+  std::vector<cd> tw = host_twiddles((int)nx, -1);
+  hipError_t e = hipMalloc(&p->H, sizeof(cd) * (size_t)(M * ny * nz));
+  if (e == hipSuccess) e = hipMalloc(&p->Q, sizeof(cd) * (size_t)(ny * nz));
+  if (e == hipSuccess) e = hipMalloc(&p->twn, sizeof(cd) * (size_t)nx);
+  if (e == hipSuccess) e = hipMemcpy(p->twn, tw.data(), sizeof(cd) * (size_t)nx, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&p->fork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&p->join, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    free_rplan(p);
+    return hip_error(e, "real plan buffers");
+  }
+  *plan = p;
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_rplan_destroy(cfp_rplan_t p) {
+  if (!p) return CFP_SUCCESS;
+  RGuard g(p->device);
+  free_rplan(p);
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_rplan_set_symbol_transport(cfp_rplan_t p, const double lam[3]) {
+  if (!p || !lam) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  const std::vector<cd> hx = host_transport_symbol(p->n[0]), hy = host_transport_symbol(p->n[1]),
+                        hz = host_transport_symbol(p->n[2]);
+  const double lam6[6] = {lam[0], 0.0, lam[1], 0.0, lam[2], 0.0};
+  // half spectrum kx < nx/2, and the Nyquist column kx = nx/2
+  CFPCHK(cfp_plan_set_symbol_separable(p->main, (const double*)hx.data(), (const double*)hy.data(),
+                                       (const double*)hz.data(), lam6));
+  CFPCHK(cfp_plan_set_symbol_separable(p->nyq, (const double*)&hx[(size_t)p->M], (const double*)hy.data(),
+                                       (const double*)hz.data(), lam6));
+  p->has_sym = true;
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_rplan_apply(cfp_rplan_t p, const double* b, double* x, void* stream) {
+  if (!p || !b || !x) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  RGuard g(p->device);
+  return run_real(p, b, x, (hipStream_t)stream, nullptr);
+}
+
+extern "C" int cfp_rplan_num_passes(cfp_rplan_t p, int* passes) {
+  if (!p || !passes) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  *passes = 4;  // r2c rows | half-spectrum y/z plan | Nyquist y/z plan | c2r rows
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_rplan_time_passes(cfp_rplan_t p, const double* b, double* x, int iters, double* ms_out,
+                                     void* stream) {
+  if (!p || !b || !x || !ms_out) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  if (iters < 1) return set_error(CFP_ERR_ARG_OUTOFRANGE, "iters must be >= 1");
+  RGuard g(p->device);
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<hipEvent_t> ev(5);
+  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  double acc[4] = {0, 0, 0, 0};
+  int rc = CFP_SUCCESS;
+  for (int it = 0; it < iters && rc == CFP_SUCCESS; ++it) {
+    rc = run_real(p, b, x, s, &ev);
+    if (rc) break;
+    if (hipEventSynchronize(ev[4]) != hipSuccess) {
+      rc = set_error(CFP_ERR_LIB, "event sync");
+      break;
+    }
+    for (int i = 0; i < 4; ++i) {
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+      acc[i] += ms;
+    }
+  }
+  for (auto& e : ev) hipEventDestroy(e);
+  if (rc) return rc;
+  for (int i = 0; i < 4; ++i) ms_out[i] = acc[i] / iters;
+  return CFP_SUCCESS;
+}

@@ -232,3 +232,60 @@ def build_diag_3d(diag: torch.Tensor, cx_hat: torch.Tensor, cy_hat: torch.Tensor
                                   _dev_ptr(cy_hat, ny, "cy_hat"), _dev_ptr(cz_hat, nz, "cz_hat"), nx, ny, nz,
                                   _lam6(lam), _stream_handle(stream)))
     return diag
+
+
+class RealPlan:
+    """Real-data apply (include/circulant_fft_real.h): x = C^{-1} b for a
+    real float64 b and a real transport symbol, r2c / half spectrum / c2r, ~80 N bytes per
+    apply.  The reference's real-scalar solve_3D (src/FftLinearSolver_3D.c:6-78, 166-190)."""
+
+    def __init__(self, dims: Sequence[int], device: int | None = None):
+        nx, ny, nz = (int(d) for d in dims)
+        self.dims = (nx, ny, nz)
+        self.N = nx * ny * nz
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        h = ctypes.c_void_p()
+        check(lib().cfp_rplan_create(ctypes.byref(h), nx, ny, nz, self.device))
+        self._h = h
+
+    def set_transport_symbol(self, lam: Sequence[float]) -> "RealPlan":
+        vals = [float(v) for v in lam]
+        if len(vals) != 3:
+            raise ValueError("lambda must have three real entries")
+        check(lib().cfp_rplan_set_symbol_transport(self._h, (ctypes.c_double * 3)(*vals)))
+        return self
+
+    def _ptr(self, t: torch.Tensor, name: str) -> int:
+        if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous() or t.numel() != self.N:
+            raise ValueError(f"{name} must be a contiguous float64 device tensor of {self.N} elements")
+        return t.data_ptr()
+
+    def apply(self, b: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+        if out is None:
+            out = torch.empty_like(b)
+        check(lib().cfp_rplan_apply(self._h, self._ptr(b, "b"), self._ptr(out, "out"), _stream_handle(stream)))
+        return out
+
+    def time_passes(self, b: torch.Tensor, x: torch.Tensor, iters: int = 20, stream=None) -> list:
+        """Mean ms of the 4 stages: r2c rows, half-spectrum y/z, Nyquist y/z, c2r rows."""
+        ms = (ctypes.c_double * 4)()
+        check(lib().cfp_rplan_time_passes(self._h, self._ptr(b, "b"), self._ptr(x, "x"), int(iters), ms,
+                                          _stream_handle(stream)))
+        return list(ms)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().cfp_rplan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

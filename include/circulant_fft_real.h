@@ -1,0 +1,40 @@
+/*
+ * circulant_fft_real.h -- real-data variant of the circulant apply.
+ *
+ * The reference's real-scalar branch of solve_3D (src/FftLinearSolver_3D.c:6-78, 166-190:
+ * MATFFTW r2c, VecPointwiseDivideForRealFFT on the half spectrum, c2r, VecScale(X, 2./size))
+ * for a PETSc built with real scalars.  For real b and a real transport symbol
+ * (lambda_d real, so Diag(-k) = conj(Diag(k))) the solution x is real and only half of the
+ * spectrum is needed: this plan reads and writes real arrays (8 bytes per cell) and moves
+ * ~80 N bytes per apply instead of the complex plan's 160 N.
+ *
+ * Schedule: r2c along x (each real row is read as nx/2 complex values, FFT of length nx/2,
+ * even/odd split with the mirror bin from the partner lane), the y and z passes of the
+ * complex plan over the nx/2 x ny x nz half spectrum (+ the Nyquist column kx = nx/2 as its own
+ * 1 x ny x nz grid), z fused with the symbol, inverse y, then c2r along x with the 1/N scale.
+ * Requires nx even with nx/2 in {16, 32, ..., 512} and ny * nz > 1.
+ */
+#ifndef CFP_CIRCULANT_FFT_REAL_H
+#define CFP_CIRCULANT_FFT_REAL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct cfp_rplan_s *cfp_rplan_t;
+int cfp_rplan_create(cfp_rplan_t *plan, int64_t nx, int64_t ny, int64_t nz, int device);
+int cfp_rplan_destroy(cfp_rplan_t plan);
+/* real lambda_x, lambda_y, lambda_z of the transport symbol 1 + sum_d lambda_d (1 - e^{-i theta_d}) */
+int cfp_rplan_set_symbol_transport(cfp_rplan_t plan, const double lam[3]);
+/* x = C^{-1} b for real b (nx*ny*nz doubles on the device); x may alias b */
+int cfp_rplan_apply(cfp_rplan_t plan, const double *b, double *x, void *stream);
+/* launches of one apply and their mean duration (ms) over `iters` applies */
+int cfp_rplan_num_passes(cfp_rplan_t plan, int *passes);
+int cfp_rplan_time_passes(cfp_rplan_t plan, const double *b, double *x, int iters, double *ms_out, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFP_CIRCULANT_FFT_REAL_H */

@@ -40,6 +40,9 @@ static const Var kVars[] = {
     V(256, 8, 4, false, 16, 2, 17) V(256, 8, 4, false, 8, 2, 16) V(256, 16, 16, false, 32, 2, 17)
     V(256, 16, 16, false, 16, 2, 19) V(256, 4, 4, false, 16, 2, 16) V(256, 8, 4, false, 32, 2, 17)
     V(256, 16, 16, false, 8, 2, 17)
+    // reversed tile order (F_REV) of the product's 256 choices (37..41): x-fwd, y-fwd, fused, y-inv, x-inv
+    V(256, 8, 4, true, 8, 0, 24) V(256, 8, 4, false, 16, 0, 8) V(256, 16, 16, false, 16, 2, 25)
+    V(256, 8, 4, false, 16, 0, 40) V(256, 8, 4, true, 8, 0, 40)
 };
 
 extern "C" int kexp_count() { return (int)(sizeof(kVars) / sizeof(kVars[0])); }
