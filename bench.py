@@ -98,6 +98,7 @@ def main() -> int:
     ap.add_argument("--chunk", type=int, default=None,
                     help="z-planes per chunk of the Infinity-Cache-resident x/y schedule (0 = off; default: plan's)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--no-real", action="store_true", help="skip the real-data variant line item")
     args = ap.parse_args()
     grid = args.grid * 3 if len(args.grid) == 1 else args.grid
     if len(grid) != 3:
@@ -228,6 +229,34 @@ def main() -> int:
                       "alltoall_ms": [round(e, 5) for e in ex],
                       "alltoall_GBps_out_per_gpu": [round(sent / (e * 1e-3) / 1e9, 1) for e in ex]}
 
+    # row f4: the real-data variant on the same grid (real b, the same real lambda), reported
+    # beside the headline; the headline stays the complex apply
+    real_variant = None
+    if world == 1 and not args.no_real:
+        try:
+            rp = cp.RealPlan(grid, device=local_rank).set_transport_symbol([float(v) for v in LAM])
+            br = b.real.contiguous()
+            xr = torch.empty_like(br)
+            for _ in range(5):
+                rp.apply(br, out=xr)
+            torch.cuda.synchronize()
+            its = max(10, min(args.steps, 200))
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(its):
+                rp.apply(br, out=xr)
+            e1.record()
+            torch.cuda.synchronize()
+            rms = e0.elapsed_time(e1) / its
+            real_variant = {"value": round(1e3 / rms, 3), "unit": "PCApply/s", "ms_per_apply": round(rms, 5),
+                            "dtype": "f64 real b and x (r2c / half spectrum / c2r)",
+                            "stage_ms": [round(v, 5) for v in rp.time_passes(br, xr, iters=10)],
+                            "stages": ["r2c rows", "half-spectrum y/z", "Nyquist y/z", "c2r rows"]}
+            rp.close()
+            del br, xr
+        except Exception as e:  # unsupported grid or failure: report, never fake
+            real_variant = {"error": str(e)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -256,6 +285,8 @@ def main() -> int:
             "roofline_apply": roof_apply,
             "cpu_baseline": cpu,
         }
+        if real_variant is not None:
+            out["real_variant"] = real_variant
         if passes_info is not None:
             out["passes"] = passes_info
         print(json.dumps(out), flush=True)
