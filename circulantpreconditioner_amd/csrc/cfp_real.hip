@@ -186,11 +186,11 @@ int run_real(cfp_rplan_s* p, const double* b, double* x, hipStream_t s, std::vec
   // small grids: the cross-stream handshake costs more than the Nyquist passes it hides
   const bool overlap = p->M * rows >= (i64(1) << 21);
   if (ev || !overlap) {  // timed, or small: the stages one after the other
-    HIPCHK(hipEventRecord((*ev)[1], s));
+    if (ev) HIPCHK(hipEventRecord((*ev)[1], s));
     CFPCHK(cfp_plan_apply(p->main, (const double*)p->H, (double*)p->H, s));
-    HIPCHK(hipEventRecord((*ev)[2], s));
+    if (ev) HIPCHK(hipEventRecord((*ev)[2], s));
     CFPCHK(cfp_plan_apply(p->nyq, (const double*)p->Q, (double*)p->Q, s));
-    HIPCHK(hipEventRecord((*ev)[3], s));
+    if (ev) HIPCHK(hipEventRecord((*ev)[3], s));
   } else {  // Nyquist grid on the side stream, concurrently with the half spectrum
     HIPCHK(hipEventRecord(p->fork, s));
     HIPCHK(hipStreamWaitEvent(p->side, p->fork, 0));
