@@ -69,7 +69,7 @@ CFP_CFG(128, true, 1, 16, 8, 32, ST)
 CFP_CFG(128, true, 2, 16, 8, 32, LD)
 CFP_CFG(256, false, 0, 8, 4, 16, 0)
 CFP_CFG(256, false, 1, 8, 4, 16, ST)
-CFP_CFG(256, false, 2, 16, 16, 16, SPL | LD)
+CFP_CFG(256, false, 2, 16, 16, 16, SPL | LD | F_OCC4)
 CFP_CFG(256, true, 0, 8, 4, 8, LD)
 CFP_CFG(256, true, 1, 8, 4, 8, ST)
 CFP_CFG(256, true, 2, 8, 4, 8, LD)
