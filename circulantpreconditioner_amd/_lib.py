@@ -97,7 +97,7 @@ def exported_symbols() -> list:
     """Names of every cfp_* / PETSc-boundary function the library must export."""
     names = []
     for hdr in ("circulant_fft.h", "circulant_fft_dist.h", "pcshell_fft3d.h", "petsc_mini.h",
-                "transport_equation.h", "wave_system.h", "circulant_fft_real.h"):
+                "transport_equation.h", "wave_system.h", "circulant_fft_real.h", "mesh_unstructured.h"):
         path = os.path.join(os.path.dirname(_HERE), "include", hdr)
         if os.path.exists(path):
             names += _parse_decls(path)

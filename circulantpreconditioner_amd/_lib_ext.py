@@ -19,12 +19,12 @@ class PetscScalar(ctypes.Structure):
 
 
 class FFTPrecTransportContext(ctypes.Structure):
-    """struct FFTPrecTransportContext (src/PCSHELLFft_3D.hxx:8-21 + trailing plan)."""
+    """struct FFTPrecTransportContext (src/PCSHELLFft_3D.hxx:8-21 + trailing plan, remapBack)."""
     _fields_ = [("spaceDim", ctypes.c_int64), ("n_x", ctypes.c_int64), ("n_y", ctypes.c_int64),
                 ("n_z", ctypes.c_int64), ("lambda_x", PetscScalar), ("lambda_y", PetscScalar),
                 ("lambda_z", PetscScalar), ("FFT_MAT", ctypes.c_void_p), ("intersectionMatrix", ctypes.c_void_p),
                 ("Diag", ctypes.c_void_p), ("b_hat", ctypes.c_void_p), ("b_cartesien", ctypes.c_void_p),
-                ("plan", ctypes.c_void_p)]
+                ("plan", ctypes.c_void_p), ("remapBack", ctypes.c_void_p)]
 
 
 class StructuredTransportContext(ctypes.Structure):
@@ -182,6 +182,23 @@ def declare(L) -> None:
         "initial_conditions_shock_cartesian": ([i64, i64, i64, P(ctypes.c_double), P(ctypes.c_double), vp], c_int),
         "cfp_transport_config_default": ([P(TransportConfig), i64], None),
         "TransportEquationGMRES": ([P(TransportConfig), P(TransportResult), P(ctypes.c_double)], c_int),
+        # unstructured meshes, the PCSHELL remap and the mesh transport loop (include/mesh_unstructured.h)
+        "cfp_mesh_read_gmsh": ([cs, P(vp)], c_int),
+        "cfp_mesh_create": ([i64, P(ctypes.c_double), i64, P(i64), P(i64), P(vp)], c_int),
+        "cfp_mesh_destroy": ([vp], c_int),
+        "cfp_mesh_info": ([vp, P(i64), P(i64), P(i64), P(ctypes.c_double)], c_int),
+        "cfp_mesh_cell_geometry": ([vp, P(ctypes.c_double), P(ctypes.c_double)], c_int),
+        "cfp_mesh_min_ratio_vol_surf": ([vp, P(ctypes.c_double)], c_int),
+        "cfp_mesh_faces": ([vp, P(i64), P(i64), P(ctypes.c_double), P(ctypes.c_double)], c_int),
+        "cfp_mesh_crude_matrix_cartesian": ([vp, i64, i64, i64, P(ctypes.c_double), P(i64), P(i64), P(i64),
+                                             P(ctypes.c_double)], c_int),
+        "cfp_mesh_transport_csr": ([vp, ctypes.c_double, P(ctypes.c_double), c_int, ctypes.c_double, P(i64), P(i64),
+                                    P(i64), P(ctypes.c_double)], c_int),
+        "MatCreateMeshCartesianRemap": ([vp, i64, i64, i64, P(ctypes.c_double), P(vp), P(vp)], c_int),
+        "getFFTPrec3DContextMesh": ([i64, S, S, S, S, vp, vp], c_int),
+        "FFTPrec3DContextDestroyRemap": ([vp], c_int),
+        "initial_conditions_shock_mesh": ([vp, vp], c_int),
+        "TransportEquationGMRESMesh": ([vp, P(TransportConfig), P(TransportResult), P(ctypes.c_double)], c_int),
         # wave system (include/wave_system.h)
         "cfp_wave_plan_create": ([P(vp), i64, i64, i64, c_int], c_int),
         "cfp_wave_plan_destroy": ([vp], c_int),

@@ -322,12 +322,19 @@ extern "C" PetscErrorCode applyFFT3DPrecTransport(PC pc, Vec b, Vec x) {
   PetscCall(PCShellGetContext(pc, &ctx));
   PetscCheck(ctx && ctx->FFT_MAT && ctx->Diag, PETSC_COMM_SELF, PETSC_ERR_ARG_WRONGSTATE,
              "applyFFT3DPrecTransport: setupFFTPrec3D has not run");
+  const PetscInt N = ctx->n_x * ctx->n_y * ctx->n_z;
   Vec src = b;
   if (ctx->intersectionMatrix) {  // mesh -> Cartesian remap (identity when NULL)
     PetscCall(MatMult(ctx->intersectionMatrix, b, ctx->b_cartesien));
     src = ctx->b_cartesien;
   }
-  PetscCall(solve_3D(ctx->FFT_MAT, x, ctx->Diag, src, ctx->b_hat, ctx->n_x * ctx->n_y * ctx->n_z));
+  if (ctx->remapBack) {  // extra (mesh_unstructured.h): solve on the grid, then back to the mesh
+    if (src != ctx->b_cartesien) PetscCall(VecCopy(src, ctx->b_cartesien));
+    PetscCall(solve_3D(ctx->FFT_MAT, ctx->b_cartesien, ctx->Diag, ctx->b_cartesien, ctx->b_hat, N));
+    PetscCall(MatMult(ctx->remapBack, ctx->b_cartesien, x));
+    PetscFunctionReturn(PETSC_SUCCESS);
+  }
+  PetscCall(solve_3D(ctx->FFT_MAT, x, ctx->Diag, src, ctx->b_hat, N));
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 

@@ -21,7 +21,8 @@
  *     creates it, item 2);
  *   - FftTransportSolver/Fft3DSolver do not destroy the caller's FFT_MAT (item 6) and cache
  *     the symbol between calls with equal lambdas (item 9);
- *   - FFTPrecTransportContext has one extra trailing member (`plan`, owned by setup/destroy).
+ *   - FFTPrecTransportContext has two extra trailing members: `plan` (owned by
+ *     setup/destroy) and `remapBack` (the caller's, include/mesh_unstructured.h).
  */
 #ifndef CFP_PCSHELL_FFT3D_H
 #define CFP_PCSHELL_FFT3D_H
@@ -47,6 +48,8 @@ struct FFTPrecTransportContext {
   Vec b_hat;
   Vec b_cartesien;
   cfp_plan_t plan; /* extra: the HIP plan behind FFT_MAT (set up by setupFFTPrec3D) */
+  Mat remapBack;   /* extra: Cartesian -> mesh remap applied to the solve's result (NULL:
+                      x stays on the Cartesian grid, as the reference's apply leaves it) */
 };
 typedef struct FFTPrecTransportContext FFTPrecTransportContext;
 

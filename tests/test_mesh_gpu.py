@@ -1,0 +1,119 @@
+"""Row f3 on the GPU: the PCSHELL apply on unstructured meshes (intersectionMatrix -> circulant
+solve -> back-remap, src/PCSHELLFft_3D.cxx:10-24 with the matrix ToDo.md:12 asks for) and the
+implicit transport GMRES loop on a tetrahedral mesh (TransportEquation_impl_mpi with
+Mesh(filename), tests/TransportEquation_SphericalExplosion_impl_mpi.cxx:248-250).
+
+Oracle: oracle/mesh.py (polytope intersection volumes, numpy remap + FFT solve, face-loop
+operator) and scipy's sparse direct solve.  The mesh files are the reference's own FVCA6 meshes
+(tests/golden/meshes/)."""
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import scipy.sparse.linalg as spla
+import torch
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+MDIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "meshes")
+
+
+@pytest.fixture(scope="module")
+def mods():
+    from circulantpreconditioner_amd import mesh as M
+    from circulantpreconditioner_amd import petsc as P
+    from circulantpreconditioner_amd import transport as T
+    assert torch.cuda.is_available()
+    return M, P, T
+
+
+def _crude(m, dims):
+    rp, cl, vl = m.crude_matrix(dims)
+    return sp.csr_matrix((vl, cl, rp), shape=(int(np.prod(dims)), m.ncells))
+
+
+@pytest.mark.parametrize("name,oracle_v", [("mesh_tetra_0.msh", True), ("mesh_tetra_1.msh", False),
+                                           ("3DKershawTetra1.msh", False), ("mesh_hexa_3.msh", False)])
+def test_pcshell_apply_on_mesh(mods, name, oracle_v):
+    from oracle import mesh as OM
+    M, P, _ = mods
+    m = M.Mesh.read(os.path.join(MDIR, name))
+    dt, a = 0.05, (1.0, 0.5, -0.25)
+    ctx = M.getFFTPrec3DContextMesh(3, dt, a[0], a[1], a[2], m)
+    n = m.ncells
+    k = int(np.floor(np.cbrt(n)))
+    assert (ctx.n_x, ctx.n_y, ctx.n_z) == (k, k, k)  # src/PCSHELLFft_3D.cxx:124
+    lam = (complex(ctx.lambda_x), complex(ctx.lambda_y), complex(ctx.lambda_z))
+    np.testing.assert_allclose(lam, [ad * dt * 1.0 / k for ad in a], rtol=1e-15)  # a dt (max-min)/n
+    if name.startswith("mesh_hexa"):  # cells already in Cartesian order: identity, no remap
+        assert not ctx.intersectionMatrix and not ctx.remapBack
+    else:
+        assert ctx.intersectionMatrix and ctx.remapBack
+    pc = P.PC.shell(ctx).setup()
+    rng = np.random.default_rng(11)
+    b = rng.standard_normal(n) + 1j * rng.standard_normal(n)
+    tb = torch.from_numpy(b).cuda()
+    tx = torch.zeros(n, dtype=torch.complex128, device="cuda")
+    pc.apply(P.Vec.from_tensor(tb), P.Vec.from_tensor(tx))
+    torch.cuda.synchronize()
+    got = tx.cpu().numpy()
+    V = OM.crude_matrix(*OM.read_gmsh(os.path.join(MDIR, name)), (k, k, k)) if oracle_v else _crude(m, (k, k, k))
+    ref = OM.pc_apply(V, (k, k, k), lam, b)
+    assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < TOL
+    # a constant field is a fixed point of remap -> C^{-1} -> remap back (C 1 = 1)
+    tb.fill_(3.0 - 1.0j)
+    pc.apply(P.Vec.from_tensor(tb), P.Vec.from_tensor(tx))
+    torch.cuda.synchronize()
+    assert np.abs(tx.cpu().numpy() - (3.0 - 1.0j)).max() < 1e-12
+    pc.destroy()
+    M.destroy_remap(ctx)
+    assert not ctx.intersectionMatrix and not ctx.remapBack
+
+
+def _one_step_reference(M, m, sign):
+    """dt, the shifted operator and the initial field of one implicit step, from the mesh API."""
+    dt = (1e3 / 3) * m.min_ratio_vol_surf() / 1.0
+    rp, cl, vl = m.transport_csr(dt, (1.0, 0.0, 0.0), sign, shift=1.0)
+    A = sp.csr_matrix((vl, cl, rp), shape=(m.ncells, m.ncells))
+    _, ctr = m.geometry()
+    u0 = np.where(np.linalg.norm(ctr - 0.5, axis=1) < 0.3, 650.0, 600.0)
+    return dt, A, u0
+
+
+@pytest.mark.parametrize("sign", ["fixed", "reference"])
+def test_gmres_transport_on_tet_mesh(mods, sign):
+    from oracle import mesh as OM
+    M, _, T = mods
+    path = os.path.join(MDIR, "mesh_tetra_1.msh")
+    m = M.Mesh.read(path)
+    dt, A, u0 = _one_step_reference(M, m, sign)
+    xyz, cells = OM.read_gmsh(path)
+    B = OM.transport_csr(xyz, cells, dt, (1.0, 0.0, 0.0), sign, shift=1.0)
+    assert abs(A - B).max() <= 1e-12 * abs(B).max()
+    exact = spla.spsolve(A.tocsc(), u0.astype(np.complex128))
+    out = {}
+    for pc in ("none", "fft"):
+        cfg = T.config(8, pc=pc, sign=sign, lam="matched", steps=1)
+        res, u = M.run_transport(m, cfg, return_field=True)
+        assert abs(res["dt"] - dt) < 1e-14 * dt
+        out[pc] = res
+        if res["all_converged"]:
+            assert np.linalg.norm(u - exact) / np.linalg.norm(exact) < 1e-4
+    assert out["none"]["all_converged"] or out["fft"]["all_converged"]
+    assert out["fft"]["pc_calls"] >= out["fft"]["total_its"]
+
+
+def test_gmres_transport_on_aligned_hexa_equals_cartesian(mods):
+    """The uniform hexahedral mesh is the Cartesian grid: the mesh loop with the (permutation)
+    remap must reproduce the Cartesian loop's iterations and field."""
+    M, _, T = mods
+    m = M.Mesh.read(os.path.join(MDIR, "mesh_hexa_3.msh"))  # 8^3 hexahedra on the unit cube
+    perm = m.crude_matrix((8, 8, 8))[1]
+    cfg_m = T.config(8, pc="fft", sign="fixed", lam="matched", steps=2)
+    res_m, u_m = M.run_transport(m, cfg_m, return_field=True)
+    cfg_c = T.config(8, pc="fft", sign="fixed", lam="matched", steps=2, xmin=(0, 0, 0), xmax=(1, 1, 1))
+    res_c, u_c = T.run(cfg_c, return_field=True)
+    assert res_m["total_its"] == res_c["total_its"]
+    np.testing.assert_allclose(res_m["lambda"], res_c["lambda"], rtol=1e-14)
+    assert np.linalg.norm(u_m[perm] - u_c) / np.linalg.norm(u_c) < 1e-10
