@@ -27,7 +27,9 @@ import time
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--system", nargs="*", default=["transport", "wave"], choices=["transport", "wave"])
+    ap.add_argument("--system", nargs="*", default=["transport", "wave"], choices=["transport", "wave", "mesh"])
+    ap.add_argument("--mesh", nargs="*", default=["mesh_tetra_1.msh", "3DKershawTetra1.msh", "mesh_hexa_3.msh"],
+                    help="tests/golden/meshes/ files for --system mesh (row f3: the PCSHELL with the remap)")
     ap.add_argument("--wave-grid", type=int, nargs="*", default=[128])
     ap.add_argument("--wave-steps", type=int, default=1,
                     help="wave time steps (the reference loop to tmax = 0.05 is ~81 steps at 128^3)")
@@ -50,6 +52,8 @@ def main(argv=None) -> int:
     lines = []
     if "wave" in args.system:
         lines += wave_lines(args)
+    if "mesh" in args.system:
+        lines += mesh_lines(args)
     for n in (args.grid if "transport" in args.system else []):
         for sign in args.sign:
             for pc in args.pc:
@@ -83,6 +87,38 @@ def main(argv=None) -> int:
             for line in lines:
                 f.write(json.dumps(line) + "\n")
     return 0
+
+
+def mesh_lines(args) -> list:
+    """The transport step on the reference's unstructured meshes (Mesh(filename) in
+    tests/TransportEquation_SphericalExplosion_impl_mpi.cxx:248-250) with PCNONE and with the
+    FFT PCSHELL behind the mesh -> Cartesian remap (row f3)."""
+    import os
+    from circulantpreconditioner_amd import mesh as M
+    from circulantpreconditioner_amd import transport as T
+    out = []
+    mdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "meshes")
+    for name in args.mesh:
+        m = M.Mesh.read(os.path.join(mdir, name))
+        for sign in args.sign:
+            for pc in args.pc:
+                kw = dict(pc=pc, sign=sign, device=True, max_its=args.max_its, lam="matched")
+                if args.steps:
+                    kw["steps"] = args.steps
+                t0 = time.perf_counter()
+                r = M.run_transport(m, T.config(8, **kw))
+                wall = time.perf_counter() - t0
+                its = max(1, r["total_its"])
+                line = {"metric": "GMRES transport step on a mesh", "mesh": name, "cells": m.ncells,
+                        "fft_grid": int(m.ncells ** (1 / 3) + 1e-9), "sign": sign, "pc": pc,
+                        "steps": r["steps"], "dt": r["dt"], "lambda": r["lambda"], "gmres_its": r["total_its"],
+                        "converged": bool(r["all_converged"]), "last_reason": r["last_reason"],
+                        "ms_per_solve": 1e3 * r["solve_seconds"] / max(1, r["steps"]),
+                        "ms_per_iteration": 1e3 * r["solve_seconds"] / its, "pc_calls": r["pc_calls"],
+                        "pc_s": r["pc_seconds"], "setup_s": r["setup_seconds"], "wall_s": wall}
+                print(json.dumps(line), flush=True)
+                out.append(line)
+    return out
 
 
 def wave_lines(args) -> list:

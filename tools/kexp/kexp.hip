@@ -43,6 +43,11 @@ static const Var kVars[] = {
     // reversed tile order (F_REV) of the product's 256 choices (37..41): x-fwd, y-fwd, fused, y-inv, x-inv
     V(256, 8, 4, true, 8, 0, 24) V(256, 8, 4, false, 16, 0, 8) V(256, 16, 16, false, 16, 2, 25)
     V(256, 8, 4, false, 16, 0, 40) V(256, 8, 4, true, 8, 0, 40)
+    // fused 256 with the 4-wave occupancy request F_OCC4 (42..49): product (split, nt loads), T 32 / 8,
+    // nt loads+stores, nt stores, PTS 8 split T 16, non-split, global twiddles
+    V(256, 16, 16, false, 16, 2, 145) V(256, 16, 16, false, 32, 2, 145) V(256, 16, 16, false, 8, 2, 145)
+    V(256, 16, 16, false, 16, 2, 133) V(256, 16, 16, false, 16, 2, 177) V(256, 8, 4, false, 16, 2, 145)
+    V(256, 16, 16, false, 16, 2, 144) V(256, 16, 16, false, 16, 2, 147)
 };
 
 extern "C" int kexp_count() { return (int)(sizeof(kVars) / sizeof(kVars[0])); }

@@ -25,6 +25,8 @@ X, Y, Y2, X2 = 1, 3, 5, 2
 if "--rev" in sys.argv:
     chains = {"product": (1, 3, 7, 5, 2), "rev y,y-inv": (1, 38, 7, 40, 2), "rev x,z,x-inv": (37, 3, 39, 5, 41),
               "rev all": (37, 38, 39, 40, 41), "rev y-fwd only": (1, 38, 7, 5, 2), "rev x-inv only": (1, 3, 7, 5, 41)}
+elif "--occ" in sys.argv:
+    chains = {L.kexp_name(f).decode(): (X, Y, f, Y2, X2) for f in [7] + list(range(42, 50))}
 else:
     chains = {L.kexp_name(f).decode(): (X, Y, f, Y2, X2) for f in [7] + list(range(27, 37))}
 res = {c: [] for c in chains}
