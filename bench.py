@@ -117,7 +117,11 @@ def main() -> int:
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("CFP_BENCH_BACKEND", "nccl")  # "gloo": one-GPU rehearsal of N > 1
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import circulantpreconditioner_amd as cp
 
