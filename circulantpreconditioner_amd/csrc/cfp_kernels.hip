@@ -19,8 +19,11 @@
 // Strided axes (y, z) give each workgroup T consecutive columns, so every wave-wide load
 // or store moves T*16 contiguous bytes per row of the tile; the contiguous axis (x) gives
 // each workgroup whole rows.
-// Generic path (any n <= 4096, incl. primes): LDS-resident mixed-radix Stockham with
-// direct O(r) sums per output, used for sizes the fast path does not instantiate.
+// Mixed-radix path (any n <= 4096, incl. primes; the reference's own 10, 100, 10x25x40 ...):
+// LDS-resident Stockham, one specialised radix (8, 4, 2, 3, 5, 7) per stage, butterflies
+// staged in VGPRs so the stages run in place in one LDS buffer.
+#include <cstring>
+
 #include "cfp_fft_device.h"
 
 namespace cfp {
@@ -162,152 +165,407 @@ static hipError_t launch_fast_n(const PassDesc& p, const cd* in, cd* out, const 
   return hipErrorInvalidValue;
 }
 
-// ----------------------------------------------------------------- generic path
-#define CFP_GEN_THREADS 256
-#define CFP_MAX_FACTORS 32
+// ----------------------------------------------------------------- mixed-radix path
+// Any n <= 4096 (the reference's own sizes are 10, 100, 10x25x40, ...; its default Cartesian
+// mesh is 100^3): an LDS-resident Stockham FFT with one radix per stage (8, 4, 2, 3, 5, 7 as
+// specialised in-register butterflies, any other prime as a direct sum).  A block owns G
+// columns (G a power of two in column mode, so the coalesced load / store of G consecutive
+// columns splits its index with a shift); stages ping-pong between two LDS buffers with one
+// barrier each; every runtime division (butterfly -> column, j mod Ns, row-mode index ->
+// column) is a multiply by a 40-bit magic number.  The symbol / wave solve of the fused modes
+// runs between the forward and the (conjugated) second transform, as in the fast path.
+#define CFP_MR_THREADS 256
+#define CFP_MR_MAXF 24
+#define CFP_MR_POINTS 2048  // target points per block (one LDS buffer: 32 KiB)
+#define CFP_MR_MAXPTS 2048  // most points per block of the in-place stages (larger: ping-pong)
 
-struct GArgs {
-  KArgs k;
-  int n;
-  int ncol_per_block;
-  i64 ncols;
-  int nfac;
-  int fac[CFP_MAX_FACTORS];
+struct MRStage {
+  int r;         // radix
+  int m;         // n / r butterflies per column
+  int ns;        // product of the earlier radices
+  int step;      // n / (ns r): twiddle W_n^{(j mod ns) step t}
+  uint64_t m_M;  // magic of m
+  uint64_t ns_M; // magic of ns
 };
 
-__device__ __forceinline__ i64 pt_off_gen(const Side& s, int k) {
-  return (i64)(k / s.seg_len) * s.seg_stride + (i64)(k % s.seg_len) * s.pt_stride;
+struct MRArgs {
+  KArgs k;
+  int n, G, gshift, L;  // points per column, columns per block, log2 G (column mode), LDS column stride
+  i64 ncols;
+  int nst;
+  MRStage st[CFP_MR_MAXF];
+  uint64_t n_M;                 // magic of n (row-mode index split)
+  uint64_t segin_M, segout_M;   // magic of the sides' segment lengths (split sides)
+  int tw_lds;                   // twiddle table copied into LDS
+  int pingpong;                 // a prime radix above 7: stages go A -> B (else in place, one buffer)
+  int nbuf;                     // LDS buffers of G * L points (2 for ping-pong or the wave solve)
+};
+
+__host__ __device__ inline uint64_t mr_magic(uint32_t d) { return ((1ull << 40) + d - 1) / d; }
+// floor(u / d) for u * d < 2^40 (u < 2^20, d <= 4096 here)
+__device__ __forceinline__ uint32_t mr_div(uint32_t u, uint64_t M) { return (uint32_t)(((uint64_t)u * M) >> 40); }
+
+__device__ __forceinline__ i64 mr_pt_off(const Side& s, int k, uint64_t segM) {
+  if (k < s.seg_len) return (i64)k * s.pt_stride;  // unsplit side (or the first segment)
+  const uint32_t q = mr_div((uint32_t)k, segM);
+  return (i64)q * s.seg_stride + (i64)(k - (int)q * s.seg_len) * s.pt_stride;
 }
 
-__device__ void gen_fft(cd*& A, cd*& B, const GArgs& g, int G) {
-  const int n = g.n;
-  int Ns = 1;
-  for (int f = 0; f < g.nfac; ++f) {
-    const int r = g.fac[f];
-    const int nr = n / r;
-    const int st1 = n / (Ns * r);
-    for (int i = threadIdx.x; i < G * n; i += blockDim.x) {
-      const int c = i / n, o = i - c * n;
-      const int q = o / Ns;
-      const int t = q % r;
-      const int jm = o % Ns;
-      const int j = (q / r) * Ns + jm;
-      const cd* col = A + c * n;
-      cd acc = make_cd(0.0, 0.0);
-      // exponent of W_n for input s: s * (jm*st1 + t*nr)  (mod n)
-      const int inc = (int)(((long long)jm * st1 + (long long)t * nr) % n);
-      int e = 0;
-      for (int sidx = 0; sidx < r; ++sidx) {
-        acc = cadd(acc, cmul(col[j + sidx * nr], g.k.tw[e]));
-        e += inc;
-        if (e >= n) e -= n;
-      }
-      B[c * n + o] = acc;
+// cos / sin(2 pi j / R), j = 0 .. R-1, for the odd specialised radices
+template <int R> struct OddTab;
+template <> struct OddTab<3> {
+  static constexpr double C[3] = {1.0, -0.5, -0.5};
+  static constexpr double S[3] = {0.0, 0.86602540378443864676, -0.86602540378443864676};
+};
+template <> struct OddTab<5> {
+  static constexpr double C[5] = {1.0, 0.30901699437494742410, -0.80901699437494742410, -0.80901699437494742410,
+                                  0.30901699437494742410};
+  static constexpr double S[5] = {0.0, 0.95105651629515357212, 0.58778525229247312917, -0.58778525229247312917,
+                                  -0.95105651629515357212};
+};
+template <> struct OddTab<7> {
+  static constexpr double C[7] = {1.0, 0.62348980185873353053, -0.22252093395631440429, -0.90096886790241912624,
+                                  -0.90096886790241912624, -0.22252093395631440429, 0.62348980185873353053};
+  static constexpr double S[7] = {0.0, 0.78183148246802980871, 0.97492791218182360702, 0.43388373911755812048,
+                                  -0.43388373911755812048, -0.97492791218182360702, -0.78183148246802980871};
+};
+
+// forward DFT of an odd R in registers, natural order: pairs a_t = x_t + x_{R-t},
+// b_t = x_t - x_{R-t};  y_k = x_0 + sum a_t cos(2 pi k t / R) - i sum b_t sin(2 pi k t / R),
+// y_{R-k} the same with +i.
+template <int R>
+__device__ __forceinline__ void dft_odd(cd* v) {
+  constexpr int H = (R - 1) / 2;
+  cd a[H], b[H];
+#pragma unroll
+  for (int t = 1; t <= H; ++t) {
+    a[t - 1] = cadd(v[t], v[R - t]);
+    b[t - 1] = csub(v[t], v[R - t]);
+  }
+  cd y0 = v[0];
+#pragma unroll
+  for (int t = 0; t < H; ++t) y0 = cadd(y0, a[t]);
+  cd out[R];
+  out[0] = y0;
+#pragma unroll
+  for (int k = 1; k <= H; ++k) {
+    double cr = v[0].x, ci = v[0].y, sr = 0.0, si = 0.0;
+#pragma unroll
+    for (int t = 1; t <= H; ++t) {
+      const double c = OddTab<R>::C[(k * t) % R], sn = OddTab<R>::S[(k * t) % R];
+      cr = fma(a[t - 1].x, c, cr);
+      ci = fma(a[t - 1].y, c, ci);
+      sr = fma(b[t - 1].x, sn, sr);
+      si = fma(b[t - 1].y, sn, si);
     }
-    __syncthreads();
-    cd* tmp = A; A = B; B = tmp;
-    Ns *= r;
+    // -i (sr + i si) = si - i sr
+    out[k] = make_cd(cr + si, ci - sr);
+    out[R - k] = make_cd(cr - si, ci + sr);
+  }
+#pragma unroll
+  for (int k = 0; k < R; ++k) v[k] = out[k];
+}
+
+template <int R>
+__device__ __forceinline__ void dft_small(cd* v) {
+  if constexpr (R == 2 || R == 4 || R == 8) dft_reg<R>(v);
+  else dft_odd<R>(v);
+}
+
+// one Stockham stage of compile-time radix R: A -> B, every butterfly of the block's columns
+template <int R>
+__device__ __forceinline__ void mr_stage(const cd* __restrict__ A, cd* __restrict__ B, const MRStage& S,
+                                         const cd* tw, int G, int L) {
+  const int nb = G * S.m;
+  for (int b = threadIdx.x; b < nb; b += CFP_MR_THREADS) {
+    const int c = (int)mr_div((uint32_t)b, S.m_M);
+    const int j = b - c * S.m;
+    const int q = (int)mr_div((uint32_t)j, S.ns_M);
+    const int jm = j - q * S.ns;
+    const cd* a = A + c * L + j;
+    cd v[R];
+    v[0] = a[0];
+    const int e = jm * S.step;
+#pragma unroll
+    for (int t = 1; t < R; ++t) v[t] = cmul(a[t * S.m], tw[e * t]);
+    dft_small<R>(v);
+    cd* o = B + c * L + q * S.ns * R + jm;
+#pragma unroll
+    for (int t = 0; t < R; ++t) o[t * S.ns] = v[t];
   }
 }
 
-__global__ void __launch_bounds__(CFP_GEN_THREADS) k_axis_generic(const cd* in, cd* out, GArgs g, int mode) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  cd* sm = reinterpret_cast<cd*>(smem_raw);
-  const int n = g.n, G = g.ncol_per_block;
-  cd* A = sm;
-  cd* B = sm + (size_t)G * n;
-  const i64 g0 = (i64)blockIdx.x * G;
-  for (int i = threadIdx.x; i < G * n; i += blockDim.x) {
-    const int c = i / n, k = i - c * n;
-    const i64 gg = g0 + c;
-    cd v = make_cd(0.0, 0.0);
-    if (gg < g.ncols) v = in[col_base(g.k.in, gg, g.k.inner_n) + pt_off_gen(g.k.in, k)];
-    if (mode == PASS_INV) v = cconj(v);
-    A[i] = v;
+// the same stage in place: every butterfly of this thread is read and transformed in VGPRs,
+// then (after a barrier) written back -- one LDS buffer instead of two, so twice the blocks
+// per CU.  QMAX bounds the butterflies per thread for blocks of at most CFP_MR_MAXPTS points.
+template <int R>
+__device__ __forceinline__ void mr_stage_inplace(cd* A, const MRStage& S, const cd* tw, int G, int L) {
+  constexpr int QMAX = (CFP_MR_MAXPTS / R + CFP_MR_THREADS - 1) / CFP_MR_THREADS;
+  const int nb = G * S.m;
+  cd v[QMAX][R];
+  int opos[QMAX];
+#pragma unroll
+  for (int qq = 0; qq < QMAX; ++qq) {
+    const int b = threadIdx.x + qq * CFP_MR_THREADS;
+    opos[qq] = -1;
+    if (b < nb) {
+      const int c = (int)mr_div((uint32_t)b, S.m_M);
+      const int j = b - c * S.m;
+      const int q = (int)mr_div((uint32_t)j, S.ns_M);
+      const int jm = j - q * S.ns;
+      const cd* a = A + c * L + j;
+      v[qq][0] = a[0];
+      const int e = jm * S.step;
+#pragma unroll
+      for (int t = 1; t < R; ++t) v[qq][t] = cmul(a[t * S.m], tw[e * t]);
+      dft_small<R>(v[qq]);
+      opos[qq] = c * L + q * S.ns * R + jm;
+    }
   }
   __syncthreads();
-  gen_fft(A, B, g, G);
-  if (mode == PASS_FUSED_WAVE) {
-    // columns 4j..4j+3 of the block are the 4 components of one cell (G % 4 == 0)
-    for (int i = threadIdx.x; i < G * n; i += blockDim.x) {
-      const int c = i / n, k = i - c * n;
-      const i64 gg = g0 + c;
-      if (gg >= g.ncols) continue;
-      double2 pq[3];
-      wave_cell_sym(g.k.wave, gg >> 2, pq);
-      pq[g.k.wave.fused] = g.k.wave.tab[g.k.wave.fused][k];
-      cd r[4];
-      const int c4 = c & ~3;
-      for (int j = 0; j < 4; ++j) r[j] = A[(c4 + j) * n + k];
-      B[i] = cconj(wave_solve(r, c & 3, pq, g.k.wave.c0sq));
+#pragma unroll
+  for (int qq = 0; qq < QMAX; ++qq) {
+    if (opos[qq] >= 0) {
+      cd* o = A + opos[qq];
+#pragma unroll
+      for (int t = 0; t < R; ++t) o[t * S.ns] = v[qq][t];
+    }
+  }
+}
+
+// a prime radix above 7: direct sums, W_R^{kt} = W_n^{((k t) mod R) m}
+__device__ __forceinline__ void mr_stage_prime(const cd* __restrict__ A, cd* __restrict__ B, const MRStage& S,
+                                               const cd* tw, int G, int L, int n) {
+  const int R = S.r;
+  const int nb = G * S.m * R;  // one output per thread iteration
+  for (int i = threadIdx.x; i < nb; i += CFP_MR_THREADS) {
+    const int b = i / R, k = i - b * R;
+    const int c = (int)mr_div((uint32_t)b, S.m_M);
+    const int j = b - c * S.m;
+    const int q = (int)mr_div((uint32_t)j, S.ns_M);
+    const int jm = j - q * S.ns;
+    const cd* a = A + c * L + j;
+    cd acc = make_cd(0.0, 0.0);
+    for (int t = 0; t < R; ++t) {
+      int ex = jm * S.step * t + ((k * t) % R) * S.m;
+      if (ex >= n) ex -= n;
+      acc = cadd(acc, cmul(a[t * S.m], tw[ex]));
+    }
+    B[c * L + q * S.ns * R + jm + k * S.ns] = acc;
+  }
+}
+
+// all stages; the result ends in *X (the buffers are swapped as the stages go)
+__device__ __forceinline__ void mr_fft(cd*& X, cd*& Y, const MRArgs& g, const cd* tw) {
+  if (!g.pingpong) {
+    for (int s = 0; s < g.nst; ++s) {
+      const MRStage& S = g.st[s];
+      switch (S.r) {
+        case 2: mr_stage_inplace<2>(X, S, tw, g.G, g.L); break;
+        case 3: mr_stage_inplace<3>(X, S, tw, g.G, g.L); break;
+        case 4: mr_stage_inplace<4>(X, S, tw, g.G, g.L); break;
+        case 5: mr_stage_inplace<5>(X, S, tw, g.G, g.L); break;
+        case 7: mr_stage_inplace<7>(X, S, tw, g.G, g.L); break;
+        default: mr_stage_inplace<8>(X, S, tw, g.G, g.L); break;
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  for (int s = 0; s < g.nst; ++s) {
+    const MRStage& S = g.st[s];
+    switch (S.r) {
+      case 2: mr_stage<2>(X, Y, S, tw, g.G, g.L); break;
+      case 3: mr_stage<3>(X, Y, S, tw, g.G, g.L); break;
+      case 4: mr_stage<4>(X, Y, S, tw, g.G, g.L); break;
+      case 5: mr_stage<5>(X, Y, S, tw, g.G, g.L); break;
+      case 7: mr_stage<7>(X, Y, S, tw, g.G, g.L); break;
+      case 8: mr_stage<8>(X, Y, S, tw, g.G, g.L); break;
+      default: mr_stage_prime(X, Y, S, tw, g.G, g.L, g.n); break;
     }
     __syncthreads();
-    cd* tmp = A; A = B; B = tmp;
-    gen_fft(A, B, g, G);
+    cd* t = X;
+    X = Y;
+    Y = t;
   }
-  if (mode == PASS_FUSED_SEP || mode == PASS_FUSED_DIAG) {
-    for (int i = threadIdx.x; i < G * n; i += blockDim.x) {
-      const int c = i / n, k = i - c * n;
+}
+
+template <bool ROW>
+__global__ void __launch_bounds__(CFP_MR_THREADS) k_axis_mixed(const cd* in, cd* out, MRArgs g, int mode) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  __shared__ i64 base_in[64], base_out[64];
+  const int n = g.n, G = g.G, L = g.L;
+  cd* X = reinterpret_cast<cd*>(smem_raw);
+  cd* Y = X + (size_t)G * L;  // second buffer (ping-pong stages, the wave solve's output)
+  const cd* tw = g.k.tw;
+  if (g.tw_lds) {
+    cd* t = X + (size_t)(g.nbuf * G * L);
+    for (int i = threadIdx.x; i < n; i += CFP_MR_THREADS) t[i] = g.k.tw[i];
+    tw = t;
+  }
+  const i64 g0 = (i64)blockIdx.x * G;
+  if (threadIdx.x < G) {
+    const i64 gg = g0 + threadIdx.x;
+    base_in[threadIdx.x] = gg < g.ncols ? col_base(g.k.in, gg, g.k.inner_n) : 0;
+    base_out[threadIdx.x] = gg < g.ncols ? col_base(g.k.out, gg, g.k.inner_n) : 0;
+  }
+  __syncthreads();
+  const int total = G * n;
+  auto split = [&](int i, int& c, int& k) {
+    if (ROW) { c = (int)mr_div((uint32_t)i, g.n_M); k = i - c * n; }
+    else { k = i >> g.gshift; c = i & (G - 1); }
+  };
+  for (int i = threadIdx.x; i < total; i += CFP_MR_THREADS) {
+    int c, k;
+    split(i, c, k);
+    cd v = make_cd(0.0, 0.0);
+    if (g0 + c < g.ncols) v = in[base_in[c] + mr_pt_off(g.k.in, k, g.segin_M)];
+    if (mode == PASS_INV) v = cconj(v);
+    X[c * L + k] = v;
+  }
+  __syncthreads();
+  mr_fft(X, Y, g, tw);
+  if (mode == PASS_FUSED_WAVE) {
+    // columns 4j..4j+3 of the block are the 4 components of one cell (G % 4 == 0)
+    for (int i = threadIdx.x; i < total; i += CFP_MR_THREADS) {
+      int c, k;
+      split(i, c, k);
+      const i64 gg = g0 + c;
+      cd r[4];
+      const int c4 = c & ~3;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = X[(c4 + j) * L + k];
+      cd w = make_cd(0.0, 0.0);
+      if (gg < g.ncols) {
+        double2 pq[3];
+        wave_cell_sym(g.k.wave, gg >> 2, pq);
+        pq[g.k.wave.fused] = g.k.wave.tab[g.k.wave.fused][k];
+        w = cconj(wave_solve(r, c & 3, pq, g.k.wave.c0sq));
+      }
+      Y[c * L + k] = w;
+    }
+    __syncthreads();
+    cd* t = X;
+    X = Y;
+    Y = t;
+    mr_fft(X, Y, g, tw);
+  } else if (mode == PASS_FUSED_SEP || mode == PASS_FUSED_DIAG) {
+    for (int i = threadIdx.x; i < total; i += CFP_MR_THREADS) {
+      int c, k;
+      split(i, c, k);
       const i64 gg = g0 + c;
       if (gg >= g.ncols) continue;
       cd d;
-      if (mode == PASS_FUSED_SEP) d = cadd(cadd(g.k.colsym[gg], g.k.axsym[k]), make_cd(1.0, 0.0));
-      else d = g.k.diag[col_base(g.k.in, gg, g.k.inner_n) + pt_off_gen(g.k.in, k)];
-      A[i] = cconj(cdiv(A[i], d));
+      if (mode == PASS_FUSED_SEP) {
+        d = cadd(cadd(g.k.colsym[gg], g.k.axsym[k]), make_cd(1.0, 0.0));
+        X[c * L + k] = cconj(cdiv_sym(X[c * L + k], d));
+      } else {
+        d = g.k.diag[base_in[c] + mr_pt_off(g.k.in, k, g.segin_M)];
+        X[c * L + k] = cconj(cdiv(X[c * L + k], d));
+      }
     }
     __syncthreads();
-    gen_fft(A, B, g, G);
+    mr_fft(X, Y, g, tw);
   }
   const double sc = g.k.scale;
   const double sy = (mode != PASS_FWD) ? -sc : sc;
-  for (int i = threadIdx.x; i < G * n; i += blockDim.x) {
-    const int c = i / n, k = i - c * n;
-    const i64 gg = g0 + c;
-    if (gg < g.ncols) out[col_base(g.k.out, gg, g.k.inner_n) + pt_off_gen(g.k.out, k)] = make_cd(A[i].x * sc, A[i].y * sy);
+  for (int i = threadIdx.x; i < total; i += CFP_MR_THREADS) {
+    int c, k;
+    split(i, c, k);
+    if (g0 + c < g.ncols) {
+      const cd v = X[c * L + k];
+      out[base_out[c] + mr_pt_off(g.k.out, k, g.segout_M)] = make_cd(v.x * sc, v.y * sy);
+    }
   }
 }
 
 static int factorize(int n, int* fac) {
   int nf = 0;
-  static const int pref[] = {16, 8, 4, 2, 3, 5, 7};
+  while (n % 8 == 0 && n > 1 && nf < CFP_MR_MAXF) { fac[nf++] = 8; n /= 8; }
+  static const int pref[] = {4, 2, 3, 5, 7};
   for (int r : pref) {
-    while (n % r == 0 && n > 1 && nf < CFP_MAX_FACTORS) { fac[nf++] = r; n /= r; }
+    while (n % r == 0 && n > 1 && nf < CFP_MR_MAXF) { fac[nf++] = r; n /= r; }
   }
-  for (int p = 11; n > 1 && nf < CFP_MAX_FACTORS; p += 2) {
+  for (int p = 11; n > 1 && nf < CFP_MR_MAXF; p += 2) {
     while (n % p == 0) { fac[nf++] = p; n /= p; }
     if ((long long)p * p > n && n > 1) { fac[nf++] = n; n = 1; }
   }
   return nf;
 }
 
-static const size_t kGenericMaxLds = 160 * 1024;
+static const size_t kMixedMaxLds = 160 * 1024 - 2 * 64 * sizeof(i64);  // minus the static base_in/base_out
 
 static hipError_t launch_generic(const PassDesc& p, const cd* in, cd* out, const KArgs& a, hipStream_t s) {
-  if (p.n < 1 || p.n > 4096) return hipErrorInvalidValue;
-  GArgs g;
+  if (p.n < 1 || p.n > 4096) return hipErrorNotSupported;
+  const bool row = p.in.pt_stride == 1 && p.out.pt_stride == 1 && p.in.seg_len >= p.n && p.out.seg_len >= p.n;
+  MRArgs g;
+  std::memset(&g, 0, sizeof(g));
   g.k = a;
   g.n = p.n;
   g.ncols = p.ncols;
-  g.nfac = p.n == 1 ? 0 : factorize(p.n, g.fac);
-  int G = 2048 / p.n;
+  int fac[CFP_MR_MAXF];
+  g.nst = p.n == 1 ? 0 : factorize(p.n, fac);
+  int G = CFP_MR_POINTS / p.n;
   if (G < 1) G = 1;
   if (G > 64) G = 64;
-  if ((i64)G > p.ncols) G = (int)p.ncols;
+  if (!row) {  // power of two for the shift split
+    int q = 1;
+    while (q * 2 <= G) q *= 2;
+    G = q;
+  }
+  if ((i64)G > p.ncols) {
+    G = (int)p.ncols;
+    if (!row) {
+      int q = 1;
+      while (q * 2 <= G) q *= 2;
+      G = q;
+    }
+  }
   if (p.mode == PASS_FUSED_WAVE) {  // whole cells (4 columns) per block
+    if (p.ncols % 4 != 0) return hipErrorInvalidValue;
     if (G < 4) G = 4;
     G &= ~3;
-    if (p.ncols % 4 != 0) return hipErrorInvalidValue;
   }
-  g.ncol_per_block = G;
-  const size_t lds = (size_t)2 * G * p.n * sizeof(cd);
-  if (lds > kGenericMaxLds) return hipErrorInvalidValue;
+  g.G = G;
+  g.gshift = ilog2(G);
+  g.L = row ? p.n : p.n + 1;
+  int ns = 1;
+  for (int i = 0; i < g.nst; ++i) {
+    MRStage& S = g.st[i];
+    S.r = fac[i];
+    S.m = p.n / fac[i];
+    S.ns = ns;
+    S.step = p.n / (ns * fac[i]);
+    S.m_M = mr_magic((uint32_t)S.m);
+    S.ns_M = mr_magic((uint32_t)ns);
+    ns *= fac[i];
+  }
+  g.n_M = mr_magic((uint32_t)p.n);
+  g.segin_M = mr_magic((uint32_t)(p.in.seg_len > 0 ? p.in.seg_len : 1));
+  g.segout_M = mr_magic((uint32_t)(p.out.seg_len > 0 ? p.out.seg_len : 1));
+  g.pingpong = 0;
+  for (int i = 0; i < g.nst; ++i)
+    if (fac[i] > 8) g.pingpong = 1;
+  if (G * p.n > CFP_MR_MAXPTS) g.pingpong = 1;
+  g.nbuf = (g.pingpong || p.mode == PASS_FUSED_WAVE) ? 2 : 1;
+  size_t lds = (size_t)g.nbuf * G * g.L * sizeof(cd);
+  g.tw_lds = lds + (size_t)p.n * sizeof(cd) <= 96 * 1024 ? 1 : 0;
+  if (g.tw_lds) lds += (size_t)p.n * sizeof(cd);
+  if (lds > kMixedMaxLds) return hipErrorInvalidConfiguration;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_axis_generic, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGenericMaxLds);
+    (void)hipFuncSetAttribute((const void*)k_axis_mixed<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kMixedMaxLds);
+    (void)hipFuncSetAttribute((const void*)k_axis_mixed<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kMixedMaxLds);
+    (void)hipGetLastError();  // a refused attribute must not surface as this launch's error
     attr_set = true;
   }
   const i64 blocks = (p.ncols + G - 1) / G;
-  hipLaunchKernelGGL(k_axis_generic, dim3((unsigned)blocks), dim3(CFP_GEN_THREADS), lds, s, in, out, g, p.mode);
+  if (row)
+    hipLaunchKernelGGL(k_axis_mixed<true>, dim3((unsigned)blocks), dim3(CFP_MR_THREADS), lds, s, in, out, g, p.mode);
+  else
+    hipLaunchKernelGGL(k_axis_mixed<false>, dim3((unsigned)blocks), dim3(CFP_MR_THREADS), lds, s, in, out, g, p.mode);
   return hipGetLastError();
 }
 
