@@ -312,6 +312,10 @@ def main() -> int:
             out["passes"] = passes_info
         print(json.dumps(out), flush=True)
     if world > 1:
+        # tear down the library's RCCL communicator on every rank together, before torch's
+        torch.cuda.synchronize()
+        dist.barrier()
+        plan.close()
         dist.barrier()
         dist.destroy_process_group()
     return 0
