@@ -27,7 +27,9 @@ import time
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--system", nargs="*", default=["transport", "wave"], choices=["transport", "wave", "mesh"])
+    ap.add_argument("--system", nargs="*", default=["transport", "wave"], choices=["transport", "wave", "mesh", "direct"])
+    ap.add_argument("--direct-grid", type=int, nargs="*", default=[10, 100, 256],
+                    help="--system direct: the direct-solver loop (TransportEquationFFT_impl) on n^3")
     ap.add_argument("--mesh", nargs="*", default=["mesh_tetra_1.msh", "3DKershawTetra1.msh", "mesh_hexa_3.msh"],
                     help="tests/golden/meshes/ files for --system mesh (row f3: the PCSHELL with the remap)")
     ap.add_argument("--wave-grid", type=int, nargs="*", default=[128])
@@ -54,6 +56,8 @@ def main(argv=None) -> int:
         lines += wave_lines(args)
     if "mesh" in args.system:
         lines += mesh_lines(args)
+    if "direct" in args.system:
+        lines += direct_lines(args)
     for n in (args.grid if "transport" in args.system else []):
         for sign in args.sign:
             for pc in args.pc:
@@ -87,6 +91,27 @@ def main(argv=None) -> int:
             for line in lines:
                 f.write(json.dumps(line) + "\n")
     return 0
+
+
+def direct_lines(args) -> list:
+    """The reference's direct-solver loop (tests/TransportEquationFFT_SphericalExplosion_impl_mpi.cxx,
+    ctests "10 10 10" and "100 100 100"): the reference run (tmax = 0.05: one step at cfl 1e3/3)
+    and 20 timed steps (one PetscFft3DTransportSolver(ctx, Un, Un) each, host-synchronous)."""
+    from circulantpreconditioner_amd import transport as T
+    out = []
+    for n in args.direct_grid:
+        for label, kw in (("reference run", {}), ("20 steps", {"steps": 20, "precision": 1e-30})):
+            t0 = time.perf_counter()
+            r = T.run_direct(T.config(n, device=True, **kw))
+            wall = time.perf_counter() - t0
+            line = {"metric": "direct FFT transport solve", "config": f"{n}^3 TransportEquationFFT, 1 MI355X",
+                    "grid": n, "run": label, "steps": r["steps"], "dt": r["dt"], "lambda": r["lambda"],
+                    "ms_per_step": 1e3 * r["solve_seconds"] / max(1, r["steps"]),
+                    "solves_per_s": r["steps"] / r["solve_seconds"] if r["solve_seconds"] > 0 else None,
+                    "setup_s": r["setup_seconds"], "wall_s": wall}
+            print(json.dumps(line), flush=True)
+            out.append(line)
+    return out
 
 
 def mesh_lines(args) -> list:

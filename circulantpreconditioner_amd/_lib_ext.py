@@ -182,6 +182,7 @@ def declare(L) -> None:
         "initial_conditions_shock_cartesian": ([i64, i64, i64, P(ctypes.c_double), P(ctypes.c_double), vp], c_int),
         "cfp_transport_config_default": ([P(TransportConfig), i64], None),
         "TransportEquationGMRES": ([P(TransportConfig), P(TransportResult), P(ctypes.c_double)], c_int),
+        "TransportEquationFFTDirect": ([P(TransportConfig), P(TransportResult), P(ctypes.c_double)], c_int),
         # unstructured meshes, the PCSHELL remap and the mesh transport loop (include/mesh_unstructured.h)
         "cfp_mesh_read_gmsh": ([cs, P(vp)], c_int),
         "cfp_mesh_create": ([i64, P(ctypes.c_double), i64, P(i64), P(i64), P(vp)], c_int),

@@ -292,4 +292,70 @@ extern "C" PetscErrorCode TransportEquationGMRES(const cfp_transport_config* cfg
   PetscCall(VecDestroy(&dUn));
   PetscFunctionReturn(PETSC_SUCCESS);
 }
+// TransportEquationFFT_impl_mpi, tests/TransportEquationFFT_SphericalExplosion_impl_mpi.cxx:20-150:
+// the direct-solver loop.  The FFT matrix is made once (:97-99) and reused every step (the
+// reference's Fft3DSolver destroys it after the first step, App. A item 6; here it survives).
+extern "C" PetscErrorCode TransportEquationFFTDirect(const cfp_transport_config* cfg, cfp_transport_result* res,
+                                                     double* U_out) {
+  PetscFunctionBeginUser;
+  PetscCheck(cfg && res, PETSC_COMM_SELF, PETSC_ERR_ARG_NULL, "TransportEquationFFTDirect: NULL argument");
+  std::memset((void*)res, 0, sizeof(*res));
+  const double t_setup = wall();
+  const PetscInt nx = cfg->nx, ny = cfg->ny, nz = cfg->nz, N = nx * ny * nz;
+  PetscCheck(nx >= 1 && ny >= 1 && nz >= 1, PETSC_COMM_SELF, PETSC_ERR_ARG_OUTOFRANGE, "grid sizes must be >= 1");
+  const int dim = nz > 1 ? 3 : (ny > 1 ? 2 : 1);
+  const double h[3] = {(cfg->xmax[0] - cfg->xmin[0]) / (double)nx, (cfg->xmax[1] - cfg->xmin[1]) / (double)ny,
+                       (cfg->xmax[2] - cfg->xmin[2]) / (double)nz};
+  // the velocity has dim components in the reference (Vector(getSpaceDimension())): the others are 0
+  const double a[3] = {cfg->a[0], dim > 1 ? cfg->a[1] : 0.0, dim > 2 ? cfg->a[2] : 0.0};
+  const double anorm = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+  PetscCheck(anorm > 0, PETSC_COMM_SELF, PETSC_ERR_ARG_OUTOFRANGE, "transport velocity is zero");
+  const double dt = cfg->cfl * cfp_cartesian_min_ratio_vol_surf(dim, h) / anorm;  // :44-45
+  res->dt = dt;
+  for (int d = 0; d < 3; ++d) res->lambda[d] = a[d] * dt / h[d];
+
+  Vec Un, dUn;
+  if (cfg->on_device) PetscCall(VecCreateSeqHIP(PETSC_COMM_SELF, N, &Un));
+  else PetscCall(VecCreateSeq(PETSC_COMM_SELF, N, &Un));
+  PetscCall(VecDuplicate(Un, &dUn));
+  PetscCall(initial_conditions_shock_cartesian(nx, ny, nz, cfg->xmin, cfg->xmax, Un));
+
+  Mat FFT_MAT;
+  const PetscInt dims[3] = {nz, ny, nx};
+  PetscCall(MatCreateFFT(PETSC_COMM_WORLD, 3, dims, MATFFTW, &FFT_MAT));  // :97-99
+  struct StructuredTransportContext ctx = {nx, ny, nz, a[0], a[1], a[2], dt, h[0], h[1], h[2], FFT_MAT};  // :100
+  res->setup_seconds = wall() - t_setup;
+
+  int64_t it = 0;
+  double time = 0.0;
+  bool stationary = false;
+  res->all_converged = 1;
+  while (it < cfg->ntmax && time <= cfg->tmax && !stationary) {  // :106
+    PetscCall(VecCopy(Un, dUn));
+    const double v = wall();
+    PetscCall(PetscFft3DTransportSolver(ctx, Un, Un));  // :111 (synchronous on return)
+    const double w = wall();
+    PetscCall(VecAXPY(dUn, -1.0, Un));
+    time += dt;
+    it += 1;
+    PetscReal norm;
+    PetscCall(VecNorm(dUn, NORM_2, &norm));
+    stationary = norm < cfg->precision;
+    res->solve_seconds += w - v;
+    res->pc_calls += 1;
+    res->last_norm_dU = norm;
+  }
+  res->steps = it;
+  res->time = time;
+  if (U_out) {
+    const PetscScalar* u;
+    PetscCall(VecGetArrayRead(Un, &u));
+    std::memcpy(U_out, (const void*)u, sizeof(double) * 2 * (size_t)N);
+    PetscCall(VecRestoreArrayRead(Un, &u));
+  }
+  PetscCall(MatDestroy(&FFT_MAT));
+  PetscCall(VecDestroy(&Un));
+  PetscCall(VecDestroy(&dUn));
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
 #endif  // CFP_WITH_PETSC

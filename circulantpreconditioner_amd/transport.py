@@ -91,3 +91,16 @@ def run(cfg: TransportConfig, return_field: bool = False):
     PetscCall(lib().TransportEquationGMRES(ctypes.byref(cfg), ctypes.byref(res), ptr))
     d = res.as_dict()
     return (d, out) if return_field else d
+
+
+def run_direct(cfg: TransportConfig, return_field: bool = False):
+    """TransportEquationFFTDirect: the reference's direct-solver time loop
+    (tests/TransportEquationFFT_SphericalExplosion_impl_mpi.cxx:20-150), one
+    PetscFft3DTransportSolver(ctx, Un, Un) per implicit step."""
+    res = TransportResult()
+    n = int(cfg.nx * cfg.ny * cfg.nz)
+    out = np.empty(n, dtype=np.complex128) if return_field else None
+    ptr = out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) if out is not None else None
+    PetscCall(lib().TransportEquationFFTDirect(ctypes.byref(cfg), ctypes.byref(res), ptr))
+    d = res.as_dict()
+    return (d, out) if return_field else d

@@ -96,6 +96,17 @@ void cfp_transport_config_default(cfp_transport_config *cfg, int64_t n);
 /* run the loop; if U_out != NULL the final field is copied there (interleaved re,im, N values) */
 PetscErrorCode TransportEquationGMRES(const cfp_transport_config *cfg, cfp_transport_result *res, double *U_out);
 
+/* ---- the direct-solver time loop (TransportEquationFFT_impl_mpi,
+ * tests/TransportEquationFFT_SphericalExplosion_impl_mpi.cxx:20-150): each implicit step is one
+ * PetscFft3DTransportSolver(ctx, Un, Un) with StructuredTransportContext {n, a, dt, delta}
+ * (:97-111), i.e. lambda_d = a_d dt / delta_d; dt = cfl minRatioVolSurf / |a| (:45); the loop
+ * runs while it < ntmax, time <= tmax and ||U^{n+1} - U^n|| >= precision (:106-118).
+ * cfg fields used: nx, ny, nz (the reference's argv; ny = nz = 1 in 1-D, nz = 1 in 2-D: its
+ * uninitialised ny / nz), xmin, xmax, a, cfl (reference main: 1e3 / dim),
+ * tmax, ntmax, precision, on_device.  res: steps, dt, time, last_norm_dU, solve_seconds (sum of
+ * the per-step solve times the reference prints as "solve cpu time", :121). */
+PetscErrorCode TransportEquationFFTDirect(const cfp_transport_config *cfg, cfp_transport_result *res, double *U_out);
+
 #ifdef __cplusplus
 }
 #endif
