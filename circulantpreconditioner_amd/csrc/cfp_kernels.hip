@@ -85,9 +85,9 @@ CFP_CFG(512, true, 2, 16, 2, 8, LD)
 CFP_CFG(1024, false, 0, 16, 4, 8, SPL | LD)
 CFP_CFG(1024, false, 1, 16, 4, 8, SPL | ST)
 CFP_CFG(1024, false, 2, 16, 4, 8, SPL | LD)
-CFP_CFG(1024, true, 0, 16, 4, 4, LD)
-CFP_CFG(1024, true, 1, 16, 4, 4, ST)
-CFP_CFG(1024, true, 2, 16, 4, 4, LD)
+CFP_CFG(1024, true, 0, 16, 4, 4, SPL | LD)
+CFP_CFG(1024, true, 1, 16, 4, 4, SPL | ST)
+CFP_CFG(1024, true, 2, 16, 4, 4, SPL | LD)
 #undef SPL
 #undef ST
 #undef LD

@@ -219,6 +219,31 @@ def test_full_size_residual(cp, n):
         assert all(p["fast"] for p in plan.passes())
 
 
+def test_max_size_1024_cubed(cp):
+    """The largest fast-path grid, 1024^3 (2^30 points, 16 GiB per vector): residual of C x = b
+    with in-place device arithmetic (peak ~4 vectors of HBM)."""
+    n = (1024, 1024, 1024)
+    N = 1024 ** 3
+    lam = (0.6, 0.15, 0.02)
+    b = torch.empty(N, dtype=torch.complex128, device="cuda")
+    cp.fill_uniform(b, 20251017)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam)
+        assert all(p["fast"] for p in plan.passes())
+        x = plan.apply(b)
+    u = x.view(1024, 1024, 1024)
+    y = x.clone().view(1024, 1024, 1024)
+    y.mul_(1 + sum(lam))
+    for l, dim in ((lam[0], 2), (lam[1], 1), (lam[2], 0)):
+        y.sub_(torch.roll(u, shifts=1, dims=dim), alpha=l)
+    y = y.view(-1)
+    y.sub_(b)
+    rel = float(torch.linalg.vector_norm(y) / torch.linalg.vector_norm(b))
+    del x, u, y, b
+    torch.cuda.empty_cache()
+    assert rel < 1e-12
+
+
 def test_errors(cp):
     with pytest.raises(cp.CirculantError):
         cp.CirculantPlan((0, 4, 4))

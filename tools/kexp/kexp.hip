@@ -48,6 +48,12 @@ static const Var kVars[] = {
     V(256, 16, 16, false, 16, 2, 145) V(256, 16, 16, false, 32, 2, 145) V(256, 16, 16, false, 8, 2, 145)
     V(256, 16, 16, false, 16, 2, 133) V(256, 16, 16, false, 16, 2, 177) V(256, 8, 4, false, 16, 2, 145)
     V(256, 16, 16, false, 16, 2, 144) V(256, 16, 16, false, 16, 2, 147)
+    // large rows (50..): 512 row T 8 nt-ld (product) / split / split T 4; 1024 row T 4 (product) /
+    // split / split T 2 / split + global twiddles; 1024 column T 8 split (product) / T 4 / tw global
+    V(512, 16, 2, true, 8, 0, 16) V(512, 16, 2, true, 8, 0, 17) V(512, 16, 2, true, 4, 0, 17)
+    V(1024, 16, 4, true, 4, 0, 16) V(1024, 16, 4, true, 4, 0, 17) V(1024, 16, 4, true, 2, 0, 17)
+    V(1024, 16, 4, true, 4, 0, 19) V(1024, 16, 4, false, 8, 0, 17) V(1024, 16, 4, false, 4, 0, 17)
+    V(1024, 16, 4, false, 8, 0, 19)
 };
 
 extern "C" int kexp_count() { return (int)(sizeof(kVars) / sizeof(kVars[0])); }

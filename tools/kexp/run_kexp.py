@@ -32,7 +32,7 @@ for n in only:
     colsym = (torch.randn(n * n, dtype=torch.complex128, device="cuda") * 0.1)
     axsym = (torch.randn(n, dtype=torch.complex128, device="cuda") * 0.1)
     bufs[n] = (a, torch.empty_like(a), tw, colsym, axsym)
-iters = {128: 50, 256: 20, 512: 4}
+iters = {128: 50, 256: 20, 512: 4, 1024: 2}
 runs = []
 for i in range(nv):
     if info[i]["n"] not in only:
