@@ -159,7 +159,11 @@ struct KArgs {
   const cd* axsym;
   const cd* diag;
   WaveSym wave;
+  Tw4 tw4;
 };
+
+// W_n^e of a long axis' four-step twiddle (e < n <= 4096^2)
+__device__ __forceinline__ cd tw4_at(const Tw4& t, i64 e) { return cmul(t.hi[e >> 12], t.lo[e & 4095]); }
 
 // ------------------------------------------------------------ wave-system block symbol
 // The periodic version of the wave-system operator (src/WaveSystem.cxx:92-176, 4 unknowns
@@ -396,6 +400,13 @@ k_axis_fast(const cd* in, cd* out, KArgs a) {
 #pragma unroll
     for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
   }
+  if constexpr (MODE == PASS_INV) {
+    if (a.tw4.lo) {  // uniform: the inverse of a long axis' first half, pre-twiddle
+      const i64 k1 = (g / a.tw4.kdiv) % a.tw4.n1;
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) v[m] = cmul(v[m], tw4_at(a.tw4, k1 * (tpc + m * TPC)));
+    }
+  }
   // the twiddle table copy is published by the first exchange's barrier
   fft_stages<N, PTS, R0, ROW, T, FLAGS>(v, lds_raw, tws, c, tpc, true);
 
@@ -437,6 +448,13 @@ k_axis_fast(const cd* in, cd* out, KArgs a) {
       }
     }
     fft_stages<N, PTS, R0, ROW, T, FLAGS>(v, lds_raw, tws, c, tpc, false);
+  }
+  if constexpr (MODE == PASS_FWD) {
+    if (a.tw4.lo) {  // uniform: a long axis' first half, post-twiddle W_n^{k1 m2}
+      const i64 k1 = (g / a.tw4.kdiv) % a.tw4.n1;
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) v[m] = cmul(v[m], tw4_at(a.tw4, k1 * (tpc + m * TPC)));
+    }
   }
   const bool conj_out = (MODE != PASS_FWD);
   const double sc = a.scale;

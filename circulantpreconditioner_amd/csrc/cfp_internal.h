@@ -40,6 +40,20 @@ enum PassMode : int {
   PASS_TP_ROWS_FWD = 5,  // x DFT + the 64-point stage of the y DFT
   PASS_TP_MID = 6,       // 4-point y stage + z DFT, symbol, and their inverses
   PASS_TP_ROWS_INV = 7,  // inverse of PASS_TP_ROWS_FWD, x 1/N
+  // long axes (n = n1 n2 > 4096, four-step) with no short axis to fuse: the symbol divide as
+  // its own sweep over the position-ordered spectrum (cfp_plan.hip); reported, not dispatched
+  PASS_SYM_DIVIDE = 8,
+};
+
+// Four-step twiddle of a long axis split n = n1 n2 (index k1 + n1 k2): the length-n2 pass over
+// k2 multiplies its output m2 of column group k1 by W_n^{k1 m2} (forward), or its input by the
+// same factor after the inverse's conjugation.  k1 = (g / kdiv) % n1 for column g;
+// W_n^e = hi[e >> 12] * lo[e & 4095].
+struct Tw4 {
+  const cd* lo = nullptr;  // W_n^j, j < 4096   (NULL: no four-step twiddle on this pass)
+  const cd* hi = nullptr;  // W_n^{4096 i}, i <= n / 4096
+  i64 kdiv = 1;
+  int n1 = 1;
 };
 
 // Separable parts of the wave-system block symbol (cfp_wave.hip): for axis d and frequency
@@ -62,6 +76,7 @@ struct PassDesc {
   const cd* axsym;   // [n]       (PASS_FUSED_SEP)
   const cd* diag;    // addressed like `in` (PASS_FUSED_DIAG)
   WaveSym wave;      // PASS_FUSED_WAVE
+  Tw4 tw4;           // four-step twiddle (PASS_FWD / PASS_INV of a long axis' first half)
 };
 
 __host__ __device__ inline cd make_cd(double x, double y) { cd r; r.x = x; r.y = y; return r; }
@@ -75,5 +90,8 @@ hipError_t launch_fill_uniform(cd* x, i64 n, uint64_t seed, i64 offset, hipStrea
 hipError_t launch_build_diag_separable(cd* diag, const cd* cx, const cd* cy, const cd* cz, i64 nx, i64 ny,
                                        i64 nz, cd lx, cd ly, cd lz, hipStream_t s);
 hipError_t launch_sym_divide_inplace(cd* x, const cd* colsym, const cd* axsym, i64 n, hipStream_t s);
+// x[i] /= 1 + sx[ix] + sy[iy] + sz[iz] over an nx*ny*nz grid (position-indexed symbol tables)
+hipError_t launch_sym_divide_positions(cd* x, const cd* sx, const cd* sy, const cd* sz, i64 nx, i64 ny, i64 nz,
+                                       hipStream_t s);
 
 }  // namespace cfp

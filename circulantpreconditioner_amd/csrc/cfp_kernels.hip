@@ -421,6 +421,7 @@ __global__ void __launch_bounds__(CFP_MR_THREADS) k_axis_mixed(const cd* in, cd*
     cd v = make_cd(0.0, 0.0);
     if (g0 + c < g.ncols) v = in[base_in[c] + mr_pt_off(g.k.in, k, g.segin_M)];
     if (mode == PASS_INV) v = cconj(v);
+    if (mode == PASS_INV && g.k.tw4.lo) v = cmul(v, tw4_at(g.k.tw4, ((g0 + c) / g.k.tw4.kdiv % g.k.tw4.n1) * k));
     X[c * L + k] = v;
   }
   __syncthreads();
@@ -473,7 +474,8 @@ __global__ void __launch_bounds__(CFP_MR_THREADS) k_axis_mixed(const cd* in, cd*
     int c, k;
     split(i, c, k);
     if (g0 + c < g.ncols) {
-      const cd v = X[c * L + k];
+      cd v = X[c * L + k];
+      if (mode == PASS_FWD && g.k.tw4.lo) v = cmul(v, tw4_at(g.k.tw4, ((g0 + c) / g.k.tw4.kdiv % g.k.tw4.n1) * k));
       out[base_out[c] + mr_pt_off(g.k.out, k, g.segout_M)] = make_cd(v.x * sc, v.y * sy);
     }
   }
@@ -580,6 +582,7 @@ hipError_t launch_axis_pass(const PassDesc& p, const cd* in, cd* out, const cd* 
   a.axsym = p.axsym;
   a.diag = p.diag;
   a.wave = p.wave;
+  a.tw4 = p.tw4;
   if (p.ncols <= 0) return hipSuccess;
   if (fast_path_supported(p)) {
     switch (p.n) {
@@ -635,6 +638,16 @@ __global__ void k_build_diag(cd* d, const cd* cx, const cd* cy, const cd* cz, i6
   }
 }
 
+// the symbol divide of a grid whose long axes are split (no short axis to fuse it into):
+// x[i] /= ((sx[ix] + sy[iy]) + sz[iz]) + 1, the reference's summation order, position-indexed
+__global__ void k_sym_divide_positions(cd* x, const cd* sx, const cd* sy, const cd* sz, i64 nx, i64 ny, i64 N) {
+  for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (i64)gridDim.x * blockDim.x) {
+    const i64 ix = i % nx, iy = (i / nx) % ny, iz = i / (nx * ny);
+    const cd d = cadd(cadd(cadd(sx[ix], sy[iy]), sz[iz]), make_cd(1.0, 0.0));
+    x[i] = cdiv(x[i], d);
+  }
+}
+
 static unsigned ew_blocks(i64 n) {
   i64 b = (n + CFP_EW_THREADS - 1) / CFP_EW_THREADS;
   if (b > 8192) b = 8192;
@@ -650,6 +663,13 @@ hipError_t launch_pointwise_divide(cd* w, const cd* x, const cd* y, i64 n, hipSt
 hipError_t launch_scale(cd* x, cd alpha, i64 n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_scale, dim3(ew_blocks(n)), dim3(CFP_EW_THREADS), 0, s, x, alpha, n);
+  return hipGetLastError();
+}
+hipError_t launch_sym_divide_positions(cd* x, const cd* sx, const cd* sy, const cd* sz, i64 nx, i64 ny, i64 nz,
+                                       hipStream_t s) {
+  const i64 N = nx * ny * nz;
+  if (N <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sym_divide_positions, dim3(ew_blocks(N)), dim3(CFP_EW_THREADS), 0, s, x, sx, sy, sz, nx, ny, N);
   return hipGetLastError();
 }
 hipError_t launch_fill_uniform(cd* x, i64 n, uint64_t seed, i64 offset, hipStream_t s) {

@@ -133,6 +133,13 @@ struct cfp_plan_s {
   i64 chunk_planes = 0;      // > 0: chunked x/y schedule (see apply_steps)
   int schedule = CFP_SCHEDULE_AUTO;
   bool external_x = false;  // x transformed by the caller (real plan): y/z passes only, no 1/N
+  // long axes (n > 4096): four-step split n = n1 n2, both <= 4096 (0: a short axis).  Their
+  // spectrum stays in position order p = m1 + n1 m2 for frequency m = m2 + n2 m1.
+  int split[3][2] = {{0, 0}, {0, 0}, {0, 0}};
+  cd* tw4lo[3] = {nullptr, nullptr, nullptr};
+  cd* tw4hi[3] = {nullptr, nullptr, nullptr};
+  cd* possym[3] = {nullptr, nullptr, nullptr};  // position-indexed symbols (the standalone divide)
+  bool long_axes() const { return split[0][0] || split[1][0] || split[2][0]; }
 };
 
 namespace {
@@ -167,6 +174,8 @@ struct Step {
   bool scale;
   i64 z0, z1;  // z-plane range of an x or y pass (z1 < 0: whole grid)
   int tp = -1; // >= 0: stage of the 3-sweep schedule (cfp_three_pass.hip)
+  int sub = 0; // long axis: 1 = the length-n2 half (with the twiddle), 2 = the length-n1 half;
+               // 3 = the standalone symbol divide (no short axis to fuse)
 };
 
 // the 3-sweep schedule serves 256^3 grids with a separable symbol
@@ -182,10 +191,17 @@ void order_axes(cfp_plan_s* p) {
   // AUTO fuses y on large grids (512^3: 4 % faster, profiles/r01_schedule_sweep.txt), z otherwise
   const bool yf = p->schedule == CFP_SCHEDULE_FIVE_PASS_YFUSED ||
                   (p->schedule == CFP_SCHEDULE_AUTO && p->n[1] >= 512 && p->n[2] >= 512);
-  const int* o = yf ? order_y : order_z;
-  for (int i = 0; i < 3; ++i)
-    if (p->n[o[i]] > 1 && !(p->external_x && o[i] == 0)) p->axes.push_back(o[i]);
-  p->fused_axis = p->axes.empty() ? 0 : p->axes.back();
+  const int* o = (yf && !p->long_axes()) ? order_y : order_z;
+  std::vector<int> longs;
+  for (int i = 0; i < 3; ++i) {
+    if (p->n[o[i]] <= 1 || (p->external_x && o[i] == 0)) continue;
+    if (p->split[o[i]][0]) longs.push_back(o[i]);
+    else p->axes.push_back(o[i]);
+  }
+  // a long axis cannot carry the fused DFT / divide / IDFT pass: the last short axis does, and
+  // the long axes run first; with no short axis the divide is a sweep of its own (fused_axis -1)
+  p->fused_axis = p->axes.empty() ? (longs.empty() ? 0 : -1) : p->axes.back();
+  p->axes.insert(p->axes.begin(), longs.begin(), longs.end());
 }
 
 // The apply schedule: forward passes over all non-trivial axes but the last, the fused
@@ -207,7 +223,8 @@ std::vector<Step> apply_steps(const cfp_plan_s* p, bool diag_override = false) {
     st.push_back({0, -1, true, true, 0, -1});  // N == 1: fused pass on a length-1 axis
     return st;
   }
-  const bool chunked = p->chunk_planes > 0 && A.size() == 3 && A.back() == 2 && p->chunk_planes < p->n[2];
+  const bool chunked = p->chunk_planes > 0 && A.size() == 3 && A.back() == 2 && p->chunk_planes < p->n[2] &&
+                       !p->long_axes();
   if (chunked) {
     const i64 C = p->chunk_planes, nz = p->n[2];
     for (i64 z = 0; z < nz; z += C) {
@@ -221,6 +238,34 @@ std::vector<Step> apply_steps(const cfp_plan_s* p, bool diag_override = false) {
       st.push_back({1, PASS_INV, false, false, z, z1});
       st.push_back({0, PASS_INV, false, true, z, z1});
     }
+    return st;
+  }
+  if (p->long_axes()) {
+    // forward over every axis but the fused one (a long axis = its two halves), the fused pass
+    // or the standalone divide, then the inverses in reverse order; 1/N on the last launch
+    std::vector<int> nf;
+    for (int a : A)
+      if (a != p->fused_axis) nf.push_back(a);
+    for (int a : nf) {
+      if (p->split[a][0]) {
+        st.push_back({a, PASS_FWD, st.empty(), false, 0, -1, -1, 1});
+        st.push_back({a, PASS_FWD, false, false, 0, -1, -1, 2});
+      } else {
+        st.push_back({a, PASS_FWD, st.empty(), false, 0, -1, -1, 0});
+      }
+    }
+    if (p->fused_axis >= 0) st.push_back({p->fused_axis, -1, st.empty(), false, 0, -1, -1, 0});
+    else st.push_back({0, PASS_SYM_DIVIDE, false, false, 0, -1, -1, 3});
+    for (int i = (int)nf.size() - 1; i >= 0; --i) {
+      const int a = nf[i];
+      if (p->split[a][0]) {
+        st.push_back({a, PASS_INV, false, false, 0, -1, -1, 2});
+        st.push_back({a, PASS_INV, false, false, 0, -1, -1, 1});
+      } else {
+        st.push_back({a, PASS_INV, false, false, 0, -1, -1, 0});
+      }
+    }
+    st.back().scale = true;
     return st;
   }
   for (size_t i = 0; i + 1 < A.size(); ++i) st.push_back({A[i], PASS_FWD, i == 0, false, 0, -1});
@@ -242,6 +287,38 @@ PassDesc make_pass(const cfp_plan_s* p, const Step& q, int mode, double scale, i
   d.axsym = p->axsym;
   d.diag = p->diag;
   *offset = 0;
+  if (q.sub == 1 || q.sub == 2) {
+    // long axis a = four-step halves over k = k1 + n1 k2; lower = positions of the axes below a
+    const int a = q.axis;
+    const i64 n1 = p->split[a][0], n2 = p->split[a][1];
+    const i64 lower = a == 0 ? 1 : (a == 1 ? p->n[0] : p->n[0] * p->n[1]);
+    const i64 upper = p->N / (lower * p->n[a]);
+    Side sd;
+    sd.seg_stride = 0;
+    sd.inner_stride = 1;
+    if (q.sub == 1) {  // DFT over k2: columns (lower, k1) contiguous, then the upper axes
+      d.n = (int)n2;
+      sd.pt_stride = n1 * lower;
+      d.inner_n = lower * n1;
+      sd.outer_stride = lower * p->n[a];
+      d.ncols = lower * n1 * upper;
+      d.tw4.lo = p->tw4lo[a];
+      d.tw4.hi = p->tw4hi[a];
+      d.tw4.kdiv = lower;
+      d.tw4.n1 = (int)n1;
+    } else {  // DFT over k1: columns (lower), then (m2, upper) with one stride lower * n1
+      d.n = (int)n1;
+      sd.pt_stride = lower;
+      d.inner_n = lower;
+      sd.outer_stride = lower * n1;
+      d.ncols = lower * n2 * upper;
+      if (lower == 1) sd.inner_stride = 0;
+    }
+    sd.seg_len = d.n;
+    sd.seg_shift = ilog2_exact(d.n);
+    d.in = d.out = sd;
+    return d;
+  }
   if (q.z1 >= 0 && q.axis < 2) {
     const i64 planes = q.z1 - q.z0;
     d.ncols = planes * (q.axis == 0 ? p->n[1] : p->n[0]);
@@ -273,6 +350,13 @@ int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStr
       if (e != hipSuccess) return hip_error(e, "3-sweep launch");
       continue;
     }
+    if (q.sub == 3) {
+      if (ev) HIPCHK(hipEventRecord((*ev)[i], s));
+      hipError_t e = launch_sym_divide_positions(x, p->possym[0], p->possym[1], p->possym[2], p->n[0], p->n[1],
+                                                 p->n[2], s);
+      if (e != hipSuccess) return hip_error(e, "symbol divide");
+      continue;
+    }
     i64 off = 0;
     PassDesc d = make_pass(p, q, step_mode(p, q, diag_override != nullptr), q.scale ? invN : 1.0, &off);
     if (diag_override) d.diag = diag_override;
@@ -287,6 +371,9 @@ int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStr
 }
 
 int run_transform(cfp_plan_s* p, bool inverse, const cd* in, cd* out, hipStream_t s) {
+  if (p->long_axes())
+    return set_error(CFP_ERR_SUP, "forward / backward transforms of axes above 4096 are not exposed (their "
+                                  "spectrum stays in four-step order inside the apply)");
   if (p->axes.empty()) {
     if (in != out) HIPCHK(hipMemcpyAsync(out, in, sizeof(cd), hipMemcpyDeviceToDevice, s));
     return CFP_SUCCESS;
@@ -310,13 +397,40 @@ void free_symbol(cfp_plan_s* p) {
   if (p->axsym) hipFree(p->axsym);
   if (p->diag) hipFree(p->diag);
   p->colsym = p->axsym = p->diag = nullptr;
+  for (int a = 0; a < 3; ++a) {
+    if (p->possym[a]) hipFree(p->possym[a]);
+    p->possym[a] = nullptr;
+  }
   p->sym_kind = 0;
+}
+
+// frequency held at position q of a long axis: q = m1 + n1 m2 holds m = m2 + n2 m1
+i64 long_freq(const cfp_plan_s* p, int a, i64 q) {
+  const i64 n1 = p->split[a][0], n2 = p->split[a][1];
+  return q / n1 + n2 * (q % n1);
 }
 
 std::complex<double> lamc(const double lam[6], int a) { return {lam[2 * a], lam[2 * a + 1]}; }
 
 // Build colsym/axsym from per-axis host vectors s_d[k] = lambda_d * c_d_hat[k].
-int upload_separable(cfp_plan_s* p, const std::vector<cd> s[3]) {
+int upload_separable(cfp_plan_s* p, const std::vector<cd> s_nat[3]) {
+  // the kernels index the symbol by position: a long axis holds frequency long_freq(q) at q
+  std::vector<cd> s[3];
+  for (int a = 0; a < 3; ++a) {
+    s[a] = s_nat[a];
+    if (p->split[a][0])
+      for (i64 q = 0; q < p->n[a]; ++q) s[a][(size_t)q] = s_nat[a][(size_t)long_freq(p, a, q)];
+  }
+  if (p->fused_axis < 0) {  // no short axis: position-indexed tables for the standalone divide
+    free_symbol(p);
+    for (int a = 0; a < 3; ++a) {
+      HIPCHK(hipMalloc(&p->possym[a], sizeof(cd) * (size_t)p->n[a]));
+      HIPCHK(hipMemcpy(p->possym[a], s[a].data(), sizeof(cd) * (size_t)p->n[a], hipMemcpyHostToDevice));
+    }
+    for (int a = 0; a < 3; ++a) p->sym1d[a] = s_nat[a];
+    p->sym_kind = 1;
+    return CFP_SUCCESS;
+  }
   const int f = p->fused_axis;
   const i64 nf = p->n[f];
   i64 ncols, inner_n;
@@ -343,7 +457,7 @@ int upload_separable(cfp_plan_s* p, const std::vector<cd> s[3]) {
   HIPCHK(hipMalloc(&p->axsym, sizeof(cd) * (size_t)nf));
   HIPCHK(hipMemcpy(p->colsym, col.data(), sizeof(cd) * (size_t)ncols, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(p->axsym, ax.data(), sizeof(cd) * (size_t)nf, hipMemcpyHostToDevice));
-  for (int a = 0; a < 3; ++a) p->sym1d[a] = s[a];
+  for (int a = 0; a < 3; ++a) p->sym1d[a] = s_nat[a];
   p->sym_kind = 1;
   return CFP_SUCCESS;
 }
@@ -370,8 +484,22 @@ extern "C" int cfp_plan_create(cfp_plan_t* plan, int64_t nx, int64_t ny, int64_t
   if (!plan) return set_error(CFP_ERR_ARG_NULL, "plan is NULL");
   *plan = nullptr;
   if (nx < 1 || ny < 1 || nz < 1) return set_error(CFP_ERR_ARG_OUTOFRANGE, "grid sizes must be >= 1");
-  if (nx > 4096 || ny > 4096 || nz > 4096)
-    return set_error(CFP_ERR_SUP, "axis lengths above 4096 are not supported");
+  const int64_t dims_in[3] = {nx, ny, nz};
+  int split[3][2] = {{0, 0}, {0, 0}, {0, 0}};
+  for (int a = 0; a < 3; ++a) {
+    if (dims_in[a] <= 4096) continue;
+    // four-step: n = n1 n2 with both halves <= 4096, as balanced as possible
+    i64 best = 0;
+    for (i64 d = 2; d <= 4096; ++d)
+      if (dims_in[a] % d == 0 && dims_in[a] / d <= 4096) {
+        const i64 o = dims_in[a] / d;
+        if (best == 0 || std::llabs(d - o) < std::llabs(best - dims_in[a] / best)) best = d;
+      }
+    if (best == 0)
+      return set_error(CFP_ERR_SUP, "axis length %lld is not a product of two factors <= 4096", (long long)dims_in[a]);
+    split[a][0] = (int)best;
+    split[a][1] = (int)(dims_in[a] / best);
+  }
   int ndev = 0;
   HIPCHK(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return set_error(CFP_ERR_ARG_OUTOFRANGE, "device %d out of range", device);
@@ -380,8 +508,32 @@ extern "C" int cfp_plan_create(cfp_plan_t* plan, int64_t nx, int64_t ny, int64_t
   p->device = device;
   p->n[0] = nx; p->n[1] = ny; p->n[2] = nz;
   p->N = nx * ny * nz;
+  std::memcpy(p->split, split, sizeof(split));
   order_axes(p.get());
   for (int a : p->axes) {
+    if (p->split[a][0]) {
+      int rc = ensure_tw(p.get(), p->split[a][0]);
+      if (!rc) rc = ensure_tw(p.get(), p->split[a][1]);
+      if (rc) return rc;
+      // four-step twiddles W_n^j (j < 4096) and W_n^{4096 i} (i <= n / 4096), long double
+      const i64 n = p->n[a];
+      const i64 nhi = n / 4096 + 1;
+      std::vector<cd> lo(4096), hi((size_t)nhi);
+      const long double two_pi = 6.283185307179586476925286766559L;
+      for (i64 j = 0; j < 4096; ++j) {
+        const long double t = two_pi * (long double)j / (long double)n;
+        lo[(size_t)j] = make_cd((double)cosl(t), (double)-sinl(t));
+      }
+      for (i64 i = 0; i < nhi; ++i) {
+        const long double t = two_pi * (long double)((4096 * i) % n) / (long double)n;
+        hi[(size_t)i] = make_cd((double)cosl(t), (double)-sinl(t));
+      }
+      HIPCHK(hipMalloc(&p->tw4lo[a], sizeof(cd) * 4096));
+      HIPCHK(hipMalloc(&p->tw4hi[a], sizeof(cd) * (size_t)nhi));
+      HIPCHK(hipMemcpy(p->tw4lo[a], lo.data(), sizeof(cd) * 4096, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(p->tw4hi[a], hi.data(), sizeof(cd) * (size_t)nhi, hipMemcpyHostToDevice));
+      continue;
+    }
     int rc = ensure_tw(p.get(), (int)p->n[a]);
     if (rc) return rc;
   }
@@ -398,6 +550,10 @@ extern "C" int cfp_plan_destroy(cfp_plan_t p) {
   DeviceGuard dg(p->device);
   free_symbol(p);
   for (auto& kv : p->tw) hipFree(kv.second);
+  for (int a = 0; a < 3; ++a) {
+    if (p->tw4lo[a]) hipFree(p->tw4lo[a]);
+    if (p->tw4hi[a]) hipFree(p->tw4hi[a]);
+  }
   if (p->host_stage) hipFree(p->host_stage);
   delete p;
   return CFP_SUCCESS;
@@ -426,6 +582,7 @@ extern "C" int cfp_plan_set_symbol_separable(cfp_plan_t p, const double* cx, con
 
 extern "C" int cfp_plan_set_diag(cfp_plan_t p, const double* diag, int on_device) {
   if (!p || !diag) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  if (p->long_axes()) return set_error(CFP_ERR_SUP, "an explicit Diag needs axes <= 4096 (use a separable symbol)");
   DeviceGuard dg(p->device);
   free_symbol(p);
   HIPCHK(hipMalloc(&p->diag, sizeof(cd) * (size_t)p->N));
@@ -465,6 +622,7 @@ extern "C" int cfp_plan_apply(cfp_plan_t p, const double* b, double* x, void* st
 
 extern "C" int cfp_plan_apply_with_diag(cfp_plan_t p, const double* diag, const double* b, double* x, void* stream) {
   if (!p || !diag || !b || !x) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  if (p->long_axes()) return set_error(CFP_ERR_SUP, "an explicit Diag needs axes <= 4096 (use a separable symbol)");
   DeviceGuard dg(p->device);
   return run_apply(p, (const cd*)diag, (const cd*)b, (cd*)x, (hipStream_t)stream, nullptr);
 }
@@ -549,6 +707,14 @@ extern "C" int cfp_plan_pass_info(cfp_plan_t p, int pass, int* axis, int* n, int
     if (n) *n = (int)p->n[0];
     if (ncols) *ncols = p->N / p->n[0];
     if (mode) *mode = st[pass].mode;
+    if (fast) *fast = 1;
+    return CFP_SUCCESS;
+  }
+  if (st[pass].sub == 3) {  // the standalone symbol divide of an all-long grid
+    if (axis) *axis = -1;
+    if (n) *n = 1;
+    if (ncols) *ncols = p->N;
+    if (mode) *mode = PASS_SYM_DIVIDE;
     if (fast) *fast = 1;
     return CFP_SUCCESS;
   }

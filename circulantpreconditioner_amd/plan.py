@@ -50,8 +50,8 @@ def _lam6(lam: Sequence) -> ctypes.Array:
 
 
 PASS_MODES = {0: "fwd", 1: "inv", 2: "fused_sep", 3: "fused_diag", 4: "fused_wave", 5: "rows_fwd", 6: "mid_fused",
-              7: "rows_inv"}
-PASS_AXES = {0: "x", 1: "y", 2: "z", 3: "xy", 4: "yz"}
+              7: "rows_inv", 8: "sym_divide"}
+PASS_AXES = {-1: "-", 0: "x", 1: "y", 2: "z", 3: "xy", 4: "yz"}
 
 
 class CirculantPlan:

@@ -244,11 +244,58 @@ def test_max_size_1024_cubed(cp):
     assert rel < 1e-12
 
 
+LONG = [(8192, 1, 1), (10000, 1, 1), (4097, 1, 1), (4100, 3, 1), (6, 5000, 2), (3, 2, 4608), (65536, 1, 1),
+        (5000, 4, 6)]
+
+
+@pytest.mark.parametrize("n", LONG, ids=lambda n: "x".join(map(str, n)))
+def test_long_axes_vs_oracle(cp, oracle, n):
+    """Axes above 4096 (four-step split n = n1 n2): 1-D (the standalone divide) and mixed grids
+    (the short axis carries the fused pass), in place and out of place."""
+    N = int(np.prod(n))
+    lam = (0.6, 0.15, 0.02)
+    b = oracle.c_fill_uniform(N, 4)
+    ref = oracle.c_solve_3d(oracle.c_build_diag_transport(n, lam), b, n)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam)
+        x = plan.apply(_dev(b))
+        assert _rel(x, ref) < TOL, plan.passes()
+        t = _dev(b)
+        plan.apply(t, out=t)
+        assert _rel(t, ref) < TOL
+
+
+def test_long_axes_2d_residual(cp):
+    """8192 x 8192 (both axes long: 9 sweeps with the standalone divide), ||C x - b|| / ||b||."""
+    n = (8192, 8192, 1)
+    N = 8192 * 8192
+    lam = (0.6, 0.15, 0.0)
+    b = torch.empty(N, dtype=torch.complex128, device="cuda")
+    cp.fill_uniform(b, 11)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam)
+        modes = [p["mode"] for p in plan.passes()]
+        assert "sym_divide" in modes and len(modes) == 9
+        x = plan.apply(b)
+    r = apply_C_torch(x, n, lam) - b
+    assert float(torch.linalg.vector_norm(r) / torch.linalg.vector_norm(b)) < 1e-12
+
+
+def test_long_axes_limits(cp):
+    with pytest.raises(cp.CirculantError):
+        cp.CirculantPlan((4099, 1, 1))  # prime above 4096
+    with cp.CirculantPlan((8192, 1, 1)) as plan:
+        with pytest.raises(cp.CirculantError):
+            plan.forward(torch.zeros(8192, dtype=torch.complex128, device="cuda"))
+        with pytest.raises(cp.CirculantError):
+            plan.set_diag(torch.ones(8192, dtype=torch.complex128, device="cuda"))
+
+
 def test_errors(cp):
     with pytest.raises(cp.CirculantError):
         cp.CirculantPlan((0, 4, 4))
     with pytest.raises(cp.CirculantError):
-        cp.CirculantPlan((8192, 1, 1))
+        cp.CirculantPlan((8198, 1, 1))  # 2 x 4099: no split into two factors <= 4096
     with cp.CirculantPlan((8, 8, 8)) as plan:
         b = torch.zeros(512, dtype=torch.complex128, device="cuda")
         with pytest.raises(cp.CirculantError):
