@@ -53,7 +53,11 @@ const char *cfp_last_error(void);
 int cfp_device_count(int *count);
 int cfp_stream_sync(void *stream);
 
-/* ---- single-GPU plan: n_x, n_y, n_z >= 1, each <= 4096; `device` = HIP ordinal. */
+/* ---- single-GPU plan: n_x, n_y, n_z >= 1; `device` = HIP ordinal.  Axes up to 4096 take one
+ * pass each (powers of two 16..1024 register-resident, others LDS mixed-radix); a longer axis
+ * must be a product n1 n2 of two factors <= 4096 (four-step: two passes, spectrum kept in
+ * four-step order) -- for such plans cfp_plan_forward/backward and an explicit Diag
+ * (cfp_plan_set_diag, cfp_plan_apply_with_diag) return CFP_ERR_SUP; the symbol applies work. */
 int cfp_plan_create(cfp_plan_t *plan, int64_t nx, int64_t ny, int64_t nz, int device);
 int cfp_plan_destroy(cfp_plan_t plan);
 
