@@ -116,6 +116,9 @@ def main() -> int:
                     help="z-planes per chunk of the Infinity-Cache-resident x/y schedule (0 = off; default: plan's)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-real", action="store_true", help="skip the real-data variant line item")
+    ap.add_argument("--scaling-grid", type=int, nargs="+", default=[512],
+                    help="grid of the scaling_512 line item (BASELINE config 5; 0 = skip)")
+    ap.add_argument("--scaling-steps", type=int, default=20)
     args = ap.parse_args()
     grid = args.grid * 3 if len(args.grid) == 1 else args.grid
     if len(grid) != 3:
@@ -144,27 +147,27 @@ def main() -> int:
 
     nx, ny, nz = grid
     N = nx * ny * nz
-    stream = torch.cuda.current_stream()
     roof = None
     roof_apply = None
     passes_info = None
-    if world == 1:
-        b = torch.empty(N, dtype=torch.complex128, device=dev)
-        x = torch.empty_like(b)
-        cp.fill_uniform(b, SEED)
-        plan = cp.CirculantPlan(grid, device=local_rank)
-        plan.set_transport_symbol(LAM)
-        if args.chunk is not None:
-            plan.set_chunking(args.chunk)
-        plan.set_schedule(args.schedule)
-        run = lambda: plan.apply(b, out=x)  # noqa: E731
-        parallelism = "single GPU"
-    else:
+
+    def make(g):
+        """(plan, b, x, run, parallelism) of the apply on grid g: one GPU, or this rank's slab."""
+        if world == 1:
+            b = torch.empty(int(g[0] * g[1] * g[2]), dtype=torch.complex128, device=dev)
+            x = torch.empty_like(b)
+            cp.fill_uniform(b, SEED)
+            plan = cp.CirculantPlan(g, device=local_rank)
+            plan.set_transport_symbol(LAM)
+            if args.chunk is not None:
+                plan.set_chunking(args.chunk)
+            plan.set_schedule(args.schedule)
+            return plan, b, x, (lambda: plan.apply(b, out=x)), "single GPU"
         from circulantpreconditioner_amd.distributed import SlabPlan
         exchange = os.environ.get("CFP_EXCHANGE", "rccl")
         plan, err = None, None
         try:
-            plan = SlabPlan(grid, rank=rank, world=world, device=local_rank, exchange=exchange)
+            plan = SlabPlan(g, rank=rank, world=world, device=local_rank, exchange=exchange)
         except Exception as e:  # the library's own RCCL communicator failed on this rank
             err = e
         ok = torch.tensor([0 if plan is None else 1], dtype=torch.int32, device=dev)
@@ -174,32 +177,36 @@ def main() -> int:
             if plan is not None:
                 plan.close()
             exchange = "torch"
-            plan = SlabPlan(grid, rank=rank, world=world, device=local_rank, exchange="torch")
+            plan = SlabPlan(g, rank=rank, world=world, device=local_rank, exchange="torch")
         plan.set_transport_symbol(LAM)
         b = torch.empty(plan.local_size, dtype=torch.complex128, device=dev)
         x = torch.empty_like(b)
         cp.fill_uniform(b, SEED, offset=plan.local_offset)
-        run = lambda: plan.apply(b, out=x)  # noqa: E731
-        parallelism = f"z-slab x{world}, all-to-all over xGMI ({exchange})"
+        return plan, b, x, (lambda: plan.apply(b, out=x)), f"z-slab x{world}, all-to-all over xGMI ({exchange})"
 
-    for _ in range(args.warmup):
-        run()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def timed(run, steps, warmup):
+        """W untimed + K timed applies between barriers and device syncs; max over ranks (s)."""
+        for _ in range(warmup):
+            run()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return elapsed
+
+    plan, b, x, run, parallelism = make(grid)
+    elapsed = timed(run, args.steps, args.warmup)
     ms_per_step = elapsed / args.steps * 1e3
     value = args.steps / elapsed  # whole-job PCApply/s (one grid per step)
 
@@ -278,6 +285,29 @@ def main() -> int:
         except Exception as e:  # unsupported grid or failure: report, never fake
             real_variant = {"error": str(e)}
 
+    # north_star's scaling curve: the same apply on the 512^3 grid (BASELINE config 5), at every
+    # N the driver launches, reported beside the 256^3 headline (strong scaling, whole job)
+    scaling = None
+    sg = [int(v) for v in args.scaling_grid]
+    sg = sg * 3 if len(sg) == 1 else sg
+    if len(sg) == 3 and min(sg) > 0 and sg != grid:
+        if world > 1:
+            plan.close()  # one library RCCL communicator at a time
+            dist.barrier()
+        del plan, b, x, run
+        torch.cuda.empty_cache()
+        try:
+            plan, b, x, run, par2 = make(sg)
+            k = max(1, args.scaling_steps)
+            el = timed(run, k, max(1, min(args.warmup, 3)))
+            scaling = {"grid": sg, "value": round(k / el, 4), "unit": "PCApply/s", "n_gpus": world,
+                       "steps": k, "ms_per_step": round(el / k * 1e3, 4), "scaling": "strong",
+                       "parallelism": par2,
+                       "B_alg_GBps_per_gpu": round(208 * (sg[0] * sg[1] * sg[2] / world) / (el / k) / 1e9, 1)}
+        except Exception as e:  # report, never fake
+            scaling = {"grid": sg, "error": str(e)}
+            plan = None
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -308,6 +338,8 @@ def main() -> int:
         }
         if real_variant is not None:
             out["real_variant"] = real_variant
+        if scaling is not None:
+            out["scaling_512"] = scaling
         if passes_info is not None:
             out["passes"] = passes_info
         print(json.dumps(out), flush=True)
@@ -315,7 +347,8 @@ def main() -> int:
         # tear down the library's RCCL communicator on every rank together, before torch's
         torch.cuda.synchronize()
         dist.barrier()
-        plan.close()
+        if plan is not None:
+            plan.close()
         dist.barrier()
         dist.destroy_process_group()
     return 0

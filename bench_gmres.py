@@ -27,12 +27,16 @@ import time
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--system", nargs="*", default=["transport", "wave"], choices=["transport", "wave", "mesh", "direct"])
+    ap.add_argument("--system", nargs="*", default=["transport", "wave"], choices=["transport", "wave", "wave2d", "mesh", "direct"])
     ap.add_argument("--direct-grid", type=int, nargs="*", default=[10, 100, 256],
                     help="--system direct: the direct-solver loop (TransportEquationFFT_impl) on n^3")
     ap.add_argument("--mesh", nargs="*", default=["mesh_tetra_1.msh", "3DKershawTetra1.msh", "mesh_hexa_3.msh"],
                     help="tests/golden/meshes/ files for --system mesh (row f3: the PCSHELL with the remap)")
     ap.add_argument("--wave-grid", type=int, nargs="*", default=[128])
+    ap.add_argument("--wave2d-grid", type=int, nargs="*", default=[50, 1024],
+                    help="2-D wave system (3 unknowns per cell): 50 is the reference main's default mesh")
+    ap.add_argument("--wave2d-loop-max", type=int, default=256,
+                    help="run the whole time loop (to tmax = 0.05) only up to this many cells a side")
     ap.add_argument("--wave-steps", type=int, default=1,
                     help="wave time steps (the reference loop to tmax = 0.05 is ~81 steps at 128^3)")
     ap.add_argument("--grid", type=int, nargs="*", default=[32, 256])
@@ -54,6 +58,8 @@ def main(argv=None) -> int:
     lines = []
     if "wave" in args.system:
         lines += wave_lines(args)
+    if "wave2d" in args.system:
+        lines += wave2d_lines(args)
     if "mesh" in args.system:
         lines += mesh_lines(args)
     if "direct" in args.system:
@@ -192,6 +198,62 @@ def wave_lines(args) -> list:
                     "ms_per_solve": 1e3 * r["solve_seconds"] / max(1, r["steps"]),
                     "ms_per_iteration": 1e3 * r["solve_seconds"] / its, "pc_calls": r["pc_calls"],
                     "pc_s": r["pc_seconds"], "setup_s": r["setup_seconds"], "wall_s": wall}
+            print(json.dumps(line), flush=True)
+            out.append(line)
+    return out
+
+
+def _time_apply(plan, b, x):
+    import torch
+    for _ in range(5):
+        plan.apply(b, x)
+    torch.cuda.synchronize()
+    iters = max(20, int(2e9 / (b.numel() * 16)))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        plan.apply(b, x)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def wave2d_lines(args) -> list:
+    """The reference mains' own wave case: a 2-D square, 3 interleaved unknowns per cell
+    (tests/WaveSystem_SphericalExplosion_impl_seq.cxx:182-212, nx = ny = 50, cfl = 1e3/2)."""
+    import torch
+    from circulantpreconditioner_amd import wave as W
+    out = []
+    for n in args.wave2d_grid:
+        dims = (n, n, 1)
+        h = 1.0 / n
+        dt = (1e3 / 2) * (h / 4) / W.C0
+        plan = W.WavePlan(dims, dim=2).set_symbol([dt / h, dt / h, 0.0])
+        m = 3 * n * n
+        b = torch.randn(m, dtype=torch.complex128, device="cuda")
+        x = torch.empty_like(b)
+        ms = _time_apply(plan, b, x)
+        passes = plan.time_passes(b, x, iters=5)
+        line = {"metric": "wave 2-D block PCApply", "config": f"WaveSystem {n}x{n} (2-D), 3x3 block-circulant, 1 MI355X",
+                "grid": n, "pcapply_per_s": 1e3 / ms, "ms_per_apply": ms,
+                "hbm_gbps_moved": len(passes) * 2 * m * 16 / (ms * 1e-3) / 1e9, "passes_ms": passes}
+        print(json.dumps(line), flush=True)
+        out.append(line)
+        del plan, b, x
+        if n > args.wave2d_loop_max:
+            continue
+        for pc in args.pc:
+            t0 = time.perf_counter()
+            r = W.run(W.config(n, dim=2, pc=pc, max_its=args.max_its))
+            wall = time.perf_counter() - t0
+            its = max(1, r["total_its"])
+            line = {"metric": "GMRES wave 2-D time loop", "config": f"WaveSystem {n}x{n} implicit to tmax=0.05, "
+                    "GMRES(30), 1 MI355X", "grid": n, "pc": pc, "steps": r["steps"], "dt": r["dt"],
+                    "kappa": r["kappa"], "gmres_its": r["total_its"], "its_per_step": [r["min_step_its"],
+                    r["max_step_its"]], "converged": bool(r["all_converged"]), "last_reason": r["last_reason"],
+                    "solve_s": r["solve_seconds"], "ms_per_solve": 1e3 * r["solve_seconds"] / max(1, r["steps"]),
+                    "ms_per_iteration": 1e3 * r["solve_seconds"] / its, "pc_calls": r["pc_calls"],
+                    "pc_s": r["pc_seconds"], "wall_s": wall}
             print(json.dumps(line), flush=True)
             out.append(line)
     return out

@@ -66,7 +66,8 @@ class WaveConfig(ctypes.Structure):
                 ("xmin", ctypes.c_double * 3), ("xmax", ctypes.c_double * 3), ("c0", ctypes.c_double),
                 ("cfl", ctypes.c_double), ("tmax", ctypes.c_double), ("ntmax", ctypes.c_int64),
                 ("precision", ctypes.c_double), ("max_its", ctypes.c_int64), ("restart", ctypes.c_int64),
-                ("pc", ctypes.c_int), ("bc", ctypes.c_int), ("pc_side", ctypes.c_int), ("on_device", ctypes.c_int)]
+                ("pc", ctypes.c_int), ("bc", ctypes.c_int), ("pc_side", ctypes.c_int), ("on_device", ctypes.c_int),
+                ("dim", ctypes.c_int)]
 
 
 class WaveResult(ctypes.Structure):
@@ -202,6 +203,7 @@ def declare(L) -> None:
         "TransportEquationGMRESMesh": ([vp, P(TransportConfig), P(TransportResult), P(ctypes.c_double)], c_int),
         # wave system (include/wave_system.h)
         "cfp_wave_plan_create": ([P(vp), i64, i64, i64, c_int], c_int),
+        "cfp_wave_plan_create_dim": ([P(vp), i64, i64, i64, c_int, c_int], c_int),
         "cfp_wave_plan_destroy": ([vp], c_int),
         "cfp_wave_plan_set_symbol": ([vp, P(ctypes.c_double), ctypes.c_double], c_int),
         "cfp_wave_plan_apply": ([vp, dp, dp, vp], c_int),
@@ -211,13 +213,18 @@ def declare(L) -> None:
         "cfp_wave_plan_time_passes": ([vp, dp, dp, c_int, dp, vp], c_int),
         "cfp_wave_csr": ([i64, i64, i64, P(ctypes.c_double), ctypes.c_double, ctypes.c_double, c_int,
                           ctypes.c_double, P(i64), P(i64), P(ctypes.c_double), P(i64)], c_int),
+        "cfp_wave_csr_dim": ([i64, i64, i64, c_int, P(ctypes.c_double), ctypes.c_double, ctypes.c_double, c_int,
+                              ctypes.c_double, P(i64), P(i64), P(ctypes.c_double), P(i64)], c_int),
         "computeDivergenceMatrixWaveCartesian": ([i64, i64, i64, P(ctypes.c_double), ctypes.c_double,
                                                   ctypes.c_double, i64, P(vp)], c_int),
+        "computeDivergenceMatrixWaveCartesianDim": ([i64, i64, i64, i64, P(ctypes.c_double), ctypes.c_double,
+                                                     ctypes.c_double, i64, P(vp)], c_int),
         "initial_conditions_shock_wave": ([i64, i64, i64, P(ctypes.c_double), P(ctypes.c_double), vp], c_int),
         "applyFFT3DPrecWave": ([vp, vp, vp], c_int),
         "setupFFTPrec3DWave": ([vp], c_int),
         "destroyFFTPrec3DWave": ([vp], c_int),
         "cfp_wave_config_default": ([P(WaveConfig), i64], None),
+        "cfp_wave_config_default_dim": ([P(WaveConfig), i64, c_int], None),
         "WaveSystemGMRES": ([P(WaveConfig), P(WaveResult), P(ctypes.c_double)], c_int),
         # the reference-named boundary
         "applyFFT3DPrecTransport": ([vp, vp, vp], c_int),

@@ -63,6 +63,7 @@ struct WaveSym {
   i64 n[3];               // grid sizes (cells)
   double c0sq;            // c0^2
   int fused;              // axis transformed by the fused pass
+  int ncomp;              // unknowns per cell: dim + 1 (pressure, dim momentum components)
 };
 
 struct PassDesc {

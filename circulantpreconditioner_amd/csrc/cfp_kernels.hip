@@ -133,7 +133,8 @@ bool fast_path_supported(const PassDesc& p) {
   } else if (p.mode == PASS_FUSED_WAVE) {
     return false;
   }
-  if (p.mode == PASS_FUSED_WAVE && T % 4 != 0) return false;
+  // the fast fused wave pass gathers a cell from the 4 lanes of a quad: 3-D only
+  if (p.mode == PASS_FUSED_WAVE && (T % 4 != 0 || p.wave.ncomp != 4)) return false;
   return true;
 }
 
@@ -191,6 +192,7 @@ struct MRStage {
 struct MRArgs {
   KArgs k;
   int n, G, gshift, L;  // points per column, columns per block, log2 G (column mode), LDS column stride
+  uint64_t G_M;         // magic of G when G is not a power of two (column mode, 3-component cells)
   i64 ncols;
   int nst;
   MRStage st[CFP_MR_MAXF];
@@ -413,7 +415,8 @@ __global__ void __launch_bounds__(CFP_MR_THREADS) k_axis_mixed(const cd* in, cd*
   const int total = G * n;
   auto split = [&](int i, int& c, int& k) {
     if (ROW) { c = (int)mr_div((uint32_t)i, g.n_M); k = i - c * n; }
-    else { k = i >> g.gshift; c = i & (G - 1); }
+    else if (g.gshift >= 0) { k = i >> g.gshift; c = i & (G - 1); }
+    else { k = (int)mr_div((uint32_t)i, g.G_M); c = i - k * G; }
   };
   for (int i = threadIdx.x; i < total; i += CFP_MR_THREADS) {
     int c, k;
@@ -427,21 +430,25 @@ __global__ void __launch_bounds__(CFP_MR_THREADS) k_axis_mixed(const cd* in, cd*
   __syncthreads();
   mr_fft(X, Y, g, tw);
   if (mode == PASS_FUSED_WAVE) {
-    // columns 4j..4j+3 of the block are the 4 components of one cell (G % 4 == 0)
+    // columns nc*j .. nc*j+nc-1 of the block are the nc = dim+1 components of one cell
+    // (G % nc == 0, g0 % nc == 0); the missing momentum rows of dim < 3 are zero, and the
+    // absent axes' symbol entries (n_d = 1) are p = q = 0, so the 4x4 algebra serves them
+    const int nc = g.k.wave.ncomp;
     for (int i = threadIdx.x; i < total; i += CFP_MR_THREADS) {
       int c, k;
       split(i, c, k);
       const i64 gg = g0 + c;
+      const int comp = c % nc;
+      const int cb = c - comp;
       cd r[4];
-      const int c4 = c & ~3;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) r[j] = X[(c4 + j) * L + k];
+      for (int j = 0; j < 4; ++j) r[j] = j < nc ? X[(cb + j) * L + k] : make_cd(0.0, 0.0);
       cd w = make_cd(0.0, 0.0);
       if (gg < g.ncols) {
         double2 pq[3];
-        wave_cell_sym(g.k.wave, gg >> 2, pq);
+        wave_cell_sym(g.k.wave, gg / nc, pq);
         pq[g.k.wave.fused] = g.k.wave.tab[g.k.wave.fused][k];
-        w = cconj(wave_solve(r, c & 3, pq, g.k.wave.c0sq));
+        w = cconj(wave_solve(r, comp, pq, g.k.wave.c0sq));
       }
       Y[c * L + k] = w;
     }
@@ -523,13 +530,21 @@ static hipError_t launch_generic(const PassDesc& p, const cd* in, cd* out, const
       G = q;
     }
   }
-  if (p.mode == PASS_FUSED_WAVE) {  // whole cells (4 columns) per block
-    if (p.ncols % 4 != 0) return hipErrorInvalidValue;
-    if (G < 4) G = 4;
-    G &= ~3;
+  if (p.mode == PASS_FUSED_WAVE) {  // whole cells (ncomp columns) per block
+    const int nc = p.wave.ncomp;
+    if (nc < 2 || nc > 4 || p.ncols % nc != 0) return hipErrorInvalidValue;
+    if (nc == 3) {  // 3 * 2^j columns; the column-mode index split divides by a magic number
+      int q = 3;
+      while (q * 2 <= G) q *= 2;
+      G = q;
+    } else {
+      if (G < nc) G = nc;
+      G &= ~(nc - 1);
+    }
   }
   g.G = G;
-  g.gshift = ilog2(G);
+  g.gshift = is_pow2(G) ? ilog2(G) : -1;
+  g.G_M = mr_magic((uint32_t)G);
   g.L = row ? p.n : p.n + 1;
   int ns = 1;
   for (int i = 0; i < g.nst; ++i) {

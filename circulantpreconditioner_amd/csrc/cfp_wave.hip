@@ -1,13 +1,16 @@
 // cfp_wave.hip -- the wave-system block-circulant plan (include/wave_system.h, SURVEY.md §8f
 // row f2).  Same 5-sweep structure as the scalar plan, over the reference's interleaved
-// layout idx = cell*4 + comp (tests/WaveSystem_SphericalExplosion_impl_seq.cxx:57-68):
+// layout idx = cell*nbComp + comp, nbComp = dim + 1 (src/WaveSystem.cxx:112-113,
+// tests/WaveSystem_SphericalExplosion_impl_seq.cxx:19,57-68):
 //
-//   x pass   : columns (comp, y, z), point stride 4 -- a tile of 16 columns is 4 whole
-//              cells-rows x 4 components, i.e. 4 contiguous runs of 4*nx values
-//   y, z pass: the scalar passes of a grid whose x extent is 4*nx (the 4 components ride
+//   x pass   : columns (comp, y, z), point stride nbComp -- in 3-D a tile of 16 columns is
+//              4 whole cells-rows x 4 components, i.e. 4 contiguous runs of 4*nx values
+//   y, z pass: the scalar passes of a grid whose x extent is nbComp*nx (the components ride
 //              along x as extra columns)
-//   fused    : DFT along the last axis, per frequency the 4x4 arrowhead solve with the 4
-//              components gathered from the lanes of one quad (DPP), IDFT
+//   fused    : DFT along the last axis, per frequency the arrowhead solve, IDFT.  3-D: the 4
+//              components are gathered from the lanes of one quad (DPP); 1-D / 2-D (2 or 3
+//              components, the reference mains' default is a 2-D 50x50 grid): the mixed-radix
+//              kernel gathers a cell's columns from LDS
 //
 // so an apply moves 5 x (read + write) x 64 bytes per cell and never materialises the 256-byte
 // per-frequency block symbol (cfp_fft_device.h: wave_solve).
@@ -31,12 +34,12 @@ using namespace cfp;
     if (_e != hipSuccess) return cfp::hip_error(_e, #expr); \
   } while (0)
 
-static const int kComp = 4;
-
 struct cfp_wave_plan_s {
   int device = 0;
   i64 n[3] = {1, 1, 1};
   i64 N = 1;  // cells
+  int dim = 3;
+  int ncomp = 4;  // dim + 1 unknowns per cell
   std::map<int, cd*> tw;
   double2* tab[3] = {nullptr, nullptr, nullptr};
   bool has_sym = false;
@@ -77,16 +80,16 @@ PassDesc wave_pass(const cfp_wave_plan_s* p, int axis, int mode, double scale) {
   if (axis == 0) {
     Side s;
     s.inner_stride = 1;
-    s.outer_stride = kComp * p->n[0];
-    s.pt_stride = kComp;
+    s.outer_stride = p->ncomp * p->n[0];
+    s.pt_stride = p->ncomp;
     s.seg_stride = 0;
     s.seg_len = (int)p->n[0];
     s.seg_shift = ilog2_exact(p->n[0]);
     d.in = d.out = s;
-    d.inner_n = kComp;
-    d.ncols = kComp * p->n[1] * p->n[2];
+    d.inner_n = p->ncomp;
+    d.ncols = p->ncomp * p->n[1] * p->n[2];
   } else {
-    const i64 m[3] = {kComp * p->n[0], p->n[1], p->n[2]};
+    const i64 m[3] = {p->ncomp * p->n[0], p->n[1], p->n[2]};
     d.in = d.out = natural_side(axis, m);
     natural_cols(axis, m, &d.ncols, &d.inner_n);
   }
@@ -99,6 +102,7 @@ PassDesc wave_pass(const cfp_wave_plan_s* p, int axis, int mode, double scale) {
   }
   d.wave.c0sq = p->c0 * p->c0;
   d.wave.fused = p->fused;
+  d.wave.ncomp = p->ncomp;
   return d;
 }
 
@@ -156,10 +160,14 @@ int run_transform(cfp_wave_plan_s* p, bool inverse, const cd* in, cd* out, hipSt
 
 }  // namespace
 
-extern "C" int cfp_wave_plan_create(cfp_wave_plan_t* plan, int64_t nx, int64_t ny, int64_t nz, int device) {
+extern "C" int cfp_wave_plan_create_dim(cfp_wave_plan_t* plan, int64_t nx, int64_t ny, int64_t nz, int dim,
+                                        int device) {
   if (!plan) return set_error(CFP_ERR_ARG_NULL, "plan is NULL");
   *plan = nullptr;
   if (nx < 1 || ny < 1 || nz < 1) return set_error(CFP_ERR_ARG_OUTOFRANGE, "grid sizes must be >= 1");
+  if (dim < 1 || dim > 3) return set_error(CFP_ERR_ARG_OUTOFRANGE, "dim must be 1, 2 or 3 (got %d)", dim);
+  if ((dim < 3 && nz != 1) || (dim < 2 && ny != 1))
+    return set_error(CFP_ERR_ARG_SIZ, "a %d-D wave system has n = 1 along the axes above its dimension", dim);
   if (nx > 1024 || ny > 1024 || nz > 1024)
     return set_error(CFP_ERR_SUP, "wave plan: axis lengths above 1024 are not supported");
   int ndev = 0;
@@ -172,6 +180,8 @@ extern "C" int cfp_wave_plan_create(cfp_wave_plan_t* plan, int64_t nx, int64_t n
   p->n[1] = ny;
   p->n[2] = nz;
   p->N = nx * ny * nz;
+  p->dim = dim;
+  p->ncomp = dim + 1;
   for (int a = 0; a < 3; ++a)
     if (p->n[a] > 1) p->axes.push_back(a);
   p->fused = p->axes.empty() ? 0 : p->axes.back();
@@ -181,6 +191,10 @@ extern "C" int cfp_wave_plan_create(cfp_wave_plan_t* plan, int64_t nx, int64_t n
   }
   *plan = p.release();
   return CFP_SUCCESS;
+}
+
+extern "C" int cfp_wave_plan_create(cfp_wave_plan_t* plan, int64_t nx, int64_t ny, int64_t nz, int device) {
+  return cfp_wave_plan_create_dim(plan, nx, ny, nz, 3, device);
 }
 
 extern "C" int cfp_wave_plan_destroy(cfp_wave_plan_t p) {

@@ -16,13 +16,14 @@
 #include <vector>
 
 #include "../../include/circulant_fft.h"
+#include "../../include/transport_equation.h"
 #include "../../include/wave_system.h"
 #include "pcshell_common.h"
 
 using namespace cfp_pc;
 
 namespace {
-const int kC = 4;  // unknowns per cell in 3-D: pressure, 3 momentum components
+const int kC = 4;  // most unknowns per cell (3-D: pressure, 3 momentum components)
 
 double wall() {
   struct timeval tv;
@@ -48,15 +49,18 @@ struct Entry {
 };
 }  // namespace
 
-extern "C" int cfp_wave_csr(int64_t nx, int64_t ny, int64_t nz, const double h[3], double dt, double c0, int bc,
-                            double shift, int64_t* rowptr, int64_t* col, double* val, int64_t* nnz) {
+extern "C" int cfp_wave_csr_dim(int64_t nx, int64_t ny, int64_t nz, int dim, const double h[3], double dt, double c0,
+                                int bc, double shift, int64_t* rowptr, int64_t* col, double* val, int64_t* nnz) {
   if (!h || !rowptr || !col || !val || !nnz) return CFP_ERR_ARG_NULL;
   if (nx < 1 || ny < 1 || nz < 1 || h[0] <= 0 || h[1] <= 0 || h[2] <= 0 || !(c0 > 0)) return CFP_ERR_ARG_OUTOFRANGE;
   if (bc != CFP_WAVE_BC_WALL && bc != CFP_WAVE_BC_PERIODIC && bc != CFP_WAVE_BC_NEUMANN) return CFP_ERR_ARG_OUTOFRANGE;
+  if (dim < 1 || dim > 3) return CFP_ERR_ARG_OUTOFRANGE;
+  if ((dim < 3 && nz != 1) || (dim < 2 && ny != 1)) return CFP_ERR_ARG_SIZ;
+  const int C = dim + 1;  // nbComp (src/WaveSystem.cxx:113)
   const int64_t n[3] = {nx, ny, nz};
   int64_t p = 0;
   rowptr[0] = 0;
-  // one cell at a time: its (at most 7) coupled cells and their 4x4 blocks
+  // one cell at a time: its (at most 2 dim + 1) coupled cells and their C x C blocks
   std::vector<Entry> row[kC];
   for (int64_t k = 0; k < nz; ++k)
     for (int64_t j = 0; j < ny; ++j)
@@ -67,7 +71,7 @@ extern "C" int cfp_wave_csr(int64_t nx, int64_t ny, int64_t nz, const double h[3
         for (int r = 0; r < kC; ++r)
           for (int c = 0; c < kC; ++c) self[r][c] = r == c ? shift : 0.0;
         for (int r = 0; r < kC; ++r) row[r].clear();
-        for (int d = 0; d < 3; ++d) {
+        for (int d = 0; d < dim; ++d) {  // a dim-D mesh has faces along its dim axes only
           const double kappa = dt / h[d];  // dt |F| / |C|
           for (int s = -1; s <= 1; s += 2) {
             double Am[kC][kC];
@@ -83,22 +87,22 @@ extern "C" int cfp_wave_csr(int64_t nx, int64_t ny, int64_t nz, const double h[3
               other = o[0] + nx * (o[1] + ny * o[2]);
             } else if (bc == CFP_WAVE_BC_WALL) {
               // -Am (2 v v^T), v = (0, n): only column 1+d is hit (src/WaveSystem.cxx:148-155)
-              for (int r = 0; r < kC; ++r) self[r][1 + d] -= 2.0 * Am[r][1 + d];
+              for (int r = 0; r < C; ++r) self[r][1 + d] -= 2.0 * Am[r][1 + d];
               continue;
             } else {
               continue;  // Neumann: nothing
             }
-            for (int r = 0; r < kC; ++r)
-              for (int c = 0; c < kC; ++c) {
+            for (int r = 0; r < C; ++r)
+              for (int c = 0; c < C; ++c) {
                 if (Am[r][c] == 0.0) continue;
-                row[r].push_back({other * kC + c, Am[r][c]});  // addValue(j, other, Am)
+                row[r].push_back({other * C + c, Am[r][c]});  // addValue(j, other, Am)
                 self[r][c] -= Am[r][c];                         // addValue(j, j, -Am)
               }
           }
         }
-        for (int r = 0; r < kC; ++r) {
-          for (int c = 0; c < kC; ++c)
-            if (self[r][c] != 0.0 || c == r) row[r].push_back({cell * kC + c, self[r][c]});
+        for (int r = 0; r < C; ++r) {
+          for (int c = 0; c < C; ++c)
+            if (self[r][c] != 0.0 || c == r) row[r].push_back({cell * C + c, self[r][c]});
           std::vector<Entry>& e = row[r];
           std::sort(e.begin(), e.end(), [](const Entry& a, const Entry& b) { return a.col < b.col; });
           // merge duplicates (periodic wrap on a 1- or 2-cell axis), keep the diagonal
@@ -116,7 +120,7 @@ extern "C" int cfp_wave_csr(int64_t nx, int64_t ny, int64_t nz, const double h[3
           // drop exact zeros except the diagonal
           int64_t w = start;
           for (int64_t q = start; q < p; ++q) {
-            if (val[2 * q] != 0.0 || col[q] == cell * kC + r) {
+            if (val[2 * q] != 0.0 || col[q] == cell * C + r) {
               col[w] = col[q];
               val[2 * w] = val[2 * q];
               val[2 * w + 1] = 0.0;
@@ -124,28 +128,42 @@ extern "C" int cfp_wave_csr(int64_t nx, int64_t ny, int64_t nz, const double h[3
             }
           }
           p = w;
-          rowptr[cell * kC + r + 1] = p;
+          rowptr[cell * C + r + 1] = p;
         }
       }
   *nnz = p;
   return CFP_SUCCESS;
 }
 
-extern "C" PetscErrorCode computeDivergenceMatrixWaveCartesian(PetscInt nx, PetscInt ny, PetscInt nz,
-                                                               const PetscReal h[3], PetscReal dt, PetscReal c0,
-                                                               PetscInt bc, Mat* A) {
+extern "C" int cfp_wave_csr(int64_t nx, int64_t ny, int64_t nz, const double h[3], double dt, double c0, int bc,
+                            double shift, int64_t* rowptr, int64_t* col, double* val, int64_t* nnz) {
+  return cfp_wave_csr_dim(nx, ny, nz, 3, h, dt, c0, bc, shift, rowptr, col, val, nnz);
+}
+
+extern "C" PetscErrorCode computeDivergenceMatrixWaveCartesianDim(PetscInt nx, PetscInt ny, PetscInt nz, PetscInt dim,
+                                                                  const PetscReal h[3], PetscReal dt, PetscReal c0,
+                                                                  PetscInt bc, Mat* A) {
   PetscFunctionBeginUser;
   PetscCheck(A && h, PETSC_COMM_SELF, PETSC_ERR_ARG_NULL, "computeDivergenceMatrixWaveCartesian: NULL argument");
   PetscCheck(nx >= 1 && ny >= 1 && nz >= 1, PETSC_COMM_SELF, PETSC_ERR_ARG_OUTOFRANGE, "grid sizes must be >= 1");
-  const int64_t M = kC * nx * ny * nz;
-  std::vector<int64_t> rowptr((size_t)M + 1), col((size_t)M * 28);
-  std::vector<PetscScalar> val((size_t)M * 28);
+  PetscCheck(dim >= 1 && dim <= 3, PETSC_COMM_SELF, PETSC_ERR_ARG_OUTOFRANGE, "Dimension should be 1, 2 or 3");
+  const int C = (int)dim + 1;
+  const int64_t M = C * nx * ny * nz;
+  const int64_t room = (int64_t)C * C * (2 * dim + 1);
+  std::vector<int64_t> rowptr((size_t)M + 1), col((size_t)(nx * ny * nz * room));
+  std::vector<PetscScalar> val((size_t)(nx * ny * nz * room));
   int64_t nnz = 0;
-  const int rc = cfp_wave_csr(nx, ny, nz, h, dt, c0, (int)bc, 0.0, rowptr.data(), col.data(),
-                              reinterpret_cast<double*>(val.data()), &nnz);
+  const int rc = cfp_wave_csr_dim(nx, ny, nz, (int)dim, h, dt, c0, (int)bc, 0.0, rowptr.data(), col.data(),
+                                  reinterpret_cast<double*>(val.data()), &nnz);
   PetscCheck(rc == CFP_SUCCESS, PETSC_COMM_SELF, rc, "computeDivergenceMatrixWaveCartesian: bad arguments");
   PetscCall(MatCreateSeqAIJWithArrays(PETSC_COMM_SELF, M, M, rowptr.data(), col.data(), val.data(), A));
   PetscFunctionReturn(PETSC_SUCCESS);
+}
+
+extern "C" PetscErrorCode computeDivergenceMatrixWaveCartesian(PetscInt nx, PetscInt ny, PetscInt nz,
+                                                               const PetscReal h[3], PetscReal dt, PetscReal c0,
+                                                               PetscInt bc, Mat* A) {
+  return computeDivergenceMatrixWaveCartesianDim(nx, ny, nz, 3, h, dt, c0, bc, A);
 }
 
 extern "C" PetscErrorCode initial_conditions_shock_wave(PetscInt nx, PetscInt ny, PetscInt nz, const PetscReal xmin[3],
@@ -154,7 +172,10 @@ extern "C" PetscErrorCode initial_conditions_shock_wave(PetscInt nx, PetscInt ny
   PetscCheck(xmin && xmax, PETSC_COMM_SELF, PETSC_ERR_ARG_NULL, "NULL domain bounds");
   PetscInt n;
   PetscCall(VecGetLocalSize(U, &n));
-  PetscCheck(n == kC * nx * ny * nz, PETSC_COMM_SELF, PETSC_ERR_ARG_SIZ, "U size differs from 4*nx*ny*nz");
+  const PetscInt N = nx * ny * nz;
+  PetscCheck(N >= 1 && n % N == 0 && n / N >= 2 && n / N <= kC, PETSC_COMM_SELF, PETSC_ERR_ARG_SIZ,
+             "U size is not (dim+1)*nx*ny*nz with dim = 1, 2 or 3");
+  const int C = (int)(n / N), dim = C - 1;  // nbComp = dim + 1
   const double hx = (xmax[0] - xmin[0]) / (double)nx, hy = (xmax[1] - xmin[1]) / (double)ny,
                hz = (xmax[2] - xmin[2]) / (double)nz;
   const double cx = (xmin[0] + xmax[0]) / 2, cy = (xmin[1] + xmax[1]) / 2, cz = (xmin[2] + xmax[2]) / 2;
@@ -164,12 +185,14 @@ extern "C" PetscErrorCode initial_conditions_shock_wave(PetscInt nx, PetscInt ny
     for (PetscInt j = 0; j < ny; ++j)
       for (PetscInt i = 0; i < nx; ++i) {
         const double x = xmin[0] + (i + 0.5) * hx, y = xmin[1] + (j + 0.5) * hy, z = xmin[2] + (k + 0.5) * hz;
+        // src/WaveSystem.cxx:48-61: y enters r for dim > 1, z for dim == 3 (a single cell
+        // layer's centre is the domain centre, so a 3-D grid with n = 1 adds 0)
         double r2 = (x - cx) * (x - cx);
-        if (ny > 1) r2 += (y - cy) * (y - cy);
-        if (nz > 1) r2 += (z - cz) * (z - cz);
-        const int64_t c = kC * (i + nx * (j + ny * k));
+        if (dim > 1 && ny > 1) r2 += (y - cy) * (y - cy);
+        if (dim == 3 && nz > 1) r2 += (z - cz) * (z - cz);
+        const int64_t c = C * (i + nx * (j + ny * k));
         u[c] = std::sqrt(r2) < 0.3 ? 155e5 : 70e5;
-        for (int d = 1; d < kC; ++d) u[c + d] = 0.0;  // rho0 * velocity, velocity = 0
+        for (int d = 1; d < C; ++d) u[c + d] = 0.0;  // rho0 * velocity, velocity = 0
       }
   PetscCall(VecRestoreArrayWrite(U, &u));
   PetscFunctionReturn(PETSC_SUCCESS);
@@ -187,7 +210,8 @@ extern "C" PetscErrorCode setupFFTPrec3DWave(PC pc) {
   PetscCheck(hipGetDevice(&dev) == hipSuccess, PETSC_COMM_SELF, PETSC_ERR_LIB, "no HIP device");
   if (ctx->plan) CFPCALL(cfp_wave_plan_destroy(ctx->plan));
   ctx->plan = nullptr;
-  CFPCALL(cfp_wave_plan_create(&ctx->plan, ctx->n_x, ctx->n_y, ctx->n_z, dev));
+  const int dim = ctx->dim ? (int)ctx->dim : 3;
+  CFPCALL(cfp_wave_plan_create_dim(&ctx->plan, ctx->n_x, ctx->n_y, ctx->n_z, dim, dev));
   const double kappa[3] = {ctx->kappa_x, ctx->kappa_y, ctx->kappa_z};
   CFPCALL(cfp_wave_plan_set_symbol(ctx->plan, kappa, ctx->c0));
   PetscFunctionReturn(PETSC_SUCCESS);
@@ -198,7 +222,7 @@ extern "C" PetscErrorCode applyFFT3DPrecWave(PC pc, Vec b, Vec x) {
   FFTPrecWaveContext* ctx = nullptr;
   PetscCall(PCShellGetContext(pc, &ctx));
   PetscCheck(ctx && ctx->plan, PETSC_COMM_SELF, PETSC_ERR_ARG_WRONGSTATE, "applyFFT3DPrecWave: setup has not run");
-  const PetscInt M = kC * ctx->n_x * ctx->n_y * ctx->n_z;
+  const PetscInt M = ((ctx->dim ? ctx->dim : 3) + 1) * ctx->n_x * ctx->n_y * ctx->n_z;
   PetscCall(check_size(b, M, "applyFFT3DPrecWave: b has the wrong size"));
   PetscCall(check_size(x, M, "applyFFT3DPrecWave: x has the wrong size"));
   DevIn in;
@@ -244,6 +268,17 @@ extern "C" void cfp_wave_config_default(cfp_wave_config* cfg, int64_t n) {
   cfg->bc = CFP_WAVE_BC_WALL;
   cfg->pc_side = PC_LEFT;
   cfg->on_device = 1;
+  cfg->dim = 3;
+}
+
+extern "C" void cfp_wave_config_default_dim(cfp_wave_config* cfg, int64_t n, int dim) {
+  if (!cfg) return;
+  cfp_wave_config_default(cfg, n);
+  if (dim < 1 || dim > 3) return;
+  cfg->dim = dim;
+  if (dim < 3) cfg->nz = 1;
+  if (dim < 2) cfg->ny = 1;
+  cfg->cfl = 1.0e3 / (double)dim;  // main: cfl = 1e3 / getSpaceDimension()
 }
 
 extern "C" PetscErrorCode WaveSystemGMRES(const cfp_wave_config* cfg, cfp_wave_result* res, double* U_out) {
@@ -253,14 +288,15 @@ extern "C" PetscErrorCode WaveSystemGMRES(const cfp_wave_config* cfg, cfp_wave_r
              "the block-circulant preconditioner runs on HIP vectors only");
   std::memset((void*)res, 0, sizeof(*res));
   const double t_setup = wall();
-  const PetscInt nx = cfg->nx, ny = cfg->ny, nz = cfg->nz, M = kC * nx * ny * nz;
+  const int dim = cfg->dim ? cfg->dim : 3;
+  PetscCheck(dim >= 1 && dim <= 3, PETSC_COMM_SELF, PETSC_ERR_ARG_OUTOFRANGE, "Dimension should be 1, 2 or 3");
+  const PetscInt nx = cfg->nx, ny = cfg->ny, nz = cfg->nz, M = (dim + 1) * nx * ny * nz;
   const double h[3] = {(cfg->xmax[0] - cfg->xmin[0]) / (double)nx, (cfg->xmax[1] - cfg->xmin[1]) / (double)ny,
                        (cfg->xmax[2] - cfg->xmin[2]) / (double)nz};
-  // dt = cfl * minRatioVolSurf / c0 (impl_seq.cxx:18,73)
-  const double dx_min = h[0] * h[1] * h[2] / (2.0 * (h[0] * h[1] + h[1] * h[2] + h[2] * h[0]));
-  const double dt = cfg->cfl * dx_min / cfg->c0;
+  // dt = cfl * minRatioVolSurf / c0 (impl_seq.cxx:18,73): cell measure over its faces' measure
+  const double dt = cfg->cfl * cfp_cartesian_min_ratio_vol_surf(dim, h) / cfg->c0;
   res->dt = dt;
-  for (int d = 0; d < 3; ++d) res->kappa[d] = dt / h[d];
+  for (int d = 0; d < 3; ++d) res->kappa[d] = d < dim ? dt / h[d] : 0.0;
 
   Vec Un, dUn;
   if (cfg->on_device) PetscCall(VecCreateSeqHIP(PETSC_COMM_SELF, M, &Un));
@@ -268,7 +304,7 @@ extern "C" PetscErrorCode WaveSystemGMRES(const cfp_wave_config* cfg, cfp_wave_r
   PetscCall(VecDuplicate(Un, &dUn));
   PetscCall(initial_conditions_shock_wave(nx, ny, nz, cfg->xmin, cfg->xmax, Un));
   Mat A;
-  PetscCall(computeDivergenceMatrixWaveCartesian(nx, ny, nz, h, dt, cfg->c0, cfg->bc, &A));
+  PetscCall(computeDivergenceMatrixWaveCartesianDim(nx, ny, nz, dim, h, dt, cfg->c0, cfg->bc, &A));
   PetscCall(MatShift(A, 1.0));  // :86
 
   KSP ksp;
@@ -289,6 +325,7 @@ extern "C" PetscErrorCode WaveSystemGMRES(const cfp_wave_config* cfg, cfp_wave_r
     ctx.kappa_y = res->kappa[1];
     ctx.kappa_z = res->kappa[2];
     ctx.c0 = cfg->c0;
+    ctx.dim = dim;
     PetscCall(PCSetType(pc, PCSHELL));
     PetscCall(PCShellSetContext(pc, &ctx));
     PetscCall(PCShellSetSetUp(pc, setupFFTPrec3DWave));

@@ -1,9 +1,10 @@
 """Wave-system block-circulant preconditioner and implicit GMRES loop (include/wave_system.h,
 SURVEY.md §8f row f2, BASELINE config 4).
 
-``WavePlan``: x = S^{-1} b for the periodic wave-system operator with 4 interleaved unknowns
-per cell (pressure, 3 momentum components; idx = cell*4 + comp as the reference's Un,
-tests/WaveSystem_SphericalExplosion_impl_seq.cxx:57-68), one HIP plan, 5 HBM sweeps.
+``WavePlan``: x = S^{-1} b for the periodic wave-system operator with dim + 1 interleaved
+unknowns per cell (pressure, dim momentum components; idx = cell*(dim+1) + comp as the
+reference's Un, tests/WaveSystem_SphericalExplosion_impl_seq.cxx:19,57-68), one HIP plan,
+at most 5 HBM sweeps.  dim = 3 by default; the reference mains' own default is 2-D (50 x 50).
 ``wave_csr``: the reference operator (src/WaveSystem.cxx:92-176) on a Cartesian grid.
 ``config``/``run``: WaveSystem_impl_seq's time loop with the block-circulant PCSHELL.
 """
@@ -30,18 +31,23 @@ def _d3(v) -> ctypes.Array:
     return (ctypes.c_double * 3)(*[float(x) for x in v])
 
 
+def _dims3(dims: Sequence[int]) -> tuple:
+    d = tuple(int(v) for v in dims)
+    return d + (1,) * (3 - len(d))
+
+
 class WavePlan:
-    """Block-circulant inverse on an nx*ny*nz grid with 4 interleaved components."""
+    """Block-circulant inverse on an nx*ny*nz grid with dim + 1 interleaved components."""
 
-    NCOMP = 4
-
-    def __init__(self, dims: Sequence[int], device: int | None = None):
-        nx, ny, nz = (int(d) for d in dims)
+    def __init__(self, dims: Sequence[int], device: int | None = None, dim: int = 3):
+        nx, ny, nz = _dims3(dims)
         self.dims = (nx, ny, nz)
-        self.size = 4 * nx * ny * nz
+        self.dim = int(dim)
+        self.ncomp = self.dim + 1
+        self.size = self.ncomp * nx * ny * nz
         self.device = torch.cuda.current_device() if device is None else int(device)
         h = ctypes.c_void_p()
-        check(lib().cfp_wave_plan_create(ctypes.byref(h), nx, ny, nz, self.device))
+        check(lib().cfp_wave_plan_create_dim(ctypes.byref(h), nx, ny, nz, self.dim, self.device))
         self._h = h
 
     def set_symbol(self, kappa: Sequence[float], c0: float = C0) -> "WavePlan":
@@ -94,30 +100,36 @@ class WavePlan:
 
 
 def wave_csr(dims: Sequence[int], h: Sequence[float], dt: float, c0: float = C0, bc: str | int = "wall",
-             shift: float = 0.0):
+             shift: float = 0.0, dim: int = 3):
     """(rowptr, col, val) of shift*I + computeDivergenceMatrix of the wave system (host)."""
-    nx, ny, nz = (int(v) for v in dims)
-    m = 4 * nx * ny * nz
+    nx, ny, nz = _dims3(dims)
+    C = int(dim) + 1
+    m = C * nx * ny * nz
+    room = C * (2 * int(dim) + 1) * m
     rowptr = np.empty(m + 1, dtype=np.int64)
-    col = np.empty(28 * m, dtype=np.int64)
-    val = np.empty(28 * m, dtype=np.complex128)
+    col = np.empty(room, dtype=np.int64)
+    val = np.empty(room, dtype=np.complex128)
     nnz = ctypes.c_int64()
     P64 = ctypes.POINTER(ctypes.c_int64)
     b = _BC[bc] if isinstance(bc, str) else int(bc)
-    check(lib().cfp_wave_csr(nx, ny, nz, _d3(h), float(dt), float(c0), b, float(shift),
-                             rowptr.ctypes.data_as(P64), col.ctypes.data_as(P64),
-                             val.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(nnz)))
+    hh = list(h) + [1.0] * (3 - len(h))
+    check(lib().cfp_wave_csr_dim(nx, ny, nz, int(dim), _d3(hh), float(dt), float(c0), b, float(shift),
+                                 rowptr.ctypes.data_as(P64), col.ctypes.data_as(P64),
+                                 val.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(nnz)))
     k = nnz.value
     return rowptr, col[:k].copy(), val[:k].copy()
 
 
-def config(n: int | Sequence[int] = 32, **kw) -> WaveConfig:
-    """WaveSystem_impl_seq's defaults (c0 = 700, cfl = 1e3/3, tmax = 0.05, precision 1e-5,
-    1000 iterations, wall boundaries) with overrides: pc='none'|'fft', bc='wall'|'periodic'|
-    'neumann', steps=ntmax, device=True/False, or any WaveConfig field."""
+def config(n: int | Sequence[int] = 32, dim: int = 3, **kw) -> WaveConfig:
+    """WaveSystem_impl_seq's defaults (c0 = 700, cfl = 1e3/dim, tmax = 0.05, precision 1e-5,
+    1000 iterations, wall boundaries) on a dim-D grid of n cells a side (or the given dims),
+    with overrides: pc='none'|'fft', bc='wall'|'periodic'|'neumann', steps=ntmax,
+    device=True/False, or any WaveConfig field.  The reference main's default is
+    ``config(50, dim=2)``."""
     cfg = WaveConfig()
-    dims = (int(n),) * 3 if np.isscalar(n) else tuple(int(v) for v in n)
-    lib().cfp_wave_config_default(ctypes.byref(cfg), dims[0])
+    dim = int(dim)
+    dims = (int(n),) * dim + (1,) * (3 - dim) if np.isscalar(n) else _dims3(n)
+    lib().cfp_wave_config_default_dim(ctypes.byref(cfg), dims[0], dim)
     cfg.nx, cfg.ny, cfg.nz = dims
     for k, v in kw.items():
         if k == "pc":
@@ -141,7 +153,7 @@ def config(n: int | Sequence[int] = 32, **kw) -> WaveConfig:
 def run(cfg: WaveConfig, return_field: bool = False):
     """WaveSystemGMRES: the implicit time loop; result dict (and the final 4N field)."""
     res = WaveResult()
-    m = int(4 * cfg.nx * cfg.ny * cfg.nz)
+    m = int(((cfg.dim or 3) + 1) * cfg.nx * cfg.ny * cfg.nz)
     out = np.empty(m, dtype=np.complex128) if return_field else None
     ptr = out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) if out is not None else None
     PetscCall(lib().WaveSystemGMRES(ctypes.byref(cfg), ctypes.byref(res), ptr))

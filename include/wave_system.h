@@ -29,13 +29,18 @@
 extern "C" {
 #endif
 
-/* ---- the block-circulant plan (C ABI, device pointers, 4 interleaved components) */
+/* ---- the block-circulant plan (C ABI, device pointers, dim + 1 interleaved components) */
 typedef struct cfp_wave_plan_s *cfp_wave_plan_t;
+/* dim = 1, 2 or 3 (nbComp = dim + 1 unknowns per cell, src/WaveSystem.cxx:112-113); the axes
+ * above dim must have n = 1.  The reference mains default to dim = 2 (a 50 x 50 square,
+ * tests/WaveSystem_SphericalExplosion_impl_seq.cxx:182-197). */
+int cfp_wave_plan_create_dim(cfp_wave_plan_t *plan, int64_t nx, int64_t ny, int64_t nz, int dim, int device);
+/* dim = 3 */
 int cfp_wave_plan_create(cfp_wave_plan_t *plan, int64_t nx, int64_t ny, int64_t nz, int device);
 int cfp_wave_plan_destroy(cfp_wave_plan_t plan);
 /* kappa[d] = dt / h_d, c0 = sound speed */
 int cfp_wave_plan_set_symbol(cfp_wave_plan_t plan, const double kappa[3], double c0);
-/* x = S^{-1} b on the periodic grid (b, x: 4*nx*ny*nz complex doubles; x may alias b) */
+/* x = S^{-1} b on the periodic grid (b, x: (dim+1)*nx*ny*nz complex doubles; x may alias b) */
 int cfp_wave_plan_apply(cfp_wave_plan_t plan, const double *b, double *x, void *stream);
 /* unnormalised forward / backward 3-D DFT of each component (tests and tools) */
 int cfp_wave_plan_forward(cfp_wave_plan_t plan, const double *in, double *out, void *stream);
@@ -52,11 +57,20 @@ enum { CFP_WAVE_BC_WALL = 0, CFP_WAVE_BC_PERIODIC = 1, CFP_WAVE_BC_NEUMANN = 2 }
  * keeps its diagonal; columns ascend. */
 int cfp_wave_csr(int64_t nx, int64_t ny, int64_t nz, const double h[3], double dt, double c0, int bc, double shift,
                  int64_t *rowptr, int64_t *col, double *val, int64_t *nnz);
+/* the same for a dim-dimensional mesh (dim + 1 unknowns per cell, faces only along the first
+ * dim axes; the axes above dim must have n = 1).  rowptr: (dim+1)n+1 entries, col/val room for
+ * (dim+1)^2 (2 dim + 1) n entries. */
+int cfp_wave_csr_dim(int64_t nx, int64_t ny, int64_t nz, int dim, const double h[3], double dt, double c0, int bc,
+                     double shift, int64_t *rowptr, int64_t *col, double *val, int64_t *nnz);
 
 /* ---- PETSc-level entry points */
 PetscErrorCode computeDivergenceMatrixWaveCartesian(PetscInt nx, PetscInt ny, PetscInt nz, const PetscReal h[3],
                                                     PetscReal dt, PetscReal c0, PetscInt bc, Mat *A);
-/* pressure 155e5 where |centre - domain centre| < 0.3 else 70e5, momentum 0 (U: 4N) */
+PetscErrorCode computeDivergenceMatrixWaveCartesianDim(PetscInt nx, PetscInt ny, PetscInt nz, PetscInt dim,
+                                                       const PetscReal h[3], PetscReal dt, PetscReal c0, PetscInt bc,
+                                                       Mat *A);
+/* pressure 155e5 where |centre - domain centre| < 0.3 else 70e5, momentum 0.  U holds
+ * (dim+1)*N values; dim is read from its size (src/WaveSystem.cxx:25-76). */
 PetscErrorCode initial_conditions_shock_wave(PetscInt nx, PetscInt ny, PetscInt nz, const PetscReal xmin[3],
                                              const PetscReal xmax[3], Vec U);
 
@@ -67,6 +81,7 @@ struct FFTPrecWaveContext {
   PetscReal kappa_x, kappa_y, kappa_z; /* dt / h_d */
   PetscReal c0;
   cfp_wave_plan_t plan; /* created by setup, destroyed by destroy */
+  PetscInt dim;         /* 1, 2 or 3; 0 = 3 */
 };
 typedef struct FFTPrecWaveContext FFTPrecWaveContext;
 PetscErrorCode applyFFT3DPrecWave(PC pc, Vec b, Vec x);
@@ -89,6 +104,7 @@ typedef struct {
   int bc;             /* CFP_WAVE_BC_*: wall as the reference mains set up */
   int pc_side;        /* PC_LEFT / PC_RIGHT */
   int on_device;
+  int dim;            /* mesh dimension 1, 2 or 3 (nbComp = dim + 1); 0 = 3 */
 } cfp_wave_config;
 
 /* same layout as cfp_transport_result (transport_equation.h); lambda[] holds kappa */
@@ -106,7 +122,10 @@ typedef struct {
 } cfp_wave_result;
 
 void cfp_wave_config_default(cfp_wave_config *cfg, int64_t n);
-/* U_out: optional 4N complex (interleaved re,im) final field */
+/* the reference main's defaults for a dim-dimensional square / cube of n cells a side
+ * (cfl = 1e3 / dim, tests/WaveSystem_SphericalExplosion_impl_seq.cxx:212) */
+void cfp_wave_config_default_dim(cfp_wave_config *cfg, int64_t n, int dim);
+/* U_out: optional (dim+1)N complex (interleaved re,im) final field */
 PetscErrorCode WaveSystemGMRES(const cfp_wave_config *cfg, cfp_wave_result *res, double *U_out);
 
 #ifdef __cplusplus

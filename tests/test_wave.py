@@ -17,9 +17,9 @@ from oracle import transport as OT
 from oracle import wave as OW
 
 
-def _csr(dims, h, dt, bc, shift=0.0, c0=700.0):
-    rp, col, val = W.wave_csr(dims, h, dt, c0, bc, shift)
-    m = 4 * int(np.prod(dims))
+def _csr(dims, h, dt, bc, shift=0.0, c0=700.0, dim=3):
+    rp, col, val = W.wave_csr(dims, h, dt, c0, bc, shift, dim=dim)
+    m = (dim + 1) * int(np.prod(dims))
     return sp.csr_matrix((val, col, rp), shape=(m, m))
 
 
@@ -38,6 +38,81 @@ def test_wave_csr_matches_face_loop(case, bc):
     assert A.has_sorted_indices
     m = A.shape[0]
     assert all(r in A.indices[A.indptr[r]:A.indptr[r + 1]] for r in range(m))
+
+
+# 1-D and 2-D meshes: nbComp = dim + 1 unknowns per cell and faces along dim axes only
+# (src/WaveSystem.cxx:111-113); the reference mains' default mesh is the 2-D 50 x 50 square
+CASES_LOWDIM = [((5, 4, 1), (0.2, 0.25, 1.0), 2e-4, 2), ((6, 1, 1), (1 / 6, 1.0, 1.0), 3e-4, 2),
+                ((1, 1, 1), (1.0, 1.0, 1.0), 1e-4, 2), ((7, 1, 1), (1 / 7, 1.0, 1.0), 5e-4, 1),
+                ((2, 1, 1), (0.5, 1.0, 1.0), 1e-4, 1)]
+
+
+@pytest.mark.parametrize("bc", ["wall", "periodic", "neumann"])
+@pytest.mark.parametrize("case", CASES_LOWDIM, ids=lambda c: f"{c[3]}d-" + "x".join(map(str, c[0])))
+def test_wave_csr_lowdim_matches_face_loop(case, bc):
+    dims, h, dt, dim = case
+    A = _csr(dims, h, dt, bc, shift=1.0, dim=dim)
+    R = OW.wave_matrix(dims, h, dt, bc=bc, shift=1.0, dim=dim)
+    assert A.shape == ((dim + 1) * int(np.prod(dims)),) * 2
+    scale = max(1.0, abs(R).max())
+    np.testing.assert_allclose(A.toarray(), R.toarray(), rtol=0, atol=1e-13 * scale)
+    m = A.shape[0]
+    assert all(r in A.indices[A.indptr[r]:A.indptr[r + 1]] for r in range(m))
+
+
+@pytest.mark.parametrize("dim,dims,h", [(2, (5, 4), (0.2, 0.25)), (1, (9,), (1 / 9,))], ids=["2d", "1d"])
+def test_block_solve_inverts_periodic_assembly_lowdim(dim, dims, h):
+    dt = 4e-4
+    kappa = [dt / v for v in h] + [0.0] * (3 - dim)
+    A = OW.wave_matrix(dims, h, dt, bc="periodic", shift=1.0, dim=dim)
+    rng = np.random.default_rng(5)
+    b = rng.standard_normal(A.shape[0]) + 1j * rng.standard_normal(A.shape[0])
+    x = OW.block_solve(dims, kappa, b, dim=dim)
+    assert np.linalg.norm(A @ x - b) <= 1e-12 * np.linalg.norm(b)
+
+
+def test_wave_csr_lowdim_errors():
+    with pytest.raises(Exception):
+        W.wave_csr((4, 4, 2), (0.25, 0.25, 0.5), 1e-4, dim=2)  # nz > 1 in 2-D
+    with pytest.raises(Exception):
+        W.wave_csr((4, 2, 1), (0.25, 0.5, 1.0), 1e-4, dim=1)  # ny > 1 in 1-D
+    with pytest.raises(Exception):
+        W.wave_csr((4, 1, 1), (0.25, 1.0, 1.0), 1e-4, dim=4)
+
+
+def test_wave_initial_condition_2d():
+    dims = (10, 8, 1)
+    v = P.Vec.seq(3 * int(np.prod(dims)))
+    lo, hi = (ctypes.c_double * 3)(-0.5, -0.5, -0.5), (ctypes.c_double * 3)(0.5, 0.5, 0.5)
+    P.PetscCall(P.lib().initial_conditions_shock_wave(*dims, lo, hi, v.h))
+    np.testing.assert_array_equal(v.array(), OW.initial_conditions_shock_wave(dims, dim=2))
+    bad = P.Vec.seq(5 * int(np.prod(dims)))
+    with pytest.raises(P.PetscError):
+        P.PetscCall(P.lib().initial_conditions_shock_wave(*dims, lo, hi, bad.h))
+
+
+def test_wave_config_reference_main_default():
+    """The reference main's default: 2-D 50 x 50 square, cfl = 1e3 / 2 (impl_seq.cxx:182-212)."""
+    cfg = W.config(50, dim=2)
+    assert (cfg.nx, cfg.ny, cfg.nz, cfg.dim) == (50, 50, 1, 2)
+    assert cfg.cfl == 500.0 and cfg.c0 == 700.0 and cfg.tmax == 0.05
+
+
+def test_wave_driver_2d_pcnone_host_matches_oracle():
+    dims = (12, 10, 1)
+    res, U = W.run(W.config(dims, dim=2, pc="none", device=False, steps=3), return_field=True)
+    dt, kappa, h = OW.dt_and_kappa(dims, dim=2)
+    assert res["dt"] == pytest.approx(dt, rel=1e-15)
+    assert res["kappa"] == pytest.approx(kappa, rel=1e-15)
+    A = OW.wave_matrix(dims, h, dt, bc="wall", shift=1.0, dim=2)
+    Uo = OW.initial_conditions_shock_wave(dims, dim=2)
+    its = 0
+    for _ in range(3):
+        Uo, k, reason, _, _ = OT.gmres(A, Uo, rtol=1e-5, abstol=1e-5, maxits=1000)
+        its += k
+    assert abs(res["total_its"] - its) <= 3
+    # three rtol = 1e-5 solves in a row: the two GMRES agree to the solver tolerance
+    np.testing.assert_allclose(U, Uo, rtol=0, atol=1e-5 * np.abs(Uo).max())
 
 
 def test_block_solve_inverts_periodic_assembly():
@@ -138,6 +213,36 @@ def test_wave_plan_matches_oracle(dims):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dim,dims", [(2, (16, 16)), (2, (50, 50)), (2, (12, 10)), (2, (64, 32)), (2, (128, 128)),
+                                      (2, (7, 1)), (2, (1, 1)), (2, (256, 8)), (1, (16,)), (1, (50,)), (1, (7,)),
+                                      (1, (1024,)), (1, (1,))],
+                         ids=lambda v: str(v) if isinstance(v, int) else "x".join(map(str, v)))
+def test_wave_plan_lowdim_matches_oracle(dim, dims):
+    """1-D / 2-D wave systems (2 or 3 interleaved unknowns per cell) against the oracle."""
+    import torch
+    kappa = (0.079, 0.05, 0.0)
+    m = (dim + 1) * int(np.prod(dims))
+    b = _rand(m, 11)
+    plan = W.WavePlan(dims, dim=dim).set_symbol(kappa)
+    x = plan.apply(torch.from_numpy(b).cuda()).cpu().numpy()
+    xo = OW.block_solve(dims, kappa, b, dim=dim)
+    assert np.linalg.norm(x - xo) <= 1e-12 * np.linalg.norm(xo)
+    t = torch.from_numpy(b).cuda()
+    plan.apply(t, out=t)  # in place
+    assert np.linalg.norm(t.cpu().numpy() - xo) <= 1e-12 * np.linalg.norm(xo)
+
+
+@pytest.mark.gpu
+def test_wave_plan_lowdim_errors():
+    with pytest.raises(Exception):
+        W.WavePlan((8, 8, 2), dim=2)
+    with pytest.raises(Exception):
+        W.WavePlan((8, 2), dim=1)
+    with pytest.raises(Exception):
+        W.WavePlan((8, 8), dim=0)
+
+
+@pytest.mark.gpu
 def test_wave_plan_aliasing_and_transforms():
     import torch
     dims = (16, 8, 32)
@@ -221,5 +326,37 @@ def test_wave_driver_fft_pc_matches_oracle():
 def test_wave_fft_pc_cuts_iterations():
     r_none = W.run(W.config(32, pc="none"))
     r_fft = W.run(W.config(32, pc="fft"))
+    assert r_fft["all_converged"] == 1
+    assert r_none["all_converged"] == 0 or r_fft["total_its"] * 3 <= r_none["total_its"]
+
+
+@pytest.mark.gpu
+def test_wave_driver_2d_fft_pc_matches_oracle():
+    dims = (32, 24, 1)
+    res, U = W.run(W.config(dims, dim=2, pc="fft", steps=2), return_field=True)
+    dt, kappa, h = OW.dt_and_kappa(dims, dim=2)
+    assert res["kappa"] == pytest.approx(kappa, rel=1e-14)
+    A = OW.wave_matrix(dims, h, dt, bc="wall", shift=1.0, dim=2)
+    U0 = OW.initial_conditions_shock_wave(dims, dim=2)
+    M = lambda v: OW.block_solve(dims, kappa, v, dim=2)  # noqa: E731
+    its, Uo = [], U0
+    for _ in range(2):
+        Uo, k, reason, _, _ = OT.gmres(A, Uo, M=M, rtol=1e-5, abstol=1e-5, maxits=1000)
+        its.append(k)
+    assert res["all_converged"] == 1
+    assert abs(res["total_its"] - sum(its)) <= max(1, sum(its) // 100)
+    Us = U0
+    for _ in range(2):
+        Us = spla.spsolve(A.tocsc(), Us)
+    assert np.linalg.norm(U - Us) <= 10 * np.linalg.norm(Uo - Us) + 1e-10 * np.linalg.norm(Us)
+
+
+@pytest.mark.gpu
+def test_wave_reference_default_2d_50x50():
+    """The reference main's own case (2-D 50 x 50 square, wall boundaries, cfl 500, tmax 0.05):
+    the whole time loop with PCNONE and with the block-circulant PCSHELL."""
+    r_none = W.run(W.config(50, dim=2, pc="none"))
+    r_fft = W.run(W.config(50, dim=2, pc="fft"))
+    assert r_fft["steps"] == r_none["steps"] > 0
     assert r_fft["all_converged"] == 1
     assert r_none["all_converged"] == 0 or r_fft["total_its"] * 3 <= r_none["total_its"]
