@@ -138,6 +138,18 @@ __device__ __forceinline__ cd gload(const cd* p) {
   }
   return *p;
 }
+// plain 16-byte load / store as a native vector (a HIP_vector_type assignment is a memcpy, which
+// keeps register arrays of cd on the stack when they are filled in one loop and used in another)
+__device__ __forceinline__ dv2 ldv(const cd* p) { return *reinterpret_cast<const dv2*>(p); }
+__device__ __forceinline__ void stv(cd* p, dv2 v) { *reinterpret_cast<dv2*>(p) = v; }
+__device__ __forceinline__ dv2 tov(cd v) {
+  dv2 w;
+  w.x = v.x;
+  w.y = v.y;
+  return w;
+}
+__device__ __forceinline__ cd fromv(dv2 v) { return make_cd(v.x, v.y); }
+
 template <int FLAGS>
 __device__ __forceinline__ void gstore(cd* p, cd v) {
   if (FLAGS & (F_NT | F_NT_ST)) {

@@ -23,6 +23,7 @@
 // LDS-resident Stockham, one specialised radix (8, 4, 2, 3, 5, 7) per stage, butterflies
 // staged in VGPRs so the stages run in place in one LDS buffer.
 #include <cstring>
+#include <type_traits>
 
 #include "cfp_fft_device.h"
 
@@ -179,6 +180,7 @@ static hipError_t launch_fast_n(const PassDesc& p, const cd* in, cd* out, const 
 #define CFP_MR_MAXF 24
 #define CFP_MR_POINTS 2048  // target points per block (one LDS buffer: 32 KiB)
 #define CFP_MR_MAXPTS 2048  // most points per block of the in-place stages (larger: ping-pong)
+#define CFP_MR_U 8          // most global loads in flight per thread (batched load loops)
 
 struct MRStage {
   int r;         // radix
@@ -202,6 +204,17 @@ struct MRArgs {
   int pingpong;                 // a prime radix above 7: stages go A -> B (else in place, one buffer)
   int nbuf;                     // LDS buffers of G * L points (2 for ping-pong or the wave solve)
 };
+
+// f(integral_constant<int, 0>) ... f(integral_constant<int, U-1>): the batched loops' slot index is
+// a front-end constant, so their register arrays never become stack (scratch) arrays
+#define CFP_INLINE __attribute__((always_inline))
+template <int U, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (U > 0) {
+    static_for<U - 1>(f);
+    f(std::integral_constant<int, U - 1>{});
+  }
+}
 
 __host__ __device__ inline uint64_t mr_magic(uint32_t d) { return ((1ull << 40) + d - 1) / d; }
 // floor(u / d) for u * d < 2^40 (u < 2^20, d <= 4096 here)
@@ -392,7 +405,9 @@ __device__ __forceinline__ void mr_fft(cd*& X, cd*& Y, const MRArgs& g, const cd
   }
 }
 
-template <bool ROW>
+// U = loads in flight per thread in the batched loops, sized to the block (2 / 4 / 8 for blocks of
+// up to 512 / 1024 / more points) so a small block does not issue clamped duplicates
+template <bool ROW, int U>
 __global__ void __launch_bounds__(CFP_MR_THREADS) k_axis_mixed(const cd* in, cd* out, MRArgs g, int mode) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   __shared__ i64 base_in[64], base_out[64];
@@ -400,9 +415,14 @@ __global__ void __launch_bounds__(CFP_MR_THREADS) k_axis_mixed(const cd* in, cd*
   cd* X = reinterpret_cast<cd*>(smem_raw);
   cd* Y = X + (size_t)G * L;  // second buffer (ping-pong stages, the wave solve's output)
   const cd* tw = g.k.tw;
-  if (g.tw_lds) {
+  if (g.tw_lds) {  // batched: up to U global loads in flight per thread
     cd* t = X + (size_t)(g.nbuf * G * L);
-    for (int i = threadIdx.x; i < n; i += CFP_MR_THREADS) t[i] = g.k.tw[i];
+    // clamped indices: the surplus slots copy tw[n-1] onto itself, so neither loop branches
+    for (int i0 = threadIdx.x; i0 < n; i0 += CFP_MR_THREADS * U) {
+      dv2 v[U];
+      static_for<U>([&](auto u) CFP_INLINE { v[u] = ldv(g.k.tw + min(i0 + u * CFP_MR_THREADS, n - 1)); });
+      static_for<U>([&](auto u) CFP_INLINE { stv(t + min(i0 + u * CFP_MR_THREADS, n - 1), v[u]); });
+    }
     tw = t;
   }
   const i64 g0 = (i64)blockIdx.x * G;
@@ -418,14 +438,25 @@ __global__ void __launch_bounds__(CFP_MR_THREADS) k_axis_mixed(const cd* in, cd*
     else if (g.gshift >= 0) { k = i >> g.gshift; c = i & (G - 1); }
     else { k = (int)mr_div((uint32_t)i, g.G_M); c = i - k * G; }
   };
-  for (int i = threadIdx.x; i < total; i += CFP_MR_THREADS) {
-    int c, k;
-    split(i, c, k);
-    cd v = make_cd(0.0, 0.0);
-    if (g0 + c < g.ncols) v = in[base_in[c] + mr_pt_off(g.k.in, k, g.segin_M)];
-    if (mode == PASS_INV) v = cconj(v);
-    if (mode == PASS_INV && g.k.tw4.lo) v = cmul(v, tw4_at(g.k.tw4, ((g0 + c) / g.k.tw4.kdiv % g.k.tw4.n1) * k));
-    X[c * L + k] = v;
+  // the column loads are batched U per thread (all in flight before the first LDS store):
+  // a block of 2,048 points is one round trip to HBM instead of 8 dependent ones
+  // (the loads are unconditional -- a clamped index, and base_in = 0 for a missing column -- so
+  // the compiler issues them back to back without branches; the second loop drops the extras)
+  // (surplus slots of the last batch repeat the last point: the same value to the same LDS slot)
+  for (int i0 = threadIdx.x; i0 < total; i0 += CFP_MR_THREADS * U) {
+    dv2 v[U];
+    int cc[U], kk[U];
+    static_for<U>([&](auto u) CFP_INLINE {
+      split(min(i0 + u * CFP_MR_THREADS, total - 1), cc[u], kk[u]);
+      v[u] = ldv(in + base_in[cc[u]] + mr_pt_off(g.k.in, kk[u], g.segin_M));  // base 0 for a missing column
+    });
+    static_for<U>([&](auto u) CFP_INLINE {
+      const int c = cc[u], k = kk[u];
+      cd v1 = g0 + c < g.ncols ? fromv(v[u]) : make_cd(0.0, 0.0);
+      if (mode == PASS_INV) v1 = cconj(v1);
+      if (mode == PASS_INV && g.k.tw4.lo) v1 = cmul(v1, tw4_at(g.k.tw4, ((g0 + c) / g.k.tw4.kdiv % g.k.tw4.n1) * k));
+      stv(X + c * L + k, tov(v1));
+    });
   }
   __syncthreads();
   mr_fft(X, Y, g, tw);
@@ -434,23 +465,35 @@ __global__ void __launch_bounds__(CFP_MR_THREADS) k_axis_mixed(const cd* in, cd*
     // (G % nc == 0, g0 % nc == 0); the missing momentum rows of dim < 3 are zero, and the
     // absent axes' symbol entries (n_d = 1) are p = q = 0, so the 4x4 algebra serves them
     const int nc = g.k.wave.ncomp;
-    for (int i = threadIdx.x; i < total; i += CFP_MR_THREADS) {
-      int c, k;
-      split(i, c, k);
-      const i64 gg = g0 + c;
-      const int comp = c % nc;
-      const int cb = c - comp;
-      cd r[4];
+    constexpr int UW = 4;  // symbol-table loads batched UW points per thread (clamped, unconditional)
+    for (int i0 = threadIdx.x; i0 < total; i0 += CFP_MR_THREADS * UW) {
+      dv2 pq[UW][3];
+      int cu[UW], ku[UW];
+      const WaveSym& w = g.k.wave;
+      static_for<UW>([&](auto u) CFP_INLINE {
+        split(min(i0 + u * CFP_MR_THREADS, total - 1), cu[u], ku[u]);
+        const i64 cell = (g0 + cu[u] < g.ncols ? g0 + cu[u] : g0) / nc;
+        // (p, q) per axis: the fused axis at frequency k, the other two at the cell's column
+        // (wave_cell_sym); an absent axis (n = 1) reads its single entry (0, 0)
+        i64 idx[3];
+        if (w.fused == 2) { idx[0] = cell % w.n[0]; idx[1] = cell / w.n[0]; idx[2] = ku[u]; }
+        else if (w.fused == 1) { idx[0] = cell % w.n[0]; idx[1] = ku[u]; idx[2] = cell / w.n[0]; }
+        else { idx[0] = ku[u]; idx[1] = cell % w.n[1]; idx[2] = cell / w.n[1]; }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) r[j] = j < nc ? X[(cb + j) * L + k] : make_cd(0.0, 0.0);
-      cd w = make_cd(0.0, 0.0);
-      if (gg < g.ncols) {
-        double2 pq[3];
-        wave_cell_sym(g.k.wave, gg / nc, pq);
-        pq[g.k.wave.fused] = g.k.wave.tab[g.k.wave.fused][k];
-        w = cconj(wave_solve(r, comp, pq, g.k.wave.c0sq));
-      }
-      Y[c * L + k] = w;
+        for (int d = 0; d < 3; ++d) pq[u][d] = ldv(w.tab[d] + idx[d]);
+      });
+      static_for<UW>([&](auto u) CFP_INLINE {  // (Y is write-only here: surplus slots repeat the same value)
+        const int c = cu[u], k = ku[u];
+        const int comp = c % nc;
+        const int cb = c - comp;
+        cd r[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = j < nc ? X[(cb + j) * L + k] : make_cd(0.0, 0.0);
+        cd res = make_cd(0.0, 0.0);
+        const double2 pq3[3] = {fromv(pq[u][0]), fromv(pq[u][1]), fromv(pq[u][2])};
+        if (g0 + c < g.ncols) res = cconj(wave_solve(r, comp, pq3, w.c0sq));
+        stv(Y + c * L + k, tov(res));
+      });
     }
     __syncthreads();
     cd* t = X;
@@ -458,19 +501,28 @@ __global__ void __launch_bounds__(CFP_MR_THREADS) k_axis_mixed(const cd* in, cd*
     Y = t;
     mr_fft(X, Y, g, tw);
   } else if (mode == PASS_FUSED_SEP || mode == PASS_FUSED_DIAG) {
-    for (int i = threadIdx.x; i < total; i += CFP_MR_THREADS) {
-      int c, k;
-      split(i, c, k);
-      const i64 gg = g0 + c;
-      if (gg >= g.ncols) continue;
-      cd d;
-      if (mode == PASS_FUSED_SEP) {
-        d = cadd(cadd(g.k.colsym[gg], g.k.axsym[k]), make_cd(1.0, 0.0));
-        X[c * L + k] = cconj(cdiv_sym(X[c * L + k], d));
-      } else {
-        d = g.k.diag[base_in[c] + mr_pt_off(g.k.in, k, g.segin_M)];
-        X[c * L + k] = cconj(cdiv(X[c * L + k], d));
-      }
+    // symbol loads batched like the column loads
+    for (int i0 = threadIdx.x; i0 < total; i0 += CFP_MR_THREADS * U) {
+      // a read-modify-write: the surplus slots must not repeat a point, they skip the store
+      dv2 d[U];
+      int pos[U];
+      static_for<U>([&](auto u) CFP_INLINE {  // unconditional loads at clamped indices, as above
+        int c, k;
+        split(min(i0 + u * CFP_MR_THREADS, total - 1), c, k);
+        const i64 gg = g0 + c;
+        const bool ok = i0 + u * CFP_MR_THREADS < total && gg < g.ncols;
+        pos[u] = ok ? c * L + k : -1;
+        if (mode == PASS_FUSED_SEP) d[u] = ldv(g.k.colsym + (ok ? gg : g0)) + ldv(g.k.axsym + k);
+        else d[u] = ldv(g.k.diag + base_in[c] + mr_pt_off(g.k.in, k, g.segin_M));
+      });
+      static_for<U>([&](auto u) CFP_INLINE {
+        if (pos[u] < 0) return;
+        const cd xv = fromv(ldv(X + pos[u]));
+        cd r;
+        if (mode == PASS_FUSED_SEP) r = cconj(cdiv_sym(xv, cadd(fromv(d[u]), make_cd(1.0, 0.0))));
+        else r = cconj(cdiv(xv, fromv(d[u])));
+        stv(X + pos[u], tov(r));
+      });
     }
     __syncthreads();
     mr_fft(X, Y, g, tw);
@@ -571,18 +623,22 @@ static hipError_t launch_generic(const PassDesc& p, const cd* in, cd* out, const
   if (lds > kMixedMaxLds) return hipErrorInvalidConfiguration;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_axis_mixed<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kMixedMaxLds);
-    (void)hipFuncSetAttribute((const void*)k_axis_mixed<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kMixedMaxLds);
+    const void* kf[] = {(const void*)k_axis_mixed<true, 2>, (const void*)k_axis_mixed<true, 4>,
+                        (const void*)k_axis_mixed<true, 8>, (const void*)k_axis_mixed<false, 2>,
+                        (const void*)k_axis_mixed<false, 4>, (const void*)k_axis_mixed<false, 8>};
+    for (const void* f : kf) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMixedMaxLds);
     (void)hipGetLastError();  // a refused attribute must not surface as this launch's error
     attr_set = true;
   }
   const i64 blocks = (p.ncols + G - 1) / G;
-  if (row)
-    hipLaunchKernelGGL(k_axis_mixed<true>, dim3((unsigned)blocks), dim3(CFP_MR_THREADS), lds, s, in, out, g, p.mode);
-  else
-    hipLaunchKernelGGL(k_axis_mixed<false>, dim3((unsigned)blocks), dim3(CFP_MR_THREADS), lds, s, in, out, g, p.mode);
+  const int pts = G * p.n;
+  const dim3 gr((unsigned)blocks), bl(CFP_MR_THREADS);
+#define CFP_MR_LAUNCH(ROWV)                                                                          \
+  if (pts <= 2 * CFP_MR_THREADS) hipLaunchKernelGGL((k_axis_mixed<ROWV, 2>), gr, bl, lds, s, in, out, g, p.mode); \
+  else if (pts <= 4 * CFP_MR_THREADS) hipLaunchKernelGGL((k_axis_mixed<ROWV, 4>), gr, bl, lds, s, in, out, g, p.mode); \
+  else hipLaunchKernelGGL((k_axis_mixed<ROWV, 8>), gr, bl, lds, s, in, out, g, p.mode);
+  if (row) { CFP_MR_LAUNCH(true) } else { CFP_MR_LAUNCH(false) }
+#undef CFP_MR_LAUNCH
   return hipGetLastError();
 }
 

@@ -1,6 +1,8 @@
 // kexp.hip -- timing harness for fast axis-pass kernel variants (not part of the product).
 // Builds the same device code as the product (cfp_fft_device.h) with several shapes/flags
 // and times them back to back in one process (methodology rule 24 of the HIP guide).
+#include <cstring>
+
 #include "../../circulantpreconditioner_amd/csrc/cfp_fft_device.h"
 
 using namespace cfp;
@@ -54,6 +56,21 @@ static const Var kVars[] = {
     V(1024, 16, 4, true, 4, 0, 16) V(1024, 16, 4, true, 4, 0, 17) V(1024, 16, 4, true, 2, 0, 17)
     V(1024, 16, 4, true, 4, 0, 19) V(1024, 16, 4, false, 8, 0, 17) V(1024, 16, 4, false, 4, 0, 17)
     V(1024, 16, 4, false, 8, 0, 19)
+    // x-fused order (60..): row-mode fused 256 shapes -- product (PTS 8, T 8, nt-ld), PTS 16 T 8 / 4 / 16
+    // (nt-ld, split), 4-wave request, non-split
+    V(256, 8, 4, true, 8, 2, 16) V(256, 16, 16, true, 8, 2, 17) V(256, 16, 16, true, 4, 2, 17)
+    V(256, 16, 16, true, 16, 2, 17) V(256, 16, 16, true, 8, 2, 145) V(256, 16, 16, true, 8, 2, 16)
+    V(256, 16, 16, true, 4, 2, 145) V(256, 8, 4, true, 16, 2, 16)
+    // N = 512 whole-apply shapes (68..): fused split T 16 / +4-wave / PTS 8 T 16 / PTS 8 T 8 split /
+    // PTS 16 T 8 split / product (PTS 8 T 8 nt-ld) / PTS 8 T 16 4-wave
+    V(512, 16, 2, false, 16, 2, 17) V(512, 16, 2, false, 16, 2, 145) V(512, 8, 8, false, 16, 2, 17)
+    V(512, 8, 8, false, 8, 2, 17) V(512, 16, 2, false, 8, 2, 17) V(512, 8, 8, false, 8, 2, 16)
+    V(512, 8, 8, false, 16, 2, 145)
+    // columns (75..80): product fwd (split nt-ld), PTS 8, T 32, product inv (split nt-st), PTS 8 inv, 4-wave
+    V(512, 16, 2, false, 16, 0, 17) V(512, 8, 8, false, 16, 0, 17) V(512, 16, 2, false, 32, 0, 17)
+    V(512, 16, 2, false, 16, 0, 33) V(512, 8, 8, false, 16, 0, 33) V(512, 16, 2, false, 16, 0, 145)
+    // rows (81, 82): product fwd (nt-ld), inv (nt-st)
+    V(512, 16, 2, true, 8, 0, 16) V(512, 16, 2, true, 8, 0, 32)
 };
 
 extern "C" int kexp_count() { return (int)(sizeof(kVars) / sizeof(kVars[0])); }
@@ -70,6 +87,7 @@ extern "C" int kexp_time(int i, const double* in, double* out, const double* tw,
   const Var& v = kVars[i];
   const i64 n = v.n, N = n * n * n;
   KArgs a;
+  memset(&a, 0, sizeof(a));
   Side s;
   s.seg_len = (int)n;
   s.seg_shift = ilog2((int)n);
@@ -101,6 +119,9 @@ extern "C" int kexp_chain(int ix, int iy, int iz, int iy2, int ix2, const double
                           const double* axsym, int iters, double* ms) {
   const i64 n = kVars[ix].n, N = n * n * n;
   KArgs ax, ay, az;
+  memset(&ax, 0, sizeof(ax));
+  memset(&ay, 0, sizeof(ay));
+  memset(&az, 0, sizeof(az));
   Side s;
   s.seg_len = (int)n; s.seg_shift = ilog2((int)n); s.seg_stride = 0;
   s.inner_stride = 0; s.outer_stride = n; s.pt_stride = 1; ax.in = ax.out = s; ax.inner_n = 1;
@@ -116,6 +137,43 @@ extern "C" int kexp_chain(int ix, int iy, int iz, int iy2, int ix2, const double
     kVars[iz].fn((const cd*)x, (cd*)x, &az, nc);
     kVars[iy2].fn((const cd*)x, (cd*)x, &ay, nc);
     kVars[ix2].fn((const cd*)x, (cd*)x, &ax, nc);
+  };
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  one();
+  (void)hipEventRecord(e0, nullptr);
+  for (int it = 0; it < iters; ++it) one();
+  (void)hipEventRecord(e1, nullptr);
+  hipError_t e = hipEventSynchronize(e1);
+  float t = 0;
+  (void)hipEventElapsedTime(&t, e0, e1);
+  *ms = t / iters;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return e == hipSuccess ? (int)hipGetLastError() : (int)e;
+}
+
+// time `iters` chained applies of `nst` steps: step i runs variant var[i] along axis ax[i]
+// (0 = x rows, 1 = y columns, 2 = z columns); the first reads b, the rest work in place on x
+extern "C" int kexp_chain_axes(int nst, const int* var, const int* axv, const double* b, double* x, const double* tw,
+                               const double* colsym, const double* axsym, int iters, double* ms) {
+  const i64 n = kVars[var[0]].n, N = n * n * n;
+  KArgs a3[3];
+  memset(a3, 0, sizeof(a3));
+  Side s;
+  s.seg_len = (int)n; s.seg_shift = ilog2((int)n); s.seg_stride = 0;
+  s.inner_stride = 0; s.outer_stride = n; s.pt_stride = 1; a3[0].in = a3[0].out = s; a3[0].inner_n = 1;
+  s.inner_stride = 1; s.outer_stride = n * n; s.pt_stride = n; a3[1].in = a3[1].out = s; a3[1].inner_n = n;
+  s.inner_stride = 1; s.outer_stride = 0; s.pt_stride = n * n; a3[2].in = a3[2].out = s; a3[2].inner_n = n * n;
+  for (KArgs& a : a3) {
+    a.scale = 1.0; a.tw = (const cd*)tw; a.colsym = (const cd*)colsym; a.axsym = (const cd*)axsym; a.diag = nullptr;
+    a.tw4.lo = a.tw4.hi = nullptr;
+  }
+  const i64 nc = N / n;
+  auto one = [&]() {
+    for (int i = 0; i < nst; ++i)
+      kVars[var[i]].fn(i == 0 ? (const cd*)b : (const cd*)x, (cd*)x, &a3[axv[i]], nc);
   };
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
