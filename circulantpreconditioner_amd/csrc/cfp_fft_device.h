@@ -122,8 +122,106 @@ __device__ __forceinline__ void dft_reg(cd* v) {
   }
 }
 
+// cos / sin(2 pi j / R), j = 0 .. R-1, for the odd in-register radices
+template <int R> struct OddTab;
+template <> struct OddTab<3> {
+  static constexpr double C[3] = {1.0, -0.5, -0.5};
+  static constexpr double S[3] = {0.0, 0.86602540378443864676, -0.86602540378443864676};
+};
+template <> struct OddTab<5> {
+  static constexpr double C[5] = {1.0, 0.30901699437494742410, -0.80901699437494742410, -0.80901699437494742410,
+                                  0.30901699437494742410};
+  static constexpr double S[5] = {0.0, 0.95105651629515357212, 0.58778525229247312917, -0.58778525229247312917,
+                                  -0.95105651629515357212};
+};
+template <> struct OddTab<7> {
+  static constexpr double C[7] = {1.0, 0.62348980185873353053, -0.22252093395631440429, -0.90096886790241912624,
+                                  -0.90096886790241912624, -0.22252093395631440429, 0.62348980185873353053};
+  static constexpr double S[7] = {0.0, 0.78183148246802980871, 0.97492791218182360702, 0.43388373911755812048,
+                                  -0.43388373911755812048, -0.97492791218182360702, -0.78183148246802980871};
+};
+
+// forward DFT of an odd R in registers, natural order: pairs a_t = x_t + x_{R-t},
+// b_t = x_t - x_{R-t};  y_k = x_0 + sum a_t cos(2 pi k t / R) - i sum b_t sin(2 pi k t / R),
+// y_{R-k} the same with +i.
+template <int R>
+__device__ __forceinline__ void dft_odd(cd* v) {
+  constexpr int H = (R - 1) / 2;
+  cd a[H], b[H];
+#pragma unroll
+  for (int t = 1; t <= H; ++t) {
+    a[t - 1] = cadd(v[t], v[R - t]);
+    b[t - 1] = csub(v[t], v[R - t]);
+  }
+  cd y0 = v[0];
+#pragma unroll
+  for (int t = 0; t < H; ++t) y0 = cadd(y0, a[t]);
+  cd out[R];
+  out[0] = y0;
+#pragma unroll
+  for (int k = 1; k <= H; ++k) {
+    double cr = v[0].x, ci = v[0].y, sr = 0.0, si = 0.0;
+#pragma unroll
+    for (int t = 1; t <= H; ++t) {
+      const double c = OddTab<R>::C[(k * t) % R], sn = OddTab<R>::S[(k * t) % R];
+      cr = fma(a[t - 1].x, c, cr);
+      ci = fma(a[t - 1].y, c, ci);
+      sr = fma(b[t - 1].x, sn, sr);
+      si = fma(b[t - 1].y, sn, si);
+    }
+    // -i (sr + i si) = si - i sr
+    out[k] = make_cd(cr + si, ci - sr);
+    out[R - k] = make_cd(cr - si, ci + sr);
+  }
+#pragma unroll
+  for (int k = 0; k < R; ++k) v[k] = out[k];
+}
+
+// 10 = 2 x 5, decimation in time: X[k] = E[k] + W10^k O[k], X[k+5] = E[k] - W10^k O[k] with
+// E, O the 5-point DFTs of the even and odd samples
+__device__ __forceinline__ void dft10(cd* v) {
+  cd e[5], o[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    e[i] = v[2 * i];
+    o[i] = v[2 * i + 1];
+  }
+  dft_odd<5>(e);
+  dft_odd<5>(o);
+  constexpr double c36 = 0.80901699437494742410, s36 = 0.58778525229247312917;
+  constexpr double c72 = 0.30901699437494742410, s72 = 0.95105651629515357212;
+  const double wr[5] = {1.0, c36, c72, -c72, -c36}, wi[5] = {0.0, -s36, -s72, -s72, -s36};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const cd t = k == 0 ? o[0] : cmul(o[k], make_cd(wr[k], wi[k]));
+    v[k] = cadd(e[k], t);
+    v[k + 5] = csub(e[k], t);
+  }
+}
+
+// in-register DFT of any radix the fast pass uses: 2^k, odd 3 / 5 / 7, 10
+template <int R>
+__device__ __forceinline__ void dft_any(cd* v) {
+  if constexpr ((R & (R - 1)) == 0) dft_reg<R>(v);
+  else if constexpr (R == 10) dft10(v);
+  else dft_odd<R>(v);
+}
+
+__host__ __device__ constexpr bool is_pow2c(int v) { return v > 0 && (v & (v - 1)) == 0; }
+// log_b(v) when v is an exact power of b, else -1
+__host__ __device__ constexpr int ilogb_exact(int v, int b) {
+  return v == 1 ? 0 : (v % b != 0 ? -1 : (ilogb_exact(v / b, b) < 0 ? -1 : 1 + ilogb_exact(v / b, b)));
+}
+
 __device__ __forceinline__ i64 pt_off(const Side& s, int k) {
   return (i64)(k >> s.seg_shift) * s.seg_stride + (i64)(k & (s.seg_len - 1)) * s.pt_stride;
+}
+// point offset in a pass of length N: powers of two may be segmented (slab chunks, four-step
+// halves); other lengths are plain strided columns (the host only routes those here)
+template <int N>
+__device__ __forceinline__ i64 kpt_off(const Side& s, int k) {
+  if constexpr (is_pow2c(N)) return pt_off(s, k);
+  else return (i64)k * s.pt_stride;
 }
 __device__ __forceinline__ i64 col_base(const Side& s, i64 g, i64 inner_n) {
   return (g % inner_n) * s.inner_stride + (g / inner_n) * s.outer_stride;
@@ -165,6 +263,7 @@ __device__ __forceinline__ void gstore(cd* p, cd v) {
 struct KArgs {
   Side in, out;
   i64 inner_n;
+  i64 ncols;  // columns of the pass (the last tile of a non-power-of-two pass may be partial)
   double scale;
   const cd* tw;
   const cd* colsym;
@@ -287,8 +386,9 @@ template <int N, int PTS, int R0>
 struct Shape {
   static constexpr int TPC = N / PTS;
   static constexpr int QQ = PTS / R0;
-  static constexpr int S = 1 + (ilog2(N / R0) / ilog2(PTS));
-  static_assert(R0 * (1 << (ilog2(PTS) * (S - 1))) == N, "N must be R0 * PTS^k");
+  static constexpr int S = 1 + ilogb_exact(N / R0, PTS);
+  static_assert(N % R0 == 0 && ilogb_exact(N / R0, PTS) >= 0, "N must be R0 * PTS^k");
+  static_assert(PTS % R0 == 0, "R0 must divide PTS");
 };
 
 // LDS index of element idx of the workgroup's column c (row mode pads every 16 elements)
@@ -336,7 +436,7 @@ __device__ __forceinline__ void fft_stages(cd* v, void* lds, const cd* tws, int 
   typedef Shape<N, PTS, R0> SH;
   constexpr int TPC = SH::TPC, QQ = SH::QQ, S = SH::S;
   if constexpr (S == 1) {
-    dft_reg<R0>(v);
+    dft_any<R0>(v);
     return;
   } else {
     // stage 0 (radix R0, Ns = 1, no twiddles): butterfly q works in place on slots
@@ -346,7 +446,7 @@ __device__ __forceinline__ void fft_stages(cd* v, void* lds, const cd* tws, int 
       cd u[R0];
 #pragma unroll
       for (int t = 0; t < R0; ++t) u[t] = v[q + t * QQ];
-      dft_reg<R0>(u);
+      dft_any<R0>(u);
 #pragma unroll
       for (int t = 0; t < R0; ++t) v[q + t * QQ] = u[t];
     }
@@ -356,11 +456,11 @@ __device__ __forceinline__ void fft_stages(cd* v, void* lds, const cd* tws, int 
     int Ns = R0;
 #pragma unroll
     for (int s = 1; s < S; ++s) {
-      const int jm = tpc & (Ns - 1);
+      const int jm = tpc % Ns;  // Ns is a constant after unrolling: a mask for powers of two
       const int step = N / (Ns * PTS);
 #pragma unroll
       for (int t = 1; t < PTS; ++t) v[t] = cmul(v[t], tws[jm * t * step]);
-      dft_reg<PTS>(v);
+      dft_any<PTS>(v);
       if (s < S - 1) {
         const int o = (tpc / Ns) * Ns * PTS + jm;
         const int NsC = Ns;
@@ -389,13 +489,17 @@ k_axis_fast(const cd* in, cd* out, KArgs a) {
   if (ROW) { tpc = tid % TPC; c = tid / TPC; }
   else { c = tid % T; tpc = tid / T; }
   const unsigned blk = (FLAGS & F_REV) ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;
-  const i64 g = (i64)blk * T + c;
+  // a partial last tile (non-power-of-two passes): its spare columns recompute the last column
+  // and store nothing; they still take part in every barrier
+  const i64 g0 = (i64)blk * T + c;
+  const bool live = g0 < a.ncols;
+  const i64 g = live ? g0 : a.ncols - 1;
   // point k = tpc + m*TPC: the bits of tpc and of m*TPC are disjoint and seg_len is a power
   // of two, so pt_off(k) = pt_off(tpc) + pt_off(m*TPC).  The first part is per thread (one
   // 64-bit VGPR base), the second is uniform per slot m (scalar ALU), so an access costs one
   // 64-bit add instead of two 64-bit multiplies.
-  const i64 bin = col_base(a.in, g, a.inner_n) + pt_off(a.in, tpc);
-  const i64 bout = col_base(a.out, g, a.inner_n) + pt_off(a.out, tpc);
+  const i64 bin = col_base(a.in, g, a.inner_n) + kpt_off<N>(a.in, tpc);
+  const i64 bout = col_base(a.out, g, a.inner_n) + kpt_off<N>(a.out, tpc);
   const cd* pin = in + bin;
   cd* pout = out + bout;
 
@@ -407,7 +511,7 @@ k_axis_fast(const cd* in, cd* out, KArgs a) {
 
   cd v[PTS];
 #pragma unroll
-  for (int m = 0; m < PTS; ++m) v[m] = gload<FLAGS>(pin + pt_off(a.in, m * TPC));
+  for (int m = 0; m < PTS; ++m) v[m] = gload<FLAGS>(pin + kpt_off<N>(a.in, m * TPC));
   if (MODE == PASS_INV) {
 #pragma unroll
     for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
@@ -455,7 +559,7 @@ k_axis_fast(const cd* in, cd* out, KArgs a) {
         d = cadd(cadd(cs, a.axsym[k]), make_cd(1.0, 0.0));
         v[m] = cconj(cdiv_sym(v[m], d));
       } else {
-        d = a.diag[bin + pt_off(a.in, m * TPC)];
+        d = a.diag[bin + kpt_off<N>(a.in, m * TPC)];
         v[m] = cconj(cdiv(v[m], d));
       }
     }
@@ -470,16 +574,17 @@ k_axis_fast(const cd* in, cd* out, KArgs a) {
   }
   const bool conj_out = (MODE != PASS_FWD);
   const double sc = a.scale;
+  if (!live) return;  // after the last barrier
   if (sc == 1.0) {  // uniform: no 1/N on this pass, only the conjugation of the inverse
 #pragma unroll
     for (int m = 0; m < PTS; ++m)
-      gstore<FLAGS>(pout + pt_off(a.out, m * TPC), make_cd(v[m].x, conj_out ? -v[m].y : v[m].y));
+      gstore<FLAGS>(pout + kpt_off<N>(a.out, m * TPC), make_cd(v[m].x, conj_out ? -v[m].y : v[m].y));
     return;
   }
   const double sy = conj_out ? -sc : sc;
 #pragma unroll
   for (int m = 0; m < PTS; ++m)
-    gstore<FLAGS>(pout + pt_off(a.out, m * TPC), make_cd(v[m].x * sc, v[m].y * sy));
+    gstore<FLAGS>(pout + kpt_off<N>(a.out, m * TPC), make_cd(v[m].x * sc, v[m].y * sy));
 }
 
 }  // namespace cfp

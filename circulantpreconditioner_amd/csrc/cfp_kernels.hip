@@ -22,6 +22,7 @@
 // Mixed-radix path (any n <= 4096, incl. primes; the reference's own 10, 100, 10x25x40 ...):
 // LDS-resident Stockham, one specialised radix (8, 4, 2, 3, 5, 7) per stage, butterflies
 // staged in VGPRs so the stages run in place in one LDS buffer.
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 
@@ -89,6 +90,38 @@ CFP_CFG(1024, false, 2, 16, 4, 8, SPL | LD)
 CFP_CFG(1024, true, 0, 16, 4, 4, SPL | LD)
 CFP_CFG(1024, true, 1, 16, 4, 4, SPL | ST)
 CFP_CFG(1024, true, 2, 16, 4, 4, SPL | LD)
+// non-power-of-two lengths the reference uses (its ctests run 10, 10^2, 10^3 and 100^3; its
+// default mesh is 100^3): radix-10 register stages, N = R0 * 10^(S-1)
+CFP_CFG(10, false, 0, 10, 10, 64, 0)
+CFP_CFG(10, false, 1, 10, 10, 64, ST)
+CFP_CFG(10, false, 2, 10, 10, 64, LD)
+CFP_CFG(10, true, 0, 10, 10, 64, LD)
+CFP_CFG(10, true, 1, 10, 10, 64, ST)
+CFP_CFG(10, true, 2, 10, 10, 64, LD)
+CFP_CFG(20, false, 0, 10, 2, 32, 0)
+CFP_CFG(20, false, 1, 10, 2, 32, ST)
+CFP_CFG(20, false, 2, 10, 2, 32, LD)
+CFP_CFG(20, true, 0, 10, 2, 32, LD)
+CFP_CFG(20, true, 1, 10, 2, 32, ST)
+CFP_CFG(20, true, 2, 10, 2, 32, LD)
+CFP_CFG(50, false, 0, 10, 5, 64, 0)
+CFP_CFG(50, false, 1, 10, 5, 64, ST)
+CFP_CFG(50, false, 2, 10, 5, 64, LD)
+CFP_CFG(50, true, 0, 10, 5, 64, LD)
+CFP_CFG(50, true, 1, 10, 5, 64, ST)
+CFP_CFG(50, true, 2, 10, 5, 64, LD)
+CFP_CFG(100, false, 0, 10, 10, 32, 0)
+CFP_CFG(100, false, 1, 10, 10, 32, ST)
+CFP_CFG(100, false, 2, 10, 10, 32, LD)
+CFP_CFG(100, true, 0, 10, 10, 32, LD)
+CFP_CFG(100, true, 1, 10, 10, 32, ST)
+CFP_CFG(100, true, 2, 10, 10, 32, LD)
+CFP_CFG(200, false, 0, 10, 2, 16, 0)
+CFP_CFG(200, false, 1, 10, 2, 16, ST)
+CFP_CFG(200, false, 2, 10, 2, 16, LD)
+CFP_CFG(200, true, 0, 10, 2, 16, LD)
+CFP_CFG(200, true, 1, 10, 2, 16, ST)
+CFP_CFG(200, true, 2, 10, 2, 16, LD)
 #undef SPL
 #undef ST
 #undef LD
@@ -116,6 +149,7 @@ static int fast_tile(const PassDesc& p) {
 #define CFP_TILE(NN) \
   case NN: return tile_of<NN>(r, role);
     CFP_TILE(16) CFP_TILE(32) CFP_TILE(64) CFP_TILE(128) CFP_TILE(256) CFP_TILE(512) CFP_TILE(1024)
+    CFP_TILE(10) CFP_TILE(20) CFP_TILE(50) CFP_TILE(100) CFP_TILE(200)
 #undef CFP_TILE
     default: return 0;
   }
@@ -124,6 +158,15 @@ static int fast_tile(const PassDesc& p) {
 bool fast_path_supported(const PassDesc& p) {
   const int T = fast_tile(p);
   if (T == 0) return false;
+  if (!is_pow2(p.n)) {
+    // radix-10 lengths: unsegmented sides only; any column count (the kernel guards a partial
+    // last tile) and any inner grouping (every column computes its own base)
+    if (p.in.seg_len < p.n || p.out.seg_len < p.n) return false;
+    if (!row_mode(p) && (p.in.inner_stride != 1 || p.out.inner_stride != 1)) return false;
+    if (p.mode == PASS_FUSED_WAVE && (row_mode(p) || T % 4 != 0 || p.wave.ncomp != 4 || p.ncols % 4 != 0))
+      return false;
+    return true;
+  }
   if (!is_pow2(p.in.seg_len) || !is_pow2(p.out.seg_len)) return false;
   if (p.in.seg_shift < 0 || p.out.seg_shift < 0) return false;
   if (p.ncols % T != 0) return false;
@@ -142,7 +185,7 @@ bool fast_path_supported(const PassDesc& p) {
 template <int N, bool ROW, int MODE>
 static hipError_t launch_fast_t(const PassDesc& p, const cd* in, cd* out, const KArgs& a, hipStream_t s) {
   typedef Cfg<N, ROW, role_of(MODE)> C;
-  const unsigned blocks = (unsigned)(p.ncols / C::T);
+  const unsigned blocks = (unsigned)((p.ncols + C::T - 1) / C::T);
   hipLaunchKernelGGL((k_axis_fast<N, C::PTS, C::R0, ROW, C::T, MODE, C::FLAGS>), dim3(blocks), dim3(C::T * C::TPC),
                      0, s, in, out, a);
   return hipGetLastError();
@@ -226,61 +269,7 @@ __device__ __forceinline__ i64 mr_pt_off(const Side& s, int k, uint64_t segM) {
   return (i64)q * s.seg_stride + (i64)(k - (int)q * s.seg_len) * s.pt_stride;
 }
 
-// cos / sin(2 pi j / R), j = 0 .. R-1, for the odd specialised radices
-template <int R> struct OddTab;
-template <> struct OddTab<3> {
-  static constexpr double C[3] = {1.0, -0.5, -0.5};
-  static constexpr double S[3] = {0.0, 0.86602540378443864676, -0.86602540378443864676};
-};
-template <> struct OddTab<5> {
-  static constexpr double C[5] = {1.0, 0.30901699437494742410, -0.80901699437494742410, -0.80901699437494742410,
-                                  0.30901699437494742410};
-  static constexpr double S[5] = {0.0, 0.95105651629515357212, 0.58778525229247312917, -0.58778525229247312917,
-                                  -0.95105651629515357212};
-};
-template <> struct OddTab<7> {
-  static constexpr double C[7] = {1.0, 0.62348980185873353053, -0.22252093395631440429, -0.90096886790241912624,
-                                  -0.90096886790241912624, -0.22252093395631440429, 0.62348980185873353053};
-  static constexpr double S[7] = {0.0, 0.78183148246802980871, 0.97492791218182360702, 0.43388373911755812048,
-                                  -0.43388373911755812048, -0.97492791218182360702, -0.78183148246802980871};
-};
-
-// forward DFT of an odd R in registers, natural order: pairs a_t = x_t + x_{R-t},
-// b_t = x_t - x_{R-t};  y_k = x_0 + sum a_t cos(2 pi k t / R) - i sum b_t sin(2 pi k t / R),
-// y_{R-k} the same with +i.
-template <int R>
-__device__ __forceinline__ void dft_odd(cd* v) {
-  constexpr int H = (R - 1) / 2;
-  cd a[H], b[H];
-#pragma unroll
-  for (int t = 1; t <= H; ++t) {
-    a[t - 1] = cadd(v[t], v[R - t]);
-    b[t - 1] = csub(v[t], v[R - t]);
-  }
-  cd y0 = v[0];
-#pragma unroll
-  for (int t = 0; t < H; ++t) y0 = cadd(y0, a[t]);
-  cd out[R];
-  out[0] = y0;
-#pragma unroll
-  for (int k = 1; k <= H; ++k) {
-    double cr = v[0].x, ci = v[0].y, sr = 0.0, si = 0.0;
-#pragma unroll
-    for (int t = 1; t <= H; ++t) {
-      const double c = OddTab<R>::C[(k * t) % R], sn = OddTab<R>::S[(k * t) % R];
-      cr = fma(a[t - 1].x, c, cr);
-      ci = fma(a[t - 1].y, c, ci);
-      sr = fma(b[t - 1].x, sn, sr);
-      si = fma(b[t - 1].y, sn, si);
-    }
-    // -i (sr + i si) = si - i sr
-    out[k] = make_cd(cr + si, ci - sr);
-    out[R - k] = make_cd(cr - si, ci + sr);
-  }
-#pragma unroll
-  for (int k = 0; k < R; ++k) v[k] = out[k];
-}
-
+// the odd specialised radices (OddTab / dft_odd) are in cfp_fft_device.h, shared with the fast path
 template <int R>
 __device__ __forceinline__ void dft_small(cd* v) {
   if constexpr (R == 2 || R == 4 || R == 8) dft_reg<R>(v);
@@ -566,7 +555,12 @@ static hipError_t launch_generic(const PassDesc& p, const cd* in, cd* out, const
   g.ncols = p.ncols;
   int fac[CFP_MR_MAXF];
   g.nst = p.n == 1 ? 0 : factorize(p.n, fac);
-  int G = CFP_MR_POINTS / p.n;
+  static const int mr_points = [] {  // CFP_MR_POINTS_OVERRIDE: experiment knob (tools/), not a setting
+    const char* e = getenv("CFP_MR_POINTS_OVERRIDE");
+    const int v = e ? atoi(e) : 0;
+    return v >= 64 && v <= CFP_MR_MAXPTS ? v : CFP_MR_POINTS;
+  }();
+  int G = mr_points / p.n;
   if (G < 1) G = 1;
   if (G > 64) G = 64;
   if (!row) {  // power of two for the shift split
@@ -647,6 +641,7 @@ hipError_t launch_axis_pass(const PassDesc& p, const cd* in, cd* out, const cd* 
   a.in = p.in;
   a.out = p.out;
   a.inner_n = p.inner_n;
+  a.ncols = p.ncols;
   a.scale = p.scale;
   a.tw = tw;
   a.colsym = p.colsym;
@@ -664,6 +659,11 @@ hipError_t launch_axis_pass(const PassDesc& p, const cd* in, cd* out, const cd* 
       case 256: return launch_fast_n<256>(p, in, out, a, s);
       case 512: return launch_fast_n<512>(p, in, out, a, s);
       case 1024: return launch_fast_n<1024>(p, in, out, a, s);
+      case 10: return launch_fast_n<10>(p, in, out, a, s);
+      case 20: return launch_fast_n<20>(p, in, out, a, s);
+      case 50: return launch_fast_n<50>(p, in, out, a, s);
+      case 100: return launch_fast_n<100>(p, in, out, a, s);
+      case 200: return launch_fast_n<200>(p, in, out, a, s);
       default: break;
     }
   }

@@ -114,7 +114,28 @@ def test_vs_oracle(cp, oracle, n, lam):
         assert _rel(x, ref) < TOL, plan.passes()
 
 
-@pytest.mark.parametrize("n", [(32, 32, 32), (64, 32, 16), (20, 30, 40), (128, 1, 1)])
+# radix-10 register passes (n = 10, 20, 50, 100, 200: the reference's ctest sizes 10, 10^2,
+# 10^3, 100^3 and its 100^3 default mesh), including partial last tiles (ncols not a multiple
+# of the tile) and mixes with the LDS mixed-radix and power-of-two passes
+RADIX10 = [(10, 10, 10), (100, 100, 100), (20, 50, 200), (200, 20, 10), (50, 100, 20), (10, 1, 1), (20, 1, 1),
+           (1, 50, 1), (1, 1, 200), (100, 7, 3), (13, 100, 1), (100, 64, 9), (3, 5, 100)]
+
+
+@pytest.mark.parametrize("n", RADIX10, ids=lambda n: "x".join(map(str, n)))
+def test_radix10_vs_oracle(cp, oracle, n):
+    N = int(np.prod(n))
+    lam = (0.6, 0.15, 0.02)
+    b = oracle.c_fill_uniform(N, 10)
+    ref = oracle.c_solve_3d(oracle.c_build_diag_transport(n, lam), b, n)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam)
+        assert _rel(plan.apply(_dev(b)), ref) < TOL, plan.passes()
+        t = _dev(b)
+        plan.apply(t, out=t)  # in place
+        assert _rel(t, ref) < TOL
+
+
+@pytest.mark.parametrize("n", [(32, 32, 32), (64, 32, 16), (20, 30, 40), (128, 1, 1), (100, 20, 50), (10, 200, 7)])
 def test_forward_backward_vs_oracle(cp, oracle, n):
     N = int(np.prod(n))
     b = oracle.c_fill_uniform(N, 3)

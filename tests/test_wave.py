@@ -199,7 +199,7 @@ def _rand(m, seed):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dims", [(16, 16, 16), (32, 16, 8), (8, 8, 64), (64, 32, 16), (6, 5, 7), (12, 10, 3),
-                                  (16, 1, 1), (8, 4, 1), (1, 1, 1)],
+                                  (16, 1, 1), (8, 4, 1), (1, 1, 1), (20, 10, 50), (10, 10, 10), (100, 3, 1)],
                          ids=lambda d: "x".join(map(str, d)))
 def test_wave_plan_matches_oracle(dims):
     import torch

@@ -96,7 +96,7 @@ extern "C" int kexp_time(int i, const double* in, double* out, const double* tw,
   if (v.row) { s.inner_stride = 0; s.outer_stride = n; s.pt_stride = 1; a.inner_n = 1; }
   else if (axis == 2) { s.inner_stride = 1; s.outer_stride = 0; s.pt_stride = n * n; a.inner_n = n * n; }
   else { s.inner_stride = 1; s.outer_stride = n * n; s.pt_stride = n; a.inner_n = n; }  // y axis
-  a.in = s; a.out = s; a.scale = 1.0;
+  a.in = s; a.out = s; a.scale = 1.0; a.ncols = ncols;
   a.tw = (const cd*)tw; a.colsym = (const cd*)colsym; a.axsym = (const cd*)axsym; a.diag = nullptr;
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
@@ -128,6 +128,7 @@ extern "C" int kexp_chain(int ix, int iy, int iz, int iy2, int ix2, const double
   s.inner_stride = 1; s.outer_stride = n * n; s.pt_stride = n; ay.in = ay.out = s; ay.inner_n = n;
   s.inner_stride = 1; s.outer_stride = 0; s.pt_stride = n * n; az.in = az.out = s; az.inner_n = n * n;
   for (KArgs* a : {&ax, &ay, &az}) {
+    a->ncols = N / n;
     a->scale = 1.0; a->tw = (const cd*)tw; a->colsym = (const cd*)colsym; a->axsym = (const cd*)axsym; a->diag = nullptr;
   }
   const i64 nc = N / n;
@@ -167,6 +168,7 @@ extern "C" int kexp_chain_axes(int nst, const int* var, const int* axv, const do
   s.inner_stride = 1; s.outer_stride = n * n; s.pt_stride = n; a3[1].in = a3[1].out = s; a3[1].inner_n = n;
   s.inner_stride = 1; s.outer_stride = 0; s.pt_stride = n * n; a3[2].in = a3[2].out = s; a3[2].inner_n = n * n;
   for (KArgs& a : a3) {
+    a.ncols = N / n;
     a.scale = 1.0; a.tw = (const cd*)tw; a.colsym = (const cd*)colsym; a.axsym = (const cd*)axsym; a.diag = nullptr;
     a.tw4.lo = a.tw4.hi = nullptr;
   }
