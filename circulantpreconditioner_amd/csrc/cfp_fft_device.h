@@ -491,8 +491,10 @@ k_axis_fast(const cd* in, cd* out, KArgs a) {
   const unsigned blk = (FLAGS & F_REV) ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;
   // a partial last tile (non-power-of-two passes): its spare columns recompute the last column
   // and store nothing; they still take part in every barrier
+  // (power-of-two passes always hold whole tiles: the host checks ncols % T, no guard code)
+  constexpr bool GUARD = !is_pow2c(N);
   const i64 g0 = (i64)blk * T + c;
-  const bool live = g0 < a.ncols;
+  const bool live = !GUARD || g0 < a.ncols;
   const i64 g = live ? g0 : a.ncols - 1;
   // point k = tpc + m*TPC: the bits of tpc and of m*TPC are disjoint and seg_len is a power
   // of two, so pt_off(k) = pt_off(tpc) + pt_off(m*TPC).  The first part is per thread (one
@@ -574,7 +576,7 @@ k_axis_fast(const cd* in, cd* out, KArgs a) {
   }
   const bool conj_out = (MODE != PASS_FWD);
   const double sc = a.scale;
-  if (!live) return;  // after the last barrier
+  if (GUARD && !live) return;  // after the last barrier
   if (sc == 1.0) {  // uniform: no 1/N on this pass, only the conjugation of the inverse
 #pragma unroll
     for (int m = 0; m < PTS; ++m)
