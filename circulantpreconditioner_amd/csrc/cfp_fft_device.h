@@ -22,6 +22,7 @@ enum : int {
   F_NT_ST = 32,     // non-temporal global stores only
   F_LDS_SYNC = 64,  // exchange barriers wait for LDS only (global loads may stay in flight)
   F_OCC4 = 128,     // ask the compiler for 4 waves per SIMD (<= 128 VGPRs)
+  F_SYM_LDS = 256,  // fused pass: stage the per-point symbol table in LDS next to the twiddles
 };
 
 // Workgroup barrier that waits only for this wave's LDS accesses: global loads issued earlier
@@ -483,6 +484,8 @@ k_axis_fast(const cd* in, cd* out, KArgs a) {
   constexpr bool TW_LDS = NEED_LDS && !(FLAGS & F_TW_GLOBAL);
   __shared__ __attribute__((aligned(16))) double lds_raw[NEED_LDS ? ((FLAGS & F_SPLIT_LDS) ? LDS_N : 2 * LDS_N) : 2];
   __shared__ cd tws_lds[TW_LDS ? N : 1];
+  constexpr bool SYM_LDS = NEED_LDS && MODE == PASS_FUSED_SEP && (FLAGS & F_SYM_LDS);
+  __shared__ cd axs_lds[SYM_LDS ? N : 1];
 
   const int tid = threadIdx.x;
   int c, tpc;
@@ -505,15 +508,28 @@ k_axis_fast(const cd* in, cd* out, KArgs a) {
   const cd* pin = in + bin;
   cd* pout = out + bout;
 
+  // the column loads go out first; the table copies (L2 hits) queue behind them, so a wave's
+  // HBM requests never wait on a twiddle round trip
+  cd v[PTS];
+#pragma unroll
+  for (int m = 0; m < PTS; ++m) v[m] = gload<FLAGS>(pin + kpt_off<N>(a.in, m * TPC));
+
   const cd* tws = a.tw;
   if constexpr (TW_LDS) {
     for (int i = tid; i < N; i += NT) tws_lds[i] = a.tw[i];
     tws = tws_lds;
   }
-
-  cd v[PTS];
-#pragma unroll
-  for (int m = 0; m < PTS; ++m) v[m] = gload<FLAGS>(pin + kpt_off<N>(a.in, m * TPC));
+  // fused separable pass: this column's symbol sum and (F_SYM_LDS) the per-point table, loaded
+  // with the twiddles instead of after the forward transform
+  const cd* axs = a.axsym;
+  cd cs_early = make_cd(0.0, 0.0);
+  if constexpr (MODE == PASS_FUSED_SEP) {
+    cs_early = a.colsym[g];
+    if constexpr (SYM_LDS) {
+      for (int i = tid; i < N; i += NT) axs_lds[i] = a.axsym[i];
+      axs = axs_lds;
+    }
+  }
   if (MODE == PASS_INV) {
 #pragma unroll
     for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
@@ -551,14 +567,13 @@ k_axis_fast(const cd* in, cd* out, KArgs a) {
     fft_stages<N, PTS, R0, ROW, T, FLAGS>(v, lds_raw, tws, c, tpc, false);
   }
   if (MODE == PASS_FUSED_SEP || MODE == PASS_FUSED_DIAG) {
-    cd cs = make_cd(0.0, 0.0);
-    if (MODE == PASS_FUSED_SEP) cs = a.colsym[g];
+    const cd cs = cs_early;
 #pragma unroll
     for (int m = 0; m < PTS; ++m) {
       const int k = tpc + m * TPC;
       cd d;
       if (MODE == PASS_FUSED_SEP) {
-        d = cadd(cadd(cs, a.axsym[k]), make_cd(1.0, 0.0));
+        d = cadd(cadd(cs, axs[k]), make_cd(1.0, 0.0));
         v[m] = cconj(cdiv_sym(v[m], d));
       } else {
         d = a.diag[bin + kpt_off<N>(a.in, m * TPC)];

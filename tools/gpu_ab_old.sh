@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 for i in 1 2 3; do
-  (cd ab_old && timeout -k 10 120 python bench.py --no-cpu-baseline --no-real --steps 300 > ../gpurun_out/abo.$i.json 2>/dev/null) || exit $?
+  (cd ab_old && timeout -k 10 120 python bench.py --no-cpu-baseline --no-real --scaling-grid 0 --steps 300 > ../gpurun_out/abo.$i.json 2>/dev/null) || exit $?
   timeout -k 10 120 python bench.py --no-cpu-baseline --no-real --scaling-grid 0 --steps 300 > gpurun_out/abn.$i.json 2>/dev/null || exit $?
 done
 python - <<PY
