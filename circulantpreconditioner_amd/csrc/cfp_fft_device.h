@@ -42,9 +42,12 @@ __device__ __forceinline__ cd cmul(cd a, cd b) {
 }
 __device__ __forceinline__ cd cconj(cd a) { return make_cd(a.x, -a.y); }
 // a / b = (a * conj(b)) / |b|^2, the complex VecPointwiseDivide of the reference
-// (src/FftLinearSolver_3D.c:174)
+// (src/FftLinearSolver_3D.c:174).  A zero divisor gives 0, as PETSc's VecPointwiseDivide does
+// (third-party semantics, PETSc src/vec/vec/impls/seq/bvec2.c): a singular symbol's null modes
+// are dropped instead of turning the whole result into inf / NaN.
+__device__ __forceinline__ bool cnonzero(cd b) { return b.x != 0.0 || b.y != 0.0; }
 __device__ __forceinline__ cd cdiv(cd a, cd b) {
-  double den = 1.0 / fma(b.x, b.x, b.y * b.y);
+  const double den = cnonzero(b) ? 1.0 / fma(b.x, b.x, b.y * b.y) : 0.0;
   return make_cd(fma(a.x, b.x, a.y * b.y) * den, fma(a.y, b.x, -a.x * b.y) * den);
 }
 
@@ -58,7 +61,7 @@ __device__ __forceinline__ double rcp_nr(double d) {
   return fma(r, fma(-d, r, 1.0), r);
 }
 __device__ __forceinline__ cd cdiv_sym(cd a, cd b) {
-  const double den = rcp_nr(fma(b.x, b.x, b.y * b.y));
+  const double den = cnonzero(b) ? rcp_nr(fma(b.x, b.x, b.y * b.y)) : 0.0;  // zero divisor -> 0
   return make_cd(fma(a.x, b.x, a.y * b.y) * den, fma(a.y, b.x, -a.x * b.y) * den);
 }
 

@@ -452,7 +452,9 @@ extern "C" PetscErrorCode VecPointwiseDivide(Vec w, Vec x, Vec y) {
   const i64 n = w ? w->n : 0;
   return binop(w, x, y,
                [&](cd* o, const cd* xa, const cd* yb) { return cfp::launch_pointwise_divide(o, xa, yb, n, g_stream); },
-               [&](cd* o, const cd* xa, const cd* yb) { for (i64 i = 0; i < n; ++i) o[i] = D(C(xa[i]) / C(yb[i])); });
+               [&](cd* o, const cd* xa, const cd* yb) {  // PETSc: a zero divisor gives 0 (bvec2.c)
+                 for (i64 i = 0; i < n; ++i) o[i] = C(yb[i]) != 0.0 ? D(C(xa[i]) / C(yb[i])) : D(0.0);
+               });
 }
 extern "C" PetscErrorCode VecPointwiseMult(Vec w, Vec x, Vec y) {
   const i64 n = w ? w->n : 0;

@@ -220,7 +220,7 @@ void oracle_solve_3d(i64 nx, i64 ny, i64 nz, const double *diag, const double *b
     oracle_fft3d(nx, ny, nz, -1, b, (double *)bh);
     const cplx *d = (const cplx *)diag;
 #pragma omp parallel for num_threads(g_threads) schedule(static)
-    for (i64 i = 0; i < N; ++i) bh[i] = bh[i] / d[i];
+    for (i64 i = 0; i < N; ++i) bh[i] = d[i] != 0 ? bh[i] / d[i] : 0;  /* PETSc VecPointwiseDivide: y = 0 -> 0 */
     oracle_fft3d(nx, ny, nz, +1, (double *)bh, x);
     cplx *xx = (cplx *)x;
     double s = 1. / (double)N;

@@ -166,7 +166,10 @@ def np_solve_3d(diag, b, n) -> np.ndarray:
     """solve_circulant_system_3D, testFftSolver_3D.py:48-52 == solve_3D (x fastest)."""
     nx, ny, nz = n
     bh = np.fft.fftn(np.asarray(b, dtype=np.complex128).reshape(nz, ny, nx))
-    return np.fft.ifftn(bh / np.asarray(diag).reshape(nz, ny, nx)).reshape(-1)
+    d = np.asarray(diag).reshape(nz, ny, nx)
+    with np.errstate(divide="ignore", invalid="ignore"):  # PETSc VecPointwiseDivide: y = 0 -> 0
+        q = np.where(d != 0, bh / np.where(d != 0, d, 1), 0)
+    return np.fft.ifftn(q).reshape(-1)
 
 
 def np_dense_C(n, lam) -> np.ndarray:

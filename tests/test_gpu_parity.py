@@ -184,6 +184,43 @@ def test_separable_symbol_custom_columns(cp, oracle):
         assert _rel(plan.get_diag(), d) < 1e-14
 
 
+@pytest.mark.parametrize("n", [(32, 16, 8), (10, 20, 7), (256, 4, 2)], ids=lambda n: "x".join(map(str, n)))
+def test_zero_divisor_rule(cp, oracle, n):
+    """A singular symbol (PETSc's VecPointwiseDivide: a zero divisor gives 0): the explicit-Diag
+    pass, the separable pass (a symbol that vanishes at k = 0) and the standalone divide all
+    drop the null frequencies, as the oracle does."""
+    N = int(np.prod(n))
+    b = oracle.c_fill_uniform(N, 12)
+    d = oracle.c_build_diag_transport(n, (0.6, 0.15, 0.02))
+    d[[0, 3, N - 1]] = 0
+    ref = oracle.c_solve_3d(d, b, n)
+    assert np.all(np.isfinite(ref))
+    with cp.CirculantPlan(n) as plan:
+        plan.set_diag(_dev(d))
+        x = plan.apply(_dev(b))
+        assert bool(torch.isfinite(x).all()) and _rel(x, ref) < TOL
+    # separable: c_x_hat = 1 - exp(-2 pi i k / n) with lam_x = -1/(1 - e^0) ... use a column whose
+    # DFT is -1 at k = 0 so that Diag[0] = 1 + (-1) + 0 + 0 = 0 exactly
+    hats = [np.fft.fft(oracle.np_transport_col(k)) for k in n]
+    hats[0] = hats[0].copy()
+    hats[0][0] = -1.0
+    lam = (1.0, 0.5, 0.25)
+    ds = oracle.c_build_diag_3d(*hats, n, lam)
+    assert ds[0] == 0
+    ref = oracle.c_solve_3d(ds, b, n)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_separable_symbol(*hats, lam)
+        x = plan.apply(_dev(b))
+        assert bool(torch.isfinite(x).all()) and _rel(x, ref) < TOL
+    y = torch.randn(100, dtype=torch.complex128, device="cuda") + 2
+    y[[4, 50]] = 0
+    xx = torch.randn(100, dtype=torch.complex128, device="cuda")
+    w = torch.empty_like(xx)
+    cp.pointwise_divide(w, xx, y)
+    expect = torch.where(y != 0, xx / torch.where(y != 0, y, torch.ones_like(y)), torch.zeros_like(xx))
+    assert _rel(w, expect) < 1e-15
+
+
 def test_build_diag_kernel(cp, oracle):
     n = (12, 10, 6)
     lam = (0.6, 0.15 + 0.1j, 0.02)

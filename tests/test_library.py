@@ -86,6 +86,14 @@ def test_host_vec_ops():
     w = P.Vec.seq(50)
     P.PetscCall(P.lib().VecPointwiseDivide(w.h, x.h, y.h))
     np.testing.assert_allclose(w.array(), (a + (2 - 1j) * b) / b, rtol=1e-14)
+    # PETSc's VecPointwiseDivide: a zero divisor gives 0 (bvec2.c), not inf / NaN
+    bz = b.copy()
+    bz[[3, 17]] = 0
+    y.set_array(bz)
+    P.PetscCall(P.lib().VecPointwiseDivide(w.h, x.h, y.h))
+    ref = (a + (2 - 1j) * b) / np.where(bz != 0, bz, 1)
+    ref[[3, 17]] = 0
+    np.testing.assert_allclose(w.array(), ref, rtol=1e-14)
 
 
 def test_pc_none_and_identical_vectors():

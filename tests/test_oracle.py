@@ -117,3 +117,23 @@ def test_solve_residual_large(oracle):
     d = oracle.c_build_diag_transport(n, lam)
     x = oracle.c_solve_3d(d, b, n)
     assert oracle.rel_l2(oracle.c_apply_circulant(x, n, lam), b) < 1e-12
+
+
+def test_zero_divisor_rule(oracle):
+    """solve_3D's VecPointwiseDivide with a singular Diag (PETSc: a zero divisor gives 0): the
+    C restatement and the numpy restatement agree, and the result is the pseudo-inverse solve
+    (the null frequencies dropped), finite everywhere."""
+    n = (8, 6, 4)
+    N = int(np.prod(n))
+    d = oracle.c_build_diag_transport(n, (0.6, 0.15, 0.02))
+    d[[0, 5, 77]] = 0
+    b = oracle.c_fill_uniform(N, 9)
+    x = oracle.c_solve_3d(d, b, n)
+    assert np.all(np.isfinite(x))
+    np.testing.assert_allclose(x, oracle.np_solve_3d(d, b, n), rtol=0, atol=1e-14 * np.abs(x).max())
+    bh = np.fft.fftn(b.reshape(n[2], n[1], n[0])).reshape(-1)
+    q = np.zeros_like(bh)
+    nz = d != 0
+    q[nz] = bh[nz] / d[nz]
+    ref = np.fft.ifftn(q.reshape(n[2], n[1], n[0])).reshape(-1)
+    np.testing.assert_allclose(x, ref, rtol=0, atol=1e-13 * np.abs(ref).max())
