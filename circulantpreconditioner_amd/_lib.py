@@ -56,6 +56,8 @@ def _declare(L) -> None:
         "cfp_plan_num_passes": ([vp, P(c_int)], c_int),
         "cfp_plan_pass_info": ([vp, c_int, P(c_int), P(c_int), P(i64), P(c_int), P(c_int)], c_int),
         "cfp_plan_time_passes": ([vp, dp, dp, c_int, dp, vp], c_int),
+        "cfp_plan_profile_begin": ([vp, c_int, c_int], c_int),
+        "cfp_plan_profile_end": ([vp, dp, ctypes.POINTER(c_int)], c_int),
         "cfp_pointwise_divide": ([dp, dp, dp, i64, vp], c_int),
         "cfp_scale": ([dp, ctypes.c_double, ctypes.c_double, i64, vp], c_int),
         "cfp_fill_uniform": ([dp, i64, u64, i64, vp], c_int),

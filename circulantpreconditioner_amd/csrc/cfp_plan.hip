@@ -140,6 +140,11 @@ struct cfp_plan_s {
   cd* tw4hi[3] = {nullptr, nullptr, nullptr};
   cd* possym[3] = {nullptr, nullptr, nullptr};  // position-indexed symbols (the standalone divide)
   bool long_axes() const { return split[0][0] || split[1][0] || split[2][0]; }
+  // profiling mode (cfp_plan_profile_begin/_end): every cfp_plan_apply records one event per
+  // launch into its own slot, so per-launch times come from the caller's own timed applies
+  std::vector<hipEvent_t> prof_ev;
+  size_t prof_stride = 0, prof_cap = 0, prof_used = 0;
+  size_t prof_every = 1, prof_calls = 0;  // record every prof_every-th apply (sampling)
 };
 
 namespace {
@@ -555,6 +560,7 @@ extern "C" int cfp_plan_destroy(cfp_plan_t p) {
     if (p->tw4hi[a]) hipFree(p->tw4hi[a]);
   }
   if (p->host_stage) hipFree(p->host_stage);
+  for (auto& e : p->prof_ev) hipEventDestroy(e);
   delete p;
   return CFP_SUCCESS;
 }
@@ -617,7 +623,71 @@ extern "C" int cfp_plan_get_diag(cfp_plan_t p, double* diag_dev, void* stream) {
 extern "C" int cfp_plan_apply(cfp_plan_t p, const double* b, double* x, void* stream) {
   if (!p || !b || !x) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
   DeviceGuard dg(p->device);
+  // profiling: this apply's own event slot (skipped if the schedule changed since begin)
+  const bool sample = p->prof_cap && (p->prof_calls++ % p->prof_every) == 0;
+  if (sample && p->prof_used < p->prof_cap && apply_steps(p).size() + 1 == p->prof_stride) {
+    std::vector<hipEvent_t> ev(p->prof_ev.begin() + (long)(p->prof_used * p->prof_stride),
+                               p->prof_ev.begin() + (long)((p->prof_used + 1) * p->prof_stride));
+    ++p->prof_used;
+    return run_apply(p, nullptr, (const cd*)b, (cd*)x, (hipStream_t)stream, &ev);
+  }
   return run_apply(p, nullptr, (const cd*)b, (cd*)x, (hipStream_t)stream, nullptr);
+}
+
+static void profile_free(cfp_plan_s* p) {
+  for (auto& e : p->prof_ev) hipEventDestroy(e);
+  p->prof_ev.clear();
+  p->prof_stride = p->prof_cap = p->prof_used = p->prof_calls = 0;
+  p->prof_every = 1;
+}
+
+// Start recording per-launch events in every `every`-th call of cfp_plan_apply (the first,
+// then every-th after it), at most `max_applies` of them.
+extern "C" int cfp_plan_profile_begin(cfp_plan_t p, int max_applies, int every) {
+  if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
+  if (max_applies < 1 || max_applies > 100000) return set_error(CFP_ERR_ARG_OUTOFRANGE, "max_applies out of range");
+  if (every < 1) return set_error(CFP_ERR_ARG_OUTOFRANGE, "every must be >= 1");
+  DeviceGuard dg(p->device);
+  profile_free(p);
+  p->prof_stride = apply_steps(p).size() + 1;
+  p->prof_ev.resize(p->prof_stride * (size_t)max_applies, nullptr);
+  for (auto& e : p->prof_ev) {
+    hipError_t r = hipEventCreate(&e);
+    if (r != hipSuccess) {
+      profile_free(p);
+      return hip_error(r, "hipEventCreate");
+    }
+  }
+  p->prof_cap = (size_t)max_applies;
+  p->prof_used = 0;
+  p->prof_every = (size_t)every;
+  p->prof_calls = 0;
+  return CFP_SUCCESS;
+}
+
+// Stop recording; ms_out[i] = mean duration of launch i over the recorded applies (ms_out holds
+// cfp_plan_num_passes entries), *applies = how many applies were recorded.
+extern "C" int cfp_plan_profile_end(cfp_plan_t p, double* ms_out, int* applies) {
+  if (!p || !ms_out || !applies) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  if (!p->prof_cap) return set_error(CFP_ERR_ARG_WRONGSTATE, "profiling was not started");
+  DeviceGuard dg(p->device);
+  const size_t np = p->prof_stride - 1, used = p->prof_used;
+  std::vector<double> acc(np, 0.0);
+  int rc = CFP_SUCCESS;
+  if (used > 0) {
+    hipError_t e = hipEventSynchronize(p->prof_ev[used * p->prof_stride - 1]);
+    if (e != hipSuccess) rc = hip_error(e, "event sync");
+  }
+  for (size_t a = 0; a < used && !rc; ++a)
+    for (size_t i = 0; i < np; ++i) {
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, p->prof_ev[a * p->prof_stride + i], p->prof_ev[a * p->prof_stride + i + 1]);
+      acc[i] += ms;
+    }
+  for (size_t i = 0; i < np; ++i) ms_out[i] = used ? acc[i] / (double)used : 0.0;
+  *applies = (int)used;
+  profile_free(p);
+  return rc;
 }
 
 extern "C" int cfp_plan_apply_with_diag(cfp_plan_t p, const double* diag, const double* b, double* x, void* stream) {

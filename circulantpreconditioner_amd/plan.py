@@ -181,6 +181,20 @@ class CirculantPlan:
                                          ms, _stream_handle(stream)))
         return list(ms)
 
+    def profile_begin(self, max_applies: int, every: int = 1) -> "CirculantPlan":
+        """Record one HIP event per launch in every `every`-th following apply (at most
+        `max_applies` of them)."""
+        check(lib().cfp_plan_profile_begin(self._h, int(max_applies), int(every)))
+        return self
+
+    def profile_end(self) -> tuple:
+        """(mean ms of each launch over the recorded applies, number of applies recorded)."""
+        npass = len(self.passes())
+        ms = (ctypes.c_double * npass)()
+        n = ctypes.c_int()
+        check(lib().cfp_plan_profile_end(self._h, ms, ctypes.byref(n)))
+        return list(ms), n.value
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             lib().cfp_plan_destroy(self._h)

@@ -112,6 +112,14 @@ int cfp_plan_num_passes(cfp_plan_t plan, int *passes);
 int cfp_plan_pass_info(cfp_plan_t plan, int pass, int *axis, int *n, int64_t *ncols, int *mode, int *fast);
 int cfp_plan_time_passes(cfp_plan_t plan, const double *b_dev, double *x_dev, int iters, double *ms_out,
                          void *stream);
+/* Profiling mode: every `every`-th following call of cfp_plan_apply (the first, then every-th
+ * after it; at most max_applies of them) records one HIP event per launch on its stream -- the
+ * caller's own timed applies, no extra launches.  Sampling keeps the events' cost (a few us
+ * per apply) out of the caller's throughput.  _profile_end synchronises on the last event and
+ * writes the mean duration (ms) of each launch (cfp_plan_num_passes entries) and the number
+ * of applies recorded. */
+int cfp_plan_profile_begin(cfp_plan_t plan, int max_applies, int every);
+int cfp_plan_profile_end(cfp_plan_t plan, double *ms_out, int *applies);
 
 /* ---- vector kernels (device arrays of n complex values) */
 int cfp_pointwise_divide(double *w_dev, const double *x_dev, const double *y_dev, int64_t n, void *stream);

@@ -435,3 +435,30 @@ def test_y_fused_schedule_vs_oracle(cp, oracle, n):
     with cp.CirculantPlan(n) as plan:
         plan.set_schedule("five_y").set_transport_symbol(lam)  # before the symbol
         assert _rel(plan.apply(_dev(b)), ref) < TOL
+
+
+def test_profile_mode_records_the_callers_applies(cp, oracle):
+    """cfp_plan_profile_begin/_end: one event per launch inside ordinary applies (bench.py's
+    timed-region kernel times); results unchanged, counts and times sane, capacity respected."""
+    n = (64, 32, 16)
+    N = int(np.prod(n))
+    lam = (0.6, 0.15, 0.02)
+    b = oracle.c_fill_uniform(N, 3)
+    ref = oracle.c_solve_3d(oracle.c_build_diag_transport(n, lam), b, n)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam)
+        tb, x = _dev(b), torch.empty(N, dtype=torch.complex128, device="cuda")
+        plan.profile_begin(3)
+        for _ in range(5):  # two more than the capacity: they run unrecorded
+            plan.apply(tb, out=x)
+        ms, napp = plan.profile_end()
+        assert napp == 3 and len(ms) == len(plan.passes())
+        plan.profile_begin(100, every=4)  # sampling: applies 0, 4, 8 of 10
+        for _ in range(10):
+            plan.apply(tb, out=x)
+        ms4, napp4 = plan.profile_end()
+        assert napp4 == 3 and all(m > 0 for m in ms4)
+        assert all(0.0 < m < 100.0 for m in ms)
+        assert _rel(x, ref) < TOL
+        with pytest.raises(Exception):
+            plan.profile_end()  # not started
