@@ -211,13 +211,21 @@ def main() -> int:
 
     plan, b, x, run, parallelism = make(grid)
     timed_region_ms = None
-    if world == 1 and not args.no_live_events:
+    live_applies = 0
+    every = max(1, args.event_every)
+    if world > 1 and not args.no_live_events and plan.exchange == "rccl":
+        # the slab plan's phases (passes and RCCL exchanges) timed inside the timed applies
+        for _ in range(args.warmup):
+            run()
+        plan.profile_begin((args.steps + every - 1) // every, every)
+        elapsed = timed(run, args.steps, 0)
+        timed_region_ms, live_applies = plan.profile_end()
+    elif world == 1 and not args.no_live_events:
         # per-launch HIP events recorded by the plan inside the timed applies themselves (on
         # the launch stream), in every EVERY-th apply: the roofline's kernel time comes from
         # the timed region, and the events' own cost (~3 us each) stays out of `value`
         for _ in range(args.warmup):
             run()
-        every = max(1, args.event_every)
         plan.profile_begin((args.steps + every - 1) // every, every)
         elapsed = timed(run, args.steps, 0)
         timed_region_ms, n_rec = plan.profile_end()
@@ -259,7 +267,13 @@ def main() -> int:
     else:
         # every rank takes part (the exchanges are collectives); rank 0 reports its own phases
         passes_info = plan.phases()
-        ms = plan.time_phases(b, x, iters=max(5, min(20, args.steps)))
+        if timed_region_ms is not None:
+            ms = timed_region_ms
+            timing_src = (f"HIP events around every phase of {live_applies} of the {args.steps} timed applies "
+                          f"(every {every}th, launch stream)")
+        else:
+            ms = plan.time_phases(b, x, iters=max(5, min(20, args.steps)))
+            timing_src = "HIP events, separate applies after the timed region (launch stream)"
         for p, m in zip(passes_info, ms):
             p["ms"] = round(m, 5)
         nloc = plan.local_size
@@ -271,7 +285,7 @@ def main() -> int:
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                 "kernel": f"phase{k}_{dom['axis']}_{dom['mode']} (rank 0 slab)", "alg_bytes_per_launch": alg,
-                "mean_ms": round(ms[k], 5)}
+                "mean_ms": round(ms[k], 5), "timing": timing_src}
         ex = [ms[i] for i, p in enumerate(passes_info) if p["kind"] == "all-to-all"]
         sent = 16 * nloc * (world - 1) / world  # bytes leaving this GPU per all-to-all
         roof_apply = {"B_alg_bytes_per_gpu": 208 * nloc,

@@ -101,6 +101,8 @@ def declare(L) -> None:
         "cfp_dist_plan_set_work_buffer": ([vp, dp], c_int),
         "cfp_dist_plan_set_symbol_transport": ([vp, dp], c_int),
         "cfp_dist_plan_apply": ([vp, dp, dp, vp], c_int),
+        "cfp_dist_plan_profile_begin": ([vp, c_int, c_int], c_int),
+        "cfp_dist_plan_profile_end": ([vp, dp, P(c_int)], c_int),
         "cfp_dist_plan_local_size": ([vp, P(i64)], c_int),
         "cfp_dist_plan_time_phases": ([vp, dp, dp, c_int, dp, vp], c_int),
         "cfp_dist_plan_num_phases": ([vp, P(c_int)], c_int),

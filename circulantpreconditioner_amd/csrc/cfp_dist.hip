@@ -189,7 +189,17 @@ struct SlabRank {
 struct cfp_dist_plan_s {
   SlabRank R;
   ncclComm_t comm = nullptr;
+  // sampled per-phase events inside the caller's applies (as cfp_plan_profile_begin)
+  std::vector<hipEvent_t> prof_ev;
+  size_t prof_stride = 0, prof_cap = 0, prof_used = 0, prof_every = 1, prof_calls = 0;
 };
+
+static void dist_profile_free(cfp_dist_plan_s* p) {
+  for (auto& e : p->prof_ev) hipEventDestroy(e);
+  p->prof_ev.clear();
+  p->prof_stride = p->prof_cap = p->prof_used = p->prof_calls = 0;
+  p->prof_every = 1;
+}
 
 struct cfp_group_s {
   std::vector<SlabRank> R;
@@ -292,6 +302,7 @@ extern "C" int cfp_dist_plan_run_segment(cfp_dist_plan_t p, int seg, const doubl
 extern "C" int cfp_dist_plan_destroy(cfp_dist_plan_t p) {
   if (!p) return CFP_SUCCESS;
   hipSetDevice(p->R.device);
+  dist_profile_free(p);
   if (p->comm) ncclCommDestroy(p->comm);
   p->R.release();
   delete p;
@@ -362,7 +373,57 @@ static int dist_apply(cfp_dist_plan_s* p, const cd* b, cd* x, hipStream_t s, std
 extern "C" int cfp_dist_plan_apply(cfp_dist_plan_t p, const double* b, double* x, void* stream) {
   if (!p || !b || !x) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
   HIPCHK(hipSetDevice(p->R.device));
+  const bool sample = p->prof_cap && (p->prof_calls++ % p->prof_every) == 0;
+  if (sample && p->prof_used < p->prof_cap) {
+    std::vector<hipEvent_t> ev(p->prof_ev.begin() + (long)(p->prof_used * p->prof_stride),
+                               p->prof_ev.begin() + (long)((p->prof_used + 1) * p->prof_stride));
+    ++p->prof_used;
+    return dist_apply(p, (const cd*)b, (cd*)x, (hipStream_t)stream, &ev);
+  }
   return dist_apply(p, (const cd*)b, (cd*)x, (hipStream_t)stream, nullptr);
+}
+
+// sampled phase events inside the caller's own applies (cfp_plan_profile_begin's contract)
+extern "C" int cfp_dist_plan_profile_begin(cfp_dist_plan_t p, int max_applies, int every) {
+  if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
+  if (max_applies < 1 || max_applies > 100000 || every < 1) return set_error(CFP_ERR_ARG_OUTOFRANGE, "bad profile range");
+  HIPCHK(hipSetDevice(p->R.device));
+  dist_profile_free(p);
+  p->prof_stride = p->R.steps.size() + 1;
+  p->prof_ev.resize(p->prof_stride * (size_t)max_applies, nullptr);
+  for (auto& e : p->prof_ev) {
+    hipError_t r = hipEventCreate(&e);
+    if (r != hipSuccess) {
+      dist_profile_free(p);
+      return hip_error(r, "hipEventCreate");
+    }
+  }
+  p->prof_cap = (size_t)max_applies;
+  p->prof_every = (size_t)every;
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_dist_plan_profile_end(cfp_dist_plan_t p, double* ms_out, int* applies) {
+  if (!p || !ms_out || !applies) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  if (!p->prof_cap) return set_error(CFP_ERR_ARG_WRONGSTATE, "profiling was not started");
+  HIPCHK(hipSetDevice(p->R.device));
+  const size_t np = p->prof_stride - 1, used = p->prof_used;
+  std::vector<double> acc(np, 0.0);
+  int rc = CFP_SUCCESS;
+  if (used > 0) {
+    hipError_t e = hipEventSynchronize(p->prof_ev[used * p->prof_stride - 1]);
+    if (e != hipSuccess) rc = hip_error(e, "event sync");
+  }
+  for (size_t a = 0; a < used && !rc; ++a)
+    for (size_t i = 0; i < np; ++i) {
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, p->prof_ev[a * p->prof_stride + i], p->prof_ev[a * p->prof_stride + i + 1]);
+      acc[i] += ms;
+    }
+  for (size_t i = 0; i < np; ++i) ms_out[i] = used ? acc[i] / (double)used : 0.0;
+  *applies = (int)used;
+  dist_profile_free(p);
+  return rc;
 }
 
 extern "C" int cfp_dist_plan_time_phases(cfp_dist_plan_t p, const double* b, double* x, int iters, double* ms_out,

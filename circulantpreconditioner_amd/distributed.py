@@ -114,6 +114,22 @@ class SlabPlan:
                             "mode": {0: "fwd", 1: "inv", 2: "fused_sep", 3: "fused_diag"}[mode.value]})
         return out
 
+    def profile_begin(self, max_applies: int, every: int = 1) -> bool:
+        """Sampled per-phase events inside the following applies (RCCL exchange only; returns
+        False for the torch-exchange path, whose exchanges are outside the library)."""
+        if self.exchange != "rccl":
+            return False
+        check(lib().cfp_dist_plan_profile_begin(self._h, int(max_applies), int(every)))
+        return True
+
+    def profile_end(self) -> tuple:
+        nph = ctypes.c_int()
+        check(lib().cfp_dist_plan_num_phases(self._h, ctypes.byref(nph)))
+        ms = (ctypes.c_double * nph.value)()
+        n = ctypes.c_int()
+        check(lib().cfp_dist_plan_profile_end(self._h, ms, ctypes.byref(n)))
+        return list(ms), n.value
+
     def time_phases(self, b: torch.Tensor, x: torch.Tensor, iters: int = 10, stream=None) -> list:
         """Mean ms of each phase (passes and exchanges, in order) over `iters` applies."""
         if self.exchange == "torch":

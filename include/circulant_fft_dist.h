@@ -61,6 +61,10 @@ int cfp_dist_plan_phase_info(cfp_dist_plan_t plan, int phase, int *is_exchange, 
 /* mean ms of each phase (kernels and exchanges, in order) over `iters` applies */
 int cfp_dist_plan_time_phases(cfp_dist_plan_t plan, const double *b_dev, double *x_dev, int iters, double *ms_out,
                               void *stream);
+/* sampled per-phase HIP events inside the caller's own applies (cfp_plan_profile_begin's
+ * contract: every `every`-th apply, at most max_applies; _end writes the mean ms per phase) */
+int cfp_dist_plan_profile_begin(cfp_dist_plan_t plan, int max_applies, int every);
+int cfp_dist_plan_profile_end(cfp_dist_plan_t plan, double *ms_out, int *applies);
 
 /* single-process group of P slabs; devices[r] = HIP device of slab r (may repeat) */
 int cfp_group_create(cfp_group_t *group, int64_t nx, int64_t ny, int64_t nz, int nranks, const int *devices);

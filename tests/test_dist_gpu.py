@@ -59,6 +59,14 @@ def test_rccl_single_rank(oracle):
         plan.set_transport_symbol(lam)
         x = plan.apply(torch.from_numpy(b).cuda())
         assert oracle.rel_l2(x.cpu().numpy(), ref) < TOL
+        # sampled phase events inside ordinary applies (bench.py's N > 1 kernel times)
+        assert plan.profile_begin(10, every=2)
+        tb = torch.from_numpy(b).cuda()
+        for _ in range(5):
+            plan.apply(tb, out=x)
+        ms, napp = plan.profile_end()
+        assert napp == 3 and len(ms) == len(plan.phases()) and all(m >= 0.0 for m in ms)
+        assert oracle.rel_l2(x.cpu().numpy(), ref) < TOL
         plan.close()
     finally:
         if created:
