@@ -23,7 +23,11 @@ enum : int {
   F_LDS_SYNC = 64,  // exchange barriers wait for LDS only (global loads may stay in flight)
   F_OCC4 = 128,     // ask the compiler for 4 waves per SIMD (<= 128 VGPRs)
   F_SYM_LDS = 256,  // fused pass: stage the per-point symbol table in LDS next to the twiddles
+  F_OCC8 = 512,     // ask the compiler for 8 waves per SIMD (<= 64 VGPRs)
 };
+__host__ __device__ constexpr int waves_req(int flags, int mode) {
+  return mode == PASS_FUSED_WAVE ? 1 : ((flags & F_OCC8) ? 8 : ((flags & F_OCC4) ? 4 : 1));
+}
 
 // Workgroup barrier that waits only for this wave's LDS accesses: global loads issued earlier
 // (a prefetch of the next work unit) stay in flight across it.
@@ -477,7 +481,7 @@ __device__ __forceinline__ void fft_stages(cd* v, void* lds, const cd* tws, int 
 }
 
 template <int N, int PTS, int R0, bool ROW, int T, int MODE, int FLAGS>
-__global__ void __launch_bounds__(T*(N / PTS)) __attribute__((amdgpu_waves_per_eu(((FLAGS & F_OCC4) && MODE != PASS_FUSED_WAVE) ? 4 : 1)))
+__global__ void __launch_bounds__(T*(N / PTS)) __attribute__((amdgpu_waves_per_eu(waves_req(FLAGS, MODE))))
 k_axis_fast(const cd* in, cd* out, KArgs a) {
   typedef Shape<N, PTS, R0> SH;
   constexpr int TPC = SH::TPC;

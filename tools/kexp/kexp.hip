@@ -71,6 +71,10 @@ static const Var kVars[] = {
     V(512, 16, 2, false, 16, 0, 33) V(512, 8, 8, false, 16, 0, 33) V(512, 16, 2, false, 16, 0, 145)
     // rows (81, 82): product fwd (nt-ld), inv (nt-st)
     V(512, 16, 2, true, 8, 0, 16) V(512, 16, 2, true, 8, 0, 32)
+    // fused 256 at higher occupancy (83..): 8-wave request (F_OCC8 = 512) with PTS 8 T 16 / T 8 split,
+    // PTS 4 T 16 split, PTS 8 T 16 split + global twiddles; PTS 8 T 32 split 4-wave
+    V(256, 8, 4, false, 16, 2, 529) V(256, 8, 4, false, 8, 2, 529) V(256, 4, 4, false, 16, 2, 529)
+    V(256, 8, 4, false, 16, 2, 531) V(256, 8, 4, false, 32, 2, 145)
 };
 
 extern "C" int kexp_count() { return (int)(sizeof(kVars) / sizeof(kVars[0])); }
