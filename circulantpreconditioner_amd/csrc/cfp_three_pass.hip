@@ -1,22 +1,31 @@
 // cfp_three_pass.hip -- the 3-sweep apply for 256^3 grids (PCApply in 96 N bytes instead of
 // the 5-pass schedule's 160 N).
 //
-// The y transform is split four-step (Cooley-Tukey, ny = N1 * N2 = 64 * 4): with
+// The y transform is split four-step (Cooley-Tukey, ny = N1 * N2, N1 = 64 or 32): with
 // y = y2 + N2 y1 and k = k1 + N1 k2,
-//   X[k1 + N1 k2] = sum_{y2} W_4^{y2 k2} W_256^{y2 k1} sum_{y1} W_64^{y1 k1} x[y2 + N2 y1].
-// The inner 64-point DFT rides with the x transform, the outer 4-point DFT with the z
+//   X[k1 + N1 k2] = sum_{y2} W_N2^{y2 k2} W_256^{y2 k1} sum_{y1} W_N1^{y1 k1} x[y2 + N2 y1].
+// The inner N1-point DFT rides with the x transform, the outer N2-point DFT with the z
 // transform, and every intermediate stays in the slot it was read from (y1 <-> k1, y2 <-> k2):
 //
-//   P1  k_tp_rows<fwd>: one z-plane, rows y2 + 4 y1 (64 rows, 256 KB): 64-point DFT down the
-//       rows (column mode, lanes = x), LDS transpose, 256-point DFT along each row
-//   P2  k_tp_mid: 16 x-columns x 4 rows y2 + 4 k1 x 256 z (256 KB): twiddle W_256^{y2 k1},
-//       4-point DFT across the lanes of a quad (DPP), 256-point z DFT, divide by the separable
-//       symbol at (kx, k1 + 64 k2, kz), then the same transforms on the conjugate (inverse)
+//   P1  k_tp_rows<fwd>: one z-plane, rows y2 + N2 y1 (N1 rows, N1 x 4 KB): N1-point DFT down
+//       the rows (column mode, lanes = x), LDS transpose, 256-point DFT along each row
+//   P2  k_tp_mid: T/N2 x-columns x N2 rows y2 + N2 k1 x 256 z: twiddle W_256^{y2 k1}, N2-point
+//       DFT across N2 neighbouring lanes (radix-2 butterflies over DPP lane permutations,
+//       frequencies left bit-reversed), 256-point z DFT, divide by the separable symbol at
+//       (kx, k1 + N1 k2, kz), then the same transforms on the conjugate (inverse)
 //   P3  k_tp_rows<inv>: P1 on the conjugate, x 1/N
 //
-// Every global access is a contiguous run of >= 256 bytes (P1 and P3 read/write whole rows,
-// P2 reads 4 rows x 16 x per wave instruction).  Workgroups are 1024 threads x 16 points
-// (256 KB in VGPRs) with a split-LDS exchange buffer of 128-136 KB, so one per CU.
+// P1/P3 workgroups are N1 x 16 threads x 16 points with a split-LDS exchange buffer of
+// N1 x 2.1 KB: one per CU at N1 = 64, two at N1 = 32.  P2 holds T columns (T = 64: one
+// 1024-thread workgroup per CU; T = 32: two of 512); its global runs are T/N2 x 16 bytes.
+//
+// Phase desynchronisation ("stagger"): a kernel whose workgroups all start together and do
+// identical work keeps every CU in the same phase -- all load, then all compute (HBM idle),
+// then all store.  With one or two workgroups per CU nothing else hides that.  Every other
+// persistent workgroup can therefore start `stagger` ticks of the 100 MHz real-time counter
+// late, so half the CUs compute while the other half stream.
+#include <cstdlib>
+
 #include "cfp_fft_device.h"
 #include "cfp_three_pass.h"
 
@@ -24,54 +33,116 @@ namespace cfp {
 
 namespace {
 constexpr int TN = 256;  // nx = ny = nz
-constexpr int TN1 = 64, TN2 = 4;
 constexpr int RS = TN + TN / 16;  // padded row stride of the row-mode LDS layout
 
-// 4-point DFT across the lanes of an aligned quad: this lane's output index is k = lane & 3
-__device__ __forceinline__ cd dft4_quad(cd v, int k) {
-  const cd r0 = make_cd(quad_bcast<0>(v.x), quad_bcast<0>(v.y));
-  const cd r1 = make_cd(quad_bcast<1>(v.x), quad_bcast<1>(v.y));
-  const cd r2 = make_cd(quad_bcast<2>(v.x), quad_bcast<2>(v.y));
-  const cd r3 = make_cd(quad_bcast<3>(v.x), quad_bcast<3>(v.y));
-  const bool odd = k & 1;
-  const cd s = odd ? csub(r0, r2) : cadd(r0, r2);
-  const cd d13 = csub(r1, r3), s13 = cadd(r1, r3);
-  const cd t = odd ? make_cd(d13.y, -d13.x) : s13;  // -i (r1 - r3) for odd k
-  return k < 2 ? cadd(s, t) : csub(s, t);
+// DPP controls: quad_perm lane ^ 1, ^ 2, ^ 3; row_half_mirror (lane ^ 7 within 8 lanes)
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_XOR3 = 0x1B, DPP_HALF_MIRROR = 0x141;
+
+template <int M>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffll), M, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), M, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int M>
+__device__ __forceinline__ cd dpp_c(cd v) { return make_cd(dpp_d<M>(v.x), dpp_d<M>(v.y)); }
+// lane ^ 4: mirror within 8 lanes (7 - j), then reverse within the quad (^ 3)
+__device__ __forceinline__ cd lane_xor4(cd v) { return dpp_c<DPP_XOR3>(dpp_c<DPP_HALF_MIRROR>(v)); }
+__device__ __forceinline__ cd mul_mi(cd v) { return make_cd(v.y, -v.x); }  // x W_4 = x (-i)
+
+// Radix-2 butterflies across lanes.  The DIF forms take points in natural lane order and
+// leave the frequencies bit-reversed; the DIT forms are the forward transform from that order
+// back to natural order (used inside the conjugate trick for the inverse).
+// 4 points over an aligned quad: lane q holds point q -> frequency brev2(q)
+__device__ __forceinline__ cd dft4_dif(cd v, int q) {
+  const cd p = dpp_c<DPP_XOR2>(v);
+  cd t = (q & 2) ? csub(p, v) : cadd(v, p);
+  if (q == 3) t = mul_mi(t);
+  const cd r = dpp_c<DPP_XOR1>(t);
+  return (q & 1) ? csub(r, t) : cadd(t, r);
+}
+// lane q holds frequency brev2(q) -> point q
+__device__ __forceinline__ cd dft4_dit(cd v, int q) {
+  const cd r = dpp_c<DPP_XOR1>(v);
+  cd u = (q & 1) ? csub(r, v) : cadd(v, r);
+  if (q == 3) u = mul_mi(u);
+  const cd p = dpp_c<DPP_XOR2>(u);
+  return (q & 2) ? csub(p, u) : cadd(u, p);
+}
+// 8 points over 8 aligned lanes: lane j holds point j -> frequency brev3(j); w8 = W_8^(j & 3)
+__device__ __forceinline__ cd dft8_dif(cd v, int j, cd w8) {
+  const cd p = lane_xor4(v);
+  const cd t = (j & 4) ? cmul(csub(p, v), w8) : cadd(v, p);
+  return dft4_dif(t, j & 3);
+}
+__device__ __forceinline__ cd dft8_dit(cd v, int j, cd w8) {
+  cd u = dft4_dit(v, j & 3);
+  if (j & 4) u = cmul(u, w8);
+  const cd p = lane_xor4(u);
+  return (j & 4) ? csub(p, u) : cadd(u, p);
+}
+template <int N2>
+__device__ __forceinline__ cd lanes_dif(cd v, int j, cd w8) {
+  if constexpr (N2 == 4) return dft4_dif(v, j);
+  else return dft8_dif(v, j, w8);
+}
+template <int N2>
+__device__ __forceinline__ cd lanes_dit(cd v, int j, cd w8) {
+  if constexpr (N2 == 4) return dft4_dit(v, j);
+  else return dft8_dit(v, j, w8);
+}
+template <int N2>
+__device__ __forceinline__ int brev(int j) {
+  return N2 == 4 ? ((j & 1) << 1) | (j >> 1) : ((j & 1) << 2) | (j & 2) | (j >> 2);
+}
+
+// every other workgroup waits `ticks` of the 100 MHz counter (bounded: the counter only grows)
+__device__ __forceinline__ void stagger_start(int ticks) {
+  if (ticks <= 0 || !(blockIdx.x & 1)) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)ticks) __builtin_amdgcn_s_sleep(4);
 }
 }  // namespace
 
-// Persistent: a workgroup walks units blockIdx.x, + gridDim.x, ... (one per CU).  Prefetching
-// the next unit into VGPRs across LDS-only barriers was tried and lost: at 1024 threads the
-// extra registers spill (profiles/r01_schedule_sweep.txt).
-template <bool INV, int FLAGS>
-__global__ void __launch_bounds__(1024) k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
+// Persistent: a workgroup walks units blockIdx.x, + gridDim.x, ...  Prefetching the next unit
+// into VGPRs across LDS-only barriers was tried and lost: at 1024 threads the extra registers
+// spill (profiles/r01_schedule_sweep.txt).
+template <bool INV, int FLAGS, int N1>
+__global__ void __launch_bounds__(N1 * 16) __attribute__((amdgpu_waves_per_eu(4)))
+k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits, int stagger) {
+  constexpr int N2 = TN / N1, NT = N1 * 16, TY = N1 / 16;
   constexpr int F = FLAGS | F_SPLIT_LDS | F_LDS_SYNC;
-  __shared__ __attribute__((aligned(16))) double lds[TN1 * RS];  // 136 KB: both layouts fit
-  __shared__ cd tw_l[TN + TN1];                                  // W_256, then W_64
+  __shared__ __attribute__((aligned(16))) double lds[N1 * RS];  // both layouts fit
+  __shared__ cd tw_l[TN + N1];                                  // W_256, then W_N1
   const int tid = threadIdx.x;
-  for (int i = tid; i < TN; i += 1024) tw_l[i] = a.tw256[i];
-  for (int i = tid; i < TN1; i += 1024) tw_l[TN + i] = a.tw256[4 * i];
-  const int x = tid & (TN - 1), ty = tid >> 8;  // phase A: column x, thread ty of 4
-  const int r = tid >> 4, tx = tid & 15;        // phase C: row r, thread tx of 16
+  for (int i = tid; i < TN; i += NT) tw_l[i] = a.tw256[i];
+  for (int i = tid; i < N1; i += NT) tw_l[TN + i] = a.tw256[N2 * i];
+  const int x0 = tid & (TN - 1), ty0 = tid >> 8;  // phase A: column x, thread ty of TY
+  const int r0 = tid >> 4, tx0 = tid & 15;        // phase C: row r, thread tx of 16
+  stagger_start(stagger);
   for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
-    // unit u = (z, y2): rows y2 + 4 y1 of plane z
-    const i64 plane = (i64)(u / TN2) * TN * TN;
-    const int y2 = u % TN2;
+    // fresh index copies every unit (no hoisted unit-invariant twiddle loads, see k_tp_mid)
+    int x = x0, ty = ty0, r = r0, tx = tx0;
+    asm volatile("" : "+v"(x), "+v"(ty), "+v"(r), "+v"(tx));
+    // unit u = (z, y2): rows y2 + N2 y1 of plane z
+    const i64 plane = (i64)(u / N2) * TN * TN;
+    const int y2 = u % N2;
+    const cd* const src = in + plane + x + (i64)TN * (y2 + N2 * ty);  // + a uniform offset per slot
     cd v[16];
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
-      v[m] = gload<FLAGS>(in + plane + x + (i64)TN * (y2 + TN2 * (ty + 4 * m)));
+      v[m] = gload<FLAGS>(src + (i64)TN * N2 * TY * m);
       if (INV) v[m] = cconj(v[m]);
     }
-    // phase A: 64-point DFT over y1 for every x (column mode, 256 columns x 4 threads)
-    fft_stages<TN1, 16, 4, false, TN, F>(v, lds, tw_l + TN, x, ty, true);  // v[m]: k1 = ty + 4 m
+    // phase A: N1-point DFT over y1 for every x (column mode, 256 columns x TY threads)
+    fft_stages<N1, 16, N1 / 16, false, TN, F>(v, lds, tw_l + TN, x, ty, true);  // v[m]: k1 = ty + TY m
     // phase B: transpose to rows k1, thread (row r, tx) gets x = tx + 16 m
     lds_barrier();  // phase A's last LDS reads are done
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
 #pragma unroll
-      for (int m = 0; m < 16; ++m) lds[(ty + 4 * m) * RS + x + (x >> 4)] = half ? v[m].y : v[m].x;
+      for (int m = 0; m < 16; ++m) lds[(ty + TY * m) * RS + x + (x >> 4)] = half ? v[m].y : v[m].x;
       lds_barrier();
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
@@ -81,48 +152,66 @@ __global__ void __launch_bounds__(1024) k_tp_rows(const cd* in, cd* out, TPArgs 
       }
       lds_barrier();
     }
-    // phase C: 256-point DFT along row r (row mode, 64 rows x 16 threads)
-    fft_stages<TN, 16, 16, true, TN1, F>(v, lds, tw_l, r, tx, true);  // v[m]: kx = tx + 16 m
+    // phase C: 256-point DFT along row r (row mode, N1 rows x 16 threads)
+    fft_stages<TN, 16, 16, true, N1, F>(v, lds, tw_l, r, tx, true);  // v[m]: kx = tx + 16 m
     const double sc = a.scale, sy = INV ? -sc : sc;
-    cd* dst = out + plane + (i64)TN * (y2 + TN2 * r) + tx;
+    cd* dst = out + plane + (i64)TN * (y2 + N2 * r) + tx;
 #pragma unroll
     for (int m = 0; m < 16; ++m) gstore<FLAGS>(dst + 16 * m, make_cd(v[m].x * sc, v[m].y * sy));
     lds_barrier();  // the next unit's first exchange overwrites LDS
   }
 }
 
-template <int FLAGS>
-__global__ void __launch_bounds__(1024) k_tp_mid(cd* data, TPArgs a) {
-  constexpr int T = 64;  // columns per workgroup: 16 x times 4 y2 (quad = y2)
-  __shared__ __attribute__((aligned(16))) double lds[T * TN];  // 128 KB (split exchange)
+// Persistent over units u = (x-tile, k1); T columns per unit = T/N2 x values times N2 y2.
+// Barriers wait for LDS only, so one unit's stores drain while the next unit loads.
+template <int FLAGS, int T, int N2>
+__global__ void __launch_bounds__(T * 16) __attribute__((amdgpu_waves_per_eu(4)))
+k_tp_mid(cd* data, TPArgs a, int nunits, int stagger) {
+  constexpr int N1 = TN / N2, NT = T * 16, XT = T / N2, NXT = TN / XT;
+  constexpr int F = FLAGS | F_SPLIT_LDS | F_LDS_SYNC;
+  static_assert(N2 == 4 || N2 == 8, "the y2 DFT runs across 4 or 8 lanes");
+  __shared__ __attribute__((aligned(16))) double lds[T * TN];  // split exchange
   __shared__ cd tw_l[TN];
   const int tid = threadIdx.x;
-  for (int i = tid; i < TN; i += 1024) tw_l[i] = a.tw256[i];
-  const int xt = blockIdx.x % (TN / 16), k1 = blockIdx.x / (TN / 16);
-  const int c = tid & (T - 1), tz = tid >> 6;
-  const int y2 = c & 3, xk = xt * 16 + (c >> 2);
-  const i64 base = xk + (i64)TN * (y2 + TN2 * k1);
+  for (int i = tid; i < TN; i += NT) tw_l[i] = a.tw256[i];
+  const int c0 = tid & (T - 1), tz0 = tid / T;
+  const int y2 = c0 & (N2 - 1);
+  const int k2 = brev<N2>(y2);           // this lane's frequency after the y2 DFT
+  const cd w8 = a.tw256[32 * (y2 & 3)];  // W_8^(y2 & 3) (N2 = 8)
   const i64 zs = (i64)TN * TN;
-  const cd w = a.tw256[(y2 * k1) & (TN - 1)];  // W_256^{y2 k1}
+  stagger_start(stagger);
+  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+    // fresh copies of the thread indices every unit: otherwise the compiler hoists the
+    // unit-invariant twiddle and symbol loads out of the loop, pins ~60 VGPRs and spills
+    int c = c0, tz = tz0;
+    asm volatile("" : "+v"(c), "+v"(tz));
+    const int xt = u % NXT, k1 = u / NXT;
+    const int xk = xt * XT + c / N2;
+    const i64 base = xk + (i64)TN * (y2 + N2 * k1);
+    const cd w = a.tw256[(y2 * k1) & (TN - 1)];  // W_256^{y2 k1}
 
-  cd v[16];
+    // per-thread base + a uniform per-slot offset: one 64-bit VGPR address for all 32 accesses
+    cd* const col = data + base + zs * tz;
+    cd v[16];
 #pragma unroll
-  for (int m = 0; m < 16; ++m) v[m] = gload<FLAGS>(data + base + zs * (tz + 16 * m));
+    for (int m = 0; m < 16; ++m) v[m] = gload<FLAGS>(col + zs * 16 * m);
 #pragma unroll
-  for (int m = 0; m < 16; ++m) v[m] = dft4_quad(cmul(v[m], w), y2);  // lane's y2 is now k2
-  fft_stages<TN, 16, 16, false, T, FLAGS | F_SPLIT_LDS>(v, lds, tw_l, c, tz, true);  // kz = tz + 16 m
+    for (int m = 0; m < 16; ++m) v[m] = lanes_dif<N2>(cmul(v[m], w), y2, w8);  // the lane now holds k2
+    fft_stages<TN, 16, 16, false, T, F>(v, lds, tw_l, c, tz, true);  // kz = tz + 16 m
 
-  const cd cs = a.colsym[xk + (i64)TN * (k1 + TN1 * y2)];
+    const cd cs = a.colsym[xk + (i64)TN * (k1 + N1 * k2)];
 #pragma unroll
-  for (int m = 0; m < 16; ++m) {
-    const cd d = cadd(cadd(cs, a.axsym[tz + 16 * m]), make_cd(1.0, 0.0));
-    v[m] = cconj(cdiv(v[m], d));
+    for (int m = 0; m < 16; ++m) {
+      const cd d = cadd(cadd(cs, a.axsym[tz + 16 * m]), make_cd(1.0, 0.0));
+      v[m] = cconj(cdiv_sym(v[m], d));
+    }
+    fft_stages<TN, 16, 16, false, T, F>(v, lds, tw_l, c, tz, false);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v[m] = cmul(lanes_dit<N2>(v[m], y2, w8), w);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) gstore<FLAGS>(col + zs * 16 * m, cconj(v[m]));
+    lds_barrier();  // the next unit's first exchange overwrites LDS
   }
-  fft_stages<TN, 16, 16, false, T, FLAGS | F_SPLIT_LDS>(v, lds, tw_l, c, tz, false);
-#pragma unroll
-  for (int m = 0; m < 16; ++m) v[m] = cmul(dft4_quad(v[m], y2), w);
-#pragma unroll
-  for (int m = 0; m < 16; ++m) gstore<FLAGS>(data + base + zs * (tz + 16 * m), cconj(v[m]));
 }
 
 bool three_pass_supported(const i64 n[3]) { return n[0] == TN && n[1] == TN && n[2] == TN; }
@@ -138,13 +227,53 @@ static int cu_count() {
   return cus;
 }
 
+static int env_int(const char* k, int d) {
+  const char* e = getenv(k);
+  return e ? atoi(e) : d;
+}
+
+// persistent grid (per_cu workgroups per CU), or one unit per workgroup (all)
+static unsigned grid_of(int units, int per_cu, bool all) {
+  const int g = all ? units : per_cu * cu_count();
+  return (unsigned)(units < g ? units : g);
+}
+
+template <int N1>
+static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s, int stag, bool all) {
+  constexpr int units = TN * (TN / N1);  // z-planes x y2
+  const unsigned g = grid_of(units, N1 == 64 ? 1 : 2, all);
+  if (stage == 0)
+    hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD, N1>), dim3(g), dim3(N1 * 16), 0, s, in, out, a, units, stag);
+  else
+    hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST, N1>), dim3(g), dim3(N1 * 16), 0, s, in, out, a, units, stag);
+}
+
+template <int T, int N2>
+static void launch_mid(cd* data, const TPArgs& a, hipStream_t s, int stag, bool all) {
+  constexpr int units = (TN / (T / N2)) * (TN / N2);  // x-tiles x k1
+  hipLaunchKernelGGL((k_tp_mid<0, T, N2>), dim3(grid_of(units, T == 64 ? 1 : 2, all)), dim3(T * 16), 0, s, data,
+                     a, units, stag);
+}
+
 hipError_t launch_three_pass(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
-  const int units = TN * TN2;  // P1/P3: z-planes x y2; P2: x-tiles x k1 (16 x 64)
-  const unsigned pgrid = (unsigned)(units < cu_count() ? units : cu_count());
-  switch (stage) {
-    case 0: hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD>), dim3(pgrid), dim3(1024), 0, s, in, out, a, units); break;
-    case 1: hipLaunchKernelGGL((k_tp_mid<0>), dim3((TN / 16) * TN1), dim3(1024), 0, s, out, a); break;
-    default: hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST>), dim3(pgrid), dim3(1024), 0, s, in, out, a, units); break;
+  // experiment knobs, read per launch (tools/gpu_tp_stagger.sh, test_three_pass_variants): the
+  // y split N1, P2's tile width T, the start stagger in 100 MHz ticks, one unit per workgroup
+  const int n1 = env_int("CFP_TP_N1", 64) == 32 ? 32 : 64;
+  const int tmid = env_int("CFP_TP_MID_T", 64) == 32 ? 32 : 64;
+  const int stag = env_int("CFP_TP_STAGGER", 0);
+  const bool all = env_int("CFP_TP_GRID_ALL", 0) != 0;
+  if (stage == 1) {
+    if (n1 == 64) {
+      if (tmid == 64) launch_mid<64, 4>(out, a, s, stag, all);
+      else launch_mid<32, 4>(out, a, s, stag, all);
+    } else {
+      if (tmid == 64) launch_mid<64, 8>(out, a, s, stag, all);
+      else launch_mid<32, 8>(out, a, s, stag, all);
+    }
+  } else if (n1 == 64) {
+    launch_rows<64>(stage, in, out, a, s, stag, all);
+  } else {
+    launch_rows<32>(stage, in, out, a, s, stag, all);
   }
   return hipGetLastError();
 }

@@ -12,7 +12,8 @@ TOL = 1e-10
 
 @pytest.mark.parametrize("dims,P", [((64, 64, 64), 2), ((64, 64, 64), 4), ((64, 64, 64), 8),
                                     ((128, 32, 16), 4), ((20, 12, 8), 4), ((256, 256, 256), 8),
-                                    ((1, 8, 8), 2), ((32, 16, 8), 1)])
+                                    ((1, 8, 8), 2), ((32, 16, 8), 1), ((100, 100, 100), 4),
+                                    ((200, 20, 10), 2)])
 def test_group_vs_oracle(dims, P, oracle):
     from circulantpreconditioner_amd.distributed import SlabGroup
     lam = (0.6, 0.15 - 0.1j, 0.02)

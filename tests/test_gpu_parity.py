@@ -419,6 +419,57 @@ def test_three_pass_schedule_rules(cp):
         assert len(plan.passes()) == 5
 
 
+@pytest.fixture(scope="module")
+def tp_case(oracle):
+    n, lam = (256, 256, 256), (0.3 + 0.2j, 1.1, 0.7 - 0.4j)
+    b = oracle.c_fill_uniform(256 ** 3, 5)
+    return n, lam, b, oracle.c_solve_3d(oracle.c_build_diag_transport(n, lam), b, n)
+
+
+@pytest.mark.parametrize("n1,t,stagger,grid_all", [(64, 64, 0, 0), (64, 32, 1000, 0), (32, 64, 0, 1),
+                                                   (32, 32, 1000, 0)])
+def test_three_pass_variants(cp, tp_case, monkeypatch, n1, t, stagger, grid_all):
+    """Both y splits (64 x 4 with a 4-lane y2 DFT, 32 x 8 with an 8-lane one), both P2 tile
+    widths, the start stagger and one unit per workgroup (cfp_three_pass.hip's CFP_TP_* knobs,
+    read per launch)."""
+    for k, v in (("CFP_TP_N1", n1), ("CFP_TP_MID_T", t), ("CFP_TP_STAGGER", stagger), ("CFP_TP_GRID_ALL", grid_all)):
+        monkeypatch.setenv(k, str(v))
+    n, lam, b, ref = tp_case
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam).set_schedule("three")
+        x = plan.apply(_dev(b))
+        assert _rel(x, ref) < TOL
+        t_ = _dev(b)
+        plan.apply(t_, out=t_)
+        assert torch.equal(t_, x)
+
+
+def _random_grids(count=48, seed=2025, max_points=1 << 21):
+    menu = [1, 2, 3, 4, 5, 7, 8, 10, 11, 12, 13, 16, 20, 24, 25, 27, 30, 31, 32, 36, 40, 49, 50, 60, 64, 81, 96,
+            97, 100, 125, 128, 200, 243, 256, 300, 512]
+    rng = np.random.default_rng(seed)
+    grids = []
+    while len(grids) < count:
+        n = tuple(int(v) for v in rng.choice(menu, 3))
+        if int(np.prod(n)) <= max_points and n not in grids:
+            grids.append(n)
+    return grids
+
+
+@pytest.mark.parametrize("n", _random_grids(), ids=lambda n: "x".join(map(str, n)))
+def test_random_grids_vs_oracle(cp, oracle, n):
+    """Seeded sweep over the kernel dispatch table: power-of-two, radix-10, mixed-radix and prime
+    sides in every axis position, each grid with its own complex lambda."""
+    N = int(np.prod(n))
+    rng = np.random.default_rng(sum(n) * 7919 + n[0])
+    lam = tuple(complex(rng.uniform(0.01, 2.0), rng.uniform(-0.5, 0.5)) for _ in range(3))
+    b = oracle.c_fill_uniform(N, 1000 + sum(n))
+    ref = oracle.c_solve_3d(oracle.c_build_diag_transport(n, lam), b, n)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam)
+        assert _rel(plan.apply(_dev(b)), ref) < TOL, plan.passes()
+
+
 @pytest.mark.parametrize("n", [(64, 32, 48), (256, 256, 256), (20, 12, 9), (32, 1, 16)])
 def test_y_fused_schedule_vs_oracle(cp, oracle, n):
     lam = (0.6, 0.15 + 0.05j, 0.02)
