@@ -120,44 +120,57 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits, int stagger) {
   for (int i = tid; i < N1; i += NT) tw_l[TN + i] = a.tw256[N2 * i];
   const int x0 = tid & (TN - 1), ty0 = tid >> 8;  // phase A: column x, thread ty of TY
   const int r0 = tid >> 4, tx0 = tid & 15;        // phase C: row r, thread tx of 16
+  // fresh (laundered) index copies at every use, as in k_tp_mid: nothing but the 16 points
+  // stays live across an FFT
+  const auto idx = [](int i) {
+    asm volatile("" : "+v"(i));
+    return i;
+  };
   stagger_start(stagger);
   for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
-    // fresh index copies every unit (no hoisted unit-invariant twiddle loads, see k_tp_mid)
-    int x = x0, ty = ty0, r = r0, tx = tx0;
-    asm volatile("" : "+v"(x), "+v"(ty), "+v"(r), "+v"(tx));
     // unit u = (z, y2): rows y2 + N2 y1 of plane z
-    const i64 plane = (i64)(u / N2) * TN * TN;
-    const int y2 = u % N2;
-    const cd* const src = in + plane + x + (i64)TN * (y2 + N2 * ty);  // + a uniform offset per slot
     cd v[16];
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      v[m] = gload<FLAGS>(src + (i64)TN * N2 * TY * m);
-      if (INV) v[m] = cconj(v[m]);
-    }
-    // phase A: N1-point DFT over y1 for every x (column mode, 256 columns x TY threads)
-    fft_stages<N1, 16, N1 / 16, false, TN, F>(v, lds, tw_l + TN, x, ty, true);  // v[m]: k1 = ty + TY m
-    // phase B: transpose to rows k1, thread (row r, tx) gets x = tx + 16 m
-    lds_barrier();  // phase A's last LDS reads are done
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-#pragma unroll
-      for (int m = 0; m < 16; ++m) lds[(ty + TY * m) * RS + x + (x >> 4)] = half ? v[m].y : v[m].x;
-      lds_barrier();
+    {
+      const int x = idx(x0), ty = idx(ty0);
+      const cd* const src = in + (i64)(u / N2) * TN * TN + x + (i64)TN * (u % N2 + N2 * ty);  // + uniform
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
-        const int xx = tx + 16 * m;
-        const double val = lds[r * RS + xx + (xx >> 4)];
-        if (half) v[m].y = val; else v[m].x = val;
+        v[m] = gload<FLAGS>(src + (i64)TN * N2 * TY * m);
+        if (INV) v[m] = cconj(v[m]);
       }
-      lds_barrier();
+      // phase A: N1-point DFT over y1 for every x (column mode, 256 columns x TY threads)
+      fft_stages<N1, 16, N1 / 16, false, TN, F>(v, lds, tw_l + TN, x, ty, true);  // v[m]: k1 = ty + TY m
     }
-    // phase C: 256-point DFT along row r (row mode, N1 rows x 16 threads)
-    fft_stages<TN, 16, 16, true, N1, F>(v, lds, tw_l, r, tx, true);  // v[m]: kx = tx + 16 m
-    const double sc = a.scale, sy = INV ? -sc : sc;
-    cd* dst = out + plane + (i64)TN * (y2 + N2 * r) + tx;
+    // phase B: transpose to rows k1, thread (row r, tx) gets x = tx + 16 m
+    lds_barrier();  // phase A's last LDS reads are done
+    {
+      const int x = idx(x0), ty = idx(ty0), r = idx(r0), tx = idx(tx0);
 #pragma unroll
-    for (int m = 0; m < 16; ++m) gstore<FLAGS>(dst + 16 * m, make_cd(v[m].x * sc, v[m].y * sy));
+      for (int half = 0; half < 2; ++half) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) lds[(ty + TY * m) * RS + x + (x >> 4)] = half ? v[m].y : v[m].x;
+        lds_barrier();
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+          const int xx = tx + 16 * m;
+          const double val = lds[r * RS + xx + (xx >> 4)];
+          if (half) v[m].y = val; else v[m].x = val;
+        }
+        lds_barrier();
+      }
+    }
+    {
+      // phase C: 256-point DFT along row r (row mode, N1 rows x 16 threads)
+      const int r = idx(r0), tx = idx(tx0);
+      fft_stages<TN, 16, 16, true, N1, F>(v, lds, tw_l, r, tx, true);  // v[m]: kx = tx + 16 m
+    }
+    {
+      const int r = idx(r0), tx = idx(tx0);
+      const double sc = a.scale, sy = INV ? -sc : sc;
+      cd* dst = out + (i64)(u / N2) * TN * TN + (i64)TN * (u % N2 + N2 * r) + tx;
+#pragma unroll
+      for (int m = 0; m < 16; ++m) gstore<FLAGS>(dst + 16 * m, make_cd(v[m].x * sc, v[m].y * sy));
+    }
     lds_barrier();  // the next unit's first exchange overwrites LDS
   }
 }
@@ -175,41 +188,61 @@ k_tp_mid(cd* data, TPArgs a, int nunits, int stagger) {
   const int tid = threadIdx.x;
   for (int i = tid; i < TN; i += NT) tw_l[i] = a.tw256[i];
   const int c0 = tid & (T - 1), tz0 = tid / T;
-  const int y2 = c0 & (N2 - 1);
-  const int k2 = brev<N2>(y2);           // this lane's frequency after the y2 DFT
-  const cd w8 = a.tw256[32 * (y2 & 3)];  // W_8^(y2 & 3) (N2 = 8)
   const i64 zs = (i64)TN * TN;
-  stagger_start(stagger);
-  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
-    // fresh copies of the thread indices every unit: otherwise the compiler hoists the
-    // unit-invariant twiddle and symbol loads out of the loop, pins ~60 VGPRs and spills
+  // Everything but the 16 points is rebuilt from laundered copies of the thread indices where
+  // it is used: 128 VGPRs hold the points plus one radix-16 stage's twiddles, and an address,
+  // twiddle or index kept live across the FFTs (or hoisted out of the unit loop) spills.
+  struct Col {
+    cd* col;  // this thread's first point; slot m adds the uniform zs * 16 m
+    int y2, xk;
+    cd w, w8;  // W_256^{y2 k1}; W_8^(y2 & 3) (N2 = 8)
+  };
+  const auto column = [&](int u) {
     int c = c0, tz = tz0;
     asm volatile("" : "+v"(c), "+v"(tz));
+    Col q;
     const int xt = u % NXT, k1 = u / NXT;
-    const int xk = xt * XT + c / N2;
-    const i64 base = xk + (i64)TN * (y2 + N2 * k1);
-    const cd w = a.tw256[(y2 * k1) & (TN - 1)];  // W_256^{y2 k1}
-
-    // per-thread base + a uniform per-slot offset: one 64-bit VGPR address for all 32 accesses
-    cd* const col = data + base + zs * tz;
+    q.y2 = c & (N2 - 1);
+    q.xk = xt * XT + c / N2;
+    q.col = data + q.xk + (i64)TN * (q.y2 + N2 * k1) + zs * tz;
+    q.w = a.tw256[(q.y2 * k1) & (TN - 1)];
+    q.w8 = a.tw256[32 * (q.y2 & 3)];
+    return q;
+  };
+  stagger_start(stagger);
+  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
     cd v[16];
+    {
+      const Col q = column(u);
 #pragma unroll
-    for (int m = 0; m < 16; ++m) v[m] = gload<FLAGS>(col + zs * 16 * m);
+      for (int m = 0; m < 16; ++m) v[m] = gload<FLAGS>(q.col + zs * 16 * m);
 #pragma unroll
-    for (int m = 0; m < 16; ++m) v[m] = lanes_dif<N2>(cmul(v[m], w), y2, w8);  // the lane now holds k2
-    fft_stages<TN, 16, 16, false, T, F>(v, lds, tw_l, c, tz, true);  // kz = tz + 16 m
-
-    const cd cs = a.colsym[xk + (i64)TN * (k1 + N1 * k2)];
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      const cd d = cadd(cadd(cs, a.axsym[tz + 16 * m]), make_cd(1.0, 0.0));
-      v[m] = cconj(cdiv_sym(v[m], d));
+      for (int m = 0; m < 16; ++m) v[m] = lanes_dif<N2>(cmul(v[m], q.w), q.y2, q.w8);  // the lane now holds k2
     }
-    fft_stages<TN, 16, 16, false, T, F>(v, lds, tw_l, c, tz, false);
+    {
+      int c = c0, tz = tz0;
+      asm volatile("" : "+v"(c), "+v"(tz));
+      fft_stages<TN, 16, 16, false, T, F>(v, lds, tw_l, c, tz, true);  // kz = tz + 16 m
+    }
+    {
+      int c = c0, tz = tz0;
+      asm volatile("" : "+v"(c), "+v"(tz));
+      const int k1 = u / NXT, y2 = c & (N2 - 1);
+      const cd cs = a.colsym[(u % NXT) * XT + c / N2 + (i64)TN * (k1 + N1 * brev<N2>(y2))];
 #pragma unroll
-    for (int m = 0; m < 16; ++m) v[m] = cmul(lanes_dit<N2>(v[m], y2, w8), w);
+      for (int m = 0; m < 16; ++m) {
+        const cd d = cadd(cadd(cs, a.axsym[tz + 16 * m]), make_cd(1.0, 0.0));
+        v[m] = cconj(cdiv_sym(v[m], d));
+      }
+      fft_stages<TN, 16, 16, false, T, F>(v, lds, tw_l, c, tz, false);
+    }
+    {
+      const Col q = column(u);
 #pragma unroll
-    for (int m = 0; m < 16; ++m) gstore<FLAGS>(col + zs * 16 * m, cconj(v[m]));
+      for (int m = 0; m < 16; ++m) v[m] = cmul(lanes_dit<N2>(v[m], q.y2, q.w8), q.w);
+#pragma unroll
+      for (int m = 0; m < 16; ++m) gstore<FLAGS>(q.col + zs * 16 * m, cconj(v[m]));
+    }
     lds_barrier();  // the next unit's first exchange overwrites LDS
   }
 }
@@ -257,8 +290,10 @@ static void launch_mid(cd* data, const TPArgs& a, hipStream_t s, int stag, bool 
 
 hipError_t launch_three_pass(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
   // experiment knobs, read per launch (tools/gpu_tp_stagger.sh, test_three_pass_variants): the
-  // y split N1, P2's tile width T, the start stagger in 100 MHz ticks, one unit per workgroup
-  const int n1 = env_int("CFP_TP_N1", 64) == 32 ? 32 : 64;
+  // y split N1, P2's tile width T, the start stagger in 100 MHz ticks, one unit per workgroup.
+  // Defaults = the measured best (profiles/r01i_three_pass_sweep.txt): N1 = 32, T = 64,
+  // persistent, no stagger.
+  const int n1 = env_int("CFP_TP_N1", 32) == 64 ? 64 : 32;
   const int tmid = env_int("CFP_TP_MID_T", 64) == 32 ? 32 : 64;
   const int stag = env_int("CFP_TP_STAGGER", 0);
   const bool all = env_int("CFP_TP_GRID_ALL", 0) != 0;

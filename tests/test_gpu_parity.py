@@ -405,8 +405,12 @@ def test_three_pass_schedule_rules(cp):
     n = (256, 256, 256)
     with cp.CirculantPlan(n) as plan:
         plan.set_transport_symbol((0.5, 0.5, 0.5))
-        assert len(plan.passes()) == 5  # default: 5 passes
-        plan.set_schedule("three")
+        assert len(plan.passes()) == 3  # default (AUTO) at 256^3: the 3-sweep schedule
+        plan.set_schedule("five")
+        assert len(plan.passes()) == 5
+        plan.set_schedule("auto").set_chunking(32)
+        assert len(plan.passes()) == 4 * 8 + 1  # chunking asked for: the chunked 5-pass schedule
+        plan.set_chunking(0).set_schedule("three")
         assert len(plan.passes()) == 3
         d = torch.ones(256 ** 3, dtype=torch.complex128, device="cuda") * 2.0
         b = torch.ones_like(d)

@@ -9,7 +9,7 @@ tail -3 gpurun_out/tp_tests.log
 B="python bench.py --no-cpu-baseline --no-real --scaling-grid 0 --steps 200 --no-live-events"
 for rep in 1 2; do
   timeout -k 10 120 $B > gpurun_out/tp.five.$rep.json 2>/dev/null || exit $?
-  for n1 in 64 32; do for t in 64 32; do for v in s0 s1000 s2000 all; do
+  for n1 in 64 32; do for t in 64 32; do for v in s0 all; do
     st=${v#s}; all=0; [ "$v" = all ] && { st=0; all=1; }
     CFP_TP_N1=$n1 CFP_TP_MID_T=$t CFP_TP_STAGGER=$st CFP_TP_GRID_ALL=$all timeout -k 10 120 $B --schedule three \
       > gpurun_out/tp.$n1.$t.$v.$rep.json 2>/dev/null || exit $?

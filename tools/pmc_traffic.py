@@ -6,7 +6,8 @@ HBM bytes for each axis-pass kernel, corrected as MI355X_MICROARCH.md §HBM pres
 
 (FETCH_SIZE, in KiB, reads exactly half of a 16-B/lane coalesced streaming read on gfx950;
 WRITE_SIZE is exact for 16-B/lane stores).  Kernels are mapped to the bench's pass names
-through the template arguments <N, PTS, R0, ROW, T, MODE> and the 5-launch schedule.
+through the template arguments <N, PTS, R0, ROW, T, MODE> and the 5-launch schedule, or
+the 3-sweep schedule's k_tp_rows / k_tp_mid.
 
     python tools/pmc_traffic.py --grid 256 --fetch gpurun_out/pmc256_fetch --write gpurun_out/pmc256_write \
         --out profiles/pmc_traffic.json
@@ -32,6 +33,12 @@ def load(d, counter):
 
 
 def pass_name(kname: str):
+    # the 3-sweep schedule's kernels (cfp_three_pass.hip): rows fwd / mid fused / rows inv
+    t = re.search(r"k_tp_rows<(true|false)", kname)
+    if t:
+        return "pass2_xy_rows_inv" if t.group(1) == "true" else "pass0_xy_rows_fwd"
+    if "k_tp_mid<" in kname:
+        return "pass1_yz_mid_fused"
     m = re.search(r"k_axis_fast<(\d+), (\d+), (\d+), (true|false), (\d+), (\d+)(?:, \d+)?>", kname)
     if not m:
         return None
