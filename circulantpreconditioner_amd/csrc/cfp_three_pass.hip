@@ -70,28 +70,10 @@ __device__ __forceinline__ cd dft4_dit(cd v, int q) {
   const cd p = dpp_c<DPP_XOR2>(u);
   return (q & 2) ? csub(p, u) : cadd(u, p);
 }
-// 8 points over 8 aligned lanes: lane j holds point j -> frequency brev3(j); w8 = W_8^(j & 3)
-__device__ __forceinline__ cd dft8_dif(cd v, int j, cd w8) {
-  const cd p = lane_xor4(v);
-  const cd t = (j & 4) ? cmul(csub(p, v), w8) : cadd(v, p);
-  return dft4_dif(t, j & 3);
-}
-__device__ __forceinline__ cd dft8_dit(cd v, int j, cd w8) {
-  cd u = dft4_dit(v, j & 3);
-  if (j & 4) u = cmul(u, w8);
-  const cd p = lane_xor4(u);
-  return (j & 4) ? csub(p, u) : cadd(u, p);
-}
-template <int N2>
-__device__ __forceinline__ cd lanes_dif(cd v, int j, cd w8) {
-  if constexpr (N2 == 4) return dft4_dif(v, j);
-  else return dft8_dif(v, j, w8);
-}
-template <int N2>
-__device__ __forceinline__ cd lanes_dit(cd v, int j, cd w8) {
-  if constexpr (N2 == 4) return dft4_dit(v, j);
-  else return dft8_dit(v, j, w8);
-}
+// The 8-point DFT over 8 aligned lanes (N2 = 8) is a lane-xor-4 radix-2 stage (twiddle
+// W_8^(j & 3) on the upper half) followed by dft4_dif, and dft4_dit followed by the mirrored
+// stage for the inverse; k_tp_mid runs each stage as its own sweep over the 16 slots, which
+// keeps the kernel out of scratch.  Lane j ends up holding frequency brev3(j).
 template <int N2>
 __device__ __forceinline__ int brev(int j) {
   return N2 == 4 ? ((j & 1) << 1) | (j >> 1) : ((j & 1) << 2) | (j & 2) | (j >> 2);
@@ -217,7 +199,15 @@ k_tp_mid(cd* data, TPArgs a, int nunits, int stagger) {
 #pragma unroll
       for (int m = 0; m < 16; ++m) v[m] = gload<FLAGS>(q.col + zs * 16 * m);
 #pragma unroll
-      for (int m = 0; m < 16; ++m) v[m] = lanes_dif<N2>(cmul(v[m], q.w), q.y2, q.w8);  // the lane now holds k2
+      for (int m = 0; m < 16; ++m) {  // the lane DFT in two sweeps over the slots: fewer live temporaries
+        v[m] = cmul(v[m], q.w);
+        if constexpr (N2 == 8) {  // dft8_dif's first stage
+          const cd p = lane_xor4(v[m]);
+          v[m] = (q.y2 & 4) ? cmul(csub(p, v[m]), q.w8) : cadd(v[m], p);
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 16; ++m) v[m] = dft4_dif(v[m], q.y2 & 3);  // the lane now holds k2
     }
     {
       int c = c0, tz = tz0;
@@ -239,7 +229,16 @@ k_tp_mid(cd* data, TPArgs a, int nunits, int stagger) {
     {
       const Col q = column(u);
 #pragma unroll
-      for (int m = 0; m < 16; ++m) v[m] = cmul(lanes_dit<N2>(v[m], q.y2, q.w8), q.w);
+      for (int m = 0; m < 16; ++m) v[m] = dft4_dit(v[m], q.y2 & 3);
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        if constexpr (N2 == 8) {  // dft8_dit's last stage
+          const cd u = (q.y2 & 4) ? cmul(v[m], q.w8) : v[m];
+          const cd p = lane_xor4(u);
+          v[m] = (q.y2 & 4) ? csub(p, u) : cadd(u, p);
+        }
+        v[m] = cmul(v[m], q.w);
+      }
 #pragma unroll
       for (int m = 0; m < 16; ++m) gstore<FLAGS>(q.col + zs * 16 * m, cconj(v[m]));
     }
