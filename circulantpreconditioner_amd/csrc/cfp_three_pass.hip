@@ -96,10 +96,10 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits, int stagger) {
   constexpr int N2 = TN / N1, NT = N1 * 16, TY = N1 / 16;
   constexpr int F = FLAGS | F_SPLIT_LDS | F_LDS_SYNC;
   __shared__ __attribute__((aligned(16))) double lds[N1 * RS];  // both layouts fit
-  __shared__ cd tw_l[TN + N1];                                  // W_256, then W_N1
+  __shared__ cd tw_l[N1];  // W_N1 for phase A; phase C reads W_256 from global memory (L2 hits),
+                           // which keeps it out of scratch (20 B/lane with the table in LDS)
   const int tid = threadIdx.x;
-  for (int i = tid; i < TN; i += NT) tw_l[i] = a.tw256[i];
-  for (int i = tid; i < N1; i += NT) tw_l[TN + i] = a.tw256[N2 * i];
+  for (int i = tid; i < N1; i += NT) tw_l[i] = a.tw256[N2 * i];
   const int x0 = tid & (TN - 1), ty0 = tid >> 8;  // phase A: column x, thread ty of TY
   const int r0 = tid >> 4, tx0 = tid & 15;        // phase C: row r, thread tx of 16
   // fresh (laundered) index copies at every use, as in k_tp_mid: nothing but the 16 points
@@ -121,7 +121,7 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits, int stagger) {
         if (INV) v[m] = cconj(v[m]);
       }
       // phase A: N1-point DFT over y1 for every x (column mode, 256 columns x TY threads)
-      fft_stages<N1, 16, N1 / 16, false, TN, F>(v, lds, tw_l + TN, x, ty, true);  // v[m]: k1 = ty + TY m
+      fft_stages<N1, 16, N1 / 16, false, TN, F>(v, lds, tw_l, x, ty, true);  // v[m]: k1 = ty + TY m
     }
     // phase B: transpose to rows k1, thread (row r, tx) gets x = tx + 16 m
     lds_barrier();  // phase A's last LDS reads are done
@@ -144,7 +144,7 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits, int stagger) {
     {
       // phase C: 256-point DFT along row r (row mode, N1 rows x 16 threads)
       const int r = idx(r0), tx = idx(tx0);
-      fft_stages<TN, 16, 16, true, N1, F>(v, lds, tw_l, r, tx, true);  // v[m]: kx = tx + 16 m
+      fft_stages<TN, 16, 16, true, N1, F | F_TW_GLOBAL>(v, lds, a.tw256, r, tx, true);  // v[m]: kx = tx + 16 m
     }
     {
       const int r = idx(r0), tx = idx(tx0);
