@@ -280,11 +280,11 @@ static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipSt
     hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST, N1>), dim3(g), dim3(N1 * 16), 0, s, in, out, a, units, stag);
 }
 
-template <int T, int N2>
+template <int T, int N2, int FLAGS = 0>
 static void launch_mid(cd* data, const TPArgs& a, hipStream_t s, int stag, bool all) {
   constexpr int units = (TN / (T / N2)) * (TN / N2);  // x-tiles x k1
-  hipLaunchKernelGGL((k_tp_mid<0, T, N2>), dim3(grid_of(units, T == 64 ? 1 : 2, all)), dim3(T * 16), 0, s, data,
-                     a, units, stag);
+  hipLaunchKernelGGL((k_tp_mid<FLAGS, T, N2>), dim3(grid_of(units, T == 64 ? 1 : 2, all)), dim3(T * 16), 0, s,
+                     data, a, units, stag);
 }
 
 hipError_t launch_three_pass(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
@@ -301,7 +301,14 @@ hipError_t launch_three_pass(int stage, const cd* in, cd* out, const TPArgs& a, 
       if (tmid == 64) launch_mid<64, 4>(out, a, s, stag, all);
       else launch_mid<32, 4>(out, a, s, stag, all);
     } else {
-      if (tmid == 64) launch_mid<64, 8>(out, a, s, stag, all);
+      if (tmid == 64) {
+        // load/store policy of the default shape (experiment knob: F_NT_LD = 16, F_NT_ST = 32)
+        const int fl = env_int("CFP_TP_MID_FLAGS", 0);
+        if (fl == F_NT_LD) launch_mid<64, 8, F_NT_LD>(out, a, s, stag, all);
+        else if (fl == F_NT_ST) launch_mid<64, 8, F_NT_ST>(out, a, s, stag, all);
+        else if (fl == (F_NT_LD | F_NT_ST)) launch_mid<64, 8, F_NT_LD | F_NT_ST>(out, a, s, stag, all);
+        else launch_mid<64, 8>(out, a, s, stag, all);
+      }
       else launch_mid<32, 8>(out, a, s, stag, all);
     }
   } else if (n1 == 64) {
