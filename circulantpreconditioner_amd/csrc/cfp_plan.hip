@@ -186,7 +186,8 @@ struct Step {
 // the 3-sweep schedule serves 256^3 grids with a separable symbol: on request, and by default
 // (AUTO without chunking), where it beats the 5-pass schedule by ~18 %
 bool use_three_pass(const cfp_plan_s* p, bool diag_override) {
-  const bool want = p->schedule == CFP_SCHEDULE_THREE_PASS || (p->schedule == CFP_SCHEDULE_AUTO && p->chunk_planes == 0);
+  const bool want = p->schedule == CFP_SCHEDULE_THREE_PASS ||
+                    (p->schedule == CFP_SCHEDULE_AUTO && p->chunk_planes == 0 && p->n[0] == 256);
   if (!want || diag_override || p->sym_kind != 1 || p->external_x) return false;
   return three_pass_supported(p->n);
 }
@@ -347,13 +348,16 @@ int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStr
   for (size_t i = 0; i < st.size(); ++i) {
     const Step& q = st[i];
     if (q.tp >= 0) {
+      const int tn = (int)p->n[0];
+      int trc = ensure_tw(p, tn);
+      if (trc) return trc;
       TPArgs a;
-      a.tw256 = p->tw[256];
+      a.tw = p->tw[tn];
       a.colsym = p->colsym;
       a.axsym = p->axsym;
       a.scale = q.scale ? invN : 1.0;
       if (ev) HIPCHK(hipEventRecord((*ev)[i], s));
-      hipError_t e = launch_three_pass(q.tp, q.from_b ? b : x, x, a, s);
+      hipError_t e = launch_three_pass(q.tp, tn, q.from_b ? b : x, x, a, s);
       if (e != hipSuccess) return hip_error(e, "3-sweep launch");
       continue;
     }
@@ -735,7 +739,7 @@ extern "C" int cfp_plan_set_schedule(cfp_plan_t p, int schedule) {
   if (schedule < CFP_SCHEDULE_AUTO || schedule > CFP_SCHEDULE_FIVE_PASS_YFUSED)
     return set_error(CFP_ERR_ARG_OUTOFRANGE, "unknown schedule %d", schedule);
   if (schedule == CFP_SCHEDULE_THREE_PASS && !three_pass_supported(p->n))
-    return set_error(CFP_ERR_SUP, "the 3-sweep schedule needs a 256x256x256 grid");
+    return set_error(CFP_ERR_SUP, "the 3-sweep schedule needs a 128^3 or 256^3 grid");
   DeviceGuard dg(p->device);
   const int f_old = p->fused_axis;
   p->schedule = schedule;

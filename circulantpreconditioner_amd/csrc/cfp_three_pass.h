@@ -1,18 +1,18 @@
-// cfp_three_pass.h -- the 3-sweep apply for 256^3 grids (cfp_three_pass.hip).
+// cfp_three_pass.h -- the 3-sweep apply for 128^3 and 256^3 grids (cfp_three_pass.hip).
 #pragma once
 #include "cfp_internal.h"
 
 namespace cfp {
 
 struct TPArgs {
-  const cd* tw256;   // W_256[k] = exp(-2 pi i k / 256)
-  const cd* colsym;  // separable symbol, z fused: [kx + 256 ky] = s_x[kx] + s_y[ky]
+  const cd* tw;      // W_n[k] = exp(-2 pi i k / n), n = the grid side (128 or 256)
+  const cd* colsym;  // separable symbol, z fused: [kx + n ky] = s_x[kx] + s_y[ky]
   const cd* axsym;   // [kz] = s_z[kz]
   double scale;      // P3 only: 1/N
 };
 
 bool three_pass_supported(const i64 n[3]);
 // stage 0: P1 (in -> out), 1: P2 (out in place), 2: P3 (in -> out)
-hipError_t launch_three_pass(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s);
+hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, hipStream_t s);
 
 }  // namespace cfp

@@ -32,8 +32,6 @@
 namespace cfp {
 
 namespace {
-constexpr int TN = 256;  // nx = ny = nz
-constexpr int RS = TN + TN / 16;  // padded row stride of the row-mode LDS layout
 
 // DPP controls: quad_perm lane ^ 1, ^ 2, ^ 3; row_half_mirror (lane ^ 7 within 8 lanes)
 constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_XOR3 = 0x1B, DPP_HALF_MIRROR = 0x141;
@@ -90,18 +88,19 @@ __device__ __forceinline__ void stagger_start(int ticks) {
 // Persistent: a workgroup walks units blockIdx.x, + gridDim.x, ...  Prefetching the next unit
 // into VGPRs across LDS-only barriers was tried and lost: at 1024 threads the extra registers
 // spill (profiles/r01_schedule_sweep.txt).
-template <bool INV, int FLAGS, int N1>
-__global__ void __launch_bounds__(N1 * 16) __attribute__((amdgpu_waves_per_eu(4)))
+template <bool INV, int FLAGS, int N1, int TN>
+__global__ void __launch_bounds__(N1 * (TN / 16)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits, int stagger) {
-  constexpr int N2 = TN / N1, NT = N1 * 16, TY = N1 / 16;
+  constexpr int N2 = TN / N1, TR = TN / 16, NT = N1 * TR, TY = N1 / 16;
+  constexpr int RS = TN + TN / 16;  // padded row stride of the row-mode LDS layout
   constexpr int F = FLAGS | F_SPLIT_LDS | F_LDS_SYNC;
   __shared__ __attribute__((aligned(16))) double lds[N1 * RS];  // both layouts fit
   __shared__ cd tw_l[N1];  // W_N1 for phase A; phase C reads W_256 from global memory (L2 hits),
                            // which keeps it out of scratch (20 B/lane with the table in LDS)
   const int tid = threadIdx.x;
-  for (int i = tid; i < N1; i += NT) tw_l[i] = a.tw256[N2 * i];
-  const int x0 = tid & (TN - 1), ty0 = tid >> 8;  // phase A: column x, thread ty of TY
-  const int r0 = tid >> 4, tx0 = tid & 15;        // phase C: row r, thread tx of 16
+  for (int i = tid; i < N1; i += NT) tw_l[i] = a.tw[N2 * i];
+  const int x0 = tid % TN, ty0 = tid / TN;  // phase A: column x, thread ty of TY
+  const int r0 = tid / TR, tx0 = tid % TR;  // phase C: row r, thread tx of TR
   // fresh (laundered) index copies at every use, as in k_tp_mid: nothing but the 16 points
   // stays live across an FFT
   const auto idx = [](int i) {
@@ -134,7 +133,7 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits, int stagger) {
         lds_barrier();
 #pragma unroll
         for (int m = 0; m < 16; ++m) {
-          const int xx = tx + 16 * m;
+          const int xx = tx + TR * m;
           const double val = lds[r * RS + xx + (xx >> 4)];
           if (half) v[m].y = val; else v[m].x = val;
         }
@@ -144,14 +143,14 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits, int stagger) {
     {
       // phase C: 256-point DFT along row r (row mode, N1 rows x 16 threads)
       const int r = idx(r0), tx = idx(tx0);
-      fft_stages<TN, 16, 16, true, N1, F | F_TW_GLOBAL>(v, lds, a.tw256, r, tx, true);  // v[m]: kx = tx + 16 m
+      fft_stages<TN, 16, TN / 16, true, N1, F | F_TW_GLOBAL>(v, lds, a.tw, r, tx, true);  // v[m]: kx = tx + TR m
     }
     {
       const int r = idx(r0), tx = idx(tx0);
       const double sc = a.scale, sy = INV ? -sc : sc;
       cd* dst = out + (i64)(u / N2) * TN * TN + (i64)TN * (u % N2 + N2 * r) + tx;
 #pragma unroll
-      for (int m = 0; m < 16; ++m) gstore<FLAGS>(dst + 16 * m, make_cd(v[m].x * sc, v[m].y * sy));
+      for (int m = 0; m < 16; ++m) gstore<FLAGS>(dst + TR * m, make_cd(v[m].x * sc, v[m].y * sy));
     }
     lds_barrier();  // the next unit's first exchange overwrites LDS
   }
@@ -159,16 +158,16 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits, int stagger) {
 
 // Persistent over units u = (x-tile, k1); T columns per unit = T/N2 x values times N2 y2.
 // Barriers wait for LDS only, so one unit's stores drain while the next unit loads.
-template <int FLAGS, int T, int N2>
-__global__ void __launch_bounds__(T * 16) __attribute__((amdgpu_waves_per_eu(4)))
+template <int FLAGS, int T, int N2, int TN>
+__global__ void __launch_bounds__(T * (TN / 16)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid(cd* data, TPArgs a, int nunits, int stagger) {
-  constexpr int N1 = TN / N2, NT = T * 16, XT = T / N2, NXT = TN / XT;
+  constexpr int N1 = TN / N2, TZ = TN / 16, NT = T * TZ, XT = T / N2, NXT = TN / XT;
   constexpr int F = FLAGS | F_SPLIT_LDS | F_LDS_SYNC;
   static_assert(N2 == 4 || N2 == 8, "the y2 DFT runs across 4 or 8 lanes");
   __shared__ __attribute__((aligned(16))) double lds[T * TN];  // split exchange
   __shared__ cd tw_l[TN];
   const int tid = threadIdx.x;
-  for (int i = tid; i < TN; i += NT) tw_l[i] = a.tw256[i];
+  for (int i = tid; i < TN; i += NT) tw_l[i] = a.tw[i];
   const int c0 = tid & (T - 1), tz0 = tid / T;
   const i64 zs = (i64)TN * TN;
   // Everything but the 16 points is rebuilt from laundered copies of the thread indices where
@@ -187,8 +186,8 @@ k_tp_mid(cd* data, TPArgs a, int nunits, int stagger) {
     q.y2 = c & (N2 - 1);
     q.xk = xt * XT + c / N2;
     q.col = data + q.xk + (i64)TN * (q.y2 + N2 * k1) + zs * tz;
-    q.w = a.tw256[(q.y2 * k1) & (TN - 1)];
-    q.w8 = a.tw256[32 * (q.y2 & 3)];
+    q.w = a.tw[(q.y2 * k1) & (TN - 1)];
+    q.w8 = a.tw[(TN / 8) * (q.y2 & 3)];
     return q;
   };
   stagger_start(stagger);
@@ -197,7 +196,7 @@ k_tp_mid(cd* data, TPArgs a, int nunits, int stagger) {
     {
       const Col q = column(u);
 #pragma unroll
-      for (int m = 0; m < 16; ++m) v[m] = gload<FLAGS>(q.col + zs * 16 * m);
+      for (int m = 0; m < 16; ++m) v[m] = gload<FLAGS>(q.col + zs * TZ * m);
 #pragma unroll
       for (int m = 0; m < 16; ++m) {  // the lane DFT in two sweeps over the slots: fewer live temporaries
         v[m] = cmul(v[m], q.w);
@@ -212,7 +211,7 @@ k_tp_mid(cd* data, TPArgs a, int nunits, int stagger) {
     {
       int c = c0, tz = tz0;
       asm volatile("" : "+v"(c), "+v"(tz));
-      fft_stages<TN, 16, 16, false, T, F>(v, lds, tw_l, c, tz, true);  // kz = tz + 16 m
+      fft_stages<TN, 16, TN / 16, false, T, F>(v, lds, tw_l, c, tz, true);  // kz = tz + 16 m
     }
     {
       int c = c0, tz = tz0;
@@ -221,10 +220,10 @@ k_tp_mid(cd* data, TPArgs a, int nunits, int stagger) {
       const cd cs = a.colsym[(u % NXT) * XT + c / N2 + (i64)TN * (k1 + N1 * brev<N2>(y2))];
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
-        const cd d = cadd(cadd(cs, a.axsym[tz + 16 * m]), make_cd(1.0, 0.0));
+        const cd d = cadd(cadd(cs, a.axsym[tz + TZ * m]), make_cd(1.0, 0.0));
         v[m] = cconj(cdiv_sym(v[m], d));
       }
-      fft_stages<TN, 16, 16, false, T, F>(v, lds, tw_l, c, tz, false);
+      fft_stages<TN, 16, TN / 16, false, T, F>(v, lds, tw_l, c, tz, false);
     }
     {
       const Col q = column(u);
@@ -240,13 +239,15 @@ k_tp_mid(cd* data, TPArgs a, int nunits, int stagger) {
         v[m] = cmul(v[m], q.w);
       }
 #pragma unroll
-      for (int m = 0; m < 16; ++m) gstore<FLAGS>(q.col + zs * 16 * m, cconj(v[m]));
+      for (int m = 0; m < 16; ++m) gstore<FLAGS>(q.col + zs * TZ * m, cconj(v[m]));
     }
     lds_barrier();  // the next unit's first exchange overwrites LDS
   }
 }
 
-bool three_pass_supported(const i64 n[3]) { return n[0] == TN && n[1] == TN && n[2] == TN; }
+bool three_pass_supported(const i64 n[3]) {
+  return n[0] == n[1] && n[1] == n[2] && (n[0] == 128 || n[0] == 256);
+}
 
 static int cu_count() {
   static int cus = 0;
@@ -270,26 +271,35 @@ static unsigned grid_of(int units, int per_cu, bool all) {
   return (unsigned)(units < g ? units : g);
 }
 
-template <int N1>
+template <int N1, int TN, int PER_CU>
 static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s, int stag, bool all) {
   constexpr int units = TN * (TN / N1);  // z-planes x y2
-  const unsigned g = grid_of(units, N1 == 64 ? 1 : 2, all);
+  const unsigned g = grid_of(units, PER_CU, all);
   if (stage == 0)
-    hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD, N1>), dim3(g), dim3(N1 * 16), 0, s, in, out, a, units, stag);
+    hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units,
+                       stag);
   else
-    hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST, N1>), dim3(g), dim3(N1 * 16), 0, s, in, out, a, units, stag);
+    hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units,
+                       stag);
 }
 
-template <int T, int N2, int FLAGS = 0>
+template <int T, int N2, int TN, int PER_CU, int FLAGS = 0>
 static void launch_mid(cd* data, const TPArgs& a, hipStream_t s, int stag, bool all) {
   constexpr int units = (TN / (T / N2)) * (TN / N2);  // x-tiles x k1
-  hipLaunchKernelGGL((k_tp_mid<FLAGS, T, N2>), dim3(grid_of(units, T == 64 ? 1 : 2, all)), dim3(T * 16), 0, s,
+  hipLaunchKernelGGL((k_tp_mid<FLAGS, T, N2, TN>), dim3(grid_of(units, PER_CU, all)), dim3(T * (TN / 16)), 0, s,
                      data, a, units, stag);
 }
 
-hipError_t launch_three_pass(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
-  // experiment knobs, read per launch (tools/gpu_tp_stagger.sh, test_three_pass_variants): the
-  // y split N1, P2's tile width T, the start stagger in 100 MHz ticks, one unit per workgroup.
+hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
+  if (n == 128) {
+    // 128^3: N1 = 32 x N2 = 4; P1/P3 256 threads and 35 KiB of LDS (4 per CU), P2 64 columns =
+    // 16 x 4 y2 (256-byte runs), 512 threads and 66 KiB (2 per CU)
+    if (stage == 1) launch_mid<64, 4, 128, 2>(out, a, s, 0, false);
+    else launch_rows<32, 128, 4>(stage, in, out, a, s, 0, false);
+    return hipGetLastError();
+  }
+  // 256^3.  Experiment knobs, read per launch (tools/gpu_tp_stagger.sh, test_three_pass_variants):
+  // the y split N1, P2's tile width T, the start stagger in 100 MHz ticks, one unit per workgroup.
   // Defaults = the measured best (profiles/r01i_three_pass_sweep.txt): N1 = 32, T = 64,
   // persistent, no stagger.
   const int n1 = env_int("CFP_TP_N1", 32) == 64 ? 64 : 32;
@@ -298,23 +308,22 @@ hipError_t launch_three_pass(int stage, const cd* in, cd* out, const TPArgs& a, 
   const bool all = env_int("CFP_TP_GRID_ALL", 0) != 0;
   if (stage == 1) {
     if (n1 == 64) {
-      if (tmid == 64) launch_mid<64, 4>(out, a, s, stag, all);
-      else launch_mid<32, 4>(out, a, s, stag, all);
+      if (tmid == 64) launch_mid<64, 4, 256, 1>(out, a, s, stag, all);
+      else launch_mid<32, 4, 256, 2>(out, a, s, stag, all);
+    } else if (tmid == 64) {
+      // load/store policy of the default shape (experiment knob: F_NT_LD = 16, F_NT_ST = 32)
+      const int fl = env_int("CFP_TP_MID_FLAGS", 0);
+      if (fl == F_NT_LD) launch_mid<64, 8, 256, 1, F_NT_LD>(out, a, s, stag, all);
+      else if (fl == F_NT_ST) launch_mid<64, 8, 256, 1, F_NT_ST>(out, a, s, stag, all);
+      else if (fl == (F_NT_LD | F_NT_ST)) launch_mid<64, 8, 256, 1, F_NT_LD | F_NT_ST>(out, a, s, stag, all);
+      else launch_mid<64, 8, 256, 1>(out, a, s, stag, all);
     } else {
-      if (tmid == 64) {
-        // load/store policy of the default shape (experiment knob: F_NT_LD = 16, F_NT_ST = 32)
-        const int fl = env_int("CFP_TP_MID_FLAGS", 0);
-        if (fl == F_NT_LD) launch_mid<64, 8, F_NT_LD>(out, a, s, stag, all);
-        else if (fl == F_NT_ST) launch_mid<64, 8, F_NT_ST>(out, a, s, stag, all);
-        else if (fl == (F_NT_LD | F_NT_ST)) launch_mid<64, 8, F_NT_LD | F_NT_ST>(out, a, s, stag, all);
-        else launch_mid<64, 8>(out, a, s, stag, all);
-      }
-      else launch_mid<32, 8>(out, a, s, stag, all);
+      launch_mid<32, 8, 256, 2>(out, a, s, stag, all);
     }
   } else if (n1 == 64) {
-    launch_rows<64>(stage, in, out, a, s, stag, all);
+    launch_rows<64, 256, 1>(stage, in, out, a, s, stag, all);
   } else {
-    launch_rows<32>(stage, in, out, a, s, stag, all);
+    launch_rows<32, 256, 2>(stage, in, out, a, s, stag, all);
   }
   return hipGetLastError();
 }

@@ -97,7 +97,7 @@ int cfp_plan_set_chunking(cfp_plan_t plan, int64_t chunk_planes);
 /* Apply schedule.  FIVE_PASS: x, y fwd, z fused with the symbol, y, x inv.
  * FIVE_PASS_YFUSED: x, z fwd, y fused, z, x inv.  AUTO (default): THREE_PASS on 256^3 plans
  * (separable symbol, no chunking), YFUSED when ny, nz >= 512, else FIVE_PASS.  THREE_PASS
- * (256^3 plans only, CFP_ERR_SUP
+ * (128^3 and 256^3 plans only, CFP_ERR_SUP
  * otherwise; an explicit Diag still takes 5 passes): x + first y stage | last y stage + z +
  * symbol + inverses | inverse of the first, 96 N bytes instead of 160 N. */
 #define CFP_SCHEDULE_AUTO 0
