@@ -50,7 +50,7 @@ def main():
     for name, calls, tot, avg, pct in rows:
         short = name.replace("HIP_vector_type<double, 2u>", "cd").replace("cfp::", "")
         short = short.split("(")[0]
-        gbs = f"{32 * N / (avg * 1e-6) / 1e9:.0f}" if (N and "k_axis" in name) else ""
+        gbs = f"{32 * N / (avg * 1e-6) / 1e9:.0f}" if (N and ("k_axis" in name or "k_tp_" in name)) else ""
         print(f"| `{short}` | {calls} | {tot:.1f} | {avg:.2f} | {pct:.1f} | {gbs} |")
 
 
