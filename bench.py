@@ -48,28 +48,46 @@ def kernel_alg_bytes(mode: str, N: int, n_axis: int) -> int:
     return b
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(grid, budget_s: float = 20.0):
-    """The oracle's C restatement (test infrastructure; the checker, never the product)."""
+    """The oracle's C restatement (test infrastructure; the checker, never the product), timed
+    on 1 thread and on all of this process's host cores."""
     import numpy as np
     from oracle import oracle as O
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
-    O.set_threads(threads)
     n = tuple(grid)
     N = int(np.prod(n))
     b = O.c_fill_uniform(N, SEED)
     d = O.c_build_diag_transport(n, LAM)
-    t0 = time.perf_counter()
-    O.c_solve_3d(d, b, n)  # warm-up (page faults, thread pool)
-    first = time.perf_counter() - t0
-    reps = max(1, min(5, int(budget_s / max(first, 1e-3))))
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        O.c_solve_3d(d, b, n)
-    dt = (time.perf_counter() - t0) / reps
-    out = {"value": round(1.0 / dt, 4), "unit": "PCApply/s", "cores": threads, "kind": "port",
-           "sample": f"{reps} timed applies (+1 warm-up) of the full {n[0]}x{n[1]}x{n[2]} grid, "
-                     f"oracle/cfp_oracle.c restatement of solve_3D, OpenMP {threads} threads, "
-                     f"{dt * 1e3:.0f} ms/apply"}
+
+    def leg(nthreads, budget):
+        O.set_threads(nthreads)
+        t0 = time.perf_counter()
+        O.c_solve_3d(d, b, n)  # warm-up (page faults, thread pool); also sizes the sample
+        first = time.perf_counter() - t0
+        reps = max(1, min(5, int(budget / max(first, 1e-3))))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            O.c_solve_3d(d, b, n)
+        dt = (time.perf_counter() - t0) / reps
+        return {"threads": nthreads, "value": round(1.0 / dt, 4), "ms_per_apply": round(dt * 1e3, 1),
+                "sample": f"{reps} timed applies (+1 warm-up) of the full {n[0]}x{n[1]}x{n[2]} grid"}
+
+    legs = [leg(1, budget_s * 0.6), leg(threads, budget_s * 0.4)] if threads > 1 else [leg(1, budget_s)]
+    top = legs[-1]
+    out = {"value": top["value"], "unit": "PCApply/s", "cores": threads, "kind": "port",
+           "sample": f"{top['sample']}, oracle/cfp_oracle.c restatement of solve_3D, OpenMP {threads} threads, "
+                     f"{top['ms_per_apply']:.0f} ms/apply",
+           "legs": legs, "cpu_model": cpu_model()}
     # SURVEY.md §8d(ii): an optimised-library proxy beside the port (FFTW is absent): scipy's
     # pocketfft, multithreaded, on the same grid and symbol -- fftn, divide, ifftn
     try:
@@ -77,6 +95,7 @@ def cpu_baseline(grid, budget_s: float = 20.0):
         bz = b.reshape(n[2], n[1], n[0])
         dz = d.reshape(n[2], n[1], n[0])
         sf.ifftn(sf.fftn(bz, workers=threads) / dz, workers=threads)
+        reps = 3
         t0 = time.perf_counter()
         for _ in range(reps):
             sf.ifftn(sf.fftn(bz, workers=threads) / dz, workers=threads)
@@ -87,6 +106,36 @@ def cpu_baseline(grid, budget_s: float = 20.0):
     except Exception as e:  # report, never fake
         out["library_proxy"] = {"error": str(e)}
     return out
+
+
+def moved_bytes(passes, N: int) -> int:
+    """Bytes one apply's launches move by design (sum of their algorithmic bytes): 96 N for the
+    3-sweep schedule, 160 N for five axis passes (+ the small symbol tables)."""
+    return int(sum(kernel_alg_bytes(p["mode"], N, p["n"]) for p in passes))
+
+
+def choose_slab_plan(create, requested, agree, warn=None):
+    """Pick the N > 1 exchange.  create(exchange) builds this rank's SlabPlan (raises on
+    failure); agree(ok) -> True when every rank's creation succeeded.  RCCL unless the
+    environment asks otherwise.  When the library's RCCL communicator fails on any rank: an
+    explicit CFP_EXCHANGE=rccl request exits non-zero; the default falls back to
+    torch.distributed collectives and says so in the label ("torch-fallback"), which bench.py
+    prints as the top-level "exchange" field.  Returns (plan, label)."""
+    exchange = requested or "rccl"
+    plan, err = None, None
+    try:
+        plan = create(exchange)
+    except Exception as e:  # the library's own communicator failed on this rank
+        err = e
+    if agree(plan is not None):
+        return plan, exchange
+    if plan is not None:
+        plan.close()
+    if requested == "rccl" or exchange != "rccl":
+        raise SystemExit(f"{exchange} exchange requested but unavailable on some rank ({err})")
+    if warn:
+        warn(f"rccl exchange unavailable ({err}); falling back to torch.distributed all_to_all_single")
+    return create("torch"), "torch-fallback"
 
 
 def load_traffic(grid, kernel_name: str):
@@ -115,6 +164,8 @@ def main() -> int:
     ap.add_argument("--chunk", type=int, default=None,
                     help="z-planes per chunk of the Infinity-Cache-resident x/y schedule (0 = off; default: plan's)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--settle-ms", type=float, default=300.0,
+                    help="untimed applies for this long after the warm-up (clock ramp-up; 0 = off)")
     ap.add_argument("--no-real", action="store_true", help="skip the real-data variant line item")
     ap.add_argument("--scaling-grid", type=int, nargs="+", default=[512],
                     help="grid of the scaling_512 line item (BASELINE config 5; 0 = skip)")
@@ -155,6 +206,8 @@ def main() -> int:
     roof_apply = None
     passes_info = None
 
+    exchange_used = ["none"]  # N > 1: "rccl", "torch" or "torch-fallback"
+
     def make(g):
         """(plan, b, x, run, parallelism) of the apply on grid g: one GPU, or this rank's slab."""
         if world == 1:
@@ -168,25 +221,45 @@ def main() -> int:
             plan.set_schedule(args.schedule)
             return plan, b, x, (lambda: plan.apply(b, out=x)), "single GPU"
         from circulantpreconditioner_amd.distributed import SlabPlan
-        exchange = os.environ.get("CFP_EXCHANGE", "rccl")
-        plan, err = None, None
-        try:
-            plan = SlabPlan(g, rank=rank, world=world, device=local_rank, exchange=exchange)
-        except Exception as e:  # the library's own RCCL communicator failed on this rank
-            err = e
-        ok = torch.tensor([0 if plan is None else 1], dtype=torch.int32, device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok.item()) == 0:
-            log(f"rank {rank}: {exchange} exchange unavailable ({err}); using torch.distributed all_to_all_single")
-            if plan is not None:
-                plan.close()
-            exchange = "torch"
-            plan = SlabPlan(g, rank=rank, world=world, device=local_rank, exchange="torch")
+
+        def agree(ok):
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                             device=dev if dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            return int(t.item()) == 1
+
+        plan, exchange = choose_slab_plan(
+            lambda ex: SlabPlan(g, rank=rank, world=world, device=local_rank, exchange=ex),
+            os.environ.get("CFP_EXCHANGE"), agree, warn=lambda m: log(f"rank {rank}: {m}"))
+        exchange_used[0] = exchange
         plan.set_transport_symbol(LAM)
         b = torch.empty(plan.local_size, dtype=torch.complex128, device=dev)
         x = torch.empty_like(b)
         cp.fill_uniform(b, SEED, offset=plan.local_offset)
         return plan, b, x, (lambda: plan.apply(b, out=x)), f"z-slab x{world}, all-to-all over xGMI ({exchange})"
+
+    def settle(run, ms):
+        """Untimed applies until `ms` of wall time have passed: the GPU leaves its idle clocks
+        (sclk reads ~100 MHz idle); without this a 20-step run measures ramp-up, ~10 % low
+        (profiles/r02a_settle.txt).  Returns (applies, ms spent)."""
+        if ms <= 0:
+            return 0, 0.0
+        t0 = time.perf_counter()
+        k = 0
+        while True:
+            for _ in range(4):
+                run()
+            k += 4
+            torch.cuda.synchronize()
+            el = (time.perf_counter() - t0) * 1e3
+            done = el >= ms
+            if world > 1:  # every rank must run the same applies (they hold collectives)
+                f = torch.tensor([1 if done else 0], dtype=torch.int32,
+                                 device=dev if dist.get_backend() == "nccl" else "cpu")
+                dist.all_reduce(f, op=dist.ReduceOp.MAX)
+                done = int(f.item()) == 1
+            if done:
+                return k, el
 
     def timed(run, steps, warmup):
         """W untimed + K timed applies between barriers and device syncs; max over ranks (s)."""
@@ -210,13 +283,14 @@ def main() -> int:
         return elapsed
 
     plan, b, x, run, parallelism = make(grid)
+    for _ in range(args.warmup):
+        run()
+    settle_n, settle_ms = settle(run, args.settle_ms)
     timed_region_ms = None
     live_applies = 0
     every = max(1, args.event_every)
     if world > 1 and not args.no_live_events and plan.exchange == "rccl":
         # the slab plan's phases (passes and RCCL exchanges) timed inside the timed applies
-        for _ in range(args.warmup):
-            run()
         plan.profile_begin((args.steps + every - 1) // every, every)
         elapsed = timed(run, args.steps, 0)
         timed_region_ms, live_applies = plan.profile_end()
@@ -224,14 +298,12 @@ def main() -> int:
         # per-launch HIP events recorded by the plan inside the timed applies themselves (on
         # the launch stream), in every EVERY-th apply: the roofline's kernel time comes from
         # the timed region, and the events' own cost (~3 us each) stays out of `value`
-        for _ in range(args.warmup):
-            run()
         plan.profile_begin((args.steps + every - 1) // every, every)
         elapsed = timed(run, args.steps, 0)
         timed_region_ms, n_rec = plan.profile_end()
         live_applies = n_rec
     else:
-        elapsed = timed(run, args.steps, args.warmup)
+        elapsed = timed(run, args.steps, 0)
     ms_per_step = elapsed / args.steps * 1e3
     value = args.steps / elapsed  # whole-job PCApply/s (one grid per step)
 
@@ -261,9 +333,18 @@ def main() -> int:
             roof["traffic_source"] = tsrc
         b_alg = 208 * N
         ach_apply = b_alg / (ms_per_step * 1e-3) / 1e9
-        roof_apply = {"B_alg_bytes": b_alg, "achieved": round(ach_apply, 1), "peak": HBM_PEAK_GBS,
+        moved = moved_bytes(passes_info, N)
+        ach_moved = moved / (ms_per_step * 1e-3) / 1e9
+        pmc = [load_traffic(grid, f"pass{i}_{p['axis']}_{p['mode']}")[0] for i, p in enumerate(passes_info)]
+        roof_apply = {"moved_bytes": moved, "moved_per_N": round(moved / N, 2),
+                      "achieved_moved": round(ach_moved, 1), "frac_moved": round(ach_moved / HBM_PEAK_GBS, 4),
+                      "pmc_bytes": int(sum(pmc)) if all(v is not None for v in pmc) else None,
+                      "B_alg_bytes": b_alg, "achieved": round(ach_apply, 1), "peak": HBM_PEAK_GBS,
                       "unit": "GB/s", "frac": round(ach_apply / HBM_PEAK_GBS, 4),
-                      "note": "SURVEY §8d: B_alg = 208 N (13 c128 sweeps) / wall time per apply"}
+                      "note": "frac_moved: the bytes this schedule's launches move (sum of their algorithmic "
+                              "bytes; pmc_bytes = the committed rocprofv3 FETCH+WRITE of the same launches) / wall "
+                              "time per apply.  frac: SURVEY §8d's convention, B_alg = 208 N (13 c128 sweeps), "
+                              "which a fused schedule can exceed"}
     else:
         # every rank takes part (the exchanges are collectives); rank 0 reports its own phases
         passes_info = plan.phases()
@@ -288,7 +369,10 @@ def main() -> int:
                 "mean_ms": round(ms[k], 5), "timing": timing_src}
         ex = [ms[i] for i, p in enumerate(passes_info) if p["kind"] == "all-to-all"]
         sent = 16 * nloc * (world - 1) / world  # bytes leaving this GPU per all-to-all
-        roof_apply = {"B_alg_bytes_per_gpu": 208 * nloc,
+        moved = sum(kernel_alg_bytes(p["mode"], nloc, p["n"]) for p in passes_info if p["kind"] == "pass")
+        roof_apply = {"moved_bytes_per_gpu": moved,
+                      "frac_moved": round(moved / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                      "B_alg_bytes_per_gpu": 208 * nloc,
                       "achieved_per_gpu": round(208 * nloc / (ms_per_step * 1e-3) / 1e9, 1),
                       "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": round(208 * nloc / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -337,11 +421,23 @@ def main() -> int:
         try:
             plan, b, x, run, par2 = make(sg)
             k = max(1, args.scaling_steps)
-            el = timed(run, k, max(1, min(args.warmup, 3)))
+            for _ in range(max(1, min(args.warmup, 3))):
+                run()
+            settle(run, min(args.settle_ms, 200.0))
+            el = timed(run, k, 0)
+            nl = sg[0] * sg[1] * sg[2] // world
+            if world == 1:
+                mv = moved_bytes(plan.passes(), nl)
+            else:
+                mv = sum(kernel_alg_bytes(p["mode"], nl, p["n"]) for p in plan.phases() if p["kind"] == "pass")
             scaling = {"grid": sg, "value": round(k / el, 4), "unit": "PCApply/s", "n_gpus": world,
                        "steps": k, "ms_per_step": round(el / k * 1e3, 4), "scaling": "strong",
                        "parallelism": par2,
-                       "B_alg_GBps_per_gpu": round(208 * (sg[0] * sg[1] * sg[2] / world) / (el / k) / 1e9, 1)}
+                       "moved_bytes_per_gpu": mv,
+                       "moved_GBps_per_gpu": round(mv / (el / k) / 1e9, 1),
+                       "frac_moved": round(mv / (el / k) / 1e9 / HBM_PEAK_GBS, 4),
+                       "B_alg_GBps_per_gpu": round(208 * nl / (el / k) / 1e9, 1),
+                       "note": "moved = the schedule's launches (exchanges excluded); B_alg = SURVEY's 208 N convention"}
         except Exception as e:  # report, never fake
             scaling = {"grid": sg, "error": str(e)}
             plan = None
@@ -370,6 +466,9 @@ def main() -> int:
             "data": f"synthetic: SplitMix64 U[-1,1) complex b, seed {SEED}, generated in HBM",
             "config": {"workload": f"{nx}x{ny}x{nz} c128 circulant PCApply, transport symbol lambda={LAM}",
                        "grid": grid, "global_batch": 1, "parallelism": parallelism},
+            "exchange": exchange_used[0],
+            "settle": {"ms": round(settle_ms, 1), "applies": settle_n,
+                       "note": "untimed applies after the W warm-up steps, before the timed region"},
             "roofline": roof,
             "roofline_apply": roof_apply,
             "cpu_baseline": cpu,

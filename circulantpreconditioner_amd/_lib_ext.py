@@ -93,6 +93,8 @@ def declare(L) -> None:
         "cfp_dist_get_unique_id": ([ctypes.c_char_p], c_int),
         "cfp_dist_unique_id_bytes": ([], c_int),
         "cfp_slab_layout": ([i64, i64, i64, c_int, c_int, P(i64)], c_int),
+        "cfp_slab_num_steps": ([i64, i64, i64, c_int, c_int, P(c_int)], c_int),
+        "cfp_slab_step_info": ([i64, i64, i64, c_int, c_int, c_int, P(i64), P(ctypes.c_double)], c_int),
         "cfp_dist_plan_create": ([P(vp), i64, i64, i64, c_int, c_int, ctypes.c_char_p, c_int], c_int),
         "cfp_dist_plan_destroy": ([vp], c_int),
         "cfp_dist_plan_create_external": ([P(vp), i64, i64, i64, c_int, c_int, c_int], c_int),
@@ -142,6 +144,9 @@ def declare(L) -> None:
         "MatCreateFFT": ([c_int, i64, P(i64), cs, P(vp)], c_int),
         "MatCreateFFTHIP": ([c_int, i64, P(i64), P(vp)], c_int),
         "MatFFTHIPGetPlan": ([vp, P(vp)], c_int),
+        "MatFFTHIPGetSolveCounts": ([vp, P(i64), P(i64)], c_int),
+        "PetscObjectStateGet": ([vp, P(i64)], c_int),
+        "PetscObjectGetId": ([vp, P(i64)], c_int),
         "MatCreateVecsFFTW": ([vp, P(vp), P(vp), P(vp)], c_int),
         "MatGetSize": ([vp, P(i64), P(i64)], c_int),
         "MatMult": ([vp, vp, vp], c_int),

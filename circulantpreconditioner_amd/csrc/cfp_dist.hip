@@ -216,6 +216,34 @@ extern "C" int cfp_slab_layout(int64_t nx, int64_t ny, int64_t nz, int P, int r,
   return CFP_SUCCESS;
 }
 
+extern "C" int cfp_slab_num_steps(int64_t nx, int64_t ny, int64_t nz, int P, int r, int* nsteps) {
+  if (!nsteps) return set_error(CFP_ERR_ARG_NULL, "nsteps is NULL");
+  SlabLayout L;
+  int rc = make_layout(nx, ny, nz, P, r, &L);
+  if (rc) return rc;
+  *nsteps = (int)slab_steps(L).size();
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_slab_step_info(int64_t nx, int64_t ny, int64_t nz, int P, int r, int i, int64_t* desc,
+                                  double* scale) {
+  if (!desc || !scale) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  SlabLayout L;
+  int rc = make_layout(nx, ny, nz, P, r, &L);
+  if (rc) return rc;
+  const std::vector<Step> st = slab_steps(L);
+  if (i < 0 || i >= (int)st.size()) return set_error(CFP_ERR_ARG_OUTOFRANGE, "step index");
+  const Step& s = st[(size_t)i];
+  const PassDesc& p = s.pass;
+  const int64_t v[18] = {s.exchange ? 1 : 0, s.src, s.dst, s.exchange ? -1 : s.axis, s.exchange ? 0 : p.n,
+                         s.exchange ? -1 : p.mode, s.exchange ? 0 : p.ncols, s.exchange ? 0 : p.inner_n,
+                         p.in.inner_stride, p.in.outer_stride, p.in.pt_stride, p.in.seg_len, p.in.seg_stride,
+                         p.out.inner_stride, p.out.outer_stride, p.out.pt_stride, p.out.seg_len, p.out.seg_stride};
+  std::memcpy(desc, v, sizeof(v));
+  *scale = s.exchange ? 1.0 : p.scale;
+  return CFP_SUCCESS;
+}
+
 extern "C" int cfp_dist_unique_id_bytes(void) { return (int)sizeof(ncclUniqueId); }
 
 extern "C" int cfp_dist_get_unique_id(char* id_out) {

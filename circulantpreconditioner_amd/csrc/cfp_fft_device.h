@@ -24,7 +24,6 @@ enum : int {
   F_OCC4 = 128,     // ask the compiler for 4 waves per SIMD (<= 128 VGPRs)
   F_SYM_LDS = 256,  // fused pass: stage the per-point symbol table in LDS next to the twiddles
   F_OCC8 = 512,     // ask the compiler for 8 waves per SIMD (<= 64 VGPRs)
-  F_NO_MEM = 1024,  // experiment only (3-sweep P2): register fills for loads, no stores; output invalid
 };
 __host__ __device__ constexpr int waves_req(int flags, int mode) {
   return mode == PASS_FUSED_WAVE ? 1 : ((flags & F_OCC8) ? 8 : ((flags & F_OCC4) ? 4 : 1));

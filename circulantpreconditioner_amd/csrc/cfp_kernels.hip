@@ -555,12 +555,7 @@ static hipError_t launch_generic(const PassDesc& p, const cd* in, cd* out, const
   g.ncols = p.ncols;
   int fac[CFP_MR_MAXF];
   g.nst = p.n == 1 ? 0 : factorize(p.n, fac);
-  static const int mr_points = [] {  // CFP_MR_POINTS_OVERRIDE: experiment knob (tools/), not a setting
-    const char* e = getenv("CFP_MR_POINTS_OVERRIDE");
-    const int v = e ? atoi(e) : 0;
-    return v >= 64 && v <= CFP_MR_MAXPTS ? v : CFP_MR_POINTS;
-  }();
-  int G = mr_points / p.n;
+  int G = CFP_MR_POINTS / p.n;  // points per block (block-size sweep: DESIGN.md, mixed-radix pass)
   if (G < 1) G = 1;
   if (G > 64) G = 64;
   if (!row) {  // power of two for the shift split

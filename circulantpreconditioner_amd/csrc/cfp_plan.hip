@@ -132,6 +132,7 @@ struct cfp_plan_s {
   std::vector<cd> sym1d[3];  // separable: lambda_d * c_d_hat (host copies)
   i64 chunk_planes = 0;      // > 0: chunked x/y schedule (see apply_steps)
   int schedule = CFP_SCHEDULE_AUTO;
+  TPShape tp_shape;          // 3-sweep kernel shape (cfp_plan_set_three_pass_shape)
   bool external_x = false;  // x transformed by the caller (real plan): y/z passes only, no 1/N
   // long axes (n > 4096): four-step split n = n1 n2, both <= 4096 (0: a short axis).  Their
   // spectrum stays in position order p = m1 + n1 m2 for frequency m = m2 + n2 m1.
@@ -357,7 +358,7 @@ int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStr
       a.axsym = p->axsym;
       a.scale = q.scale ? invN : 1.0;
       if (ev) HIPCHK(hipEventRecord((*ev)[i], s));
-      hipError_t e = launch_three_pass(q.tp, tn, q.from_b ? b : x, x, a, s);
+      hipError_t e = launch_three_pass(q.tp, tn, q.from_b ? b : x, x, a, p->tp_shape, s);
       if (e != hipSuccess) return hip_error(e, "3-sweep launch");
       continue;
     }
@@ -749,6 +750,15 @@ extern "C" int cfp_plan_set_schedule(cfp_plan_t p, int schedule) {
     std::vector<cd> s[3] = {p->sym1d[0], p->sym1d[1], p->sym1d[2]};
     return upload_separable(p, s);
   }
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_plan_set_three_pass_shape(cfp_plan_t p, int n1, int mid) {
+  if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
+  if (!three_pass_shape_valid(n1, mid))
+    return set_error(CFP_ERR_ARG_OUTOFRANGE, "3-sweep shape n1=%d mid=%d is not one of the built shapes", n1, mid);
+  p->tp_shape.n1 = n1;
+  p->tp_shape.mid = mid;
   return CFP_SUCCESS;
 }
 

@@ -11,8 +11,17 @@ struct TPArgs {
   double scale;      // P3 only: 1/N
 };
 
+// kernel shape at 256^3 (cfp_plan_set_three_pass_shape); zeros = the measured default
+enum { TP_MID_DEFAULT = 0, TP_MID_LANE64 = 1, TP_MID_LANE32 = 2 };
+struct TPShape {
+  int n1 = 0;   // y split ny = n1 * n2: 0 (default 32), 32 or 64
+  int mid = 0;  // TP_MID_*
+};
+
 bool three_pass_supported(const i64 n[3]);
+bool three_pass_shape_valid(int n1, int mid);
 // stage 0: P1 (in -> out), 1: P2 (out in place), 2: P3 (in -> out)
-hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, hipStream_t s);
+hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, TPShape shape,
+                             hipStream_t s);
 
 }  // namespace cfp

@@ -19,13 +19,6 @@
 // N1 x 2.1 KB: one per CU at N1 = 64, two at N1 = 32.  P2 holds T columns (T = 64: one
 // 1024-thread workgroup per CU; T = 32: two of 512); its global runs are T/N2 x 16 bytes.
 //
-// Phase desynchronisation ("stagger"): a kernel whose workgroups all start together and do
-// identical work keeps every CU in the same phase -- all load, then all compute (HBM idle),
-// then all store.  With one or two workgroups per CU nothing else hides that.  Every other
-// persistent workgroup can therefore start `stagger` ticks of the 100 MHz real-time counter
-// late, so half the CUs compute while the other half stream.
-#include <cstdlib>
-
 #include "cfp_fft_device.h"
 #include "cfp_three_pass.h"
 
@@ -77,12 +70,6 @@ __device__ __forceinline__ int brev(int j) {
   return N2 == 4 ? ((j & 1) << 1) | (j >> 1) : ((j & 1) << 2) | (j & 2) | (j >> 2);
 }
 
-// every other workgroup waits `ticks` of the 100 MHz counter (bounded: the counter only grows)
-__device__ __forceinline__ void stagger_start(int ticks) {
-  if (ticks <= 0 || !(blockIdx.x & 1)) return;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)ticks) __builtin_amdgcn_s_sleep(4);
-}
 }  // namespace
 
 // Persistent: a workgroup walks units blockIdx.x, + gridDim.x, ...  Prefetching the next unit
@@ -90,7 +77,7 @@ __device__ __forceinline__ void stagger_start(int ticks) {
 // spill (profiles/r01_schedule_sweep.txt).
 template <bool INV, int FLAGS, int N1, int TN>
 __global__ void __launch_bounds__(N1 * (TN / 16)) __attribute__((amdgpu_waves_per_eu(4)))
-k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits, int stagger) {
+k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
   constexpr int N2 = TN / N1, TR = TN / 16, NT = N1 * TR, TY = N1 / 16;
   constexpr int RS = TN + TN / 16;  // padded row stride of the row-mode LDS layout
   constexpr int F = FLAGS | F_SPLIT_LDS | F_LDS_SYNC;
@@ -107,7 +94,6 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits, int stagger) {
     asm volatile("" : "+v"(i));
     return i;
   };
-  stagger_start(stagger);
   for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
     // unit u = (z, y2): rows y2 + N2 y1 of plane z
     cd v[16];
@@ -160,7 +146,7 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits, int stagger) {
 // Barriers wait for LDS only, so one unit's stores drain while the next unit loads.
 template <int FLAGS, int T, int N2, int TN>
 __global__ void __launch_bounds__(T * (TN / 16)) __attribute__((amdgpu_waves_per_eu(4)))
-k_tp_mid(cd* data, TPArgs a, int nunits, int stagger) {
+k_tp_mid(cd* data, TPArgs a, int nunits) {
   constexpr int N1 = TN / N2, TZ = TN / 16, NT = T * TZ, XT = T / N2, NXT = TN / XT;
   constexpr int F = FLAGS | F_SPLIT_LDS | F_LDS_SYNC;
   static_assert(N2 == 4 || N2 == 8, "the y2 DFT runs across 4 or 8 lanes");
@@ -190,17 +176,13 @@ k_tp_mid(cd* data, TPArgs a, int nunits, int stagger) {
     q.w8 = a.tw[(TN / 8) * (q.y2 & 3)];
     return q;
   };
-  stagger_start(stagger);
   for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
     cd v[16];
     {
       const Col q = column(u);
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
-        if constexpr (FLAGS & F_NO_MEM)  // compute-only timing: values the compiler cannot fold
-          v[m] = make_cd((double)(q.xk + m), (double)(q.y2 - m));
-        else
-          v[m] = gload<FLAGS>(q.col + zs * TZ * m);
+        v[m] = gload<FLAGS>(q.col + zs * TZ * m);
       }
 #pragma unroll
       for (int m = 0; m < 16; ++m) {  // the lane DFT in two sweeps over the slots: fewer live temporaries
@@ -244,13 +226,7 @@ k_tp_mid(cd* data, TPArgs a, int nunits, int stagger) {
         v[m] = cmul(v[m], q.w);
       }
 #pragma unroll
-      for (int m = 0; m < 16; ++m) {
-        if constexpr (FLAGS & F_NO_MEM) {  // keep the FFTs live without writing the grid
-          if (v[m].x == 1.25e300) gstore<0>(q.col + zs * TZ * m, v[m]);
-        } else {
-          gstore<FLAGS>(q.col + zs * TZ * m, cconj(v[m]));
-        }
-      }
+      for (int m = 0; m < 16; ++m) gstore<FLAGS>(q.col + zs * TZ * m, cconj(v[m]));
     }
     lds_barrier();  // the next unit's first exchange overwrites LDS
   }
@@ -271,71 +247,60 @@ static int cu_count() {
   return cus;
 }
 
-static int env_int(const char* k, int d) {
-  const char* e = getenv(k);
-  return e ? atoi(e) : d;
-}
-
-// persistent grid (per_cu workgroups per CU), or one unit per workgroup (all)
-static unsigned grid_of(int units, int per_cu, bool all) {
-  const int g = all ? units : per_cu * cu_count();
+// persistent grid: per_cu workgroups per CU, at most one per unit
+static unsigned grid_of(int units, int per_cu) {
+  const int g = per_cu * cu_count();
   return (unsigned)(units < g ? units : g);
 }
 
 template <int N1, int TN, int PER_CU>
-static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s, int stag, bool all) {
+static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
   constexpr int units = TN * (TN / N1);  // z-planes x y2
-  const unsigned g = grid_of(units, PER_CU, all);
+  const unsigned g = grid_of(units, PER_CU);
   if (stage == 0)
-    hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units,
-                       stag);
+    hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units);
   else
-    hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units,
-                       stag);
+    hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units);
 }
 
-template <int T, int N2, int TN, int PER_CU, int FLAGS = 0>
-static void launch_mid(cd* data, const TPArgs& a, hipStream_t s, int stag, bool all) {
+template <int T, int N2, int TN, int PER_CU>
+static void launch_mid(cd* data, const TPArgs& a, hipStream_t s) {
   constexpr int units = (TN / (T / N2)) * (TN / N2);  // x-tiles x k1
-  hipLaunchKernelGGL((k_tp_mid<FLAGS, T, N2, TN>), dim3(grid_of(units, PER_CU, all)), dim3(T * (TN / 16)), 0, s,
-                     data, a, units, stag);
+  hipLaunchKernelGGL((k_tp_mid<0, T, N2, TN>), dim3(grid_of(units, PER_CU)), dim3(T * (TN / 16)), 0, s, data, a,
+                     units);
 }
 
-hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
+bool three_pass_shape_valid(int n1, int mid) {
+  return (n1 == 0 || n1 == 32 || n1 == 64) && (mid >= 0 && mid <= TP_MID_LANE32);
+}
+
+hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, TPShape shape,
+                             hipStream_t s) {
   if (n == 128) {
     // 128^3: N1 = 32 x N2 = 4; P1/P3 256 threads and 35 KiB of LDS (4 per CU), P2 64 columns =
     // 16 x 4 y2 (256-byte runs), 512 threads and 66 KiB (2 per CU)
-    if (stage == 1) launch_mid<64, 4, 128, 2>(out, a, s, 0, false);
-    else launch_rows<32, 128, 4>(stage, in, out, a, s, 0, false);
+    if (stage == 1) launch_mid<64, 4, 128, 2>(out, a, s);
+    else launch_rows<32, 128, 4>(stage, in, out, a, s);
     return hipGetLastError();
   }
-  // 256^3.  Experiment knobs, read per launch (tools/gpu_tp_stagger.sh, test_three_pass_variants):
-  // the y split N1, P2's tile width T, the start stagger in 100 MHz ticks, one unit per workgroup.
-  // Defaults = the measured best (profiles/r01i_three_pass_sweep.txt): N1 = 32, T = 64,
-  // persistent, no stagger.
-  const int n1 = env_int("CFP_TP_N1", 32) == 64 ? 64 : 32;
-  const int tmid = env_int("CFP_TP_MID_T", 64) == 32 ? 32 : 64;
-  const int stag = env_int("CFP_TP_STAGGER", 0);
-  const bool all = env_int("CFP_TP_GRID_ALL", 0) != 0;
+  // 256^3.  Default shape = the measured best (profiles/r01i_three_pass_sweep.txt): N1 = 32,
+  // P2 tiles of 64 columns (8 x times 8 y2, 128-byte runs), persistent grids.  The other shapes
+  // are selected per plan (cfp_plan_set_three_pass_shape) for tests and measurements.
+  const int n1 = shape.n1 == 64 ? 64 : 32;
+  const bool t32 = shape.mid == TP_MID_LANE32;
   if (stage == 1) {
     if (n1 == 64) {
-      if (tmid == 64) launch_mid<64, 4, 256, 1>(out, a, s, stag, all);
-      else launch_mid<32, 4, 256, 2>(out, a, s, stag, all);
-    } else if (tmid == 64) {
-      // load/store policy of the default shape (experiment knob: F_NT_LD = 16, F_NT_ST = 32)
-      const int fl = env_int("CFP_TP_MID_FLAGS", 0);
-      if (fl == F_NT_LD) launch_mid<64, 8, 256, 1, F_NT_LD>(out, a, s, stag, all);
-      else if (fl == F_NT_ST) launch_mid<64, 8, 256, 1, F_NT_ST>(out, a, s, stag, all);
-      else if (fl == (F_NT_LD | F_NT_ST)) launch_mid<64, 8, 256, 1, F_NT_LD | F_NT_ST>(out, a, s, stag, all);
-      else if (fl == F_NO_MEM) launch_mid<64, 8, 256, 1, F_NO_MEM>(out, a, s, stag, all);  // timing only
-      else launch_mid<64, 8, 256, 1>(out, a, s, stag, all);
+      if (t32) launch_mid<32, 4, 256, 2>(out, a, s);
+      else launch_mid<64, 4, 256, 1>(out, a, s);
+    } else if (t32) {
+      launch_mid<32, 8, 256, 2>(out, a, s);
     } else {
-      launch_mid<32, 8, 256, 2>(out, a, s, stag, all);
+      launch_mid<64, 8, 256, 1>(out, a, s);
     }
   } else if (n1 == 64) {
-    launch_rows<64, 256, 1>(stage, in, out, a, s, stag, all);
+    launch_rows<64, 256, 1>(stage, in, out, a, s);
   } else {
-    launch_rows<32, 256, 2>(stage, in, out, a, s, stag, all);
+    launch_rows<32, 256, 2>(stage, in, out, a, s);
   }
   return hipGetLastError();
 }

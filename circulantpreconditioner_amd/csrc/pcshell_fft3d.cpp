@@ -7,16 +7,16 @@
 //
 // The FFT matrix is a MATSHELL whose context is a cfp plan: MatMult = unnormalised forward
 // 3-D DFT, MatMultTranspose = backward (the MATFFTW semantics the reference relies on).
-// solve_3D runs the fused 5-launch apply; when the Diag vector is the one setupFFTPrec3D
-// materialised from the plan's own symbol (and nobody has written to it since), the apply
-// evaluates that symbol in registers instead of streaming Diag from HBM.
+// solve_3D divides by the Diag it is given (src/FftLinearSolver_3D.c:174).  When that Diag is
+// the one setupFFTPrec3D materialised from the plan's own symbol -- same object id, the
+// object state recorded after the write (PetscObjectStateGet: every write access bumps it),
+// and the plan's symbol unchanged since -- the apply evaluates the symbol in registers
+// instead of streaming Diag from HBM; anything else takes the explicit-Diag apply.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
 #include <complex>
 #include <cstring>
-#include <map>
-#include <mutex>
 
 #include "../../include/circulant_fft.h"
 #include "../../include/pcshell_fft3d.h"
@@ -33,17 +33,14 @@ struct FFTShell {
   PetscInt dims[3] = {1, 1, 1};  // n_x, n_y, n_z
   bool has_lam = false;
   double lam[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t sym_gen = 0;  // bumped whenever the plan's symbol changes
+  // the Diag setupFFTPrec3D materialised from the symbol of generation diag_gen: its object id
+  // and its state right after that write (0 id: none)
+  PetscObjectId diag_id = 0;
+  PetscObjectState diag_state = 0;
+  uint64_t diag_gen = 0;
+  PetscInt solves_own = 0, solves_diag = 0;  // solve_3D calls per path (MatFFTHIPGetSolveCounts)
 };
-
-// Diag vectors materialised from a plan's symbol: Vec -> (plan, snapshot of the device array
-// pointer).  Any write access through VecGetArray*/VecHIPGetArray* invalidates it through
-// the explicit `touch` below; a conservative check also compares a checksum-free tag.
-struct DiagTag {
-  cfp_plan_t plan;
-  const void* devptr;
-};
-std::mutex g_mu;
-std::map<Vec, DiagTag> g_diag;
 
 PetscErrorCode fft_shell(Mat A, FFTShell** out) {
   void* ctx = nullptr;
@@ -79,11 +76,6 @@ PetscErrorCode fft_mult_transpose(Mat A, Vec x, Vec y) { return fft_mult_impl(A,
 PetscErrorCode fft_destroy(Mat A) {
   FFTShell* s;
   PetscCall(fft_shell(A, &s));
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    for (auto it = g_diag.begin(); it != g_diag.end();)
-      it = it->second.plan == s->plan ? g_diag.erase(it) : std::next(it);
-  }
   cfp_plan_destroy(s->plan);
   s->magic = 0;
   delete s;
@@ -103,6 +95,19 @@ PetscErrorCode ensure_transport_symbol(FFTShell* s, const double lam[6]) {
   CFPCALL(cfp_plan_set_symbol_transport(s->plan, lam));
   std::memcpy(s->lam, lam, sizeof(s->lam));
   s->has_lam = true;
+  ++s->sym_gen;
+  return PETSC_SUCCESS;
+}
+
+// Diag holds exactly the plan's current symbol (materialised by setupFFTPrec3D, untouched since)
+PetscErrorCode diag_is_own_symbol(FFTShell* s, Vec Diag, bool* own) {
+  *own = false;
+  if (!s->diag_id || s->diag_gen != s->sym_gen) return PETSC_SUCCESS;
+  PetscObjectId id;
+  PetscObjectState st;
+  PetscCall(PetscObjectGetId((PetscObject)Diag, &id));
+  PetscCall(PetscObjectStateGet((PetscObject)Diag, &st));
+  *own = id == s->diag_id && st == s->diag_state;
   return PETSC_SUCCESS;
 }
 
@@ -112,6 +117,16 @@ PetscErrorCode ensure_transport_symbol(FFTShell* s, const double lam[6]) {
 extern "C" PetscErrorCode MatCreateFFTHIP(MPI_Comm comm, PetscInt ndim, const PetscInt dims[], Mat* A) {
   PetscCheck(ndim >= 1 && ndim <= 3, PETSC_COMM_SELF, PETSC_ERR_ARG_OUTOFRANGE, "ndim must be 1, 2 or 3");
   PetscCheck(dims && A, PETSC_COMM_SELF, PETSC_ERR_ARG_NULL, "NULL argument");
+#ifdef CFP_WITH_PETSC
+  // one rank per FFT matrix: the local size is the global size.  Several ranks use the slab
+  // plan (include/circulant_fft_dist.h) instead.
+  PetscMPIInt nranks = 1;
+  PetscCallMPI(MPI_Comm_size(comm, &nranks));
+  PetscCheck(nranks == 1, comm, PETSC_ERR_SUP,
+             "MatCreateFFTHIP: the communicator has more than one rank; use cfp_dist_plan_* (z slabs) instead");
+#else
+  (void)comm;  // the stand-in PETSc is single-process by construction
+#endif
   FFTShell* s = new FFTShell;
   // dims are row-major {n_z, n_y, n_x} (src/PCSHELLFft_3D.cxx:34): last = fastest = x
   for (PetscInt d = 0; d < ndim; ++d) s->dims[d] = dims[ndim - 1 - d];
@@ -134,6 +149,14 @@ extern "C" PetscErrorCode MatFFTHIPGetPlan(Mat A, cfp_plan_t* plan) {
   FFTShell* s;
   PetscCall(fft_shell(A, &s));
   *plan = s->plan;
+  return PETSC_SUCCESS;
+}
+
+extern "C" PetscErrorCode MatFFTHIPGetSolveCounts(Mat A, PetscInt* own_symbol, PetscInt* explicit_diag) {
+  FFTShell* s;
+  PetscCall(fft_shell(A, &s));
+  if (own_symbol) *own_symbol = s->solves_own;
+  if (explicit_diag) *explicit_diag = s->solves_diag;
   return PETSC_SUCCESS;
 }
 
@@ -170,14 +193,10 @@ extern "C" PetscErrorCode build_diag_mat_vec_3D(Vec Diag, Vec cx, Vec cy, Vec cz
   lam6(lx, ly, lz, lam);
   int rc = cfp_build_diag_3d(d.ptr(), a.ptr(), b.ptr(), c.ptr(), nx, ny, nz, lam, nullptr);
   if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
-  PetscCall(d.put());
+  PetscCall(d.put());  // a write access: Diag's state moves on, so no plan treats it as its own symbol
   PetscCall(c.put());
   PetscCall(b.put());
   PetscCall(a.put());
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    g_diag.erase(Diag);
-  }
   CFPCALL(rc);
   PetscFunctionReturn(PETSC_SUCCESS);
 }
@@ -194,16 +213,12 @@ extern "C" PetscErrorCode solve_3D(Mat FFT_MAT, Vec X, Vec Diag, Vec b, Vec b_ha
   PetscCall(check_size(X, N, "solve_3D: X has the wrong size"));
   PetscCall(check_size(b, N, "solve_3D: b has the wrong size"));
   PetscCall(check_size(Diag, N, "solve_3D: Diag has the wrong size"));
-  DevIn bin, din;
-  PetscCall(din.get(Diag, N));
-  // the plan's own symbol, if Diag was materialised from it and is unchanged
+  // the plan's own symbol, if Diag was materialised from it and nothing has written to it since
   bool own = false;
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    auto it = g_diag.find(Diag);
-    own = it != g_diag.end() && it->second.plan == s->plan && it->second.devptr == (const void*)din.ptr() &&
-          din.mt != PETSC_MEMTYPE_HOST;
-  }
+  PetscCall(diag_is_own_symbol(s, Diag, &own));
+  ++(own ? s->solves_own : s->solves_diag);
+  DevIn bin, din;
+  if (!own) PetscCall(din.get(Diag, N));
   int rc;
   if (b == X) {
     // in-place direct solve (PetscFft3DTransportSolver(ctx, Un, Un)): read-write access
@@ -234,7 +249,7 @@ extern "C" PetscErrorCode solve_3D(Mat FFT_MAT, Vec X, Vec Diag, Vec b, Vec b_ha
     PetscCall(xout.put());
     PetscCall(bin.put());
   }
-  PetscCall(din.put());
+  if (!own) PetscCall(din.put());
   CFPCALL(rc);
   PetscFunctionReturn(PETSC_SUCCESS);
 }
@@ -363,13 +378,12 @@ extern "C" PetscErrorCode setupFFTPrec3D(PC pc) {
   PetscCall(d.get(ctx->Diag, N));
   int rc = cfp_plan_get_diag(s->plan, d.ptr(), nullptr);
   if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
-  const void* devptr = d.tmp ? nullptr : (const void*)d.arr;
   PetscCall(d.put());
   CFPCALL(rc);
-  if (devptr) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    g_diag[ctx->Diag] = DiagTag{s->plan, devptr};
-  }
+  // remember which object and state hold the symbol (solve_3D's register-symbol fast path)
+  PetscCall(PetscObjectGetId((PetscObject)ctx->Diag, &s->diag_id));
+  PetscCall(PetscObjectStateGet((PetscObject)ctx->Diag, &s->diag_state));
+  s->diag_gen = s->sym_gen;
   ctx->plan = s->plan;
   PetscFunctionReturn(PETSC_SUCCESS);
 }
@@ -380,10 +394,6 @@ extern "C" PetscErrorCode destroyFFTPrec3D(PC pc) {
   FFTPrecTransportContext* ctx = nullptr;
   PetscCall(PCShellGetContext(pc, &ctx));
   if (!ctx) PetscFunctionReturn(PETSC_SUCCESS);
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    g_diag.erase(ctx->Diag);
-  }
   PetscCall(VecDestroy(&ctx->Diag));
   PetscCall(VecDestroy(&ctx->b_cartesien));
   PetscCall(VecDestroy(&ctx->b_hat));

@@ -7,6 +7,8 @@
 // compiled out when building against a real PETSc (-DCFP_WITH_PETSC).
 #ifndef CFP_WITH_PETSC
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <sys/time.h>
 
 #include <cmath>
@@ -63,7 +65,12 @@ struct _p_Vec {
   bool own_d = false, own_h = false;
   int mask = MASK_NONE;
   int device = 0;
+  PetscObjectId id = 0;
+  PetscObjectState state = 0;  // bumped by every write access (PetscObjectStateGet)
 };
+
+static std::atomic<int64_t> g_object_ids{0};
+static inline void touch(Vec v) { ++v->state; }
 
 static PetscErrorCode vcheck(Vec v, const char* f) {
   if (!v || v->magic != kVecMagic) return PetscErrorSet(PETSC_ERR_ARG_NULL, f, "invalid Vec");
@@ -104,6 +111,7 @@ static PetscErrorCode vec_new(PetscInt n, bool hip, const PetscScalar* devarr, V
   if (!out) return ERR(PETSC_ERR_ARG_NULL, "NULL output");
   if (n < 0) return ERR(PETSC_ERR_ARG_OUTOFRANGE, "negative size");
   Vec v = new _p_Vec;
+  v->id = ++g_object_ids;
   v->n = n;
   v->hip = hip;
   if (hip) {
@@ -152,6 +160,20 @@ extern "C" PetscErrorCode VecDestroy(Vec* pv) {
   *pv = nullptr;
   return PETSC_SUCCESS;
 }
+extern "C" PetscErrorCode PetscObjectStateGet(PetscObject obj, PetscObjectState* state) {
+  Vec v = (Vec)obj;
+  if (!v || v->magic != kVecMagic) return ERR(PETSC_ERR_ARG_WRONG, "PetscObjectStateGet: Vec objects only");
+  if (!state) return ERR(PETSC_ERR_ARG_NULL, "NULL output");
+  *state = v->state;
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode PetscObjectGetId(PetscObject obj, PetscObjectId* id) {
+  Vec v = (Vec)obj;
+  if (!v || v->magic != kVecMagic) return ERR(PETSC_ERR_ARG_WRONG, "PetscObjectGetId: Vec objects only");
+  if (!id) return ERR(PETSC_ERR_ARG_NULL, "NULL output");
+  *id = v->id;
+  return PETSC_SUCCESS;
+}
 extern "C" PetscErrorCode VecGetType(Vec v, VecType* t) {
   VCHK(v);
   *t = v->hip ? VECSEQHIP : VECSEQ;
@@ -175,6 +197,7 @@ extern "C" PetscErrorCode VecGetArray(Vec v, PetscScalar** a) {
 extern "C" PetscErrorCode VecRestoreArray(Vec v, PetscScalar** a) {
   VCHK(v);
   v->mask = MASK_CPU;
+  touch(v);
   if (a) *a = nullptr;
   return PETSC_SUCCESS;
 }
@@ -217,6 +240,7 @@ extern "C" PetscErrorCode VecHIPGetArray(Vec v, PetscScalar** a) {
 extern "C" PetscErrorCode VecHIPRestoreArray(Vec v, PetscScalar** a) {
   VCHK(v);
   v->mask = MASK_GPU;
+  touch(v);
   if (a) *a = nullptr;
   return PETSC_SUCCESS;
 }
@@ -287,6 +311,7 @@ static PetscErrorCode dev_read(Vec v, const cd** p) {
 static PetscErrorCode dev_rw(Vec v, cd** p) {
   PetscCall(sync_to_device(v));
   v->mask = MASK_GPU;
+  touch(v);
   *p = v->d;
   return PETSC_SUCCESS;
 }
@@ -298,6 +323,7 @@ static PetscErrorCode host_read(Vec v, const cd** p) {
 static PetscErrorCode host_rw(Vec v, cd** p) {
   PetscCall(sync_to_host(v));
   v->mask = MASK_CPU;
+  touch(v);
   *p = v->h;
   return PETSC_SUCCESS;
 }
@@ -305,6 +331,7 @@ static PetscErrorCode host_rw(Vec v, cd** p) {
 
 extern "C" PetscErrorCode VecSet(Vec v, PetscScalar a) {
   VCHK(v);
+  touch(v);
   if (v->hip) {
     v->mask = MASK_GPU;
     HIPK(cfp::blas_set(v->d, tocd(a), v->n, g_stream));
@@ -347,6 +374,7 @@ extern "C" PetscErrorCode VecCopy(Vec x, Vec y) {
   VCHK(x); VCHK(y);
   PetscCall(same_size(x, y));
   if (x == y) return PETSC_SUCCESS;
+  touch(y);
   if (y->hip) {
     cd* yd;
     if (x->hip) {

@@ -12,6 +12,7 @@ contiguous elements [r N/P, (r+1) N/P) -- PETSc's PETSC_DECIDE Vec layout.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 from typing import Sequence
 
@@ -30,13 +31,37 @@ def slab_layout(dims: Sequence[int], nranks: int, rank: int) -> dict:
     return dict(zip(keys, list(out)))
 
 
+STEP_KEYS = ("kind", "src", "dst", "axis", "n", "mode", "ncols", "inner_n",
+             "in_inner", "in_outer", "in_pt", "in_seg_len", "in_seg_stride",
+             "out_inner", "out_outer", "out_pt", "out_seg_len", "out_seg_stride")
+
+
+def slab_steps(dims: Sequence[int], nranks: int, rank: int) -> list:
+    """Host-only: the steps rank `rank`'s cfp_dist_plan_apply runs, as dicts (STEP_KEYS + scale);
+    buffers 0 = b, 1 = x, 2 = work (include/circulant_fft_dist.h)."""
+    nx, ny, nz = (int(d) for d in dims)
+    n = ctypes.c_int()
+    check(lib().cfp_slab_num_steps(nx, ny, nz, int(nranks), int(rank), ctypes.byref(n)))
+    out = []
+    for i in range(n.value):
+        desc = (ctypes.c_int64 * 18)()
+        sc = ctypes.c_double()
+        check(lib().cfp_slab_step_info(nx, ny, nz, int(nranks), int(rank), i, desc, ctypes.byref(sc)))
+        d = dict(zip(STEP_KEYS, list(desc)))
+        d["scale"] = sc.value
+        out.append(d)
+    return out
+
+
 class SlabPlan:
     """This rank's part of a slab-distributed plan.
 
     exchange="rccl": the library's own RCCL communicator does both all-to-alls inside
     cfp_dist_plan_apply.  exchange="torch": the library runs the three kernel segments and
     the two all-to-alls go through torch.distributed.all_to_all_single on `group` (RCCL
-    under torch's "nccl" backend).  Both are one stream-ordered apply.
+    under torch's "nccl" backend; under "gloo" the chunks are staged through host memory,
+    which lets several ranks share one GPU in tests).  Both are one stream-ordered apply:
+    the exchanges are issued on the apply's stream.
     """
 
     def __init__(self, dims: Sequence[int], rank: int, world: int, device: int | None = None, group=None,
@@ -82,20 +107,32 @@ class SlabPlan:
         check(lib().cfp_dist_plan_set_symbol_transport(self._h, _lam6(lam)))
         return self
 
+    def _all_to_all(self, dst: torch.Tensor, src: torch.Tensor) -> None:
+        import torch.distributed as dist
+        if dist.get_backend(self.group) == "gloo":  # gloo exchanges host tensors only
+            h = torch.empty(dst.numel(), dtype=dst.dtype)
+            dist.all_to_all_single(h, src.cpu(), group=self.group)
+            dst.copy_(h)
+        else:
+            dist.all_to_all_single(dst, src, group=self.group)
+
     def apply(self, b: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
         if out is None:
             out = torch.empty_like(b)
         n = self.local_size
-        bp, xp, sh = _dev_ptr(b, n, "b"), _dev_ptr(out, n, "out"), _stream_handle(stream)
+        bp, xp = _dev_ptr(b, n, "b", self.device), _dev_ptr(out, n, "out", self.device)
+        sh = _stream_handle(stream)
         if self.exchange == "rccl":
             check(lib().cfp_dist_plan_apply(self._h, bp, xp, sh))
             return out
-        import torch.distributed as dist
-        check(lib().cfp_dist_plan_run_segment(self._h, 0, bp, xp, sh))
-        dist.all_to_all_single(out, self.work, group=self.group)  # work chunks -> x chunks
-        check(lib().cfp_dist_plan_run_segment(self._h, 1, bp, xp, sh))
-        dist.all_to_all_single(self.work, out, group=self.group)  # x chunks -> work chunks
-        check(lib().cfp_dist_plan_run_segment(self._h, 2, bp, xp, sh))
+        # the segments run on `stream`; the collectives are ordered on torch's current stream,
+        # so make that the same stream for the whole apply
+        with (torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()):
+            check(lib().cfp_dist_plan_run_segment(self._h, 0, bp, xp, sh))
+            self._all_to_all(out, self.work)  # work chunks -> x chunks
+            check(lib().cfp_dist_plan_run_segment(self._h, 1, bp, xp, sh))
+            self._all_to_all(self.work, out)  # x chunks -> work chunks
+            check(lib().cfp_dist_plan_run_segment(self._h, 2, bp, xp, sh))
         return out
 
     def phases(self) -> list:
@@ -138,15 +175,15 @@ class SlabPlan:
         check(lib().cfp_dist_plan_num_phases(self._h, ctypes.byref(nph)))
         ms = (ctypes.c_double * nph.value)()
         n = self.local_size
-        check(lib().cfp_dist_plan_time_phases(self._h, _dev_ptr(b, n, "b"), _dev_ptr(x, n, "x"), int(iters), ms,
+        check(lib().cfp_dist_plan_time_phases(self._h, _dev_ptr(b, n, "b", self.device),
+                                              _dev_ptr(x, n, "x", self.device), int(iters), ms,
                                               _stream_handle(stream)))
         return list(ms)
 
     def _time_phases_torch(self, b, x, iters):
-        import torch.distributed as dist
         ph = self.phases()
         n = self.local_size
-        bp, xp = _dev_ptr(b, n, "b"), _dev_ptr(x, n, "x")
+        bp, xp = _dev_ptr(b, n, "b", self.device), _dev_ptr(x, n, "x", self.device)
         sh = _stream_handle()
         acc = [0.0] * len(ph)
         for _ in range(iters):
@@ -156,9 +193,9 @@ class SlabPlan:
                 ev[i].record()
                 if p["kind"] == "all-to-all":
                     if seg == 1:
-                        dist.all_to_all_single(x, self.work, group=self.group)
+                        self._all_to_all(x, self.work)
                     else:
-                        dist.all_to_all_single(self.work, x, group=self.group)
+                        self._all_to_all(self.work, x)
                     continue
                 # run this single pass: segments hold consecutive passes, so time per segment
                 # once (the first pass of a segment carries the whole segment)
@@ -215,8 +252,10 @@ class SlabGroup:
     def apply(self, bs: Sequence[torch.Tensor], xs: Sequence[torch.Tensor] | None = None) -> list:
         if xs is None:
             xs = [torch.empty_like(b) for b in bs]
-        bp = (ctypes.c_void_p * self.P)(*[_dev_ptr(b, L["local_size"], "b") for b, L in zip(bs, self.layouts)])
-        xp = (ctypes.c_void_p * self.P)(*[_dev_ptr(x, L["local_size"], "x") for x, L in zip(xs, self.layouts)])
+        bp = (ctypes.c_void_p * self.P)(*[_dev_ptr(b, L["local_size"], "b", d)
+                                          for b, L, d in zip(bs, self.layouts, self.devices)])
+        xp = (ctypes.c_void_p * self.P)(*[_dev_ptr(x, L["local_size"], "x", d)
+                                          for x, L, d in zip(xs, self.layouts, self.devices)])
         check(lib().cfp_group_apply(self._h, bp, xp))
         return list(xs)
 

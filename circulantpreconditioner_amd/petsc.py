@@ -121,6 +121,30 @@ class Vec:
         PetscCall(lib().VecAXPY(self.h, _S(alpha), x.h))
         return self
 
+    def scale(self, alpha) -> "Vec":
+        PetscCall(lib().VecScale(self.h, _S(alpha)))
+        return self
+
+    def state(self) -> int:
+        """PetscObjectStateGet: increases on every write access."""
+        v = ctypes.c_int64()
+        PetscCall(lib().PetscObjectStateGet(self.h, ctypes.byref(v)))
+        return v.value
+
+    def hip_array(self):
+        """Context manager: VecHIPGetArray / VecHIPRestoreArray (read-write device pointer)."""
+        vec = self
+
+        class _Arr:
+            def __enter__(self_):
+                self_.p = ctypes.c_void_p()
+                PetscCall(lib().VecHIPGetArray(vec.h, ctypes.byref(self_.p)))
+                return self_.p.value
+
+            def __exit__(self_, *exc):
+                PetscCall(lib().VecHIPRestoreArray(vec.h, ctypes.byref(self_.p)))
+        return _Arr()
+
     def destroy(self) -> None:
         if self.owned and self.h is not None and self.h.value:
             PetscCall(lib().VecDestroy(ctypes.byref(self.h)))
@@ -165,6 +189,12 @@ class Mat:
         refs = [ctypes.byref(hs[i]) if i < nvec else None for i in range(3)]
         PetscCall(lib().MatCreateVecsFFTW(self.h, *refs))
         return [Vec(hs[i]) for i in range(nvec)]
+
+    def solve_counts(self) -> tuple:
+        """(solve_3D calls that used the plan's own symbol, calls that streamed the given Diag)."""
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        PetscCall(lib().MatFFTHIPGetSolveCounts(self.h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
 
     def mult(self, x: Vec, y: Vec) -> Vec:
         PetscCall(lib().MatMult(self.h, x.h, y.h))

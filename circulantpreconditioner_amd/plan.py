@@ -25,13 +25,15 @@ def _stream_handle(stream=None) -> int:
     return int(stream.cuda_stream)
 
 
-def _dev_ptr(t: torch.Tensor, n: int, name: str) -> int:
+def _dev_ptr(t: torch.Tensor, n: int, name: str, device: int | None = None) -> int:
     if not isinstance(t, torch.Tensor):
         raise TypeError(f"{name} must be a torch.Tensor")
     if t.dtype != torch.complex128:
         raise TypeError(f"{name} must be complex128, got {t.dtype}")
     if not t.is_cuda:
         raise ValueError(f"{name} must be a device (HIP) tensor")
+    if device is not None and t.device.index != device:
+        raise ValueError(f"{name} is on cuda:{t.device.index}, the plan on cuda:{device}")
     if not t.is_contiguous():
         raise ValueError(f"{name} must be contiguous")
     if t.numel() != n:
@@ -87,7 +89,7 @@ class CirculantPlan:
     def set_diag(self, diag) -> "CirculantPlan":
         """General symbol: explicit Diag vector (device tensor or host array)."""
         if isinstance(diag, torch.Tensor) and diag.is_cuda:
-            check(lib().cfp_plan_set_diag(self._h, _dev_ptr(diag, self.N, "diag"), 1))
+            check(lib().cfp_plan_set_diag(self._h, _dev_ptr(diag, self.N, "diag", self.device), 1))
             torch.cuda.synchronize(diag.device)
         else:
             d = np.ascontiguousarray(np.asarray(diag.cpu() if isinstance(diag, torch.Tensor) else diag,
@@ -105,20 +107,21 @@ class CirculantPlan:
     # ---------------------------------------------------------------- apply
     def apply(self, b: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
         """x = (1/N) IDFT(DFT(b) ./ Diag).  `out` may be `b` (in place)."""
-        bp = _dev_ptr(b, self.N, "b")
+        bp = _dev_ptr(b, self.N, "b", self.device)
         if out is None:
             out = torch.empty_like(b)
-        xp = _dev_ptr(out, self.N, "out")
+        xp = _dev_ptr(out, self.N, "out", self.device)
         check(lib().cfp_plan_apply(self._h, bp, xp, _stream_handle(stream)))
         return out
 
     def apply_with_diag(self, diag: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
                         stream=None) -> torch.Tensor:
-        bp = _dev_ptr(b, self.N, "b")
-        dp = _dev_ptr(diag, self.N, "diag")
+        bp = _dev_ptr(b, self.N, "b", self.device)
+        dp = _dev_ptr(diag, self.N, "diag", self.device)
         if out is None:
             out = torch.empty_like(b)
-        check(lib().cfp_plan_apply_with_diag(self._h, dp, bp, _dev_ptr(out, self.N, "out"), _stream_handle(stream)))
+        check(lib().cfp_plan_apply_with_diag(self._h, dp, bp, _dev_ptr(out, self.N, "out", self.device),
+                                             _stream_handle(stream)))
         return out
 
     def apply_host(self, b) -> np.ndarray:
@@ -134,7 +137,8 @@ class CirculantPlan:
         """Unnormalised 3-D DFT (MatMult on MATFFTW)."""
         if out is None:
             out = torch.empty_like(x)
-        check(lib().cfp_plan_forward(self._h, _dev_ptr(x, self.N, "x"), _dev_ptr(out, self.N, "out"),
+        check(lib().cfp_plan_forward(self._h, _dev_ptr(x, self.N, "x", self.device),
+                                     _dev_ptr(out, self.N, "out", self.device),
                                      _stream_handle(stream)))
         return out
 
@@ -142,7 +146,8 @@ class CirculantPlan:
         """Unnormalised inverse 3-D DFT (MatMultTranspose on MATFFTW)."""
         if out is None:
             out = torch.empty_like(x)
-        check(lib().cfp_plan_backward(self._h, _dev_ptr(x, self.N, "x"), _dev_ptr(out, self.N, "out"),
+        check(lib().cfp_plan_backward(self._h, _dev_ptr(x, self.N, "x", self.device),
+                                      _dev_ptr(out, self.N, "out", self.device),
                                       _stream_handle(stream)))
         return out
 
@@ -157,6 +162,15 @@ class CirculantPlan:
         """'auto'/'five' (z fused), 'five_y' (y fused) or 'three' (256^3: 3 sweeps)."""
         v = self.SCHEDULES[schedule] if isinstance(schedule, str) else int(schedule)
         check(lib().cfp_plan_set_schedule(self._h, v))
+        return self
+
+    TP_MIDS = {"default": 0, "lane64": 1, "lane32": 2}
+
+    def set_three_pass_shape(self, n1: int = 0, mid: str | int = "default") -> "CirculantPlan":
+        """Kernel shape of the 256^3 3-sweep schedule (tests / measurements): the y split n1
+        (0 = default, 32 or 64) and the middle kernel ('default', 'lane64', 'lane32')."""
+        m = self.TP_MIDS[mid] if isinstance(mid, str) else int(mid)
+        check(lib().cfp_plan_set_three_pass_shape(self._h, int(n1), m))
         return self
 
     # ---------------------------------------------------------------- introspection
@@ -177,7 +191,8 @@ class CirculantPlan:
         """Mean device time (ms) of each launch of one apply, HIP events on `stream`."""
         npass = len(self.passes())
         ms = (ctypes.c_double * npass)()
-        check(lib().cfp_plan_time_passes(self._h, _dev_ptr(b, self.N, "b"), _dev_ptr(x, self.N, "x"), int(iters),
+        check(lib().cfp_plan_time_passes(self._h, _dev_ptr(b, self.N, "b", self.device),
+                                         _dev_ptr(x, self.N, "x", self.device), int(iters),
                                          ms, _stream_handle(stream)))
         return list(ms)
 

@@ -35,6 +35,22 @@ typedef struct cfp_group_s *cfp_group_t;
  * nranks} */
 int cfp_slab_layout(int64_t nx, int64_t ny, int64_t nz, int nranks, int rank, int64_t *out);
 
+/* Host-only description of rank `rank`'s apply: the steps cfp_dist_plan_apply runs, in order
+ * (no GPU needed; tests replay them on the CPU across processes).  desc[0..18):
+ *   [0] kind (0 axis pass, 1 all-to-all), [1] source buffer, [2] destination buffer
+ *   (0 = b, 1 = x, 2 = the plan's work buffer), [3] axis, [4] length n, [5] mode (PASS_*: 0 fwd,
+ *   1 inv, 2 fused with the separable symbol), [6] columns, [7] inner_n, then for the source and
+ *   the destination side: inner_stride, outer_stride, pt_stride, seg_len, seg_stride.
+ * Element (column g, point k) of a side sits at
+ *   (g % inner_n) * inner_stride + (g / inner_n) * outer_stride
+ *   + (k / seg_len) * seg_stride + (k % seg_len) * pt_stride.
+ * *scale = the factor the step applies to its output (1/N on the last pass).  An all-to-all
+ * sends chunk q (elements [q*chunk, (q+1)*chunk)) of the source to rank q, which stores it as
+ * chunk `rank` of its destination. */
+int cfp_slab_num_steps(int64_t nx, int64_t ny, int64_t nz, int nranks, int rank, int *nsteps);
+int cfp_slab_step_info(int64_t nx, int64_t ny, int64_t nz, int nranks, int rank, int step, int64_t *desc,
+                       double *scale);
+
 /* RCCL unique id (128 bytes): created on rank 0, broadcast by the caller, passed to every rank */
 int cfp_dist_unique_id_bytes(void);
 int cfp_dist_get_unique_id(char *id_out);

@@ -100,6 +100,10 @@ PetscErrorCode build_transport_col(Vec c, PetscInt size);
 PetscErrorCode MatCreateFFTHIP(MPI_Comm comm, PetscInt ndim, const PetscInt dims[], Mat *A);
 /* the plan behind an FFT matrix made by MatCreateFFT/MatCreateFFTHIP (NULL otherwise) */
 PetscErrorCode MatFFTHIPGetPlan(Mat A, cfp_plan_t *plan);
+/* How many solve_3D calls on this FFT matrix divided by the plan's own symbol in registers
+ * (Diag untouched since setupFFTPrec3D materialised it: same object id and PetscObjectState,
+ * symbol unchanged) and how many streamed the Diag they were given. */
+PetscErrorCode MatFFTHIPGetSolveCounts(Mat A, PetscInt *own_symbol, PetscInt *explicit_diag);
 PetscErrorCode FFTPrecTransportContextCreate(FFTPrecTransportContext **ctx);
 PetscErrorCode FFTPrecTransportContextDestroy(FFTPrecTransportContext **ctx);
 

@@ -64,6 +64,9 @@ typedef enum { PETSC_MEMTYPE_HOST = 0, PETSC_MEMTYPE_DEVICE = 1, PETSC_MEMTYPE_H
 typedef enum { NORM_1 = 0, NORM_2 = 1, NORM_FROBENIUS = 2, NORM_INFINITY = 3 } NormType;
 typedef enum { INSERT_VALUES = 1, ADD_VALUES = 2 } InsertMode;
 
+typedef struct _p_PetscObject *PetscObject;
+typedef int64_t PetscObjectState;
+typedef int64_t PetscObjectId;
 typedef struct _p_Vec *Vec;
 typedef struct _p_Mat *Mat;
 typedef struct _p_PC *PC;
@@ -99,6 +102,12 @@ const char *PetscErrorLastMessage(void);
     if (!(cond)) return PetscErrorSet((code), __func__, (msg)); \
   } while (0)
 PetscErrorCode PetscTime(PetscLogDouble *t);
+
+/* Object state and id, as PETSc's: the state of a Vec increases on every write access (write
+ * Get/RestoreArray, VecSet, VecScale, VecCopy into it, ...); the id is unique per object.
+ * Vecs only in this stand-in (PETSC_ERR_ARG_WRONG for other objects). */
+PetscErrorCode PetscObjectStateGet(PetscObject obj, PetscObjectState *state);
+PetscErrorCode PetscObjectGetId(PetscObject obj, PetscObjectId *id);
 
 /* ---- Vec */
 PetscErrorCode VecCreateSeq(MPI_Comm comm, PetscInt n, Vec *v);

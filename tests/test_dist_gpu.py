@@ -1,7 +1,16 @@
-"""GPU parity of the slab-decomposed pass schedule (cfp_dist.hip) on one device: the
-single-process group executor runs P slabs with device copies as the exchange, so the
-split y layouts, the per-rank symbol and the chunk bookkeeping are checked on real
-kernels.  The RCCL executor shares the schedule; it is exercised by bench.py --gpus N."""
+"""GPU parity of the slab-decomposed pass schedule (cfp_dist.hip) on one device.
+
+* The single-process group executor runs P slabs with device copies as the exchange, so the
+  split y layouts, the per-rank symbol and the chunk bookkeeping are checked on real
+  kernels, up to BASELINE config 5's grid (512^3 in 8 slabs).
+* SlabPlan runs in fresh child processes, one per rank, sharing cuda:0: each rank runs the
+  library's kernel segments and the two all-to-alls go through torch.distributed (gloo,
+  staged through host memory), so the per-rank plan is exercised across processes.
+* The RCCL executor with world = 1; with more ranks it is exercised by bench.py --gpus N.
+"""
+import os
+import socket
+
 import numpy as np
 import pytest
 import torch
@@ -26,6 +35,83 @@ def test_group_vs_oracle(dims, P, oracle):
         xs = g.apply(g.scatter(full))
         got = torch.cat([x.cpu() for x in xs]).numpy()
     assert oracle.rel_l2(got, ref) < TOL
+
+
+def test_group_config5_512_in_8_slabs(oracle):
+    """BASELINE config 5's decomposition (512^3, z slabs of 64 planes, 8 ranks) on one device,
+    against the oracle's full-grid solve."""
+    from circulantpreconditioner_amd.distributed import SlabGroup
+    dims, P, lam = (512, 512, 512), 8, (0.6, 0.15, 0.02)
+    N = int(np.prod(dims))
+    b = oracle.c_fill_uniform(N, 512)
+    ref = oracle.c_solve_3d(oracle.c_build_diag_transport(dims, lam), b, dims)
+    with SlabGroup(dims, P) as g:
+        g.set_transport_symbol(lam)
+        bs = g.scatter(torch.from_numpy(b).cuda())
+        xs = g.apply(bs)
+        got = torch.cat([x.cpu() for x in xs]).numpy()
+        del bs, xs
+    assert oracle.rel_l2(got, ref) < TOL
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _slab_rank(rank, world, port, dims, lam, seed, q):
+    """One rank of a SlabPlan in its own process (exchange through torch.distributed / gloo)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import circulantpreconditioner_amd as cp
+        from circulantpreconditioner_amd.distributed import SlabPlan
+        torch.cuda.set_device(0)
+        plan = SlabPlan(dims, rank=rank, world=world, device=0, exchange="torch")
+        plan.set_transport_symbol(lam)
+        b = torch.empty(plan.local_size, dtype=torch.complex128, device="cuda:0")
+        cp.fill_uniform(b, seed, offset=plan.local_offset)
+        x = plan.apply(b)
+        t = b.clone()
+        plan.apply(t, out=t)  # in place, as the direct solver's (Un, Un)
+        torch.cuda.synchronize()
+        q.put((rank, plan.local_offset, x.cpu().numpy(), bool(torch.equal(t, x))))
+        plan.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dims,world", [((64, 32, 16), 2), ((128, 128, 128), 2), ((64, 64, 64), 4),
+                                        ((100, 20, 10), 2)])
+def test_slab_plan_processes_vs_oracle(dims, world, oracle):
+    """`world` fresh processes, one SlabPlan rank each, on cuda:0; gathered x vs the oracle."""
+    import torch.multiprocessing as mp
+    lam, seed = (0.6, 0.15 - 0.1j, 0.02), 29
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_slab_rank, args=(r, world, port, dims, lam, seed, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        parts = [q.get(timeout=240) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    N = int(np.prod(dims))
+    x = np.empty(N, dtype=np.complex128)
+    for _, off, part, inplace_ok in parts:
+        assert inplace_ok
+        x[off:off + part.size] = part
+    b = oracle.c_fill_uniform(N, seed)
+    ref = oracle.c_solve_3d(oracle.c_build_diag_transport(dims, lam), b, dims)
+    assert oracle.rel_l2(x, ref) < TOL
 
 
 def test_group_inplace(oracle):

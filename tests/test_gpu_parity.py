@@ -416,6 +416,9 @@ def test_three_pass_schedule_rules(cp):
         b = torch.ones_like(d)
         x = plan.apply_with_diag(d, b)  # explicit Diag: the 5-pass fused-Diag path serves it
         assert torch.allclose(x, b / 2.0)
+        for n1, mid in ((16, 0), (32, 9), (-1, 0), (0, -1)):  # only built shapes; nothing from the environment
+            with pytest.raises(cp.CirculantError):
+                plan.set_three_pass_shape(n1, mid)
     with cp.CirculantPlan((64, 64, 64)) as plan:
         with pytest.raises(cp.CirculantError):
             plan.set_schedule("three")
@@ -449,17 +452,13 @@ def tp_case(oracle):
     return n, lam, b, oracle.c_solve_3d(oracle.c_build_diag_transport(n, lam), b, n)
 
 
-@pytest.mark.parametrize("n1,t,stagger,grid_all", [(64, 64, 0, 0), (64, 32, 1000, 0), (32, 64, 0, 1),
-                                                   (32, 32, 1000, 0)])
-def test_three_pass_variants(cp, tp_case, monkeypatch, n1, t, stagger, grid_all):
-    """Both y splits (64 x 4 with a 4-lane y2 DFT, 32 x 8 with an 8-lane one), both P2 tile
-    widths, the start stagger and one unit per workgroup (cfp_three_pass.hip's CFP_TP_* knobs,
-    read per launch)."""
-    for k, v in (("CFP_TP_N1", n1), ("CFP_TP_MID_T", t), ("CFP_TP_STAGGER", stagger), ("CFP_TP_GRID_ALL", grid_all)):
-        monkeypatch.setenv(k, str(v))
+@pytest.mark.parametrize("n1,mid", [(64, "lane64"), (64, "lane32"), (32, "lane64"), (32, "lane32"), (0, "default")])
+def test_three_pass_variants(cp, tp_case, n1, mid):
+    """Both y splits (64 x 4 with a 4-lane y2 DFT, 32 x 8 with an 8-lane one) and both P2 tile
+    widths, selected per plan through cfp_plan_set_three_pass_shape."""
     n, lam, b, ref = tp_case
     with cp.CirculantPlan(n) as plan:
-        plan.set_transport_symbol(lam).set_schedule("three")
+        plan.set_transport_symbol(lam).set_schedule("three").set_three_pass_shape(n1, mid)
         x = plan.apply(_dev(b))
         assert _rel(x, ref) < TOL
         t_ = _dev(b)
