@@ -161,6 +161,9 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--schedule", default="auto", choices=["auto", "five", "five_y", "three"],
                     help="apply schedule: 5 axis passes fused on z (auto) or y, or 3 sweeps (256^3)")
+    ap.add_argument("--tp-shape", default=None, metavar="N1,MID",
+                    help="3-sweep kernel shape (measurements): y split n1 (0/32/64) and middle kernel "
+                         "(default, lane64, lane32, swap64); default: the plan's")
     ap.add_argument("--chunk", type=int, default=None,
                     help="z-planes per chunk of the Infinity-Cache-resident x/y schedule (0 = off; default: plan's)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
@@ -219,6 +222,9 @@ def main() -> int:
             if args.chunk is not None:
                 plan.set_chunking(args.chunk)
             plan.set_schedule(args.schedule)
+            if args.tp_shape:
+                n1, mid = args.tp_shape.split(",")
+                plan.set_three_pass_shape(int(n1), mid)
             return plan, b, x, (lambda: plan.apply(b, out=x)), "single GPU"
         from circulantpreconditioner_amd.distributed import SlabPlan
 

@@ -9,10 +9,11 @@
 //
 //   P1  k_tp_rows<fwd>: one z-plane, rows y2 + N2 y1 (N1 rows, N1 x 4 KB): N1-point DFT down
 //       the rows (column mode, lanes = x), LDS transpose, 256-point DFT along each row
-//   P2  k_tp_mid: T/N2 x-columns x N2 rows y2 + N2 k1 x 256 z: twiddle W_256^{y2 k1}, N2-point
-//       DFT across N2 neighbouring lanes (radix-2 butterflies over DPP lane permutations,
-//       frequencies left bit-reversed), 256-point z DFT, divide by the separable symbol at
-//       (kx, k1 + N1 k2, kz), then the same transforms on the conjugate (inverse)
+//   P2  k_tp_mid_sw (default) / k_tp_mid: T/N2 x-columns x N2 rows y2 + N2 k1 x 256 z: twiddle
+//       W_256^{y2 k1}, N2-point DFT across lanes (k_tp_mid_sw: radix-2 stages on permlane
+//       register transposes; k_tp_mid: DPP lane permutations; frequencies left bit-reversed),
+//       256-point z DFT, divide by the separable symbol at (kx, k1 + N1 k2, kz), then the same
+//       transforms on the conjugate (inverse)
 //   P3  k_tp_rows<inv>: P1 on the conjugate, x 1/N
 //
 // P1/P3 workgroups are N1 x 16 threads x 16 points with a split-LDS exchange buffer of
@@ -232,6 +233,285 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// P2 with the y2 DFT on register transposes (k_tp_mid_sw).  A wave is one z-group tz and all
+// 64 columns c = x + XT * y2 of the tile (XT = 64 / N2), so the y2 bits are the top lane bits:
+// N2 = 8: y2 = lane bits 3..5; N2 = 4: lane bits 4..5.  A radix-2 stage over lane bit 5 / 4
+// transposes a register pair with v_permlane32_swap / v_permlane16_swap (lane bit <-> register
+// bit, 2 swaps per double) and then runs a plain butterfly on the pair: no per-lane selects, no
+// duplicated butterfly halves.  Lane bit 3 (N2 = 8 only) has no swap instruction: DPP row_ror:8
+// brings the partner's value, and one fma with a per-lane sign forms sum or difference.
+//
+// The y2 DFT commutes with the z DFT, so it runs between the z transform's first radix-16 stage
+// (per lane, over the 16 slots) and the LDS exchange; the exchange writes each value from its
+// transposed register straight to its (column, z) place, so the transposes are never undone.
+// Register r at lane L then holds slot s = (r & 12) | L5 | 2 L4 and y2 position
+// p = 4 r0 + 2 r1 + L3 (N2 = 8) or p = 2 r0 + r1 (N2 = 4).  Forward: DIF, natural order in,
+// bit-reversed frequencies out (the symbol index follows, as in k_tp_mid).  Inverse: DIT from
+// the bit-reversed order back to natural, same register map, so the second exchange lands in
+// the load layout.
+namespace {
+// (a, b) -> lanes with bit B clear: (a[L], a[L ^ 2^B]); set: (b[L ^ 2^B], b[L])
+template <int B>
+__device__ __forceinline__ void swap32(unsigned& a, unsigned& b) {
+  if constexpr (B == 5) {
+    const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+    a = r[0];
+    b = r[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+    a = r[0];
+    b = r[1];
+  }
+}
+template <int B>
+__device__ __forceinline__ void swap_d(double& a, double& b) {
+  unsigned long long ua = (unsigned long long)__double_as_longlong(a),
+                     ub = (unsigned long long)__double_as_longlong(b);
+  unsigned al = (unsigned)ua, ah = (unsigned)(ua >> 32), bl = (unsigned)ub, bh = (unsigned)(ub >> 32);
+  swap32<B>(al, bl);
+  swap32<B>(ah, bh);
+  a = __longlong_as_double((long long)(((unsigned long long)ah << 32) | al));
+  b = __longlong_as_double((long long)(((unsigned long long)bh << 32) | bl));
+}
+template <int B>
+__device__ __forceinline__ void swap_c(cd& a, cd& b) {
+  swap_d<B>(a.x, b.x);
+  swap_d<B>(a.y, b.y);
+}
+// partner across lane bit 3 (row_ror:8 inside each 16-lane row)
+__device__ __forceinline__ double ror8_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffll), 0x128, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0x128, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// radix-2 over lane bit 3 without twiddle: bit clear -> own + partner, set -> partner - own
+__device__ __forceinline__ cd bfly_l3(cd v, double sgn) {
+  return make_cd(fma(sgn, v.x, ror8_d(v.x)), fma(sgn, v.y, ror8_d(v.y)));
+}
+}  // namespace
+
+// DIF stage over register pairs (k, k + D) after a swap on lane bit B: a + b, (a - b) w
+// (TW = false: no twiddle)
+template <int B, int D, bool TW = true>
+__device__ __forceinline__ void dif_pairs(cd* v, cd w) {
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    if ((k & D) == 0) swap_c<B>(v[k], v[k + D]);
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    if ((k & D) == 0) {
+      const cd a = v[k], b = v[k + D];
+      v[k] = cadd(a, b);
+      v[k + D] = TW ? cmul(csub(a, b), w) : csub(a, b);
+    }
+}
+
+// PROBE != 0 only in tools/kexp (tp_probe.hip, built with CFP_KEXP): timing probes that drop a
+// part of the work (output invalid).  The product library instantiates PROBE = 0 only.
+enum { PR_NO_Y2 = 1, PR_NO_ZMATH = 2, PR_NO_XCHG = 4, PR_NO_LOAD = 8, PR_NO_STORE = 16 };
+template <int T, int N2, int TN, int PROBE = 0>
+__global__ void __launch_bounds__(T * (TN / 16)) __attribute__((amdgpu_waves_per_eu(4)))
+k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
+#ifndef CFP_KEXP
+  static_assert(PROBE == 0, "timing probes are built in tools/kexp only");
+#endif
+  static_assert(T == 64, "one wave = all 64 columns of a z group");
+  static_assert(N2 == 4 || N2 == 8, "y2 = the top 2 or 3 lane bits");
+  static_assert(TN == 256, "z = 16 x 16: radix-16 stage A in registers, one exchange, radix-16 stage B");
+  constexpr int N1 = TN / N2, TZ = TN / 16, NT = T * TZ, XT = T / N2, NXT = TN / XT;
+  constexpr int XB = ilog2(XT);  // lane bits of x
+  __shared__ __attribute__((aligned(16))) double lds[T * TN];  // split exchange
+  __shared__ cd tw_l[TN];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < TN; i += NT) tw_l[i] = a.tw[i];
+  __syncthreads();  // the y2 stages read tw_l before the first exchange barrier
+  const int c0 = tid & (T - 1), tz0 = tid / T;
+  const i64 zs = (i64)TN * TN;
+  const auto idx = [](int i) {
+    asm volatile("" : "+v"(i));
+    return i;
+  };
+  // this lane's first point and the twiddle W_TN^{y2 k1} (natural layout: x = c % XT, y2 = c / XT)
+  const auto col_ptr = [&](int u, int c, int tz) {
+    const int xt = u % NXT, k1 = u / NXT;
+    return data + xt * XT + (c & (XT - 1)) + (i64)TN * ((c >> XB) + N2 * k1) + zs * tz;
+  };
+  const auto tw_y = [&](int u, int c) { return a.tw[((c >> XB) * (u / NXT)) & (TN - 1)]; };
+  // split exchange from the transposed registers (first radix-16 stage done) to the column
+  // layout: v[t] = point tz + 16 t of column c
+  const auto exchange_t = [&](cd* v, bool first) {
+    if constexpr (PROBE & PR_NO_XCHG) return;
+    const int c = idx(c0), tz = idx(tz0);
+    const int l3 = N2 == 8 ? ((c >> 3) & 1) : 0, l4 = (c >> 4) & 1, l5 = (c >> 5) & 1;
+    const int wbase = (tz * 16 + l5 + 2 * l4) * T + (c & (XT - 1)) + XT * l3;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (!(first && h == 0)) lds_barrier();
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int p = N2 == 8 ? 4 * (r & 1) + 2 * ((r >> 1) & 1) : 2 * (r & 1) + ((r >> 1) & 1);
+        const int off = (r & 12) * T + XT * (N2 == 8 ? p & 6 : p);
+        lds[wbase + off] = h ? v[r].y : v[r].x;
+      }
+      lds_barrier();
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const double d = lds[(tz + TZ * t) * T + c];
+        if (h) v[t].y = d; else v[t].x = d;
+      }
+    }
+  };
+  // second radix-16 stage (Ns = 16): twiddles W_TN^{tz t}, then the in-register DFT
+  const auto stage_b = [&](cd* v) {
+    if constexpr (PROBE & PR_NO_ZMATH) return;
+    const int tz = idx(tz0);
+#pragma unroll
+    for (int t = 1; t < 16; ++t) v[t] = cmul(v[t], tw_l[tz * t]);
+    dft_reg<16>(v);
+  };
+  const auto lane_sign = [&]() {  // +1 where lane bit 3 is clear, -1 where set
+    const int c = idx(c0);
+    return (c & 8) ? -1.0 : 1.0;
+  };
+
+  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+    cd v[16];
+    if constexpr (PROBE & PR_NO_LOAD) {
+      const int c = idx(c0), tz = idx(tz0);
+#pragma unroll
+      for (int m = 0; m < 16; ++m) v[m] = make_cd(c + m, tz + u);
+    } else {
+      const int c = idx(c0), tz = idx(tz0);
+      const cd* src = col_ptr(u, c, tz);
+#pragma unroll
+      for (int m = 0; m < 16; ++m) v[m] = src[zs * TZ * m];
+    }
+    {
+      const int c = idx(c0);
+      const cd w = tw_y(u, c);
+#pragma unroll
+      for (int m = 0; m < 16; ++m) v[m] = cmul(v[m], w);
+    }
+    if constexpr (!(PROBE & PR_NO_ZMATH)) dft_reg<16>(v);  // z stage A (Ns = 1: no twiddles), per lane
+    // y2 DFT, DIF: natural positions in, bit-reversed frequencies out
+    if constexpr (PROBE & PR_NO_Y2) {
+    } else if constexpr (N2 == 8) {
+      {
+        const int c = idx(c0);
+        dif_pairs<5, 1>(v, tw_l[(TN / 8) * ((c >> 3) & 3)]);  // W_8^{y2 & 3}
+      }
+      {
+        const int c = idx(c0);
+        dif_pairs<4, 2>(v, tw_l[(TN / 4) * ((c >> 3) & 1)]);  // W_4^{y2 & 1}
+      }
+      const double s = lane_sign();
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = bfly_l3(v[r], s);
+    } else {
+      {
+        const int c = idx(c0);
+        dif_pairs<5, 1>(v, tw_l[(TN / 4) * ((c >> 4) & 1)]);  // W_4^{y2 & 1}
+      }
+      dif_pairs<4, 2, false>(v, make_cd(1.0, 0.0));
+    }
+    exchange_t(v, true);
+    stage_b(v);  // v[m]: kz = tz + 16 m; column c = x + XT p
+    {
+      const int c = idx(c0), tz = idx(tz0);
+      const int k1 = u / NXT, p = c >> XB;
+      const cd cs = a.colsym[(u % NXT) * XT + (c & (XT - 1)) + (i64)TN * (k1 + N1 * brev<N2>(p))];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const cd d = cadd(cadd(cs, a.axsym[tz + TZ * m]), make_cd(1.0, 0.0));
+        v[m] = (PROBE & PR_NO_ZMATH) ? cconj(v[m]) : cconj(cdiv_sym(v[m], d));
+      }
+    }
+    if constexpr (!(PROBE & PR_NO_ZMATH)) dft_reg<16>(v);  // inverse (on the conjugate): z stage A
+    // y2 DFT, DIT: bit-reversed positions in, natural out
+    if constexpr (PROBE & PR_NO_Y2) {
+    } else if constexpr (N2 == 8) {
+      {
+        const double s = lane_sign();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = bfly_l3(v[r], s);
+      }
+      {
+        const int c = idx(c0);
+        const cd w = tw_l[(TN / 4) * ((c >> 3) & 1)];  // W_4^{p & 1}, p bit 0 = lane bit 3
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if ((k & 2) == 0) swap_c<4>(v[k], v[k + 2]);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if ((k & 2) == 0) {
+            const cd x = v[k], y = cmul(v[k + 2], w);
+            v[k] = cadd(x, y);
+            v[k + 2] = csub(x, y);
+          }
+      }
+      {
+        // W_8^{p & 3}: p bit 0 = lane bit 3, p bit 1 = register bit 1 -> W_8^{l3} (x -i if r1)
+        const int c = idx(c0);
+        const cd w = tw_l[(TN / 8) * ((c >> 3) & 1)];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if ((k & 1) == 0) swap_c<5>(v[k], v[k + 1]);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if ((k & 1) == 0) {
+            cd y = cmul(v[k + 1], w);
+            if (k & 2) y = mul_mi(y);
+            const cd x = v[k];
+            v[k] = cadd(x, y);
+            v[k + 1] = csub(x, y);
+          }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if ((k & 2) == 0) swap_c<4>(v[k], v[k + 2]);
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if ((k & 2) == 0) {
+          const cd x = v[k], y = v[k + 2];
+          v[k] = cadd(x, y);
+          v[k + 2] = csub(x, y);
+        }
+      // W_4^{p & 1}, p bit 0 = register bit 1
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if ((k & 1) == 0) swap_c<5>(v[k], v[k + 1]);
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if ((k & 1) == 0) {
+          const cd y = (k & 2) ? mul_mi(v[k + 1]) : v[k + 1];
+          const cd x = v[k];
+          v[k] = cadd(x, y);
+          v[k + 1] = csub(x, y);
+        }
+    }
+    exchange_t(v, false);
+    stage_b(v);  // natural layout again: column c = x + XT y2, slot m = z
+    {
+      const int c = idx(c0), tz = idx(tz0);
+      const cd w = tw_y(u, c);
+      cd* dst = col_ptr(u, c, tz);
+      if constexpr (PROBE & PR_NO_STORE) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) acc += v[m].x * w.x + v[m].y;
+        if (acc == 1.2345e300) dst[0] = make_cd(acc, 0.0);  // keeps the work live, never true
+      } else {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) dst[zs * TZ * m] = cconj(cmul(v[m], w));
+      }
+    }
+    lds_barrier();  // the next unit's first exchange overwrites LDS
+  }
+}
+
 bool three_pass_supported(const i64 n[3]) {
   return n[0] == n[1] && n[1] == n[2] && (n[0] == 128 || n[0] == 256);
 }
@@ -270,8 +550,14 @@ static void launch_mid(cd* data, const TPArgs& a, hipStream_t s) {
                      units);
 }
 
+template <int N2, int TN>
+static void launch_mid_sw(cd* data, const TPArgs& a, hipStream_t s) {
+  constexpr int units = (TN / (64 / N2)) * (TN / N2);
+  hipLaunchKernelGGL((k_tp_mid_sw<64, N2, TN>), dim3(grid_of(units, 1)), dim3(64 * (TN / 16)), 0, s, data, a, units);
+}
+
 bool three_pass_shape_valid(int n1, int mid) {
-  return (n1 == 0 || n1 == 32 || n1 == 64) && (mid >= 0 && mid <= TP_MID_LANE32);
+  return (n1 == 0 || n1 == 32 || n1 == 64) && (mid >= 0 && mid <= TP_MID_SWAP64);
 }
 
 hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, TPShape shape,
@@ -283,13 +569,17 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
     else launch_rows<32, 128, 4>(stage, in, out, a, s);
     return hipGetLastError();
   }
-  // 256^3.  Default shape = the measured best (profiles/r01i_three_pass_sweep.txt): N1 = 32,
-  // P2 tiles of 64 columns (8 x times 8 y2, 128-byte runs), persistent grids.  The other shapes
-  // are selected per plan (cfp_plan_set_three_pass_shape) for tests and measurements.
+  // 256^3.  Default shape = the measured best: N1 = 32, P2 tiles of 64 columns (8 x times 8 y2,
+  // 128-byte runs) with the y2 DFT on permlane transposes (k_tp_mid_sw; r02: 138 vs 144 us for
+  // the DPP lane kernel in the apply chain, profiles/r02e_p2_ab.txt), persistent grids.  The
+  // other shapes are selected per plan (cfp_plan_set_three_pass_shape) for tests and measurements.
   const int n1 = shape.n1 == 64 ? 64 : 32;
   const bool t32 = shape.mid == TP_MID_LANE32;
   if (stage == 1) {
-    if (n1 == 64) {
+    if (shape.mid == TP_MID_SWAP64 || shape.mid == TP_MID_DEFAULT) {
+      if (n1 == 64) launch_mid_sw<4, 256>(out, a, s);
+      else launch_mid_sw<8, 256>(out, a, s);
+    } else if (n1 == 64) {
       if (t32) launch_mid<32, 4, 256, 2>(out, a, s);
       else launch_mid<64, 4, 256, 1>(out, a, s);
     } else if (t32) {

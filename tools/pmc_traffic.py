@@ -37,7 +37,7 @@ def pass_name(kname: str):
     t = re.search(r"k_tp_rows<(true|false)", kname)
     if t:
         return "pass2_xy_rows_inv" if t.group(1) == "true" else "pass0_xy_rows_fwd"
-    if "k_tp_mid<" in kname:
+    if re.search(r"k_tp_mid(_sw)?<", kname):
         return "pass1_yz_mid_fused"
     m = re.search(r"k_axis_fast<(\d+), (\d+), (\d+), (true|false), (\d+), (\d+)(?:, \d+)?>", kname)
     if not m:
