@@ -115,6 +115,8 @@ int cfp_plan_set_schedule(cfp_plan_t plan, int schedule);
 #define CFP_TP_MID_LANE64 1
 #define CFP_TP_MID_LANE32 2
 #define CFP_TP_MID_SWAP64 3
+#define CFP_TP_MID_SWAP64_PF 4 /* SWAP64 + LDS-DMA prefetch of half the next unit */
+#define CFP_TP_MID_SWAP64_PF2 5 /* ... + one more slot staged early in the spare LDS */
 int cfp_plan_set_three_pass_shape(cfp_plan_t plan, int n1, int mid);
 
 /* Introspection: number of kernel launches of one apply, and per-launch timing.
