@@ -321,9 +321,7 @@ enum { PR_NO_Y2 = 1, PR_NO_ZMATH = 2, PR_NO_XCHG = 4, PR_NO_LOAD = 8, PR_NO_STOR
 // drained early.
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
-// PF = 2 also stages slot 8 in the 16 KiB of LDS left over, issued as soon as the unit has read
-// its own copy, so that one flies during the whole transform.
-template <int T, int N2, int TN, int PROBE = 0, int PF = 0>
+template <int T, int N2, int TN, int PROBE = 0, bool PF = false>
 __global__ void __launch_bounds__(T * (TN / 16)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
 #ifndef CFP_KEXP
@@ -336,7 +334,6 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
   constexpr int XB = ilog2(XT);  // lane bits of x
   __shared__ __attribute__((aligned(16))) double lds[T * TN];  // split exchange
   __shared__ cd tw_l[TN];
-  __shared__ __attribute__((aligned(16))) double lds_e[PF == 2 ? NT * 2 : 2];  // one early slot per lane
   const int tid = threadIdx.x;
   for (int i = tid; i < TN; i += NT) tw_l[i] = a.tw[i];
   __syncthreads();  // the y2 stages read tw_l before the first exchange barrier
@@ -352,8 +349,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
     return data + xt * XT + (c & (XT - 1)) + (i64)TN * ((c >> XB) + N2 * k1) + zs * tz;
   };
   const auto tw_y = [&](int u, int c) { return tw_l[((c >> XB) * (u / NXT)) & (TN - 1)]; };
-  constexpr int NPF = PF ? 8 : 0;        // slots 0 .. NPF-1 come from the LDS prefetch (exchange buffer)
-  constexpr int NE = PF == 2 ? 1 : 0;     // slots NPF .. NPF+NE-1 from the early prefetch (lds_e)
+  constexpr int NPF = PF ? 8 : 0;  // slots 0 .. NPF-1 come from the LDS prefetch (exchange buffer)
   const int wv = __builtin_amdgcn_readfirstlane(tid / 64);
   const auto prefetch = [&](int u) {  // this wave's slots 0 .. NPF-1 of unit u -> LDS
     const int c = idx(c0), tz = idx(tz0);
@@ -363,17 +359,9 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
       __builtin_amdgcn_global_load_lds((glb_void_t*)(src + zs * TZ * m), (lds_void_t*)(lds + (wv * NPF + m) * 128),
                                        16, 0, 0);
   };
-  const auto prefetch_e = [&](int u) {  // slot NPF of unit u -> lds_e (this wave's 1 KiB)
-    const int c = idx(c0), tz = idx(tz0);
-    const cd* src = col_ptr(u, c, tz);
-    __builtin_amdgcn_global_load_lds((glb_void_t*)(src + zs * TZ * NPF), (lds_void_t*)(lds_e + wv * 128), 16, 0, 0);
-  };
   static_assert(!PF || 16 * NPF * 128 <= T * TN, "the prefetch fits the exchange buffer");
   if constexpr (PF) {
-    if ((int)blockIdx.x < nunits) {
-      prefetch(blockIdx.x);
-      if constexpr (NE) prefetch_e(blockIdx.x);
-    }
+    if ((int)blockIdx.x < nunits) prefetch(blockIdx.x);
   }
   // split exchange from the transposed registers (first radix-16 stage done) to the column
   // layout: v[t] = point tz + 16 t of column c
@@ -422,16 +410,11 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
       const int c = idx(c0), tz = idx(tz0);
       const cd* src = col_ptr(u, c, tz);
 #pragma unroll
-      for (int m = NPF + NE; m < 16; ++m) v[m] = src[zs * TZ * m];
+      for (int m = NPF; m < 16; ++m) v[m] = src[zs * TZ * m];
       if constexpr (PF) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA (and loads) landed
 #pragma unroll
         for (int m = 0; m < NPF; ++m) v[m] = fromv(*reinterpret_cast<const dv2*>(lds + (wv * NPF + m) * 128 + 2 * c));
-        if constexpr (NE) {
-          v[NPF] = fromv(*reinterpret_cast<const dv2*>(lds_e + wv * 128 + 2 * c));
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read before the next DMA overwrites it
-          if (u + (int)gridDim.x < nunits) prefetch_e(u + gridDim.x);
-        }
       }
     }
     {
@@ -600,7 +583,7 @@ static void launch_mid(cd* data, const TPArgs& a, hipStream_t s) {
                      units);
 }
 
-template <int N2, int TN, int PF = 0>
+template <int N2, int TN, bool PF = false>
 static void launch_mid_sw(cd* data, const TPArgs& a, hipStream_t s) {
   constexpr int units = (TN / (64 / N2)) * (TN / N2);
   hipLaunchKernelGGL((k_tp_mid_sw<64, N2, TN, 0, PF>), dim3(grid_of(units, 1)), dim3(64 * (TN / 16)), 0, s, data, a,
@@ -608,7 +591,7 @@ static void launch_mid_sw(cd* data, const TPArgs& a, hipStream_t s) {
 }
 
 bool three_pass_shape_valid(int n1, int mid) {
-  return (n1 == 0 || n1 == 32 || n1 == 64) && (mid >= 0 && mid <= TP_MID_SWAP64_PF2);
+  return (n1 == 0 || n1 == 32 || n1 == 64) && (mid >= 0 && mid <= TP_MID_SWAP64_PF);
 }
 
 hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, TPShape shape,
@@ -621,19 +604,17 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
     return hipGetLastError();
   }
   // 256^3.  Default shape = the measured best: N1 = 32, P2 tiles of 64 columns (8 x times 8 y2,
-  // 128-byte runs) with the y2 DFT on permlane transposes (k_tp_mid_sw; r02: 138 vs 144 us for
-  // the DPP lane kernel in the apply chain, profiles/r02e_p2_ab.txt), persistent grids.  The
+  // 128-byte runs) with the y2 DFT on permlane transposes and the LDS-DMA prefetch of half the
+  // next unit (k_tp_mid_sw<.., PF>; r02 A/B in the apply chain, profiles/r02e_p2_ab.txt: 138 us
+  // without the prefetch, 144 us for the DPP lane kernel, 128 us with it), persistent grids.  The
   // other shapes are selected per plan (cfp_plan_set_three_pass_shape) for tests and measurements.
   const int n1 = shape.n1 == 64 ? 64 : 32;
   const bool t32 = shape.mid == TP_MID_LANE32;
   if (stage == 1) {
-    if (shape.mid == TP_MID_SWAP64_PF) {
-      if (n1 == 64) launch_mid_sw<4, 256, 1>(out, a, s);
-      else launch_mid_sw<8, 256, 1>(out, a, s);
-    } else if (shape.mid == TP_MID_SWAP64_PF2) {
-      if (n1 == 64) launch_mid_sw<4, 256, 2>(out, a, s);
-      else launch_mid_sw<8, 256, 2>(out, a, s);
-    } else if (shape.mid == TP_MID_SWAP64 || shape.mid == TP_MID_DEFAULT) {
+    if (shape.mid == TP_MID_SWAP64_PF || shape.mid == TP_MID_DEFAULT) {
+      if (n1 == 64) launch_mid_sw<4, 256, true>(out, a, s);
+      else launch_mid_sw<8, 256, true>(out, a, s);
+    } else if (shape.mid == TP_MID_SWAP64) {
       if (n1 == 64) launch_mid_sw<4, 256>(out, a, s);
       else launch_mid_sw<8, 256>(out, a, s);
     } else if (n1 == 64) {

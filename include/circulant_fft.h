@@ -107,7 +107,7 @@ int cfp_plan_set_chunking(cfp_plan_t plan, int64_t chunk_planes);
 int cfp_plan_set_schedule(cfp_plan_t plan, int schedule);
 /* Kernel shape of the 3-sweep schedule at 256^3, for tests and measurements (0, 0 = the
  * measured default; the shape never changes the result beyond rounding).  n1: the y split
- * ny = n1 * (256 / n1), 0 (default), 32 or 64.  mid: the middle kernel, 0 (default = SWAP64),
+ * ny = n1 * (256 / n1), 0 (default), 32 or 64.  mid: the middle kernel, 0 (default = SWAP64_PF),
  * CFP_TP_MID_LANE64 (y2 DFT across lanes, 64-column tile), CFP_TP_MID_LANE32 (32-column tile) or
  * CFP_TP_MID_SWAP64 (y2 DFT on v_permlane32/16_swap register transposes, 64-column tile;
  * 256^3 only, 128^3 keeps its default).  Other values: CFP_ERR_ARG_OUTOFRANGE. */
@@ -116,7 +116,6 @@ int cfp_plan_set_schedule(cfp_plan_t plan, int schedule);
 #define CFP_TP_MID_LANE32 2
 #define CFP_TP_MID_SWAP64 3
 #define CFP_TP_MID_SWAP64_PF 4 /* SWAP64 + LDS-DMA prefetch of half the next unit */
-#define CFP_TP_MID_SWAP64_PF2 5 /* ... + one more slot staged early in the spare LDS */
 int cfp_plan_set_three_pass_shape(cfp_plan_t plan, int n1, int mid);
 
 /* Introspection: number of kernel launches of one apply, and per-launch timing.
