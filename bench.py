@@ -407,7 +407,10 @@ def main() -> int:
             real_variant = {"value": round(1e3 / rms, 3), "unit": "PCApply/s", "ms_per_apply": round(rms, 5),
                             "dtype": "f64 real b and x (r2c / half spectrum / c2r)",
                             "stage_ms": [round(v, 5) for v in rp.time_passes(br, xr, iters=10)],
-                            "stages": ["r2c rows", "half-spectrum y/z", "Nyquist y/z", "c2r rows"]}
+                            "schedule": "3 sweeps" if rp.three_sweep else "r2c + 3 half-spectrum passes + c2r",
+                            "stages": (["r2c rows + y1", "half-spectrum y2/z", "Nyquist y/z", "y1 inverse + c2r rows"]
+                                       if rp.three_sweep else
+                                       ["r2c rows", "half-spectrum y/z", "Nyquist y/z", "c2r rows"])}
             rp.close()
             del br, xr
         except Exception as e:  # unsupported grid or failure: report, never fake

@@ -54,6 +54,8 @@ def _declare(L) -> None:
         "cfp_rplan_apply": ([vp, vp, vp, vp], c_int),
         "cfp_rplan_num_passes": ([vp, P(c_int)], c_int),
         "cfp_rplan_time_passes": ([vp, vp, vp, c_int, P(ctypes.c_double), vp], c_int),
+        "cfp_rplan_set_schedule": ([vp, c_int], c_int),
+        "cfp_rplan_schedule": ([vp, P(c_int)], c_int),
         "cfp_plan_num_passes": ([vp, P(c_int)], c_int),
         "cfp_plan_pass_info": ([vp, c_int, P(c_int), P(c_int), P(i64), P(c_int), P(c_int)], c_int),
         "cfp_plan_time_passes": ([vp, dp, dp, c_int, dp, vp], c_int),

@@ -20,6 +20,7 @@
 #include "../../include/circulant_fft_real.h"
 #include "cfp_fft_device.h"
 #include "cfp_host.h"
+#include "cfp_three_pass.h"
 
 namespace cfp {
 
@@ -148,7 +149,14 @@ struct cfp_rplan_s {
   bool has_sym = false;
   hipStream_t side = nullptr;  // the Nyquist grid's passes overlap the half-spectrum passes
   hipEvent_t fork = nullptr, join = nullptr;
+  // 3-sweep schedule at 256^3 (cfp_three_pass.hip): separable symbol of the half spectrum
+  int schedule = CFP_RSCHEDULE_AUTO;
+  cd* colsym3 = nullptr;  // [kx + M ky], kx < M
+  cd* axsym3 = nullptr;   // [kz]
 };
+
+static bool three_ok(const cfp_rplan_s* p) { return p->n[0] == 256 && p->n[1] == 256 && p->n[2] == 256; }
+static bool use_three(const cfp_rplan_s* p) { return three_ok(p) && p->schedule != CFP_RSCHEDULE_FIVE; }
 
 namespace {
 struct RGuard {
@@ -170,14 +178,41 @@ void free_rplan(cfp_rplan_s* p) {
   if (p->H) hipFree(p->H);
   if (p->Q) hipFree(p->Q);
   if (p->twn) hipFree(p->twn);
+  if (p->colsym3) hipFree(p->colsym3);
+  if (p->axsym3) hipFree(p->axsym3);
   if (p->fork) hipEventDestroy(p->fork);
   if (p->join) hipEventDestroy(p->join);
   if (p->side) hipStreamDestroy(p->side);
   delete p;
 }
 
+// 3 sweeps at 256^3: P1r (r2c rows + y1, Nyquist column to Q) | P2 on the half spectrum |
+// P3r (y1 inverse + c2r rows).  The Nyquist column's own y/z plan runs in between; it cannot
+// overlap P2 (P2's workgroups fill every CU), so it simply follows P1r on the same stream.
+int run_real_three(cfp_rplan_s* p, const double* b, double* x, hipStream_t s, std::vector<hipEvent_t>* ev) {
+  TPArgs a;
+  a.tw = p->twn;  // W_256: nx = ny = nz = 256
+  a.colsym = p->colsym3;
+  a.axsym = p->axsym3;
+  a.scale = 2.0 / (double)(p->n[0] * p->n[1] * p->n[2]);
+  if (ev) HIPCHK(hipEventRecord((*ev)[0], s));
+  hipError_t e = launch_three_pass_real(0, b, p->H, p->Q, nullptr, a, s);
+  if (e != hipSuccess) return hip_error(e, "r2c rows + y1 pass");
+  if (ev) HIPCHK(hipEventRecord((*ev)[1], s));
+  e = launch_three_pass_real(1, nullptr, p->H, nullptr, nullptr, a, s);
+  if (e != hipSuccess) return hip_error(e, "half-spectrum y2/z pass");
+  if (ev) HIPCHK(hipEventRecord((*ev)[2], s));
+  CFPCHK(cfp_plan_apply(p->nyq, (const double*)p->Q, (double*)p->Q, s));
+  if (ev) HIPCHK(hipEventRecord((*ev)[3], s));
+  e = launch_three_pass_real(2, nullptr, p->H, p->Q, x, a, s);
+  if (e != hipSuccess) return hip_error(e, "y1 inverse + c2r rows pass");
+  if (ev) HIPCHK(hipEventRecord((*ev)[4], s));
+  return CFP_SUCCESS;
+}
+
 int run_real(cfp_rplan_s* p, const double* b, double* x, hipStream_t s, std::vector<hipEvent_t>* ev) {
   if (!p->has_sym) return set_error(CFP_ERR_ARG_WRONGSTATE, "no symbol set (call cfp_rplan_set_symbol_transport)");
+  if (use_three(p)) return run_real_three(p, b, x, s, ev);
   const i64 rows = p->n[1] * p->n[2];
   const double sc = 2.0 / (double)(p->n[0] * p->n[1] * p->n[2]);
   if (ev) HIPCHK(hipEventRecord((*ev)[0], s));
@@ -262,7 +297,37 @@ extern "C" int cfp_rplan_set_symbol_transport(cfp_rplan_t p, const double lam[3]
                                        (const double*)hz.data(), lam6));
   CFPCHK(cfp_plan_set_symbol_separable(p->nyq, (const double*)&hx[(size_t)p->M], (const double*)hy.data(),
                                        (const double*)hz.data(), lam6));
+  if (three_ok(p)) {  // the 3-sweep tables: colsym [kx + M ky] = lx hx[kx] + ly hy[ky], axsym = lz hz
+    RGuard g(p->device);
+    const i64 M = p->M, ny = p->n[1], nz = p->n[2];
+    std::vector<cd> col((size_t)(M * ny)), ax((size_t)nz);
+    for (i64 ky = 0; ky < ny; ++ky)
+      for (i64 kx = 0; kx < M; ++kx)
+        col[(size_t)(kx + M * ky)] = make_cd(lam[0] * hx[(size_t)kx].x + lam[1] * hy[(size_t)ky].x,
+                                             lam[0] * hx[(size_t)kx].y + lam[1] * hy[(size_t)ky].y);
+    for (i64 kz = 0; kz < nz; ++kz) ax[(size_t)kz] = make_cd(lam[2] * hz[(size_t)kz].x, lam[2] * hz[(size_t)kz].y);
+    if (!p->colsym3) HIPCHK(hipMalloc(&p->colsym3, sizeof(cd) * col.size()));
+    if (!p->axsym3) HIPCHK(hipMalloc(&p->axsym3, sizeof(cd) * ax.size()));
+    HIPCHK(hipMemcpy(p->colsym3, col.data(), sizeof(cd) * col.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(p->axsym3, ax.data(), sizeof(cd) * ax.size(), hipMemcpyHostToDevice));
+  }
   p->has_sym = true;
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_rplan_set_schedule(cfp_rplan_t p, int schedule) {
+  if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
+  if (schedule != CFP_RSCHEDULE_AUTO && schedule != CFP_RSCHEDULE_FIVE && schedule != CFP_RSCHEDULE_THREE)
+    return set_error(CFP_ERR_ARG_OUTOFRANGE, "unknown real-plan schedule %d", schedule);
+  if (schedule == CFP_RSCHEDULE_THREE && !three_ok(p))
+    return set_error(CFP_ERR_SUP, "the 3-sweep real schedule needs a 256^3 grid");
+  p->schedule = schedule;
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_rplan_schedule(cfp_rplan_t p, int* three) {
+  if (!p || !three) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  *three = use_three(p) ? 1 : 0;
   return CFP_SUCCESS;
 }
 

@@ -23,5 +23,10 @@ bool three_pass_shape_valid(int n1, int mid);
 // stage 0: P1 (in -> out), 1: P2 (out in place), 2: P3 (in -> out)
 hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, TPShape shape,
                              hipStream_t s);
+// real-data plan at 256^3 (cfp_real.hip): stage 0 P1r (b -> H, Q), 1 P2 on H (128 x 256 x 256,
+// in place), 2 P3r (H, Q -> x, x a.scale); a.tw = W_256, a.colsym = [kx + 128 ky], a.axsym = [kz].
+// Q (256 x 256, the Nyquist column kx = 128) takes its own y/z plan between P1r and P3r.
+hipError_t launch_three_pass_real(int stage, const double* b, cd* H, cd* Q, double* x, const TPArgs& a,
+                                  hipStream_t s);
 
 }  // namespace cfp

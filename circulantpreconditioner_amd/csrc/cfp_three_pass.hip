@@ -321,7 +321,9 @@ enum { PR_NO_Y2 = 1, PR_NO_ZMATH = 2, PR_NO_XCHG = 4, PR_NO_LOAD = 8, PR_NO_STOR
 // drained early.
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
-template <int T, int N2, int TN, int PROBE = 0, bool PF = false>
+// NX: x extent (row length in points) of the grid P2 runs on: TN for the complex apply, TN / 2
+// for the real-data plan's half spectrum (cfp_real.hip); y and z are TN long.
+template <int T, int N2, int TN, int PROBE = 0, bool PF = false, int NX = TN>
 __global__ void __launch_bounds__(T * (TN / 16)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
 #ifndef CFP_KEXP
@@ -330,15 +332,16 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
   static_assert(T == 64, "one wave = all 64 columns of a z group");
   static_assert(N2 == 4 || N2 == 8, "y2 = the top 2 or 3 lane bits");
   static_assert(TN == 256, "z = 16 x 16: radix-16 stage A in registers, one exchange, radix-16 stage B");
-  constexpr int N1 = TN / N2, TZ = TN / 16, NT = T * TZ, XT = T / N2, NXT = TN / XT;
+  constexpr int N1 = TN / N2, TZ = TN / 16, NT = T * TZ, XT = T / N2, NXT = NX / XT;
   constexpr int XB = ilog2(XT);  // lane bits of x
+  static_assert(NX % XT == 0, "whole x tiles");
   __shared__ __attribute__((aligned(16))) double lds[T * TN];  // split exchange
   __shared__ cd tw_l[TN];
   const int tid = threadIdx.x;
   for (int i = tid; i < TN; i += NT) tw_l[i] = a.tw[i];
   __syncthreads();  // the y2 stages read tw_l before the first exchange barrier
   const int c0 = tid & (T - 1), tz0 = tid / T;
-  const i64 zs = (i64)TN * TN;
+  const i64 zs = (i64)NX * TN;
   const auto idx = [](int i) {
     asm volatile("" : "+v"(i));
     return i;
@@ -346,7 +349,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
   // this lane's first point and the twiddle W_TN^{y2 k1} (natural layout: x = c % XT, y2 = c / XT)
   const auto col_ptr = [&](int u, int c, int tz) {
     const int xt = u % NXT, k1 = u / NXT;
-    return data + xt * XT + (c & (XT - 1)) + (i64)TN * ((c >> XB) + N2 * k1) + zs * tz;
+    return data + xt * XT + (c & (XT - 1)) + (i64)NX * ((c >> XB) + N2 * k1) + zs * tz;
   };
   const auto tw_y = [&](int u, int c) { return tw_l[((c >> XB) * (u / NXT)) & (TN - 1)]; };
   constexpr int NPF = PF ? 8 : 0;  // slots 0 .. NPF-1 come from the LDS prefetch (exchange buffer)
@@ -450,7 +453,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
     {
       const int c = idx(c0), tz = idx(tz0);
       const int k1 = u / NXT, p = c >> XB;
-      const cd cs = a.colsym[(u % NXT) * XT + (c & (XT - 1)) + (i64)TN * (k1 + N1 * brev<N2>(p))];
+      const cd cs = a.colsym[(u % NXT) * XT + (c & (XT - 1)) + (i64)NX * (k1 + N1 * brev<N2>(p))];
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const cd d = cadd(cadd(cs, a.axsym[tz + TZ * m]), make_cd(1.0, 0.0));
@@ -565,6 +568,172 @@ static unsigned grid_of(int units, int per_cu) {
   const int g = per_cu * cu_count();
   return (unsigned)(units < g ? units : g);
 }
+
+// ---------------------------------------------------------------------------------------------
+// Real-data 3-sweep (cfp_real.hip, row f4) at 256^3: the half spectrum H = M x 256 x 256
+// (M = 128) takes the complex schedule's four-step split of y with the x transform replaced by
+// r2c / c2r (the even/odd split of k_rx):
+//   P1r k_tp_rows_r2c<false>: one z-plane's rows y2 + 8 y1 (32 real rows of 2 KiB): r2c along x
+//       (128-point FFT in row mode, mirror bin from the partner lane), Nyquist X[128] of each
+//       row to Q, LDS transpose, 32-point y1 DFT per kx (column mode), store H in slot layout
+//   P2  k_tp_mid_sw<.., NX = 128> on H (y2 + z + divide + inverse)
+//   P3r k_tp_rows_r2c<true>: y1 inverse, transpose, c2r merge with Q (after the Nyquist
+//       column's own y/z plan), inverse 128-point FFT, x 2/N
+// P1r/P3r move 8 N + 8 N bytes, P2 16 N: 32 N per apply against ~80 N for r2c + 3 half-spectrum
+// passes + c2r.  (Folding the Nyquist column into P2 as a 17th x tile was measured slower: 544
+// units on 256 CUs take a third round, P2 70 -> 89 us.)
+__device__ __forceinline__ cd shfl_c(cd v, int lane) { return make_cd(__shfl(v.x, lane), __shfl(v.y, lane)); }
+
+// 8 points per thread (512 threads): the even/odd split needs every point and its mirror live
+// at once, which at 16 points per thread spills.
+template <bool INV>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nunits) {
+  constexpr int M = 128, N1 = 32, N2 = 8, NY = 256, PTS = 8;
+  constexpr int TPC = M / PTS;  // 16 threads per row (row mode)
+  constexpr int TY = N1 / PTS;  // 4 threads per column (column mode)
+  constexpr int NT = N1 * TPC;  // 512
+  constexpr int RS = M + M / 16;
+  constexpr int F = F_SPLIT_LDS | F_LDS_SYNC;
+  __shared__ __attribute__((aligned(16))) double lds[N1 * RS];  // row layout; the column layout (N1 x M) fits
+  __shared__ cd tw_m[M];   // W_128 (row FFT)
+  __shared__ cd tw_1[N1];  // W_32 (y1 DFT)
+  const int tid = threadIdx.x;
+  for (int i = tid; i < M; i += NT) tw_m[i] = a.tw[2 * i];
+  for (int i = tid; i < N1; i += NT) tw_1[i] = a.tw[8 * i];
+  const int r0 = tid / TPC, tpc0 = tid % TPC;  // row mode: row r (= y1), thread tpc
+  const int x0 = tid % M, ty0 = tid / M;       // column mode: column kx, thread ty
+  const int lane = tid & 63;
+  const int pl = lane - tpc0 + ((TPC - tpc0) & (TPC - 1));  // lane of the mirror partner (bin M - k)
+  const auto idx = [](int i) {
+    asm volatile("" : "+v"(i));
+    return i;
+  };
+  const auto to_columns = [&](cd* v) {  // row mode (row r, k = tpc + TPC t) -> column mode (kx, y1 = ty + TY m)
+    const int r = idx(r0), tpc = idx(tpc0), x = idx(x0), ty = idx(ty0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      lds_barrier();
+#pragma unroll
+      for (int t = 0; t < PTS; ++t) {
+        const int k = tpc + TPC * t;
+        lds[r * RS + k + (k >> 4)] = h ? v[t].y : v[t].x;
+      }
+      lds_barrier();
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) {
+        const double d = lds[(ty + TY * m) * RS + x + (x >> 4)];
+        if (h) v[m].y = d; else v[m].x = d;
+      }
+    }
+    lds_barrier();
+  };
+  const auto to_rows = [&](cd* v) {  // the reverse, conjugating (the y1 inverse ran on the conjugate)
+    const int r = idx(r0), tpc = idx(tpc0), x = idx(x0), ty = idx(ty0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      lds_barrier();
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) lds[(ty + TY * m) * RS + x + (x >> 4)] = h ? -v[m].y : v[m].x;
+      lds_barrier();
+#pragma unroll
+      for (int t = 0; t < PTS; ++t) {
+        const int k = tpc + TPC * t;
+        const double d = lds[r * RS + k + (k >> 4)];
+        if (h) v[t].y = d; else v[t].x = d;
+      }
+    }
+    lds_barrier();
+  };
+  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+    const int z = u / N2, y2 = u % N2;
+    cd v[PTS];
+    if constexpr (!INV) {
+      {
+        const int r = idx(r0), tpc = idx(tpc0);
+        const cd* src = reinterpret_cast<const cd*>(in_r) + ((i64)z * NY + y2 + N2 * r) * M + tpc;
+#pragma unroll
+        for (int t = 0; t < PTS; ++t) v[t] = src[TPC * t];
+        fft_stages<M, PTS, 2, true, N1, F>(v, lds, tw_m, r, tpc, true);  // 128 = 2 x 8 x 8; v[t] = Z[tpc + TPC t]
+      }
+      {
+        const int r = idx(r0), tpc = idx(tpc0);
+        cd X[PTS];
+#pragma unroll
+        for (int t = 0; t < PTS; ++t) {
+          const int k = tpc + TPC * t;
+          const cd za = shfl_c(v[(PTS - t) % PTS], pl), zb = shfl_c(v[PTS - 1 - t], pl);
+          const cd zm = tpc == 0 ? za : zb;  // Z[M - k]
+          const cd e = make_cd(0.5 * (v[t].x + zm.x), 0.5 * (v[t].y - zm.y));
+          const cd d = make_cd(v[t].x - zm.x, v[t].y + zm.y);  // Z[k] - conj Z[M-k]
+          const cd o = make_cd(0.5 * d.y, -0.5 * d.x);          // d / 2i
+          X[t] = cadd(e, cmul(a.tw[k], o));
+          if (t == 0 && tpc == 0) Q[(i64)z * NY + y2 + N2 * r] = csub(e, o);  // Nyquist bin X[M]
+        }
+#pragma unroll
+        for (int t = 0; t < PTS; ++t) v[t] = X[t];
+      }
+      to_columns(v);
+      {
+        const int x = idx(x0), ty = idx(ty0);
+        fft_stages<N1, PTS, 4, false, M, F>(v, lds, tw_1, x, ty, true);  // 32 = 4 x 8; v[m]: k1 = ty + TY m
+        cd* dst = H + ((i64)z * NY + y2 + N2 * ty) * M + x;
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) dst[(i64)N2 * TY * M * m] = v[m];
+      }
+    } else {
+      {
+        const int x = idx(x0), ty = idx(ty0);
+        const cd* src = H + ((i64)z * NY + y2 + N2 * ty) * M + x;
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) v[m] = cconj(src[(i64)N2 * TY * M * m]);
+        fft_stages<N1, PTS, 4, false, M, F>(v, lds, tw_1, x, ty, true);  // v[m]: y1 = ty + TY m
+      }
+      to_rows(v);
+      {
+        const int r = idx(r0), tpc = idx(tpc0);
+        const cd xn = tpc == 0 ? Q[(i64)z * NY + y2 + N2 * r] : make_cd(0.0, 0.0);
+        cd Z[PTS];
+#pragma unroll
+        for (int t = 0; t < PTS; ++t) {
+          const int k = tpc + TPC * t;
+          const cd xa = shfl_c(v[(PTS - t) % PTS], pl), xb = shfl_c(v[PTS - 1 - t], pl);
+          const cd xm = tpc == 0 ? (t == 0 ? xn : xa) : xb;  // X[M - k]
+          const cd e = make_cd(0.5 * (v[t].x + xm.x), 0.5 * (v[t].y - xm.y));
+          const cd d = make_cd(0.5 * (v[t].x - xm.x), 0.5 * (v[t].y + xm.y));
+          const cd o = cmul(d, cconj(a.tw[k]));            // (X[k] - conj X[M-k]) W^-k / 2
+          Z[t] = cconj(make_cd(e.x - o.y, e.y + o.x));     // E + i O, conjugated: inverse by conjugation
+        }
+#pragma unroll
+        for (int t = 0; t < PTS; ++t) v[t] = Z[t];
+        fft_stages<M, PTS, 2, true, N1, F>(v, lds, tw_m, r, tpc, true);
+        const double sc = a.scale;
+        cd* dst = reinterpret_cast<cd*>(out_r) + ((i64)z * NY + y2 + N2 * r) * M + tpc;
+#pragma unroll
+        for (int t = 0; t < PTS; ++t) dst[TPC * t] = make_cd(v[t].x * sc, -v[t].y * sc);
+      }
+    }
+    lds_barrier();  // the next unit's first exchange overwrites LDS
+  }
+}
+
+hipError_t launch_three_pass_real(int stage, const double* b, cd* H, cd* Q, double* x, const TPArgs& a,
+                                  hipStream_t s) {
+  if (stage == 1) {
+    constexpr int units = (128 / 8) * 32;  // x tiles of the half spectrum x k1
+    hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true, 128>), dim3(grid_of(units, 1)), dim3(1024), 0, s, H, a,
+                       units);
+  } else {
+    constexpr int units = 256 * 8;  // z-planes x y2
+    const unsigned g = grid_of(units, 2);
+    if (stage == 0)
+      hipLaunchKernelGGL((k_tp_rows_r2c<false>), dim3(g), dim3(512), 0, s, b, H, Q, nullptr, a, units);
+    else
+      hipLaunchKernelGGL((k_tp_rows_r2c<true>), dim3(g), dim3(512), 0, s, nullptr, H, Q, x, a, units);
+  }
+  return hipGetLastError();
+}
+
 
 template <int N1, int TN, int PER_CU>
 static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {

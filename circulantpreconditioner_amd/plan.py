@@ -286,6 +286,22 @@ class RealPlan:
         check(lib().cfp_rplan_set_symbol_transport(self._h, (ctypes.c_double * 3)(*vals)))
         return self
 
+    SCHEDULES = {"auto": 0, "five": 1, "three": 2}
+
+    def set_schedule(self, schedule: str | int) -> "RealPlan":
+        """'auto' (3 sweeps at 256^3), 'five' (r2c + 3 half-spectrum passes + c2r) or 'three'
+        (256^3 only)."""
+        v = self.SCHEDULES[schedule] if isinstance(schedule, str) else int(schedule)
+        check(lib().cfp_rplan_set_schedule(self._h, v))
+        return self
+
+    @property
+    def three_sweep(self) -> bool:
+        """True when the next apply runs the 3-sweep schedule."""
+        t = ctypes.c_int()
+        check(lib().cfp_rplan_schedule(self._h, ctypes.byref(t)))
+        return bool(t.value)
+
     def _ptr(self, t: torch.Tensor, name: str) -> int:
         if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous() or t.numel() != self.N:
             raise ValueError(f"{name} must be a contiguous float64 device tensor of {self.N} elements")
@@ -298,7 +314,8 @@ class RealPlan:
         return out
 
     def time_passes(self, b: torch.Tensor, x: torch.Tensor, iters: int = 20, stream=None) -> list:
-        """Mean ms of the 4 stages: r2c rows, half-spectrum y/z, Nyquist y/z, c2r rows."""
+        """Mean ms of the 4 stages: r2c rows (+ y1 in the 3-sweep schedule), half-spectrum y/z
+        (y2/z), Nyquist y/z, (y1 inverse +) c2r rows."""
         ms = (ctypes.c_double * 4)()
         check(lib().cfp_rplan_time_passes(self._h, self._ptr(b, "b"), self._ptr(x, "x"), int(iters), ms,
                                           _stream_handle(stream)))

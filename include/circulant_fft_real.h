@@ -13,6 +13,10 @@
  * complex plan over the nx/2 x ny x nz half spectrum (+ the Nyquist column kx = nx/2 as its own
  * 1 x ny x nz grid), z fused with the symbol, inverse y, then c2r along x with the 1/N scale.
  * Requires nx even with nx/2 in {16, 32, ..., 512} and ny * nz > 1.
+ *
+ * At 256^3 the default is a 3-sweep schedule (cfp_three_pass.hip): r2c rows + the 32-point y1
+ * DFT of a four-step y split | y2 + z + divide + inverse on the half spectrum | y1 inverse + c2r
+ * rows, ~32 N bytes per apply.
  */
 #ifndef CFP_CIRCULANT_FFT_REAL_H
 #define CFP_CIRCULANT_FFT_REAL_H
@@ -30,6 +34,14 @@ int cfp_rplan_destroy(cfp_rplan_t plan);
 int cfp_rplan_set_symbol_transport(cfp_rplan_t plan, const double lam[3]);
 /* x = C^{-1} b for real b (nx*ny*nz doubles on the device); x may alias b */
 int cfp_rplan_apply(cfp_rplan_t plan, const double *b, double *x, void *stream);
+/* schedule: CFP_RSCHEDULE_AUTO (3 sweeps at 256^3, else r2c + 3 half-spectrum passes + c2r),
+ * CFP_RSCHEDULE_FIVE (always the latter) or CFP_RSCHEDULE_THREE (256^3 only, else CFP_ERR_SUP) */
+#define CFP_RSCHEDULE_AUTO 0
+#define CFP_RSCHEDULE_FIVE 1
+#define CFP_RSCHEDULE_THREE 2
+int cfp_rplan_set_schedule(cfp_rplan_t plan, int schedule);
+/* *three = 1 when the next apply runs the 3-sweep schedule */
+int cfp_rplan_schedule(cfp_rplan_t plan, int *three);
 /* launches of one apply and their mean duration (ms) over `iters` applies */
 int cfp_rplan_num_passes(cfp_rplan_t plan, int *passes);
 int cfp_rplan_time_passes(cfp_rplan_t plan, const double *b, double *x, int iters, double *ms_out, void *stream);
