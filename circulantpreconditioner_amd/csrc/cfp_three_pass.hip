@@ -582,8 +582,6 @@ static unsigned grid_of(int units, int per_cu) {
 // P1r/P3r move 8 N + 8 N bytes, P2 16 N: 32 N per apply against ~80 N for r2c + 3 half-spectrum
 // passes + c2r.  (Folding the Nyquist column into P2 as a 17th x tile was measured slower: 544
 // units on 256 CUs take a third round, P2 70 -> 89 us.)
-__device__ __forceinline__ cd shfl_c(cd v, int lane) { return make_cd(__shfl(v.x, lane), __shfl(v.y, lane)); }
-
 // 8 points per thread (512 threads): the even/odd split needs every point and its mirror live
 // at once, which at 16 points per thread spills.
 template <bool INV>
@@ -603,14 +601,17 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
   for (int i = tid; i < N1; i += NT) tw_1[i] = a.tw[8 * i];
   const int r0 = tid / TPC, tpc0 = tid % TPC;  // row mode: row r (= y1), thread tpc
   const int x0 = tid % M, ty0 = tid / M;       // column mode: column kx, thread ty
-  const int lane = tid & 63;
-  const int pl = lane - tpc0 + ((TPC - tpc0) & (TPC - 1));  // lane of the mirror partner (bin M - k)
   const auto idx = [](int i) {
     asm volatile("" : "+v"(i));
     return i;
   };
-  const auto to_columns = [&](cd* v) {  // row mode (row r, k = tpc + TPC t) -> column mode (kx, y1 = ty + TY m)
+  // row mode (row r, Z[k], k = tpc + TPC t) -> column mode (column kx, rows ty + TY m), with the
+  // r2c even/odd split done on the way: each thread also reads its mirror bin Z[M - kx] of the
+  // same rows from the transpose buffer (no cross-lane shuffles)
+  const auto to_columns_r2c = [&](cd* v, int z, int y2) {
     const int r = idx(r0), tpc = idx(tpc0), x = idx(x0), ty = idx(ty0);
+    const int xm = (M - x) & (M - 1);
+    cd zm[PTS];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       lds_barrier();
@@ -622,14 +623,27 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
       lds_barrier();
 #pragma unroll
       for (int m = 0; m < PTS; ++m) {
-        const double d = lds[(ty + TY * m) * RS + x + (x >> 4)];
-        if (h) v[m].y = d; else v[m].x = d;
+        const int row = (ty + TY * m) * RS;
+        const double d = lds[row + x + (x >> 4)], dm = lds[row + xm + (xm >> 4)];
+        if (h) { v[m].y = d; zm[m].y = dm; } else { v[m].x = d; zm[m].x = dm; }
       }
     }
     lds_barrier();
+    const cd w = a.tw[x];  // W_2M^kx
+#pragma unroll
+    for (int m = 0; m < PTS; ++m) {
+      const cd e = make_cd(0.5 * (v[m].x + zm[m].x), 0.5 * (v[m].y - zm[m].y));
+      const cd d = make_cd(v[m].x - zm[m].x, v[m].y + zm[m].y);  // Z[k] - conj Z[M-k]
+      const cd o = make_cd(0.5 * d.y, -0.5 * d.x);                // d / 2i
+      v[m] = cadd(e, cmul(w, o));
+      if (x == 0) Q[(i64)z * NY + y2 + N2 * (ty + TY * m)] = csub(e, o);  // Nyquist bin X[M]
+    }
   };
-  const auto to_rows = [&](cd* v) {  // the reverse, conjugating (the y1 inverse ran on the conjugate)
+  // column mode (column kx, rows y1 = ty + TY m, conjugated) -> row mode with the c2r merge: each
+  // thread reads X[k] and its mirror X[M - k] of its row (X[M] = the Nyquist bin from Q)
+  const auto to_rows_c2r = [&](cd* v, int z, int y2) {
     const int r = idx(r0), tpc = idx(tpc0), x = idx(x0), ty = idx(ty0);
+    cd xm[PTS];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       lds_barrier();
@@ -638,12 +652,21 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
       lds_barrier();
 #pragma unroll
       for (int t = 0; t < PTS; ++t) {
-        const int k = tpc + TPC * t;
-        const double d = lds[r * RS + k + (k >> 4)];
-        if (h) v[t].y = d; else v[t].x = d;
+        const int k = tpc + TPC * t, km = (M - k) & (M - 1);
+        const double d = lds[r * RS + k + (k >> 4)], dm = lds[r * RS + km + (km >> 4)];
+        if (h) { v[t].y = d; xm[t].y = dm; } else { v[t].x = d; xm[t].x = dm; }
       }
     }
     lds_barrier();
+    if (tpc == 0) xm[0] = Q[(i64)z * NY + y2 + N2 * r];  // k = 0: the mirror is the Nyquist bin
+#pragma unroll
+    for (int t = 0; t < PTS; ++t) {
+      const int k = tpc + TPC * t;
+      const cd e = make_cd(0.5 * (v[t].x + xm[t].x), 0.5 * (v[t].y - xm[t].y));
+      const cd d = make_cd(0.5 * (v[t].x - xm[t].x), 0.5 * (v[t].y + xm[t].y));
+      const cd o = cmul(d, cconj(a.tw[k]));               // (X[k] - conj X[M-k]) W^-k / 2
+      v[t] = cconj(make_cd(e.x - o.y, e.y + o.x));        // E + i O, conjugated: inverse by conjugation
+    }
   };
   for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
     const int z = u / N2, y2 = u % N2;
@@ -656,24 +679,7 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
         for (int t = 0; t < PTS; ++t) v[t] = src[TPC * t];
         fft_stages<M, PTS, 2, true, N1, F>(v, lds, tw_m, r, tpc, true);  // 128 = 2 x 8 x 8; v[t] = Z[tpc + TPC t]
       }
-      {
-        const int r = idx(r0), tpc = idx(tpc0);
-        cd X[PTS];
-#pragma unroll
-        for (int t = 0; t < PTS; ++t) {
-          const int k = tpc + TPC * t;
-          const cd za = shfl_c(v[(PTS - t) % PTS], pl), zb = shfl_c(v[PTS - 1 - t], pl);
-          const cd zm = tpc == 0 ? za : zb;  // Z[M - k]
-          const cd e = make_cd(0.5 * (v[t].x + zm.x), 0.5 * (v[t].y - zm.y));
-          const cd d = make_cd(v[t].x - zm.x, v[t].y + zm.y);  // Z[k] - conj Z[M-k]
-          const cd o = make_cd(0.5 * d.y, -0.5 * d.x);          // d / 2i
-          X[t] = cadd(e, cmul(a.tw[k], o));
-          if (t == 0 && tpc == 0) Q[(i64)z * NY + y2 + N2 * r] = csub(e, o);  // Nyquist bin X[M]
-        }
-#pragma unroll
-        for (int t = 0; t < PTS; ++t) v[t] = X[t];
-      }
-      to_columns(v);
+      to_columns_r2c(v, z, y2);
       {
         const int x = idx(x0), ty = idx(ty0);
         fft_stages<N1, PTS, 4, false, M, F>(v, lds, tw_1, x, ty, true);  // 32 = 4 x 8; v[m]: k1 = ty + TY m
@@ -689,23 +695,9 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
         for (int m = 0; m < PTS; ++m) v[m] = cconj(src[(i64)N2 * TY * M * m]);
         fft_stages<N1, PTS, 4, false, M, F>(v, lds, tw_1, x, ty, true);  // v[m]: y1 = ty + TY m
       }
-      to_rows(v);
+      to_rows_c2r(v, z, y2);
       {
         const int r = idx(r0), tpc = idx(tpc0);
-        const cd xn = tpc == 0 ? Q[(i64)z * NY + y2 + N2 * r] : make_cd(0.0, 0.0);
-        cd Z[PTS];
-#pragma unroll
-        for (int t = 0; t < PTS; ++t) {
-          const int k = tpc + TPC * t;
-          const cd xa = shfl_c(v[(PTS - t) % PTS], pl), xb = shfl_c(v[PTS - 1 - t], pl);
-          const cd xm = tpc == 0 ? (t == 0 ? xn : xa) : xb;  // X[M - k]
-          const cd e = make_cd(0.5 * (v[t].x + xm.x), 0.5 * (v[t].y - xm.y));
-          const cd d = make_cd(0.5 * (v[t].x - xm.x), 0.5 * (v[t].y + xm.y));
-          const cd o = cmul(d, cconj(a.tw[k]));            // (X[k] - conj X[M-k]) W^-k / 2
-          Z[t] = cconj(make_cd(e.x - o.y, e.y + o.x));     // E + i O, conjugated: inverse by conjugation
-        }
-#pragma unroll
-        for (int t = 0; t < PTS; ++t) v[t] = Z[t];
         fft_stages<M, PTS, 2, true, N1, F>(v, lds, tw_m, r, tpc, true);
         const double sc = a.scale;
         cd* dst = reinterpret_cast<cd*>(out_r) + ((i64)z * NY + y2 + N2 * r) * M + tpc;
