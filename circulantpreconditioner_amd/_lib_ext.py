@@ -113,6 +113,8 @@ def declare(L) -> None:
         "cfp_group_destroy": ([vp], c_int),
         "cfp_group_set_symbol_transport": ([vp, dp], c_int),
         "cfp_group_apply": ([vp, P(vp), P(vp)], c_int),
+        "cfp_group_set_schedule": ([vp, c_int], c_int),
+        "cfp_dist_plan_set_schedule": ([vp, c_int], c_int),
         # PETSc stand-in
         "PetscErrorLastMessage": ([], cs),
         "VecMiniSetStream": ([vp], c_int),

@@ -18,6 +18,7 @@
 #include "../../include/circulant_fft_dist.h"
 #include "cfp_host.h"
 #include "cfp_internal.h"
+#include "cfp_three_pass.h"
 
 using namespace cfp;
 
@@ -75,10 +76,46 @@ struct Step {
   int src, dst;   // buffer ids
   int fused;      // 1 if this is the symbol pass
   int axis;       // 0, 1, 2 (kernel steps)
+  int tp;         // >= 0: stage of the 3-sweep slab schedule (cfp_three_pass.hip)
 };
 
-std::vector<Step> slab_steps(const SlabLayout& L) {
+// 256^3 with P | 32: 3 local sweeps per rank (x + y1 | y2 + z + symbol + inverses | inverse),
+// the same two exchanges; otherwise 5 axis passes
+bool slab_three(const SlabLayout& L, int schedule) {
+  const i64 n[3] = {L.nx, L.ny, L.nz};
+  return schedule != CFP_SCHEDULE_FIVE_PASS && three_pass_slab_supported(n, L.P);
+}
+
+std::vector<Step> slab_steps(const SlabLayout& L, int schedule = CFP_SCHEDULE_AUTO) {
   std::vector<Step> st;
+  if (slab_three(L, schedule)) {
+    // P1 natural planes -> per-peer chunks (work), exchange into x as [nz][nyl][nx] (the rank's k1
+    // rows), P2 in place, exchange back into work (chunks), P3 -> x natural, x 1/N
+    auto tp = [&](int stage, int src, int dst) {
+      Step s;
+      std::memset(&s, 0, sizeof(s));
+      s.exchange = false;
+      s.tp = stage;
+      s.axis = stage == 1 ? 2 : 0;
+      s.pass.n = (int)L.nx;
+      s.pass.mode = stage == 0 ? PASS_TP_ROWS_FWD : (stage == 1 ? PASS_TP_MID : PASS_TP_ROWS_INV);
+      s.pass.scale = stage == 2 ? 1.0 / (double)(L.nx * L.ny * L.nz) : 1.0;
+      s.src = src; s.dst = dst; s.fused = stage == 1;
+      st.push_back(s);
+    };
+    auto ex = [&](int src, int dst) {
+      Step s;
+      std::memset(&s, 0, sizeof(s));
+      s.exchange = true; s.src = src; s.dst = dst; s.tp = -1;
+      st.push_back(s);
+    };
+    tp(0, B_IN, B_W);
+    ex(B_W, B_X);
+    tp(1, B_X, B_X);
+    ex(B_X, B_W);
+    tp(2, B_W, B_X);
+    return st;
+  }
   const i64 nx = L.nx, ny = L.ny, nz = L.nz, nzl = L.nzl, nyl = L.nyl;
   auto kern = [&](int axis, int n, i64 ncols, i64 inner_n, Side in, Side out, int mode, int src, int dst,
                   int fused) {
@@ -88,13 +125,13 @@ std::vector<Step> slab_steps(const SlabLayout& L) {
     s.pass.n = n; s.pass.ncols = ncols; s.pass.inner_n = inner_n;
     s.pass.in = in; s.pass.out = out; s.pass.mode = mode; s.pass.scale = 1.0;
     s.pass.colsym = s.pass.axsym = s.pass.diag = nullptr;
-    s.src = src; s.dst = dst; s.fused = fused;
+    s.src = src; s.dst = dst; s.fused = fused; s.tp = -1;
     st.push_back(s);
   };
   auto exch = [&](int src, int dst) {
     Step s;
     std::memset(&s, 0, sizeof(s));
-    s.exchange = true; s.src = src; s.dst = dst;
+    s.exchange = true; s.src = src; s.dst = dst; s.tp = -1;
     st.push_back(s);
   };
   const Side xs = side(0, nx, 1, nx, 0);                    // x rows of the local slab
@@ -121,16 +158,27 @@ struct SlabRank {
   int device = 0;
   std::map<int, cd*> tw;
   cd* colsym = nullptr;
+  cd* colsym3 = nullptr;  // 3-sweep schedule: the global [kx + nx ky] table
   cd* axsym = nullptr;
   cd* work = nullptr;
   bool own_work = true;
   bool sym = false;
+  int schedule = CFP_SCHEDULE_AUTO;
+  double lam_[6] = {0, 0, 0, 0, 0, 0};
   std::vector<Step> steps;
 
   int init(const SlabLayout& lay, int dev) {
     L = lay;
     device = dev;
-    steps = slab_steps(L);
+    int rc = set_steps(CFP_SCHEDULE_AUTO);
+    if (rc) return rc;
+    HIPCHK(hipMalloc(&work, sizeof(cd) * (size_t)L.local));
+    return CFP_SUCCESS;
+  }
+  bool three() const { return !steps.empty() && steps[0].tp >= 0; }
+  int set_steps(int sched) {
+    schedule = sched;
+    steps = slab_steps(L, sched);
     for (const Step& s : steps) {
       if (s.exchange || tw.count(s.pass.n)) continue;
       std::vector<cd> h = host_twiddles(s.pass.n, -1);
@@ -139,16 +187,16 @@ struct SlabRank {
       HIPCHK(hipMemcpy(d, h.data(), sizeof(cd) * h.size(), hipMemcpyHostToDevice));
       tw[s.pass.n] = d;
     }
-    HIPCHK(hipMalloc(&work, sizeof(cd) * (size_t)L.local));
-    return CFP_SUCCESS;
+    return sym ? set_transport(lam_) : CFP_SUCCESS;  // the new schedule's symbol tables
   }
   void release() {
     for (auto& kv : tw) hipFree(kv.second);
     tw.clear();
     if (colsym) hipFree(colsym);
+    if (colsym3) hipFree(colsym3);
     if (axsym) hipFree(axsym);
     if (work && own_work) hipFree(work);
-    colsym = axsym = work = nullptr;
+    colsym = colsym3 = axsym = work = nullptr;
   }
   // colsym over the z-pass columns g = ix + nx*iyl (global ky = y0 + iyl); axsym over kz
   int set_transport(const double lam[6]) {
@@ -172,11 +220,32 @@ struct SlabRank {
     if (!axsym) HIPCHK(hipMalloc(&axsym, sizeof(cd) * (size_t)L.nz));
     HIPCHK(hipMemcpy(colsym, col.data(), sizeof(cd) * (size_t)ncols, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(axsym, s[2].data(), sizeof(cd) * (size_t)L.nz, hipMemcpyHostToDevice));
+    if (three()) {  // every rank holds the global column table: P2 indexes it with global ky
+      std::vector<cd> g((size_t)(L.nx * L.ny));
+      for (i64 ky = 0; ky < L.ny; ++ky)
+        for (i64 ix = 0; ix < L.nx; ++ix)
+          g[(size_t)(ix + L.nx * ky)] = make_cd(s[0][ix].x + s[1][ky].x, s[0][ix].y + s[1][ky].y);
+      if (!colsym3) HIPCHK(hipMalloc(&colsym3, sizeof(cd) * g.size()));
+      HIPCHK(hipMemcpy(colsym3, g.data(), sizeof(cd) * g.size(), hipMemcpyHostToDevice));
+    }
+    std::memcpy(lam_, lam, sizeof(lam_));
     sym = true;
     return CFP_SUCCESS;
   }
   cd* buf(int id, const cd* b, cd* x) const { return id == B_IN ? (cd*)b : (id == B_X ? x : work); }
   int launch(const Step& s, const cd* b, cd* x, hipStream_t st) const {
+    if (s.tp >= 0) {
+      TPArgs a;
+      a.tw = tw.at((int)L.nx);
+      a.colsym = colsym3;
+      a.axsym = axsym;
+      a.scale = s.pass.scale;
+      a.lnyl = ilog2_exact(L.nyl);
+      a.chunk = L.chunk;
+      a.k1_off = (int)(L.r * (L.nyl / 8));  // N2 = 8 rows per k1
+      hipError_t e = launch_three_pass_slab(s.tp, buf(s.src, b, x), buf(s.dst, b, x), a, (int)L.nzl, st);
+      return e == hipSuccess ? CFP_SUCCESS : hip_error(e, "slab 3-sweep launch");
+    }
     PassDesc p = s.pass;
     if (s.fused) { p.colsym = colsym; p.axsym = axsym; }
     hipError_t e = launch_axis_pass(p, buf(s.src, b, x), buf(s.dst, b, x), tw.at(p.n), st);
@@ -221,7 +290,7 @@ extern "C" int cfp_slab_num_steps(int64_t nx, int64_t ny, int64_t nz, int P, int
   SlabLayout L;
   int rc = make_layout(nx, ny, nz, P, r, &L);
   if (rc) return rc;
-  *nsteps = (int)slab_steps(L).size();
+  *nsteps = (int)slab_steps(L, CFP_SCHEDULE_FIVE_PASS).size();  // the axis-pass step list (host replays)
   return CFP_SUCCESS;
 }
 
@@ -231,7 +300,7 @@ extern "C" int cfp_slab_step_info(int64_t nx, int64_t ny, int64_t nz, int P, int
   SlabLayout L;
   int rc = make_layout(nx, ny, nz, P, r, &L);
   if (rc) return rc;
-  const std::vector<Step> st = slab_steps(L);
+  const std::vector<Step> st = slab_steps(L, CFP_SCHEDULE_FIVE_PASS);
   if (i < 0 || i >= (int)st.size()) return set_error(CFP_ERR_ARG_OUTOFRANGE, "step index");
   const Step& s = st[(size_t)i];
   const PassDesc& p = s.pass;
@@ -334,6 +403,38 @@ extern "C" int cfp_dist_plan_destroy(cfp_dist_plan_t p) {
   if (p->comm) ncclCommDestroy(p->comm);
   p->R.release();
   delete p;
+  return CFP_SUCCESS;
+}
+
+// schedule of the slab plan's local passes: CFP_SCHEDULE_AUTO (3 sweeps at 256^3 with P | 32),
+// CFP_SCHEDULE_FIVE_PASS, or CFP_SCHEDULE_THREE_PASS (CFP_ERR_SUP where not supported)
+static int slab_schedule_check(const SlabLayout& L, int schedule) {
+  if (schedule != CFP_SCHEDULE_AUTO && schedule != CFP_SCHEDULE_FIVE_PASS && schedule != CFP_SCHEDULE_THREE_PASS)
+    return set_error(CFP_ERR_ARG_OUTOFRANGE, "slab schedule must be AUTO, FIVE_PASS or THREE_PASS");
+  const i64 n[3] = {L.nx, L.ny, L.nz};
+  if (schedule == CFP_SCHEDULE_THREE_PASS && !three_pass_slab_supported(n, L.P))
+    return set_error(CFP_ERR_SUP, "the 3-sweep slab schedule needs a 256^3 grid and nranks | 32");
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_dist_plan_set_schedule(cfp_dist_plan_t p, int schedule) {
+  if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
+  int rc = slab_schedule_check(p->R.L, schedule);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(p->R.device));
+  dist_profile_free(p);
+  return p->R.set_steps(schedule);
+}
+
+extern "C" int cfp_group_set_schedule(cfp_group_t g, int schedule) {
+  if (!g) return set_error(CFP_ERR_ARG_NULL, "NULL group");
+  for (auto& R : g->R) {
+    int rc = slab_schedule_check(R.L, schedule);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(R.device));
+    rc = R.set_steps(schedule);
+    if (rc) return rc;
+  }
   return CFP_SUCCESS;
 }
 

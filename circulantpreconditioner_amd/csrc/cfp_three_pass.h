@@ -6,9 +6,16 @@ namespace cfp {
 
 struct TPArgs {
   const cd* tw;      // W_n[k] = exp(-2 pi i k / n), n = the grid side (128 or 256)
-  const cd* colsym;  // separable symbol, z fused: [kx + n ky] = s_x[kx] + s_y[ky]
+  const cd* colsym;  // separable symbol, z fused: [kx + n ky] = s_x[kx] + s_y[ky] (global ky)
   const cd* axsym;   // [kz] = s_z[kz]
   double scale;      // P3 only: 1/N
+  // z-slab layout (cfp_dist.hip); the defaults are one GPU's natural layout.
+  //   P1 writes / P3 reads the per-peer exchange chunks: row y of local plane z at
+  //   (y >> lnyl) * chunk + (z << lnyl) * n + (y & (nyl - 1)) * n;  P2 runs on [n z][nyl][nx]
+  //   with the k1 range [k1_off, k1_off + nyl / N2) of the four-step split.
+  int lnyl = 0;     // log2 of the rows per chunk (0: nyl = n, one chunk)
+  i64 chunk = 0;    // elements per peer chunk
+  int k1_off = 0;   // first global k1 of this rank (P2)
 };
 
 // kernel shape at 256^3 (cfp_plan_set_three_pass_shape); zeros = the measured default
@@ -23,6 +30,11 @@ bool three_pass_shape_valid(int n1, int mid);
 // stage 0: P1 (in -> out), 1: P2 (out in place), 2: P3 (in -> out)
 hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, TPShape shape,
                              hipStream_t s);
+// z-slab rank of a 256^3 grid (cfp_dist.hip): stage 0 P1 on nzl local planes (in natural ->
+// out chunked), 1 P2 on [256][nyl][256] in place, 2 P3 (in chunked -> out natural, x a.scale);
+// the default shape (N1 = 32, permlane P2 with prefetch)
+bool three_pass_slab_supported(const i64 n[3], int P);
+hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs& a, int nzl, hipStream_t s);
 // real-data plan at 256^3 (cfp_real.hip): stage 0 P1r (b -> H, Q), 1 P2 on H (128 x 256 x 256,
 // in place), 2 P3r (H, Q -> x, x a.scale); a.tw = W_256, a.colsym = [kx + 128 ky], a.axsym = [kz].
 // Q (256 x 256, the Nyquist column kx = 128) takes its own y/z plan between P1r and P3r.

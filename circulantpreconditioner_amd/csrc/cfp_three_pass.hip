@@ -95,16 +95,25 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
     asm volatile("" : "+v"(i));
     return i;
   };
+  // rows of the chunked side (P1 output, P3 input): one GPU: nyl = TN, one chunk = natural
+  const int lnyl = a.lnyl ? a.lnyl : ilog2(TN);
+  const int nyl = 1 << lnyl;
+  const auto crow = [&](int z, int y) -> i64 {
+    return (i64)(y >> lnyl) * a.chunk + ((i64)z << lnyl) * TN + (i64)(y & (nyl - 1)) * TN;
+  };
   for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
-    // unit u = (z, y2): rows y2 + N2 y1 of plane z
+    // unit u = (z, y2): rows y2 + N2 y1 of (local) plane z
     cd v[16];
     {
       const int x = idx(x0), ty = idx(ty0);
-      const cd* const src = in + (i64)(u / N2) * TN * TN + x + (i64)TN * (u % N2 + N2 * ty);  // + uniform
+      if (INV) {  // chunked rows y2 + N2 ty + N2 TY m: per-thread part + uniform part (nyl >= N2 TY)
+        const cd* const src = in + crow(u / N2, u % N2 + N2 * ty) + x;
 #pragma unroll
-      for (int m = 0; m < 16; ++m) {
-        v[m] = gload<FLAGS>(src + (i64)TN * N2 * TY * m);
-        if (INV) v[m] = cconj(v[m]);
+        for (int m = 0; m < 16; ++m) v[m] = cconj(gload<FLAGS>(src + crow(0, N2 * TY * m)));
+      } else {
+        const cd* const src = in + (i64)(u / N2) * TN * TN + x + (i64)TN * (u % N2 + N2 * ty);  // + uniform
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = gload<FLAGS>(src + (i64)TN * N2 * TY * m);
       }
       // phase A: N1-point DFT over y1 for every x (column mode, 256 columns x TY threads)
       fft_stages<N1, 16, N1 / 16, false, TN, F>(v, lds, tw_l, x, ty, true);  // v[m]: k1 = ty + TY m
@@ -135,7 +144,7 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
     {
       const int r = idx(r0), tx = idx(tx0);
       const double sc = a.scale, sy = INV ? -sc : sc;
-      cd* dst = out + (i64)(u / N2) * TN * TN + (i64)TN * (u % N2 + N2 * r) + tx;
+      cd* dst = out + (INV ? (i64)(u / N2) * TN * TN + (i64)TN * (u % N2 + N2 * r) : crow(u / N2, u % N2 + N2 * r)) + tx;
 #pragma unroll
       for (int m = 0; m < 16; ++m) gstore<FLAGS>(dst + TR * m, make_cd(v[m].x * sc, v[m].y * sy));
     }
@@ -341,7 +350,8 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
   for (int i = tid; i < TN; i += NT) tw_l[i] = a.tw[i];
   __syncthreads();  // the y2 stages read tw_l before the first exchange barrier
   const int c0 = tid & (T - 1), tz0 = tid / T;
-  const i64 zs = (i64)NX * TN;
+  // rows of this rank's block [TN z][nyl][NX] (one GPU: nyl = TN); unit u = (x tile, local k1)
+  const i64 zs = (i64)NX << (a.lnyl ? a.lnyl : ilog2(TN));
   const auto idx = [](int i) {
     asm volatile("" : "+v"(i));
     return i;
@@ -351,7 +361,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
     const int xt = u % NXT, k1 = u / NXT;
     return data + xt * XT + (c & (XT - 1)) + (i64)NX * ((c >> XB) + N2 * k1) + zs * tz;
   };
-  const auto tw_y = [&](int u, int c) { return tw_l[((c >> XB) * (u / NXT)) & (TN - 1)]; };
+  const auto tw_y = [&](int u, int c) { return tw_l[((c >> XB) * (a.k1_off + u / NXT)) & (TN - 1)]; };
   constexpr int NPF = PF ? 8 : 0;  // slots 0 .. NPF-1 come from the LDS prefetch (exchange buffer)
   const int wv = __builtin_amdgcn_readfirstlane(tid / 64);
   const auto prefetch = [&](int u) {  // this wave's slots 0 .. NPF-1 of unit u -> LDS
@@ -452,7 +462,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
     stage_b(v);  // v[m]: kz = tz + 16 m; column c = x + XT p
     {
       const int c = idx(c0), tz = idx(tz0);
-      const int k1 = u / NXT, p = c >> XB;
+      const int k1 = a.k1_off + u / NXT, p = c >> XB;  // global k1
       const cd cs = a.colsym[(u % NXT) * XT + (c & (XT - 1)) + (i64)NX * (k1 + N1 * brev<N2>(p))];
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
@@ -749,6 +759,27 @@ static void launch_mid_sw(cd* data, const TPArgs& a, hipStream_t s) {
   constexpr int units = (TN / (64 / N2)) * (TN / N2);
   hipLaunchKernelGGL((k_tp_mid_sw<64, N2, TN, 0, PF>), dim3(grid_of(units, 1)), dim3(64 * (TN / 16)), 0, s, data, a,
                      units);
+}
+
+bool three_pass_slab_supported(const i64 n[3], int P) {
+  // N1 = 32 rows per P1 unit, k1 split over the ranks; P3 reads chunk rows 16 apart (nyl >= 16)
+  return n[0] == 256 && n[1] == 256 && n[2] == 256 && P >= 1 && P <= 16 && (32 % P) == 0;
+}
+
+hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs& a, int nzl, hipStream_t s) {
+  if (stage == 1) {
+    const int nk1 = a.lnyl ? (1 << a.lnyl) / 8 : 32;  // local k1 values: nyl / N2
+    const int units = 32 * nk1;                        // x tiles x local k1
+    hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true>), dim3(grid_of(units, 1)), dim3(1024), 0, s, out, a, units);
+  } else {
+    const int units = nzl * 8;  // local z-planes x y2
+    const unsigned g = grid_of(units, 2);
+    if (stage == 0)
+      hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD, 32, 256>), dim3(g), dim3(512), 0, s, in, out, a, units);
+    else
+      hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST, 32, 256>), dim3(g), dim3(512), 0, s, in, out, a, units);
+  }
+  return hipGetLastError();
 }
 
 bool three_pass_shape_valid(int n1, int mid) {

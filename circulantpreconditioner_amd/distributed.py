@@ -19,7 +19,12 @@ from typing import Sequence
 import torch
 
 from ._lib import check, lib
-from .plan import _dev_ptr, _lam6, _stream_handle
+from .plan import PASS_MODES, _dev_ptr, _lam6, _stream_handle
+
+
+def _slab_schedule(schedule) -> int:
+    """'auto' | 'five' | 'three' (CFP_SCHEDULE_AUTO / _FIVE_PASS / _THREE_PASS)"""
+    return {"auto": 0, "five": 1, "three": 2}[schedule] if isinstance(schedule, str) else int(schedule)
 
 
 def slab_layout(dims: Sequence[int], nranks: int, rank: int) -> dict:
@@ -107,6 +112,11 @@ class SlabPlan:
         check(lib().cfp_dist_plan_set_symbol_transport(self._h, _lam6(lam)))
         return self
 
+    def set_schedule(self, schedule: str | int) -> "SlabPlan":
+        """Local passes: 'auto' (3 sweeps at 256^3 with world | 32), 'five' or 'three'."""
+        check(lib().cfp_dist_plan_set_schedule(self._h, _slab_schedule(schedule)))
+        return self
+
     def _all_to_all(self, dst: torch.Tensor, src: torch.Tensor) -> None:
         import torch.distributed as dist
         if dist.get_backend(self.group) == "gloo":  # gloo exchanges host tensors only
@@ -147,8 +157,7 @@ class SlabPlan:
             if ex.value:
                 out.append({"kind": "all-to-all"})
             else:
-                out.append({"kind": "pass", "axis": "xyz"[ax.value], "n": n.value,
-                            "mode": {0: "fwd", 1: "inv", 2: "fused_sep", 3: "fused_diag"}[mode.value]})
+                out.append({"kind": "pass", "axis": "xyz"[ax.value], "n": n.value, "mode": PASS_MODES[mode.value]})
         return out
 
     def profile_begin(self, max_applies: int, every: int = 1) -> bool:
@@ -240,6 +249,11 @@ class SlabGroup:
 
     def set_transport_symbol(self, lam) -> "SlabGroup":
         check(lib().cfp_group_set_symbol_transport(self._h, _lam6(lam)))
+        return self
+
+    def set_schedule(self, schedule: str | int) -> "SlabGroup":
+        """Local passes per slab: 'auto' (3 sweeps at 256^3 with P | 32), 'five' or 'three'."""
+        check(lib().cfp_group_set_schedule(self._h, _slab_schedule(schedule)))
         return self
 
     def scatter(self, full: torch.Tensor) -> list:

@@ -81,6 +81,11 @@ int cfp_dist_plan_time_phases(cfp_dist_plan_t plan, const double *b_dev, double 
  * contract: every `every`-th apply, at most max_applies; _end writes the mean ms per phase) */
 int cfp_dist_plan_profile_begin(cfp_dist_plan_t plan, int max_applies, int every);
 int cfp_dist_plan_profile_end(cfp_dist_plan_t plan, double *ms_out, int *applies);
+/* local passes of each rank: CFP_SCHEDULE_AUTO (3 sweeps -- x + y1 | y2 + z + symbol + inverses |
+ * inverse, cfp_three_pass.hip -- for a 256^3 grid with nranks | 32, else 5 axis passes),
+ * CFP_SCHEDULE_FIVE_PASS, or CFP_SCHEDULE_THREE_PASS (CFP_ERR_SUP where unsupported).  The
+ * exchanges and the per-peer chunk layout are the same for both. */
+int cfp_dist_plan_set_schedule(cfp_dist_plan_t plan, int schedule);
 
 /* single-process group of P slabs; devices[r] = HIP device of slab r (may repeat) */
 int cfp_group_create(cfp_group_t *group, int64_t nx, int64_t ny, int64_t nz, int nranks, const int *devices);
@@ -88,6 +93,7 @@ int cfp_group_destroy(cfp_group_t group);
 int cfp_group_set_symbol_transport(cfp_group_t group, const double lam[6]);
 /* b_devs[r], x_devs[r]: slab r on devices[r]; synchronous */
 int cfp_group_apply(cfp_group_t group, const double *const *b_devs, double *const *x_devs);
+int cfp_group_set_schedule(cfp_group_t group, int schedule); /* as cfp_dist_plan_set_schedule */
 
 #ifdef __cplusplus
 }

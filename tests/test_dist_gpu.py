@@ -7,6 +7,9 @@
   library's kernel segments and the two all-to-alls go through torch.distributed (gloo,
   staged through host memory), so the per-rank plan is exercised across processes.
 * The RCCL executor with world = 1; with more ranks it is exercised by bench.py --gpus N.
+* At 256^3 with P | 32 every rank runs the 3-sweep schedule (x + y1 into the per-peer chunks |
+  y2 + z + symbol + inverses on its k1 rows | inverse), checked against the oracle and
+  against the 5-pass slab schedule.
 """
 import os
 import socket
@@ -54,6 +57,49 @@ def test_group_config5_512_in_8_slabs(oracle):
     assert oracle.rel_l2(got, ref) < TOL
 
 
+@pytest.fixture(scope="module")
+def case256(oracle):
+    dims, lam = (256, 256, 256), (0.6, 0.15 - 0.1j, 0.02)
+    b = oracle.c_fill_uniform(256 ** 3, 17)
+    return dims, lam, b, oracle.c_solve_3d(oracle.c_build_diag_transport(dims, lam), b, dims)
+
+
+@pytest.mark.parametrize("P", [1, 2, 4, 16])
+def test_group_three_sweep_256(P, case256, oracle):
+    """The 3-sweep slab schedule (AUTO at 256^3, P | 32) against the oracle and against the
+    5-pass slab schedule; P = 4 also in place."""
+    from circulantpreconditioner_amd.distributed import SlabGroup
+    dims, lam, b, ref = case256
+    full = torch.from_numpy(b).cuda()
+    with SlabGroup(dims, P) as g:
+        g.set_transport_symbol(lam)
+        bs = g.scatter(full)
+        x3 = torch.cat(g.apply(bs))
+        assert oracle.rel_l2(x3.cpu().numpy(), ref) < TOL
+        g.set_schedule("five")
+        x5 = torch.cat(g.apply(bs))
+        assert float(torch.linalg.vector_norm(x5 - x3) / torch.linalg.vector_norm(x3)) < 1e-13
+        g.set_schedule("three")
+        if P == 4:
+            g.apply(bs, bs)  # in place, as the direct solver's (Un, Un)
+            assert torch.equal(torch.cat(bs), x3)
+        del bs
+
+
+def test_slab_schedule_rules():
+    from circulantpreconditioner_amd import CirculantError
+    from circulantpreconditioner_amd.distributed import SlabGroup
+    with SlabGroup((64, 64, 64), 2) as g:
+        with pytest.raises(CirculantError):
+            g.set_schedule("three")  # 256^3 only
+        g.set_schedule("five").set_schedule("auto")
+    with SlabGroup((256, 256, 256), 32) as g:  # 8 rows per chunk: below the 16 the 3-sweep P3 reads
+        with pytest.raises(CirculantError):
+            g.set_schedule("three")
+        with pytest.raises(CirculantError):
+            g.set_schedule(9)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -87,7 +133,7 @@ def _slab_rank(rank, world, port, dims, lam, seed, q):
 
 
 @pytest.mark.parametrize("dims,world", [((64, 32, 16), 2), ((128, 128, 128), 2), ((64, 64, 64), 4),
-                                        ((100, 20, 10), 2)])
+                                        ((100, 20, 10), 2), ((256, 256, 256), 2)])
 def test_slab_plan_processes_vs_oracle(dims, world, oracle):
     """`world` fresh processes, one SlabPlan rank each, on cuda:0; gathered x vs the oracle."""
     import torch.multiprocessing as mp
@@ -153,6 +199,16 @@ def test_rccl_single_rank(oracle):
             plan.apply(tb, out=x)
         ms, napp = plan.profile_end()
         assert napp == 3 and len(ms) == len(plan.phases()) and all(m >= 0.0 for m in ms)
+        assert oracle.rel_l2(x.cpu().numpy(), ref) < TOL
+        plan.close()
+        # 256^3: the 3-sweep slab schedule through the RCCL executor
+        dims = (256, 256, 256)
+        b = oracle.c_fill_uniform(256 ** 3, 23)
+        ref = oracle.c_solve_3d(oracle.c_build_diag_transport(dims, lam), b, dims)
+        plan = SlabPlan(dims, rank=0, world=1, device=0)
+        plan.set_transport_symbol(lam)
+        assert [p.get("mode") for p in plan.phases()] == ["rows_fwd", None, "mid_fused", None, "rows_inv"]
+        x = plan.apply(torch.from_numpy(b).cuda())
         assert oracle.rel_l2(x.cpu().numpy(), ref) < TOL
         plan.close()
     finally:
