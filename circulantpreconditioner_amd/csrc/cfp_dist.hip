@@ -79,11 +79,14 @@ struct Step {
   int tp;         // >= 0: stage of the 3-sweep slab schedule (cfp_three_pass.hip)
 };
 
-// 256^3 with P | 32: 3 local sweeps per rank (x + y1 | y2 + z + symbol + inverses | inverse),
-// the same two exchanges; otherwise 5 axis passes
+// 256^3: 3 local sweeps per rank (x + y1 | y2 + z + symbol + inverses | inverse), the same two
+// exchanges; otherwise 5 axis passes.  AUTO takes 3 sweeps for P <= 4 only: measured per rank
+// (tools/slab_local_timing.py, profiles/r02i_slab_local.txt) 174 vs 219 us at P = 2 and 90 vs
+// 119 us at P = 4, a tie at P = 8 (P2 has 128 units for 256 CUs) and a loss at P = 16.
 bool slab_three(const SlabLayout& L, int schedule) {
   const i64 n[3] = {L.nx, L.ny, L.nz};
-  return schedule != CFP_SCHEDULE_FIVE_PASS && three_pass_slab_supported(n, L.P);
+  if (schedule == CFP_SCHEDULE_FIVE_PASS || !three_pass_slab_supported(n, L.P)) return false;
+  return schedule == CFP_SCHEDULE_THREE_PASS || L.P <= 4;
 }
 
 std::vector<Step> slab_steps(const SlabLayout& L, int schedule = CFP_SCHEDULE_AUTO) {

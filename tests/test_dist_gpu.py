@@ -7,9 +7,9 @@
   library's kernel segments and the two all-to-alls go through torch.distributed (gloo,
   staged through host memory), so the per-rank plan is exercised across processes.
 * The RCCL executor with world = 1; with more ranks it is exercised by bench.py --gpus N.
-* At 256^3 with P | 32 every rank runs the 3-sweep schedule (x + y1 into the per-peer chunks |
-  y2 + z + symbol + inverses on its k1 rows | inverse), checked against the oracle and
-  against the 5-pass slab schedule.
+* At 256^3 (AUTO for P <= 4, on request up to P = 16) every rank runs the 3-sweep schedule
+  (x + y1 into the per-peer chunks | y2 + z + symbol + inverses on its k1 rows | inverse),
+  checked against the oracle and against the 5-pass slab schedule.
 """
 import os
 import socket
@@ -64,7 +64,7 @@ def case256(oracle):
     return dims, lam, b, oracle.c_solve_3d(oracle.c_build_diag_transport(dims, lam), b, dims)
 
 
-@pytest.mark.parametrize("P", [1, 2, 4, 16])
+@pytest.mark.parametrize("P", [1, 2, 4, 8, 16])
 def test_group_three_sweep_256(P, case256, oracle):
     """The 3-sweep slab schedule (AUTO at 256^3, P | 32) against the oracle and against the
     5-pass slab schedule; P = 4 also in place."""
@@ -72,7 +72,7 @@ def test_group_three_sweep_256(P, case256, oracle):
     dims, lam, b, ref = case256
     full = torch.from_numpy(b).cuda()
     with SlabGroup(dims, P) as g:
-        g.set_transport_symbol(lam)
+        g.set_transport_symbol(lam).set_schedule("three")  # AUTO picks it for P <= 4
         bs = g.scatter(full)
         x3 = torch.cat(g.apply(bs))
         assert oracle.rel_l2(x3.cpu().numpy(), ref) < TOL
