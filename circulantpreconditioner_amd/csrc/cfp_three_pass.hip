@@ -109,11 +109,18 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
       if (INV) {  // chunked rows y2 + N2 ty + N2 TY m: per-thread part + uniform part (nyl >= N2 TY)
         const cd* const src = in + crow(u / N2, u % N2 + N2 * ty) + x;
 #pragma unroll
-        for (int m = 0; m < 16; ++m) v[m] = cconj(gload<FLAGS>(src + crow(0, N2 * TY * m)));
+        for (int m = 0; m < 16; ++m) v[m] = gload<FLAGS>(src + crow(0, N2 * TY * m));
+        // all 16 loads go out before the first butterfly: with runtime strides the scheduler
+        // otherwise starts the DFT after 9 of them and issues the rest a memory latency later
+        // (P3 100 -> 93 us at 256^3)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = cconj(v[m]);
       } else {
         const cd* const src = in + (i64)(u / N2) * TN * TN + x + (i64)TN * (u % N2 + N2 * ty);  // + uniform
 #pragma unroll
         for (int m = 0; m < 16; ++m) v[m] = gload<FLAGS>(src + (i64)TN * N2 * TY * m);
+        __builtin_amdgcn_sched_barrier(0);
       }
       // phase A: N1-point DFT over y1 for every x (column mode, 256 columns x TY threads)
       fft_stages<N1, 16, N1 / 16, false, TN, F>(v, lds, tw_l, x, ty, true);  // v[m]: k1 = ty + TY m
