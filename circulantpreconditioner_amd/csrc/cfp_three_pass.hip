@@ -694,6 +694,7 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
         const cd* src = reinterpret_cast<const cd*>(in_r) + ((i64)z * NY + y2 + N2 * r) * M + tpc;
 #pragma unroll
         for (int t = 0; t < PTS; ++t) v[t] = src[TPC * t];
+        __builtin_amdgcn_sched_barrier(0);  // all loads out before the first butterfly
         fft_stages<M, PTS, 2, true, N1, F>(v, lds, tw_m, r, tpc, true);  // 128 = 2 x 8 x 8; v[t] = Z[tpc + TPC t]
       }
       to_columns_r2c(v, z, y2);
@@ -709,7 +710,10 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
         const int x = idx(x0), ty = idx(ty0);
         const cd* src = H + ((i64)z * NY + y2 + N2 * ty) * M + x;
 #pragma unroll
-        for (int m = 0; m < PTS; ++m) v[m] = cconj(src[(i64)N2 * TY * M * m]);
+        for (int m = 0; m < PTS; ++m) v[m] = src[(i64)N2 * TY * M * m];
+        __builtin_amdgcn_sched_barrier(0);  // all loads out before the first butterfly (measured neutral here)
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
         fft_stages<N1, PTS, 4, false, M, F>(v, lds, tw_1, x, ty, true);  // v[m]: y1 = ty + TY m
       }
       to_rows_c2r(v, z, y2);
