@@ -813,11 +813,14 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
   // other shapes are selected per plan (cfp_plan_set_three_pass_shape) for tests and measurements.
   const int n1 = shape.n1 == 64 ? 64 : 32;
   const bool t32 = shape.mid == TP_MID_LANE32;
+  // the LDS-DMA prefetch (global_load_lds_dwordx4) takes 16-byte aligned addresses: a buffer that
+  // is only 8-byte aligned runs the same kernel without it
+  const bool pf_ok = ((uintptr_t)out & 15) == 0;
   if (stage == 1) {
-    if (shape.mid == TP_MID_SWAP64_PF || shape.mid == TP_MID_DEFAULT) {
+    if ((shape.mid == TP_MID_SWAP64_PF || shape.mid == TP_MID_DEFAULT) && pf_ok) {
       if (n1 == 64) launch_mid_sw<4, 256, true>(out, a, s);
       else launch_mid_sw<8, 256, true>(out, a, s);
-    } else if (shape.mid == TP_MID_SWAP64) {
+    } else if (shape.mid == TP_MID_SWAP64 || shape.mid == TP_MID_SWAP64_PF || shape.mid == TP_MID_DEFAULT) {
       if (n1 == 64) launch_mid_sw<4, 256>(out, a, s);
       else launch_mid_sw<8, 256>(out, a, s);
     } else if (n1 == 64) {

@@ -467,6 +467,27 @@ def test_three_pass_variants(cp, tp_case, n1, mid):
         assert torch.equal(t_, x)
 
 
+def test_three_pass_8_byte_aligned(cp, tp_case):
+    """The 3-sweep apply on buffers that are 8- but not 16-byte aligned (the LDS-DMA prefetch of
+    the middle kernel needs 16-byte addresses; such buffers run it without the prefetch)."""
+    n, lam, b, ref = tp_case
+    N = 256 ** 3
+    raw = torch.empty(2 * N + 1, dtype=torch.float64, device="cuda")  # raw[1:] starts 8 bytes past a 16-byte boundary
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam)
+        bd = _dev(b)
+        x = plan.apply(bd)
+        assert _rel(x, ref) < TOL
+        # drive the ABI directly with an 8-byte offset into a float64 buffer holding b
+        raw[1:].copy_(torch.view_as_real(bd).reshape(-1))
+        ptr = raw.data_ptr() + 8
+        from circulantpreconditioner_amd._lib import check, lib
+        check(lib().cfp_plan_apply(plan._h, ptr, ptr, None))
+        torch.cuda.synchronize()
+        got = torch.view_as_complex(raw[1:].clone().reshape(-1, 2))
+        assert torch.equal(got, x)
+
+
 def _random_grids(count=48, seed=2025, max_points=1 << 21):
     menu = [1, 2, 3, 4, 5, 7, 8, 10, 11, 12, 13, 16, 20, 24, 25, 27, 30, 31, 32, 36, 40, 49, 50, 60, 64, 81, 96,
             97, 100, 125, 128, 200, 243, 256, 300, 512]
