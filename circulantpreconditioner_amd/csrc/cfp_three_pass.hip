@@ -781,7 +781,10 @@ hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs
   if (stage == 1) {
     const int nk1 = a.lnyl ? (1 << a.lnyl) / 8 : 32;  // local k1 values: nyl / N2
     const int units = 32 * nk1;                        // x tiles x local k1
-    hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true>), dim3(grid_of(units, 1)), dim3(1024), 0, s, out, a, units);
+    if (((uintptr_t)out & 15) == 0)  // the LDS-DMA prefetch needs 16-byte addresses
+      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true>), dim3(grid_of(units, 1)), dim3(1024), 0, s, out, a, units);
+    else
+      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, false>), dim3(grid_of(units, 1)), dim3(1024), 0, s, out, a, units);
   } else {
     const int units = nzl * 8;  // local z-planes x y2
     const unsigned g = grid_of(units, 2);
