@@ -152,6 +152,8 @@ extern "C" PetscErrorCode KSPMiniSetUpWork(KSP k, Vec v) {
 }
 
 static PetscErrorCode pc_apply(KSP k, Vec x, Vec y) {
+  // drain the MatMult queued just before, so pc_seconds holds only PCApply's own time
+  PetscCall(VecMiniSynchronize(x));
   const double t0 = now();
   PetscCall(PCApply(k->pc, x, y));
   k->pc_seconds += now() - t0;

@@ -78,6 +78,14 @@ static PetscErrorCode vcheck(Vec v, const char* f) {
 }
 #define VCHK(v) PetscCall(vcheck((v), __func__))
 
+// wait for the kernels already queued on the Vec stream (no-op for a host vector), so a
+// host-timed region that starts here does not include earlier asynchronous work
+extern "C" PetscErrorCode VecMiniSynchronize(Vec v) {
+  VCHK(v);
+  if (v->hip) HCHK(hipStreamSynchronize(g_stream));
+  return PETSC_SUCCESS;
+}
+
 static PetscErrorCode ensure_host(Vec v) {
   if (!v->h) {
     v->h = (cd*)calloc((size_t)(v->n > 0 ? v->n : 1), sizeof(cd));

@@ -160,6 +160,8 @@ PetscErrorCode VecDuplicateVecs(Vec v, PetscInt m, Vec *V[]);
 PetscErrorCode VecDestroyVecs(PetscInt m, Vec *V[]);
 /* stream the Vec kernels are enqueued on (hipStream_t, NULL = default); not in PETSc */
 PetscErrorCode VecMiniSetStream(void *stream);
+/* wait for the work queued on that stream if v is a device vector; not in PETSc */
+PetscErrorCode VecMiniSynchronize(Vec v);
 
 /* ---- Mat */
 PetscErrorCode MatCreateShell(MPI_Comm comm, PetscInt m, PetscInt n, PetscInt M, PetscInt N, void *ctx, Mat *A);
