@@ -159,8 +159,9 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--grid", type=int, nargs="+", default=[256])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--schedule", default="auto", choices=["auto", "five", "five_y", "three"],
-                    help="apply schedule: 5 axis passes fused on z (auto) or y, or 3 sweeps (256^3)")
+    ap.add_argument("--schedule", default="auto", choices=["auto", "five", "five_y", "three", "plane"],
+                    help="apply schedule: 5 axis passes fused on z or y, 3 sweeps (256^3), or plane "
+                         "(n_x = n_y in {64, 100, 128}); auto = the plan's default")
     ap.add_argument("--tp-shape", default=None, metavar="N1,MID",
                     help="3-sweep kernel shape (measurements): y split n1 (0/32/64) and middle kernel "
                          "(default, lane64, lane32, swap64); default: the plan's")

@@ -24,6 +24,7 @@ enum : int {
   F_OCC4 = 128,     // ask the compiler for 4 waves per SIMD (<= 128 VGPRs)
   F_SYM_LDS = 256,  // fused pass: stage the per-point symbol table in LDS next to the twiddles
   F_OCC8 = 512,     // ask the compiler for 8 waves per SIMD (<= 64 VGPRs)
+  F_PAD1 = 1024,    // row-mode LDS rows padded by one element (n + 1) instead of n / 16
 };
 __host__ __device__ constexpr int waves_req(int flags, int mode) {
   return mode == PASS_FUSED_WAVE ? 1 : ((flags & F_OCC8) ? 8 : ((flags & F_OCC4) ? 4 : 1));
@@ -399,9 +400,11 @@ struct Shape {
   static_assert(PTS % R0 == 0, "R0 must divide PTS");
 };
 
-// LDS index of element idx of the workgroup's column c (row mode pads every 16 elements)
-template <int N, bool ROW, int T>
+// LDS index of element idx of the workgroup's column c (row mode pads every 16 elements, or
+// with F_PAD1 one element per row)
+template <int N, bool ROW, int T, int FLAGS = 0>
 __device__ __forceinline__ int lds_idx(int c, int idx) {
+  if constexpr (FLAGS & F_PAD1) return ROW ? c * (N + 1) + idx : idx * T + c;
   constexpr int RS = N + N / 16;
   return ROW ? c * RS + idx + (idx >> 4) : idx * T + c;
 }
@@ -417,23 +420,23 @@ __device__ __forceinline__ void exchange(void* ldsv, cd* vals, WP wpos, cd* dst,
   if (FLAGS & F_SPLIT_LDS) {
     double* lds = (double*)ldsv;
 #pragma unroll
-    for (int k = 0; k < K; ++k) lds[lds_idx<N, ROW, T>(c, wpos(k))] = vals[k].x;
+    for (int k = 0; k < K; ++k) lds[lds_idx<N, ROW, T, FLAGS>(c, wpos(k))] = vals[k].x;
     xbarrier<FLAGS>();
 #pragma unroll
-    for (int t = 0; t < PTS; ++t) dst[t].x = lds[lds_idx<N, ROW, T>(c, rpos(t))];
+    for (int t = 0; t < PTS; ++t) dst[t].x = lds[lds_idx<N, ROW, T, FLAGS>(c, rpos(t))];
     xbarrier<FLAGS>();
 #pragma unroll
-    for (int k = 0; k < K; ++k) lds[lds_idx<N, ROW, T>(c, wpos(k))] = vals[k].y;
+    for (int k = 0; k < K; ++k) lds[lds_idx<N, ROW, T, FLAGS>(c, wpos(k))] = vals[k].y;
     xbarrier<FLAGS>();
 #pragma unroll
-    for (int t = 0; t < PTS; ++t) dst[t].y = lds[lds_idx<N, ROW, T>(c, rpos(t))];
+    for (int t = 0; t < PTS; ++t) dst[t].y = lds[lds_idx<N, ROW, T, FLAGS>(c, rpos(t))];
   } else {
     cd* lds = (cd*)ldsv;
 #pragma unroll
-    for (int k = 0; k < K; ++k) lds[lds_idx<N, ROW, T>(c, wpos(k))] = vals[k];
+    for (int k = 0; k < K; ++k) lds[lds_idx<N, ROW, T, FLAGS>(c, wpos(k))] = vals[k];
     xbarrier<FLAGS>();
 #pragma unroll
-    for (int t = 0; t < PTS; ++t) dst[t] = lds[lds_idx<N, ROW, T>(c, rpos(t))];
+    for (int t = 0; t < PTS; ++t) dst[t] = lds[lds_idx<N, ROW, T, FLAGS>(c, rpos(t))];
   }
 }
 

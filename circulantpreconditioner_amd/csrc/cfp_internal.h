@@ -43,6 +43,9 @@ enum PassMode : int {
   // long axes (n = n1 n2 > 4096, four-step) with no short axis to fuse: the symbol divide as
   // its own sweep over the position-ordered spectrum (cfp_plan.hip); reported, not dispatched
   PASS_SYM_DIVIDE = 8,
+  // plane schedule (n_x = n_y small): x and y DFTs of whole z-planes in one launch
+  PASS_PLANE_FWD = 9,
+  PASS_PLANE_INV = 10,
 };
 
 // Four-step twiddle of a long axis split n = n1 n2 (index k1 + n1 k2): the length-n2 pass over
@@ -85,6 +88,11 @@ __host__ __device__ inline cd make_cd(double x, double y) { cd r; r.x = x; r.y =
 // Launchers (cfp_kernels.hip).  tw = forward twiddle table W_n[k] = exp(-2 pi i k / n), k < n.
 hipError_t launch_axis_pass(const PassDesc& p, const cd* in, cd* out, const cd* tw, hipStream_t s);
 bool fast_path_supported(const PassDesc& p);
+// plane pass: the x and y DFTs of `planes` whole n x n z-planes in one launch (forward, or the
+// conjugated inverse with `scale`); plane_supported(n) lists the built n
+bool plane_supported(i64 n);
+hipError_t launch_plane_pass(bool inverse, int n, i64 planes, const cd* in, cd* out, const cd* tw, double scale,
+                             hipStream_t s);
 hipError_t launch_pointwise_divide(cd* w, const cd* x, const cd* y, i64 n, hipStream_t s);
 hipError_t launch_scale(cd* x, cd alpha, i64 n, hipStream_t s);
 hipError_t launch_fill_uniform(cd* x, i64 n, uint64_t seed, i64 offset, hipStream_t s);

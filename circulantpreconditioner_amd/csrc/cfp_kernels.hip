@@ -665,6 +665,113 @@ hipError_t launch_axis_pass(const PassDesc& p, const cd* in, cd* out, const cd* 
   return launch_generic(p, in, out, a, s);
 }
 
+// ----------------------------------------------------------------- plane pass
+// The x and y DFTs of one whole n x n z-plane per workgroup (n * n/PTS <= 1024 threads, the
+// plane staged through LDS: PlaneCfg), so the apply of an
+// n^2 x n_z grid is 3 sweeps -- plane forward, the fused z pass, plane inverse -- instead of 5.
+// At the reference's default mesh (100^3) the five passes are launch-cost bound (11-15 us for a
+// 32 MB sweep that sits in the Infinity Cache; profiles/r02r_100_kernel_stats.md).
+//   forward: rows (thread = row y, points x = t + m TPC, row mode) -> x DFT -> transpose through
+//            LDS -> columns (thread = column kx, points y) -> y DFT -> coalesced store along kx
+//   inverse: the mirror (conjugated input, column y DFT first, row x DFT, conjugate * scale)
+// SPLIT: the plane moves through LDS in real / imaginary halves (n (n + n/16) doubles), else
+// whole complex values with rows padded by one element (n (n + 1) complex: 158 KiB at n = 100)
+template <int N> struct PlaneCfg;
+template <> struct PlaneCfg<64> { static constexpr int PTS = 8, R0 = 8; static constexpr bool SPLIT = false; };
+template <> struct PlaneCfg<100> { static constexpr int PTS = 10, R0 = 10; static constexpr bool SPLIT = false; };
+template <> struct PlaneCfg<128> { static constexpr int PTS = 16, R0 = 8; static constexpr bool SPLIT = true; };
+
+// element (y, x) of the plane at LDS y * N + x
+template <int N, int PTS, int FLAGS, class WP, class RP>
+__device__ __forceinline__ void plane_transpose(double* lds, cd* v, WP wpos, RP rpos) {
+  xbarrier<FLAGS>();  // the previous exchange's reads
+  if constexpr (!(FLAGS & F_SPLIT_LDS)) {
+    cd* l = (cd*)lds;
+#pragma unroll
+    for (int m = 0; m < PTS; ++m) l[wpos(m)] = v[m];
+    xbarrier<FLAGS>();
+#pragma unroll
+    for (int m = 0; m < PTS; ++m) v[m] = l[rpos(m)];
+    return;
+  }
+#pragma unroll
+  for (int m = 0; m < PTS; ++m) lds[wpos(m)] = v[m].x;
+  xbarrier<FLAGS>();
+#pragma unroll
+  for (int m = 0; m < PTS; ++m) v[m].x = lds[rpos(m)];
+  xbarrier<FLAGS>();
+#pragma unroll
+  for (int m = 0; m < PTS; ++m) lds[wpos(m)] = v[m].y;
+  xbarrier<FLAGS>();
+#pragma unroll
+  for (int m = 0; m < PTS; ++m) v[m].y = lds[rpos(m)];
+}
+
+template <int N, bool INV>
+__global__ void __launch_bounds__(N*(N / PlaneCfg<N>::PTS)) k_plane(const cd* in, cd* out, const cd* tw, double scale) {
+  constexpr int PTS = PlaneCfg<N>::PTS, R0 = PlaneCfg<N>::R0, TPC = N / PTS, NT = N * TPC;
+  // the forward pass reads b (cold); the inverse writes x (not read again by this apply)
+  constexpr bool SPLIT = PlaneCfg<N>::SPLIT;
+  constexpr int FLAGS = (SPLIT ? F_SPLIT_LDS : F_PAD1) | (INV ? F_NT_ST : F_NT_LD);
+  __shared__ __attribute__((aligned(16))) double lds[SPLIT ? N * (N + N / 16) : 2 * N * (N + 1)];
+  __shared__ cd tws[N];
+  const int tid = threadIdx.x;
+  const int ry = tid / TPC, rt = tid % TPC;  // row mode: row y, points x = rt + m TPC
+  const int cx = tid % N, ct = tid / N;      // column mode: column x, points y = ct + m TPC
+  const i64 base = (i64)blockIdx.x * N * N;
+  const cd* pin = in + base;
+  cd* pout = out + base;
+  cd v[PTS];
+  if (!INV) {
+#pragma unroll
+    for (int m = 0; m < PTS; ++m) v[m] = gload<FLAGS>(pin + ry * N + rt + m * TPC);
+  } else {
+#pragma unroll
+    for (int m = 0; m < PTS; ++m) v[m] = gload<FLAGS>(pin + (ct + m * TPC) * N + cx);
+  }
+  for (int i = tid; i < N; i += NT) tws[i] = tw[i];  // published by the first exchange's barrier
+  if (!INV) {
+    fft_stages<N, PTS, R0, true, N, FLAGS>(v, lds, tws, ry, rt, true);
+    plane_transpose<N, PTS, FLAGS>(
+        lds, v, [&](int m) { return ry * N + rt + m * TPC; }, [&](int m) { return (ct + m * TPC) * N + cx; });
+    fft_stages<N, PTS, R0, false, N, FLAGS>(v, lds, tws, cx, ct, false);
+#pragma unroll
+    for (int m = 0; m < PTS; ++m) gstore<FLAGS>(pout + (ct + m * TPC) * N + cx, v[m]);
+  } else {
+#pragma unroll
+    for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
+    fft_stages<N, PTS, R0, false, N, FLAGS>(v, lds, tws, cx, ct, true);
+    plane_transpose<N, PTS, FLAGS>(
+        lds, v, [&](int m) { return (ct + m * TPC) * N + cx; }, [&](int m) { return ry * N + rt + m * TPC; });
+    fft_stages<N, PTS, R0, true, N, FLAGS>(v, lds, tws, ry, rt, false);
+    const double sy = -scale;
+#pragma unroll
+    for (int m = 0; m < PTS; ++m) gstore<FLAGS>(pout + ry * N + rt + m * TPC, make_cd(v[m].x * scale, v[m].y * sy));
+  }
+}
+
+bool plane_supported(i64 n) { return n == 64 || n == 100 || n == 128; }
+
+template <int N>
+static hipError_t launch_plane_t(bool inverse, i64 planes, const cd* in, cd* out, const cd* tw, double scale,
+                                 hipStream_t s) {
+  constexpr int NT = N * (N / PlaneCfg<N>::PTS);
+  if (inverse) hipLaunchKernelGGL((k_plane<N, true>), dim3((unsigned)planes), dim3(NT), 0, s, in, out, tw, scale);
+  else hipLaunchKernelGGL((k_plane<N, false>), dim3((unsigned)planes), dim3(NT), 0, s, in, out, tw, scale);
+  return hipGetLastError();
+}
+
+hipError_t launch_plane_pass(bool inverse, int n, i64 planes, const cd* in, cd* out, const cd* tw, double scale,
+                             hipStream_t s) {
+  if (planes <= 0) return hipSuccess;
+  switch (n) {
+    case 64: return launch_plane_t<64>(inverse, planes, in, out, tw, scale, s);
+    case 100: return launch_plane_t<100>(inverse, planes, in, out, tw, scale, s);
+    case 128: return launch_plane_t<128>(inverse, planes, in, out, tw, scale, s);
+    default: return hipErrorNotSupported;
+  }
+}
+
 // ----------------------------------------------------------------- elementwise kernels
 #define CFP_EW_THREADS 256
 

@@ -193,6 +193,17 @@ bool use_three_pass(const cfp_plan_s* p, bool diag_override) {
   return three_pass_supported(p->n);
 }
 
+// the plane schedule (n_x = n_y in {64, 100, 128}, n_z > 1): plane forward (x + y DFTs of
+// whole z-planes), the fused z pass, plane inverse -- on request, and by default for 100^2 and
+// 64^2 planes, where the five passes are launch-cost bound
+bool use_plane(const cfp_plan_s* p) {
+  if (p->external_x || p->long_axes() || p->n[0] != p->n[1] || !plane_supported(p->n[0]) || p->n[2] < 2)
+    return false;
+  if (p->schedule == CFP_SCHEDULE_PLANE) return true;
+  // (128^2 planes lose to the 5 passes: 15,400 vs 17,100 PCApply/s, profiles/r02t_plane_schedule.md)
+  return p->schedule == CFP_SCHEDULE_AUTO && p->chunk_planes == 0 && (p->n[0] == 100 || p->n[0] == 64);
+}
+
 // axis order of the 5-pass schedule: the last one is fused with the symbol
 void order_axes(cfp_plan_s* p) {
   p->axes.clear();
@@ -225,6 +236,12 @@ std::vector<Step> apply_steps(const cfp_plan_s* p, bool diag_override = false) {
     st.push_back({0, PASS_TP_ROWS_FWD, true, false, 0, -1, 0});
     st.push_back({2, PASS_TP_MID, false, false, 0, -1, 1});
     st.push_back({0, PASS_TP_ROWS_INV, false, true, 0, -1, 2});
+    return st;
+  }
+  if (use_plane(p)) {
+    st.push_back({3, PASS_PLANE_FWD, true, false, 0, -1, -1, 4});
+    st.push_back({2, -1, false, false, 0, -1, -1, 0});
+    st.push_back({3, PASS_PLANE_INV, false, true, 0, -1, -1, 4});
     return st;
   }
   const std::vector<int>& A = p->axes;
@@ -360,6 +377,16 @@ int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStr
       if (ev) HIPCHK(hipEventRecord((*ev)[i], s));
       hipError_t e = launch_three_pass(q.tp, tn, q.from_b ? b : x, x, a, p->tp_shape, s);
       if (e != hipSuccess) return hip_error(e, "3-sweep launch");
+      continue;
+    }
+    if (q.sub == 4) {
+      const int pn = (int)p->n[0];
+      int prc = ensure_tw(p, pn);
+      if (prc) return prc;
+      if (ev) HIPCHK(hipEventRecord((*ev)[i], s));
+      hipError_t e = launch_plane_pass(q.mode == PASS_PLANE_INV, pn, p->n[2], q.from_b ? b : x, x, p->tw[pn],
+                                       q.scale ? invN : 1.0, s);
+      if (e != hipSuccess) return hip_error(e, "plane pass launch");
       continue;
     }
     if (q.sub == 3) {
@@ -737,8 +764,11 @@ extern "C" int cfp_plan_set_chunking(cfp_plan_t p, int64_t chunk_planes) {
 
 extern "C" int cfp_plan_set_schedule(cfp_plan_t p, int schedule) {
   if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
-  if (schedule < CFP_SCHEDULE_AUTO || schedule > CFP_SCHEDULE_FIVE_PASS_YFUSED)
+  if (schedule < CFP_SCHEDULE_AUTO || schedule > CFP_SCHEDULE_PLANE)
     return set_error(CFP_ERR_ARG_OUTOFRANGE, "unknown schedule %d", schedule);
+  if (schedule == CFP_SCHEDULE_PLANE &&
+      (p->n[0] != p->n[1] || !plane_supported(p->n[0]) || p->n[2] < 2 || p->long_axes() || p->external_x))
+    return set_error(CFP_ERR_SUP, "the plane schedule needs n_x = n_y in {64, 100, 128} and n_z > 1");
   if (schedule == CFP_SCHEDULE_THREE_PASS && !three_pass_supported(p->n))
     return set_error(CFP_ERR_SUP, "the 3-sweep schedule needs a 128^3 or 256^3 grid");
   DeviceGuard dg(p->device);
@@ -792,6 +822,14 @@ extern "C" int cfp_plan_pass_info(cfp_plan_t p, int pass, int* axis, int* n, int
     if (axis) *axis = st[pass].tp == 1 ? 4 : 3;
     if (n) *n = (int)p->n[0];
     if (ncols) *ncols = p->N / p->n[0];
+    if (mode) *mode = st[pass].mode;
+    if (fast) *fast = 1;
+    return CFP_SUCCESS;
+  }
+  if (st[pass].sub == 4) {  // plane passes: axis 3 = "x + y"
+    if (axis) *axis = 3;
+    if (n) *n = (int)p->n[0];
+    if (ncols) *ncols = p->n[2];
     if (mode) *mode = st[pass].mode;
     if (fast) *fast = 1;
     return CFP_SUCCESS;

@@ -52,7 +52,7 @@ def _lam6(lam: Sequence) -> ctypes.Array:
 
 
 PASS_MODES = {0: "fwd", 1: "inv", 2: "fused_sep", 3: "fused_diag", 4: "fused_wave", 5: "rows_fwd", 6: "mid_fused",
-              7: "rows_inv", 8: "sym_divide"}
+              7: "rows_inv", 8: "sym_divide", 9: "plane_fwd", 10: "plane_inv"}
 PASS_AXES = {-1: "-", 0: "x", 1: "y", 2: "z", 3: "xy", 4: "yz"}
 
 
@@ -156,10 +156,11 @@ class CirculantPlan:
         check(lib().cfp_plan_set_chunking(self._h, int(chunk_planes)))
         return self
 
-    SCHEDULES = {"auto": 0, "five": 1, "three": 2, "five_y": 3}
+    SCHEDULES = {"auto": 0, "five": 1, "three": 2, "five_y": 3, "plane": 4}
 
     def set_schedule(self, schedule: str | int) -> "CirculantPlan":
-        """'auto'/'five' (z fused), 'five_y' (y fused) or 'three' (256^3: 3 sweeps)."""
+        """'auto'/'five' (z fused), 'five_y' (y fused), 'three' (256^3: 3 sweeps) or 'plane'
+        (n_x = n_y in {64, 100, 128}: x + y DFTs of whole z-planes | fused z | inverse planes)."""
         v = self.SCHEDULES[schedule] if isinstance(schedule, str) else int(schedule)
         check(lib().cfp_plan_set_schedule(self._h, v))
         return self

@@ -99,11 +99,15 @@ int cfp_plan_set_chunking(cfp_plan_t plan, int64_t chunk_planes);
  * (separable symbol, no chunking), YFUSED when ny, nz >= 512, else FIVE_PASS.  THREE_PASS
  * (128^3 and 256^3 plans only, CFP_ERR_SUP
  * otherwise; an explicit Diag still takes 5 passes): x + first y stage | last y stage + z +
- * symbol + inverses | inverse of the first, 96 N bytes instead of 160 N. */
+ * symbol + inverses | inverse of the first, 96 N bytes instead of 160 N.
+ * PLANE (n_x = n_y in {64, 100, 128}, n_z > 1; CFP_ERR_SUP otherwise; AUTO picks it for
+ * n_x = n_y = 100 -- the reference's default mesh -- and 64): x + y DFTs of whole z-planes | z fused with
+ * the symbol | inverse planes, 3 launches instead of 5 (any symbol, explicit Diag included). */
 #define CFP_SCHEDULE_AUTO 0
 #define CFP_SCHEDULE_FIVE_PASS 1
 #define CFP_SCHEDULE_THREE_PASS 2
 #define CFP_SCHEDULE_FIVE_PASS_YFUSED 3
+#define CFP_SCHEDULE_PLANE 4
 int cfp_plan_set_schedule(cfp_plan_t plan, int schedule);
 /* Kernel shape of the 3-sweep schedule at 256^3, for tests and measurements (0, 0 = the
  * measured default; the shape never changes the result beyond rounding).  n1: the y split

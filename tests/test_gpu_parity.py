@@ -422,7 +422,7 @@ def test_three_pass_schedule_rules(cp):
     with cp.CirculantPlan((64, 64, 64)) as plan:
         with pytest.raises(cp.CirculantError):
             plan.set_schedule("three")
-        plan.set_transport_symbol((0.5, 0.5, 0.5))
+        plan.set_transport_symbol((0.5, 0.5, 0.5)).set_schedule("five")
         assert len(plan.passes()) == 5
 
 
@@ -443,6 +443,51 @@ def test_three_pass_128_vs_oracle(cp, oracle, lam):
         assert torch.equal(t, x)
         plan.set_schedule("five")
         assert _rel(plan.apply(_dev(b)), x) < 1e-13
+
+
+# ------------------------------------------------------------------ plane schedule (n_x = n_y)
+@pytest.mark.parametrize("n", [(100, 100, 100), (64, 64, 64), (128, 128, 128), (100, 100, 7), (64, 64, 2),
+                               (128, 128, 10)])
+def test_plane_vs_oracle(cp, oracle, n):
+    """x + y DFTs of whole z-planes | fused z | inverse planes: against the oracle (separable
+    symbol and explicit Diag), in place, and against the 5-pass schedule."""
+    lam = (0.3 + 0.2j, 1.1, 0.7 - 0.4j)
+    N = int(np.prod(n))
+    b = oracle.c_fill_uniform(N, 41)
+    diag = oracle.c_build_diag_transport(n, lam)
+    ref = oracle.c_solve_3d(diag, b, n)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam).set_schedule("plane")
+        assert [p["mode"] for p in plan.passes()] == ["plane_fwd", "fused_sep", "plane_inv"]
+        x = plan.apply(_dev(b))
+        assert _rel(x, ref) < TOL
+        t = _dev(b)
+        plan.apply(t, out=t)
+        assert torch.equal(t, x)
+        assert _rel(plan.apply_with_diag(_dev(diag), _dev(b)), ref) < TOL
+        plan.set_schedule("five")
+        assert len(plan.passes()) == 5
+        assert _rel(plan.apply(_dev(b)), x) < 1e-13
+
+
+def test_plane_schedule_rules(cp):
+    with cp.CirculantPlan((100, 100, 100)) as plan:
+        plan.set_transport_symbol((0.5, 0.5, 0.5))
+        assert [p["mode"] for p in plan.passes()] == ["plane_fwd", "fused_sep", "plane_inv"]  # AUTO at 100^3
+        plan.set_chunking(10)
+        assert len(plan.passes()) == 4 * 10 + 1  # chunking asked for: the chunked 5-pass schedule
+        plan.set_chunking(0).set_schedule("five")
+        assert len(plan.passes()) == 5
+    for n in ((64, 32, 16), (256, 256, 256), (100, 100, 1), (50, 50, 50)):
+        with cp.CirculantPlan(n) as plan:
+            with pytest.raises(cp.CirculantError):
+                plan.set_schedule("plane")
+    with cp.CirculantPlan((64, 64, 64)) as plan:  # AUTO: planes for 64^2 too
+        plan.set_transport_symbol((0.5, 0.5, 0.5))
+        assert len(plan.passes()) == 3
+    with cp.CirculantPlan((128, 128, 128)) as plan:  # ... but not for 128^2 (slower there)
+        plan.set_transport_symbol((0.5, 0.5, 0.5))
+        assert len(plan.passes()) == 5
 
 
 @pytest.fixture(scope="module")
