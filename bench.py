@@ -167,6 +167,8 @@ def main() -> int:
                          "(default, lane64, lane32, swap64); default: the plan's")
     ap.add_argument("--chunk", type=int, default=None,
                     help="z-planes per chunk of the Infinity-Cache-resident x/y schedule (0 = off; default: plan's)")
+    ap.add_argument("--graph", action="store_true",
+                    help="single GPU: replay each apply as one captured HIP graph (cfp_plan_set_graph)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--settle-ms", type=float, default=300.0,
                     help="untimed applies for this long after the warm-up (clock ramp-up; 0 = off)")
@@ -226,6 +228,8 @@ def main() -> int:
             if args.tp_shape:
                 n1, mid = args.tp_shape.split(",")
                 plan.set_three_pass_shape(int(n1), mid)
+            if args.graph:
+                plan.set_graph(True)
             return plan, b, x, (lambda: plan.apply(b, out=x)), "single GPU"
         from circulantpreconditioner_amd.distributed import SlabPlan
 

@@ -46,6 +46,7 @@ def _declare(L) -> None:
         "cfp_plan_forward": ([vp, dp, dp, vp], c_int),
         "cfp_plan_backward": ([vp, dp, dp, vp], c_int),
         "cfp_plan_set_chunking": ([vp, i64], c_int),
+        "cfp_plan_set_graph": ([vp, c_int], c_int),
         "cfp_plan_set_schedule": ([vp, c_int], c_int),
         "cfp_plan_set_three_pass_shape": ([vp, c_int, c_int], c_int),
         "cfp_rplan_create": ([P(vp), i64, i64, i64, c_int], c_int),

@@ -127,6 +127,18 @@ struct cfp_plan_s {
   cd* axsym = nullptr;    //            per point of the fused axis
   cd* diag = nullptr;     // explicit
   cd* host_stage = nullptr;  // device staging buffers for cfp_plan_apply_host
+  // HIP-graph replay (cfp_plan_set_graph): one instantiated graph of the apply's launches per
+  // (b, x) pair, captured on a private stream and launched into the caller's stream.  A graph
+  // holds device pointers, not values: every setter that can move a buffer or change the
+  // launch list drops them (graph_clear); a value written into a symbol or Diag buffer is seen.
+  struct GraphEntry {
+    const cd* b;
+    cd* x;
+    hipGraphExec_t exec;
+  };
+  bool graph_on = false;
+  hipStream_t cap_stream = nullptr;
+  std::vector<GraphEntry> graphs;
   std::vector<int> axes;     // non-trivial axes, x..z
   int fused_axis = 0;
   std::vector<cd> sym1d[3];  // separable: lambda_d * c_d_hat (host copies)
@@ -431,7 +443,15 @@ int run_transform(cfp_plan_s* p, bool inverse, const cd* in, cd* out, hipStream_
   return CFP_SUCCESS;
 }
 
+constexpr size_t kMaxGraphs = 64;  // GMRES(30) applies the PC to ~32 distinct Krylov vectors
+
+void graph_clear(cfp_plan_s* p) {
+  for (auto& g : p->graphs) hipGraphExecDestroy(g.exec);
+  p->graphs.clear();
+}
+
 void free_symbol(cfp_plan_s* p) {
+  graph_clear(p);
   if (p->colsym) hipFree(p->colsym);
   if (p->axsym) hipFree(p->axsym);
   if (p->diag) hipFree(p->diag);
@@ -594,6 +614,8 @@ extern "C" int cfp_plan_destroy(cfp_plan_t p) {
     if (p->tw4hi[a]) hipFree(p->tw4hi[a]);
   }
   if (p->host_stage) hipFree(p->host_stage);
+  graph_clear(p);
+  if (p->cap_stream) hipStreamDestroy(p->cap_stream);
   for (auto& e : p->prof_ev) hipEventDestroy(e);
   delete p;
   return CFP_SUCCESS;
@@ -654,6 +676,46 @@ extern "C" int cfp_plan_get_diag(cfp_plan_t p, double* diag_dev, void* stream) {
   return CFP_SUCCESS;
 }
 
+// Graph mode: replay the captured launches of this (b, x) pair, or run the apply eagerly
+// (which also builds anything allocated lazily, e.g. twiddle tables) and capture the same
+// launch list for the next call.
+static int graph_apply(cfp_plan_s* p, const cd* b, cd* x, hipStream_t s) {
+  for (const auto& g : p->graphs)
+    if (g.b == b && g.x == x) {
+      HIPCHK(hipGraphLaunch(g.exec, s));
+      return CFP_SUCCESS;
+    }
+  int rc = run_apply(p, nullptr, b, x, s, nullptr);
+  if (rc) return rc;
+  if (!p->cap_stream) HIPCHK(hipStreamCreateWithFlags(&p->cap_stream, hipStreamNonBlocking));
+  HIPCHK(hipStreamBeginCapture(p->cap_stream, hipStreamCaptureModeThreadLocal));
+  rc = run_apply(p, nullptr, b, x, p->cap_stream, nullptr);
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamEndCapture(p->cap_stream, &g);
+  if (rc || e != hipSuccess) {
+    if (g) hipGraphDestroy(g);
+    return rc ? rc : hip_error(e, "apply graph capture");
+  }
+  hipGraphExec_t exec = nullptr;
+  e = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  if (e != hipSuccess) return hip_error(e, "apply graph instantiate");
+  if (p->graphs.size() >= kMaxGraphs) {
+    hipGraphExecDestroy(p->graphs.front().exec);
+    p->graphs.erase(p->graphs.begin());
+  }
+  p->graphs.push_back({b, x, exec});
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_plan_set_graph(cfp_plan_t p, int on) {
+  if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
+  DeviceGuard dg(p->device);
+  graph_clear(p);
+  p->graph_on = on != 0;
+  return CFP_SUCCESS;
+}
+
 extern "C" int cfp_plan_apply(cfp_plan_t p, const double* b, double* x, void* stream) {
   if (!p || !b || !x) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
   DeviceGuard dg(p->device);
@@ -665,6 +727,7 @@ extern "C" int cfp_plan_apply(cfp_plan_t p, const double* b, double* x, void* st
     ++p->prof_used;
     return run_apply(p, nullptr, (const cd*)b, (cd*)x, (hipStream_t)stream, &ev);
   }
+  if (p->graph_on) return graph_apply(p, (const cd*)b, (cd*)x, (hipStream_t)stream);
   return run_apply(p, nullptr, (const cd*)b, (cd*)x, (hipStream_t)stream, nullptr);
 }
 
@@ -757,6 +820,7 @@ extern "C" int cfp_plan_backward(cfp_plan_t p, const double* in, double* out, vo
 
 extern "C" int cfp_plan_set_chunking(cfp_plan_t p, int64_t chunk_planes) {
   if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
+  graph_clear(p);
   if (chunk_planes < 0) return set_error(CFP_ERR_ARG_OUTOFRANGE, "chunk_planes must be >= 0");
   p->chunk_planes = chunk_planes;
   return CFP_SUCCESS;
@@ -772,6 +836,7 @@ extern "C" int cfp_plan_set_schedule(cfp_plan_t p, int schedule) {
   if (schedule == CFP_SCHEDULE_THREE_PASS && !three_pass_supported(p->n))
     return set_error(CFP_ERR_SUP, "the 3-sweep schedule needs a 128^3 or 256^3 grid");
   DeviceGuard dg(p->device);
+  graph_clear(p);
   const int f_old = p->fused_axis;
   p->schedule = schedule;
   order_axes(p);
@@ -785,6 +850,7 @@ extern "C" int cfp_plan_set_schedule(cfp_plan_t p, int schedule) {
 
 extern "C" int cfp_plan_set_three_pass_shape(cfp_plan_t p, int n1, int mid) {
   if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
+  graph_clear(p);
   if (!three_pass_shape_valid(n1, mid))
     return set_error(CFP_ERR_ARG_OUTOFRANGE, "3-sweep shape n1=%d mid=%d is not one of the built shapes", n1, mid);
   p->tp_shape.n1 = n1;
@@ -797,6 +863,7 @@ extern "C" int cfp_plan_set_three_pass_shape(cfp_plan_t p, int n1, int mid) {
 extern "C" int cfp_plan_set_external_x(cfp_plan_t p, int on) {
   if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
   DeviceGuard dg(p->device);
+  graph_clear(p);
   const int f_old = p->fused_axis;
   p->external_x = on != 0;
   order_axes(p);

@@ -156,6 +156,12 @@ class CirculantPlan:
         check(lib().cfp_plan_set_chunking(self._h, int(chunk_planes)))
         return self
 
+    def set_graph(self, on: bool = True) -> "CirculantPlan":
+        """HIP-graph replay of apply(): the launches of each (b, out) pair are captured once and
+        replayed as one graph launch (cfp_plan_set_graph)."""
+        check(lib().cfp_plan_set_graph(self._h, int(bool(on))))
+        return self
+
     SCHEDULES = {"auto": 0, "five": 1, "three": 2, "five_y": 3, "plane": 4}
 
     def set_schedule(self, schedule: str | int) -> "CirculantPlan":

@@ -94,6 +94,16 @@ int cfp_plan_backward(cfp_plan_t plan, const double *in_dev, double *out_dev, vo
  * 0 (default) = one launch per axis pass. */
 int cfp_plan_set_chunking(cfp_plan_t plan, int64_t chunk_planes);
 
+/* HIP-graph replay of cfp_plan_apply (off by default).  On: the first apply of a (b, x) pair
+ * runs eagerly and captures its launches into a graph; later applies of the same pair launch
+ * that graph into the caller's stream (one host call instead of 3-5 kernel launches, for the
+ * launch-bound small grids inside GMRES).  Up to 64 pairs are kept; every setter that changes
+ * buffers or the schedule drops them.  Values written into the plan's symbol / Diag are seen;
+ * profiling applies (cfp_plan_profile_begin) run eagerly.  Measured on MI355X / ROCm 7 it is
+ * ~6 us SLOWER per host-synchronous apply than the direct launches at every grid from 32^3 to
+ * 256^3 (profiles/r02z_graph_timing.txt), so it stays off by default. */
+int cfp_plan_set_graph(cfp_plan_t plan, int on);
+
 /* Apply schedule.  FIVE_PASS: x, y fwd, z fused with the symbol, y, x inv.
  * FIVE_PASS_YFUSED: x, z fwd, y fused, z, x inv.  AUTO (default): THREE_PASS on 256^3 plans
  * (separable symbol, no chunking), YFUSED when ny, nz >= 512, else FIVE_PASS.  THREE_PASS

@@ -602,3 +602,43 @@ def test_profile_mode_records_the_callers_applies(cp, oracle):
         assert _rel(x, ref) < TOL
         with pytest.raises(Exception):
             plan.profile_end()  # not started
+
+
+# ------------------------------------------------------------------ HIP-graph replay
+@pytest.mark.parametrize("n", [(32, 32, 32), (100, 100, 100), (64, 32, 16), (256, 256, 256)])
+def test_graph_replay_vs_oracle(cp, oracle, n):
+    """cfp_plan_set_graph: replayed applies equal the eager apply bit for bit, follow a new
+    symbol, a new schedule and an in-place pair, and match the oracle."""
+    lam = (0.6, 0.15, 0.02)
+    lam2 = (1.3 - 0.2j, 0.4, 2.0)
+    N = int(np.prod(n))
+    b_h = oracle.c_fill_uniform(N, 77)
+    ref = oracle.c_solve_3d(oracle.c_build_diag_transport(n, lam), b_h, n)
+    ref2 = oracle.c_solve_3d(oracle.c_build_diag_transport(n, lam2), b_h, n)
+    b = _dev(b_h)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam)
+        eager = plan.apply(b)
+        plan.set_graph(True)
+        x = torch.empty_like(b)
+        for _ in range(3):  # miss (eager + capture), then two replays
+            x.zero_()
+            plan.apply(b, out=x)
+            torch.cuda.synchronize()
+            assert torch.equal(x, eager)
+        assert _rel(x, ref) < TOL
+        plan.set_transport_symbol(lam2)  # moves the symbol buffers: the graphs are dropped
+        for _ in range(2):
+            plan.apply(b, out=x)
+        assert _rel(x, ref2) < TOL
+        plan.set_schedule("five")
+        for _ in range(2):
+            plan.apply(b, out=x)
+        assert _rel(x, ref2) < TOL
+        t = b.clone()
+        for _ in range(2):  # in place: each replay solves against the previous result
+            t.copy_(b)
+            plan.apply(t, out=t)
+        assert _rel(t, ref2) < TOL
+        plan.set_graph(False)
+        assert torch.equal(plan.apply(b), x)
