@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 LAM = (0.6, 0.15, 0.02)  # lambda set A, testFftSolver_3D.py:85-91
 SEED = 20251017
+RES_TOL = 1e-10  # north_star's parity bar, applied to the residual of the timed applies
 
 
 def log(*a):
@@ -249,6 +250,34 @@ def main() -> int:
         cp.fill_uniform(b, SEED, offset=plan.local_offset)
         return plan, b, x, (lambda: plan.apply(b, out=x)), f"z-slab x{world}, all-to-all over xGMI ({exchange})"
 
+    def residual(b, x, g):
+        """Output check of the timed applies, on the GPU, without the oracle: ||C x - b|| / ||b||
+        with C the transport circulant the plan inverts, C x = x + sum_d lam_d (x - roll_d(x, 1))
+        (Diag[k] = 1 + sum_d lam_d (1 - e^{-2 pi i k_d / n_d}), src/FftLinearSolver_3D.c:80-164).
+        Slabs: the z-roll takes the plane below from the previous rank (periodic)."""
+        gx, gy, gz = g
+        lx, ly, lz = LAM
+        nzl = gz // world
+        X = x.view(nzl, gy, gx)
+        B = b.view(nzl, gy, gx)
+        if world == 1:
+            Xz = torch.roll(X, 1, 0)
+        else:
+            on_gpu = dist.get_backend() == "nccl"
+            last = X[-1].contiguous() if on_gpu else X[-1].cpu()
+            prev = torch.empty_like(last)
+            ops = [dist.P2POp(dist.isend, last, (rank + 1) % world), dist.P2POp(dist.irecv, prev, (rank - 1) % world)]
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+            Xz = torch.cat([prev.to(X.device).unsqueeze(0), X[:-1]], 0)
+        r = X * (1.0 + lx + ly + lz) - lx * torch.roll(X, 1, 2) - ly * torch.roll(X, 1, 1) - lz * Xz - B
+        nd = torch.stack([r.abs().pow(2).sum(), B.abs().pow(2).sum()])
+        del r, Xz
+        if world > 1:
+            nd = nd.to(dev) if dist.get_backend() == "nccl" else nd.cpu()
+            dist.all_reduce(nd)
+        return float((nd[0] / nd[1]).sqrt())
+
     def settle(run, ms):
         """Untimed applies until `ms` of wall time have passed: the GPU leaves its idle clocks
         (sclk reads ~100 MHz idle); without this a 20-step run measures ramp-up, ~10 % low
@@ -317,6 +346,10 @@ def main() -> int:
         elapsed = timed(run, args.steps, 0)
     ms_per_step = elapsed / args.steps * 1e3
     value = args.steps / elapsed  # whole-job PCApply/s (one grid per step)
+    torch.cuda.synchronize()
+    res = residual(b, x, grid)
+    check = {"residual": res, "tol": RES_TOL, "ok": res < RES_TOL,
+             "what": "||C x - b|| / ||b|| of the last timed apply (transport circulant C, on the GPU)"}
 
     # per-launch timing of the dominant kernel (HIP events on the launch stream)
     if world == 1:
@@ -439,6 +472,8 @@ def main() -> int:
                 run()
             settle(run, min(args.settle_ms, 200.0))
             el = timed(run, k, 0)
+            torch.cuda.synchronize()
+            res2 = residual(b, x, sg)
             nl = sg[0] * sg[1] * sg[2] // world
             if world == 1:
                 mv = moved_bytes(plan.passes(), nl)
@@ -451,7 +486,11 @@ def main() -> int:
                        "moved_GBps_per_gpu": round(mv / (el / k) / 1e9, 1),
                        "frac_moved": round(mv / (el / k) / 1e9 / HBM_PEAK_GBS, 4),
                        "B_alg_GBps_per_gpu": round(208 * nl / (el / k) / 1e9, 1),
-                       "note": "moved = the schedule's launches (exchanges excluded); B_alg = SURVEY's 208 N convention"}
+                       "note": "moved = the schedule's launches (exchanges excluded); B_alg = SURVEY's 208 N convention",
+                       "check": {"residual": res2, "tol": RES_TOL, "ok": res2 < RES_TOL}}
+            if not res2 < RES_TOL:
+                check["ok"] = False
+                check["scaling_512_failed"] = True
         except Exception as e:  # report, never fake
             scaling = {"grid": sg, "error": str(e)}
             plan = None
@@ -483,6 +522,7 @@ def main() -> int:
             "exchange": exchange_used[0],
             "settle": {"ms": round(settle_ms, 1), "applies": settle_n,
                        "note": "untimed applies after the W warm-up steps, before the timed region"},
+            "check": check,
             "roofline": roof,
             "roofline_apply": roof_apply,
             "cpu_baseline": cpu,
@@ -502,6 +542,9 @@ def main() -> int:
             plan.close()
         dist.barrier()
         dist.destroy_process_group()
+    if not check["ok"]:
+        log(f"bench: output check FAILED: {check}")
+        return 3
     return 0
 
 
