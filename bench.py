@@ -35,6 +35,42 @@ SEED = 20251017
 RES_TOL = 1e-10  # north_star's parity bar, applied to the residual of the timed applies
 
 
+
+def transport_residual(b, x, g, lam, rank: int = 0, world: int = 1, dev=None) -> float:
+    """Output check of the timed applies, on the device holding x, without the oracle:
+    ||C x - b|| / ||b|| with C the transport circulant the plan inverts,
+    C x = x + sum_d lam_d (x - roll_d(x, 1))
+    (Diag[k] = 1 + sum_d lam_d (1 - e^{-2 pi i k_d / n_d}), src/FftLinearSolver_3D.c:80-164).
+    With world > 1, b and x are this rank's z-slab ([nz/world][ny][nx], PETSC_DECIDE rows) and
+    the z-roll takes the plane below from the previous rank (periodic)."""
+    import torch
+    import torch.distributed as dist
+
+    gx, gy, gz = g
+    lx, ly, lz = lam
+    nzl = gz // world
+    X = x.view(nzl, gy, gx)
+    B = b.view(nzl, gy, gx)
+    on_gpu = world > 1 and dist.get_backend() == "nccl"
+    if world == 1:
+        Xz = torch.roll(X, 1, 0)
+    else:
+        # every rank's last plane through one all_gather on the default communicator (a
+        # collective like the all_reduce below: no extra point-to-point communicator)
+        last = X[-1].contiguous() if on_gpu else X[-1].cpu()
+        planes = [torch.empty_like(last) for _ in range(world)]
+        dist.all_gather(planes, last)
+        prev = planes[(rank - 1) % world]
+        Xz = torch.cat([prev.to(X.device).unsqueeze(0), X[:-1]], 0)
+        del planes
+    r = X * (1.0 + lx + ly + lz) - lx * torch.roll(X, 1, 2) - ly * torch.roll(X, 1, 1) - lz * Xz - B
+    nd = torch.stack([r.abs().pow(2).sum(), B.abs().pow(2).sum()])
+    del r, Xz
+    if world > 1:
+        nd = nd.to(dev) if on_gpu else nd.cpu()
+        dist.all_reduce(nd)
+    return float((nd[0] / nd[1]).sqrt())
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -251,32 +287,7 @@ def main() -> int:
         return plan, b, x, (lambda: plan.apply(b, out=x)), f"z-slab x{world}, all-to-all over xGMI ({exchange})"
 
     def residual(b, x, g):
-        """Output check of the timed applies, on the GPU, without the oracle: ||C x - b|| / ||b||
-        with C the transport circulant the plan inverts, C x = x + sum_d lam_d (x - roll_d(x, 1))
-        (Diag[k] = 1 + sum_d lam_d (1 - e^{-2 pi i k_d / n_d}), src/FftLinearSolver_3D.c:80-164).
-        Slabs: the z-roll takes the plane below from the previous rank (periodic)."""
-        gx, gy, gz = g
-        lx, ly, lz = LAM
-        nzl = gz // world
-        X = x.view(nzl, gy, gx)
-        B = b.view(nzl, gy, gx)
-        if world == 1:
-            Xz = torch.roll(X, 1, 0)
-        else:
-            on_gpu = dist.get_backend() == "nccl"
-            last = X[-1].contiguous() if on_gpu else X[-1].cpu()
-            prev = torch.empty_like(last)
-            ops = [dist.P2POp(dist.isend, last, (rank + 1) % world), dist.P2POp(dist.irecv, prev, (rank - 1) % world)]
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
-            Xz = torch.cat([prev.to(X.device).unsqueeze(0), X[:-1]], 0)
-        r = X * (1.0 + lx + ly + lz) - lx * torch.roll(X, 1, 2) - ly * torch.roll(X, 1, 1) - lz * Xz - B
-        nd = torch.stack([r.abs().pow(2).sum(), B.abs().pow(2).sum()])
-        del r, Xz
-        if world > 1:
-            nd = nd.to(dev) if dist.get_backend() == "nccl" else nd.cpu()
-            dist.all_reduce(nd)
-        return float((nd[0] / nd[1]).sqrt())
+        return transport_residual(b, x, g, LAM, rank, world, dev)
 
     def settle(run, ms):
         """Untimed applies until `ms` of wall time have passed: the GPU leaves its idle clocks

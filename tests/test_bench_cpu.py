@@ -110,3 +110,62 @@ def test_moved_bytes_of_the_schedules():
             {"mode": "inv", "n": 256}, {"mode": "inv", "n": 256}]
     assert 96 * N <= bench.moved_bytes(three, N) < 96.1 * N
     assert 160 * N <= bench.moved_bytes(five, N) < 160.1 * N
+
+
+def _residual_case(n, lam, seed, wrong=False):
+    import numpy as np
+    import torch
+    from oracle import oracle as O
+
+    N = int(np.prod(n))
+    b = O.c_fill_uniform(N, seed)
+    x = O.c_solve_3d(O.c_build_diag_transport(n, lam), b, n)
+    if wrong:
+        x = x * (1 + 1e-6)
+    return torch.from_numpy(b), torch.from_numpy(x)
+
+
+def test_transport_residual_one_rank():
+    """bench.py's output check: ~1e-16 on the oracle's solve, far above 1e-10 on a perturbed one."""
+    n, lam = (12, 10, 8), (0.6, 0.15, 0.02)
+    b, x = _residual_case(n, lam, 5)
+    assert bench.transport_residual(b, x, n, lam) < 1e-14
+    b, x = _residual_case(n, lam, 5, wrong=True)
+    assert bench.transport_residual(b, x, n, lam) > bench.RES_TOL
+
+
+def _residual_rank(rank, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench as B
+
+        n, lam = (12, 10, 8), (0.6, 0.15, 0.02)
+        b, x = _residual_case(n, lam, 5)
+        loc = 12 * 10 * 4  # this rank's z-slab (PETSC_DECIDE rows)
+        sl = slice(rank * loc, (rank + 1) * loc)
+        q.put((rank, B.transport_residual(b[sl].clone(), x[sl].clone(), n, lam, rank, 2)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_transport_residual_two_slabs_gloo():
+    """The slab form of the check (z-roll across ranks through all_gather) equals the one-rank value."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_residual_rank, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n, lam = (12, 10, 8), (0.6, 0.15, 0.02)
+    b, x = _residual_case(n, lam, 5)
+    one = bench.transport_residual(b, x, n, lam)
+    assert res[0][1] == pytest.approx(one, rel=1e-6) and res[1][1] == pytest.approx(one, rel=1e-6)
+    assert one < 1e-14
