@@ -40,9 +40,11 @@ def _declare(L) -> None:
         "cfp_plan_set_symbol_separable": ([vp, dp, dp, dp, dp], c_int),
         "cfp_plan_set_diag": ([vp, dp, c_int], c_int),
         "cfp_plan_get_diag": ([vp, dp, vp], c_int),
+        "cfp_plan_symbol_version": ([vp, P(u64)], c_int),
         "cfp_plan_apply": ([vp, dp, dp, vp], c_int),
         "cfp_plan_apply_with_diag": ([vp, dp, dp, dp, vp], c_int),
         "cfp_plan_apply_host": ([vp, dp, dp], c_int),
+        "cfp_plan_apply_with_diag_host": ([vp, dp, dp, dp], c_int),
         "cfp_plan_forward": ([vp, dp, dp, vp], c_int),
         "cfp_plan_backward": ([vp, dp, dp, vp], c_int),
         "cfp_plan_set_chunking": ([vp, i64], c_int),

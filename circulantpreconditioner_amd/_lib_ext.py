@@ -19,12 +19,13 @@ class PetscScalar(ctypes.Structure):
 
 
 class FFTPrecTransportContext(ctypes.Structure):
-    """struct FFTPrecTransportContext (src/PCSHELLFft_3D.hxx:8-21 + trailing plan, remapBack)."""
+    """struct FFTPrecTransportContext, the reference's exact 12 members (src/PCSHELLFft_3D.hxx:8-21);
+    this build's additions live in a side table (FFTPrecTransportContextSetRemapBack) and the
+    plan behind FFT_MAT (MatFFTHIPGetPlan)."""
     _fields_ = [("spaceDim", ctypes.c_int64), ("n_x", ctypes.c_int64), ("n_y", ctypes.c_int64),
                 ("n_z", ctypes.c_int64), ("lambda_x", PetscScalar), ("lambda_y", PetscScalar),
                 ("lambda_z", PetscScalar), ("FFT_MAT", ctypes.c_void_p), ("intersectionMatrix", ctypes.c_void_p),
-                ("Diag", ctypes.c_void_p), ("b_hat", ctypes.c_void_p), ("b_cartesien", ctypes.c_void_p),
-                ("plan", ctypes.c_void_p), ("remapBack", ctypes.c_void_p)]
+                ("Diag", ctypes.c_void_p), ("b_hat", ctypes.c_void_p), ("b_cartesien", ctypes.c_void_p)]
 
 
 class StructuredTransportContext(ctypes.Structure):
@@ -241,6 +242,8 @@ def declare(L) -> None:
         "destroyFFTPrec3D": ([vp], c_int),
         "getFFTPrec3DContext": ([i64, S, i64, S, S, S, S, S, S, S, S, S, P(FFTPrecTransportContext)], c_int),
         "FFTPrecTransportContextCreate": ([P(vp)], c_int),
+        "FFTPrecTransportContextSetRemapBack": ([P(FFTPrecTransportContext), vp], c_int),
+        "FFTPrecTransportContextGetRemapBack": ([P(FFTPrecTransportContext), P(vp)], c_int),
         "FFTPrecTransportContextDestroy": ([P(vp)], c_int),
         "solve_3D": ([vp, vp, vp, vp, vp, i64], c_int),
         "build_transport_col": ([vp, i64], c_int),

@@ -681,6 +681,19 @@ template <> struct PlaneCfg<64> { static constexpr int PTS = 8, R0 = 8; static c
 template <> struct PlaneCfg<100> { static constexpr int PTS = 10, R0 = 10; static constexpr bool SPLIT = false; };
 template <> struct PlaneCfg<128> { static constexpr int PTS = 16, R0 = 8; static constexpr bool SPLIT = true; };
 
+// static LDS of k_plane<N>: the plane buffer plus the twiddle table.  It must fit one gfx950
+// CU's 160 KiB (k_plane<100> uses 163,200 of the 163,840 bytes); this library builds for gfx950
+// only (Makefile --offload-arch=gfx950), and a config change that overflows fails to compile.
+template <int N>
+constexpr size_t plane_lds_bytes() {
+  return (PlaneCfg<N>::SPLIT ? sizeof(double) * N * (N + N / 16) : sizeof(double) * 2 * N * (N + 1)) +
+         sizeof(cd) * N;
+}
+constexpr size_t kGfx950LdsBytes = 160 * 1024;
+static_assert(plane_lds_bytes<64>() <= kGfx950LdsBytes, "k_plane<64> exceeds the CU's LDS");
+static_assert(plane_lds_bytes<100>() <= kGfx950LdsBytes, "k_plane<100> exceeds the CU's LDS");
+static_assert(plane_lds_bytes<128>() <= kGfx950LdsBytes, "k_plane<128> exceeds the CU's LDS");
+
 // element (y, x) of the plane at LDS y * N + x
 template <int N, int PTS, int FLAGS, class WP, class RP>
 __device__ __forceinline__ void plane_transpose(double* lds, cd* v, WP wpos, RP rpos) {
@@ -750,6 +763,7 @@ __global__ void __launch_bounds__(N*(N / PlaneCfg<N>::PTS)) k_plane(const cd* in
   }
 }
 
+// gated on the static_asserts above (the kernels are only built when they fit gfx950's LDS)
 bool plane_supported(i64 n) { return n == 64 || n == 100 || n == 128; }
 
 template <int N>

@@ -123,6 +123,7 @@ struct cfp_plan_s {
   i64 N = 1;
   std::map<int, cd*> tw;  // device forward twiddles per axis length
   int sym_kind = 0;       // 0 none, 1 separable, 2 explicit diag
+  uint64_t sym_version = 0;  // bumped by every symbol setter (cfp_plan_symbol_version)
   cd* colsym = nullptr;   // separable: per column of the fused axis (sum over the other axes)
   cd* axsym = nullptr;    //            per point of the fused axis
   cd* diag = nullptr;     // explicit
@@ -445,7 +446,12 @@ int run_transform(cfp_plan_s* p, bool inverse, const cd* in, cd* out, hipStream_
 
 constexpr size_t kMaxGraphs = 64;  // GMRES(30) applies the PC to ~32 distinct Krylov vectors
 
+// A cached graph may still be running in the caller's stream (hipGraphLaunch is
+// asynchronous), so the device is drained before any executable graph is destroyed.  The
+// callers are setters and the 65th (b, x) pair, never the steady-state apply.
 void graph_clear(cfp_plan_s* p) {
+  if (p->graphs.empty()) return;
+  hipDeviceSynchronize();
   for (auto& g : p->graphs) hipGraphExecDestroy(g.exec);
   p->graphs.clear();
 }
@@ -534,6 +540,7 @@ int set_separable(cfp_plan_s* p, const std::vector<cd> hat[3], const double lam[
       s[a][k] = make_cd(re, im);
     }
   }
+  ++p->sym_version;
   return upload_separable(p, s);
 }
 
@@ -621,6 +628,12 @@ extern "C" int cfp_plan_destroy(cfp_plan_t p) {
   return CFP_SUCCESS;
 }
 
+extern "C" int cfp_plan_symbol_version(cfp_plan_t p, uint64_t* version) {
+  if (!p || !version) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  *version = p->sym_version;
+  return CFP_SUCCESS;
+}
+
 extern "C" int cfp_plan_set_symbol_transport(cfp_plan_t p, const double lam[6]) {
   if (!p || !lam) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
   DeviceGuard dg(p->device);
@@ -647,6 +660,7 @@ extern "C" int cfp_plan_set_diag(cfp_plan_t p, const double* diag, int on_device
   if (p->long_axes()) return set_error(CFP_ERR_SUP, "an explicit Diag needs axes <= 4096 (use a separable symbol)");
   DeviceGuard dg(p->device);
   free_symbol(p);
+  ++p->sym_version;
   HIPCHK(hipMalloc(&p->diag, sizeof(cd) * (size_t)p->N));
   HIPCHK(hipMemcpy(p->diag, diag, sizeof(cd) * (size_t)p->N, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
   p->sym_kind = 2;
@@ -701,6 +715,7 @@ static int graph_apply(cfp_plan_s* p, const cd* b, cd* x, hipStream_t s) {
   hipGraphDestroy(g);
   if (e != hipSuccess) return hip_error(e, "apply graph instantiate");
   if (p->graphs.size() >= kMaxGraphs) {
+    HIPCHK(hipDeviceSynchronize());  // the evicted graph may still be in flight
     hipGraphExecDestroy(p->graphs.front().exec);
     p->graphs.erase(p->graphs.begin());
   }
@@ -794,16 +809,29 @@ extern "C" int cfp_plan_apply_with_diag(cfp_plan_t p, const double* diag, const 
   return run_apply(p, (const cd*)diag, (const cd*)b, (cd*)x, (hipStream_t)stream, nullptr);
 }
 
-extern "C" int cfp_plan_apply_host(cfp_plan_t p, const double* b, double* x) {
-  if (!p || !b || !x) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
-  DeviceGuard dg(p->device);
+// host b -> the plan's persistent device staging buffer (allocated once) -> in-place apply ->
+// host x; every copy is checked (a failed copy is CFP_ERR_LIB, never stale data)
+static int apply_host_impl(cfp_plan_s* p, const cd* diag, const double* b, double* x) {
   const size_t bytes = sizeof(cd) * (size_t)p->N;
   if (!p->host_stage) HIPCHK(hipMalloc(&p->host_stage, bytes));
   HIPCHK(hipMemcpy(p->host_stage, b, bytes, hipMemcpyHostToDevice));
-  int rc = run_apply(p, nullptr, p->host_stage, p->host_stage, nullptr, nullptr);
+  int rc = run_apply(p, diag, p->host_stage, p->host_stage, nullptr, nullptr);
   if (rc) return rc;
   HIPCHK(hipMemcpy(x, p->host_stage, bytes, hipMemcpyDeviceToHost));
   return CFP_SUCCESS;
+}
+
+extern "C" int cfp_plan_apply_host(cfp_plan_t p, const double* b, double* x) {
+  if (!p || !b || !x) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  DeviceGuard dg(p->device);
+  return apply_host_impl(p, nullptr, b, x);
+}
+
+extern "C" int cfp_plan_apply_with_diag_host(cfp_plan_t p, const double* diag_dev, const double* b, double* x) {
+  if (!p || !diag_dev || !b || !x) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  if (p->long_axes()) return set_error(CFP_ERR_SUP, "an explicit Diag needs axes <= 4096 (use a separable symbol)");
+  DeviceGuard dg(p->device);
+  return apply_host_impl(p, (const cd*)diag_dev, b, x);
 }
 
 extern "C" int cfp_plan_forward(cfp_plan_t p, const double* in, double* out, void* stream) {

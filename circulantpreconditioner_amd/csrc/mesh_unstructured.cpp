@@ -665,7 +665,7 @@ extern "C" PetscErrorCode getFFTPrec3DContextMesh(PetscInt ndim, PetscScalar dt,
     PetscCall(MatCreateMeshCartesianRemap(m, ctx->n_x, ctx->n_y, ctx->n_z, b, &toCart, &toMesh));
   }
   ctx->intersectionMatrix = toCart;
-  ctx->remapBack = toMesh;
+  PetscCall(FFTPrecTransportContextSetRemapBack(ctx, toMesh));
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
@@ -673,7 +673,10 @@ extern "C" PetscErrorCode FFTPrec3DContextDestroyRemap(FFTPrecTransportContext* 
   PetscFunctionBeginUser;
   if (!ctx) PetscFunctionReturn(PETSC_SUCCESS);
   PetscCall(MatDestroy(&ctx->intersectionMatrix));
-  PetscCall(MatDestroy(&ctx->remapBack));
+  Mat back = nullptr;
+  PetscCall(FFTPrecTransportContextGetRemapBack(ctx, &back));
+  PetscCall(MatDestroy(&back));
+  PetscCall(FFTPrecTransportContextSetRemapBack(ctx, nullptr));
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 

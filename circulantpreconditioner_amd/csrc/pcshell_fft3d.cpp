@@ -17,6 +17,8 @@
 #include <cmath>
 #include <complex>
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 
 #include "../../include/circulant_fft.h"
 #include "../../include/pcshell_fft3d.h"
@@ -33,12 +35,14 @@ struct FFTShell {
   PetscInt dims[3] = {1, 1, 1};  // n_x, n_y, n_z
   bool has_lam = false;
   double lam[6] = {0, 0, 0, 0, 0, 0};
-  uint64_t sym_gen = 0;  // bumped whenever the plan's symbol changes
-  // the Diag setupFFTPrec3D materialised from the symbol of generation diag_gen: its object id
-  // and its state right after that write (0 id: none)
+  uint64_t lam_version = 0;  // the plan's symbol version right after lam was set
+  // the Diag setupFFTPrec3D materialised from the plan's symbol of version diag_version: its
+  // object id and its state right after that write (0 id: none).  The version is the plan's
+  // own counter (cfp_plan_symbol_version), so a symbol set on the plan directly through
+  // MatFFTHIPGetPlan also invalidates the fast path.
   PetscObjectId diag_id = 0;
   PetscObjectState diag_state = 0;
-  uint64_t diag_gen = 0;
+  uint64_t diag_version = 0;
   PetscInt solves_own = 0, solves_diag = 0;  // solve_3D calls per path (MatFFTHIPGetSolveCounts)
 };
 
@@ -90,19 +94,28 @@ void lam6(PetscScalar lx, PetscScalar ly, PetscScalar lz, double out[6]) {
 
 // Use (or refresh) the plan's separable transport symbol for these lambdas (App. A item 9:
 // the reference rebuilds Diag on every direct-solve call; equal lambdas reuse it here).
+PetscErrorCode symbol_version(FFTShell* s, uint64_t* v) {
+  CFPCALL(cfp_plan_symbol_version(s->plan, v));
+  return PETSC_SUCCESS;
+}
+
 PetscErrorCode ensure_transport_symbol(FFTShell* s, const double lam[6]) {
-  if (s->has_lam && std::memcmp(s->lam, lam, sizeof(s->lam)) == 0) return PETSC_SUCCESS;
+  uint64_t v;
+  PetscCall(symbol_version(s, &v));
+  if (s->has_lam && v == s->lam_version && std::memcmp(s->lam, lam, sizeof(s->lam)) == 0) return PETSC_SUCCESS;
   CFPCALL(cfp_plan_set_symbol_transport(s->plan, lam));
   std::memcpy(s->lam, lam, sizeof(s->lam));
   s->has_lam = true;
-  ++s->sym_gen;
+  PetscCall(symbol_version(s, &s->lam_version));
   return PETSC_SUCCESS;
 }
 
 // Diag holds exactly the plan's current symbol (materialised by setupFFTPrec3D, untouched since)
 PetscErrorCode diag_is_own_symbol(FFTShell* s, Vec Diag, bool* own) {
   *own = false;
-  if (!s->diag_id || s->diag_gen != s->sym_gen) return PETSC_SUCCESS;
+  uint64_t v;
+  PetscCall(symbol_version(s, &v));
+  if (!s->diag_id || s->diag_version != v) return PETSC_SUCCESS;
   PetscObjectId id;
   PetscObjectState st;
   PetscCall(PetscObjectGetId((PetscObject)Diag, &id));
@@ -111,7 +124,38 @@ PetscErrorCode diag_is_own_symbol(FFTShell* s, Vec Diag, bool* own) {
   return PETSC_SUCCESS;
 }
 
+// Per-context additions of this build, keyed by the context's address, so that the context
+// keeps the reference's exact layout (src/PCSHELLFft_3D.hxx:8-21; include/pcshell_fft3d.h).
+struct CtxExtra {
+  Mat remapBack = nullptr;
+};
+std::mutex g_extra_mu;
+std::unordered_map<const void*, CtxExtra> g_extra;
+
+Mat ctx_remap_back(const FFTPrecTransportContext* ctx) {
+  std::lock_guard<std::mutex> g(g_extra_mu);
+  auto it = g_extra.find(ctx);
+  return it == g_extra.end() ? nullptr : it->second.remapBack;
+}
+void ctx_forget(const FFTPrecTransportContext* ctx) {
+  std::lock_guard<std::mutex> g(g_extra_mu);
+  g_extra.erase(ctx);
+}
+
 }  // namespace
+
+extern "C" PetscErrorCode FFTPrecTransportContextSetRemapBack(FFTPrecTransportContext* ctx, Mat remapBack) {
+  PetscCheck(ctx, PETSC_COMM_SELF, PETSC_ERR_ARG_NULL, "NULL context");
+  std::lock_guard<std::mutex> g(g_extra_mu);
+  if (remapBack) g_extra[ctx].remapBack = remapBack;
+  else g_extra.erase(ctx);
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode FFTPrecTransportContextGetRemapBack(const FFTPrecTransportContext* ctx, Mat* remapBack) {
+  PetscCheck(ctx && remapBack, PETSC_COMM_SELF, PETSC_ERR_ARG_NULL, "NULL argument");
+  *remapBack = ctx_remap_back(ctx);
+  return PETSC_SUCCESS;
+}
 
 // ------------------------------------------------------------------ FFT matrix
 extern "C" PetscErrorCode MatCreateFFTHIP(MPI_Comm comm, PetscInt ndim, const PetscInt dims[], Mat* A) {
@@ -225,18 +269,14 @@ extern "C" PetscErrorCode solve_3D(Mat FFT_MAT, Vec X, Vec Diag, Vec b, Vec b_ha
     PetscScalar* arr;
     PetscMemType mt;
     PetscCall(VecGetArrayAndMemType(X, &arr, &mt));
-    void* tmp = nullptr;
     double* p = (double*)arr;
     if (mt == PETSC_MEMTYPE_HOST) {
-      PetscCheck(hipMalloc(&tmp, sizeof(PetscScalar) * (size_t)N) == hipSuccess, PETSC_COMM_SELF, PETSC_ERR_MEM, "staging");
-      hipMemcpy(tmp, arr, sizeof(PetscScalar) * (size_t)N, hipMemcpyHostToDevice);
-      p = (double*)tmp;
-    }
-    rc = own ? cfp_plan_apply(s->plan, p, p, nullptr) : cfp_plan_apply_with_diag(s->plan, din.ptr(), p, p, nullptr);
-    if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
-    if (tmp) {
-      hipMemcpy(arr, tmp, sizeof(PetscScalar) * (size_t)N, hipMemcpyDeviceToHost);
-      hipFree(tmp);
+      // staged through the plan's persistent device buffer; both copies are checked, so a
+      // failed copy returns PETSC_ERR_LIB instead of leaving stale data behind
+      rc = own ? cfp_plan_apply_host(s->plan, p, p) : cfp_plan_apply_with_diag_host(s->plan, din.ptr(), p, p);
+    } else {
+      rc = own ? cfp_plan_apply(s->plan, p, p, nullptr) : cfp_plan_apply_with_diag(s->plan, din.ptr(), p, p, nullptr);
+      if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
     }
     PetscCall(VecRestoreArrayAndMemType(X, &arr));
   } else {
@@ -343,10 +383,10 @@ extern "C" PetscErrorCode applyFFT3DPrecTransport(PC pc, Vec b, Vec x) {
     PetscCall(MatMult(ctx->intersectionMatrix, b, ctx->b_cartesien));
     src = ctx->b_cartesien;
   }
-  if (ctx->remapBack) {  // extra (mesh_unstructured.h): solve on the grid, then back to the mesh
+  if (Mat back = ctx_remap_back(ctx)) {  // extra (mesh_unstructured.h): solve on the grid, then back to the mesh
     if (src != ctx->b_cartesien) PetscCall(VecCopy(src, ctx->b_cartesien));
     PetscCall(solve_3D(ctx->FFT_MAT, ctx->b_cartesien, ctx->Diag, ctx->b_cartesien, ctx->b_hat, N));
-    PetscCall(MatMult(ctx->remapBack, ctx->b_cartesien, x));
+    PetscCall(MatMult(back, ctx->b_cartesien, x));
     PetscFunctionReturn(PETSC_SUCCESS);
   }
   PetscCall(solve_3D(ctx->FFT_MAT, x, ctx->Diag, src, ctx->b_hat, N));
@@ -383,8 +423,7 @@ extern "C" PetscErrorCode setupFFTPrec3D(PC pc) {
   // remember which object and state hold the symbol (solve_3D's register-symbol fast path)
   PetscCall(PetscObjectGetId((PetscObject)ctx->Diag, &s->diag_id));
   PetscCall(PetscObjectStateGet((PetscObject)ctx->Diag, &s->diag_state));
-  s->diag_gen = s->sym_gen;
-  ctx->plan = s->plan;
+  PetscCall(symbol_version(s, &s->diag_version));
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
@@ -398,7 +437,6 @@ extern "C" PetscErrorCode destroyFFTPrec3D(PC pc) {
   PetscCall(VecDestroy(&ctx->b_cartesien));
   PetscCall(VecDestroy(&ctx->b_hat));
   PetscCall(MatDestroy(&ctx->FFT_MAT));
-  ctx->plan = nullptr;
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
@@ -425,6 +463,7 @@ extern "C" PetscErrorCode getFFTPrec3DContext(PetscInt ndim, PetscScalar dt, Pet
     nz = 1;
   }
   std::memset((void*)ctx, 0, sizeof(*ctx));
+  ctx_forget(ctx);  // a fresh context: no remapBack left from a previous one at this address
   ctx->spaceDim = ndim;
   ctx->n_x = nx;
   ctx->n_y = ny;
@@ -443,6 +482,7 @@ extern "C" PetscErrorCode FFTPrecTransportContextCreate(FFTPrecTransportContext*
 }
 extern "C" PetscErrorCode FFTPrecTransportContextDestroy(FFTPrecTransportContext** ctx) {
   if (ctx && *ctx) {
+    ctx_forget(*ctx);
     delete *ctx;
     *ctx = nullptr;
   }

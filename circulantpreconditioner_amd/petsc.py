@@ -386,7 +386,24 @@ def make_context(dims: Sequence[int], lam: Sequence, space_dim: int = 3) -> FFTP
     ctx.spaceDim = space_dim
     ctx.n_x, ctx.n_y, ctx.n_z = (int(d) for d in dims)
     ctx.lambda_x, ctx.lambda_y, ctx.lambda_z = (PetscScalar.of(v) for v in lam)
+    PetscCall(lib().FFTPrecTransportContextSetRemapBack(ctypes.byref(ctx), None))  # fresh side-table entry
     return ctx
+
+
+def context_plan(ctx: FFTPrecTransportContext) -> int:
+    """The HIP plan behind ctx.FFT_MAT after setupFFTPrec3D (MatFFTHIPGetPlan), as an int handle."""
+    if not ctx.FFT_MAT:
+        return 0
+    h = ctypes.c_void_p()
+    PetscCall(lib().MatFFTHIPGetPlan(ctypes.c_void_p(ctx.FFT_MAT), ctypes.byref(h)))
+    return h.value or 0
+
+
+def context_remap_back(ctx: FFTPrecTransportContext) -> int:
+    """This build's Cartesian -> mesh remap of ctx (side table; 0 = none)."""
+    h = ctypes.c_void_p()
+    PetscCall(lib().FFTPrecTransportContextGetRemapBack(ctypes.byref(ctx), ctypes.byref(h)))
+    return h.value or 0
 
 
 def applyFFT3DPrecTransport(pc: PC, b: Vec, x: Vec) -> None:

@@ -312,6 +312,8 @@ class RealPlan:
     def _ptr(self, t: torch.Tensor, name: str) -> int:
         if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous() or t.numel() != self.N:
             raise ValueError(f"{name} must be a contiguous float64 device tensor of {self.N} elements")
+        if t.device.index != self.device:
+            raise ValueError(f"{name} is on cuda:{t.device.index}, the plan on cuda:{self.device}")
         return t.data_ptr()
 
     def apply(self, b: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:

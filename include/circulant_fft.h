@@ -73,6 +73,9 @@ int cfp_plan_set_symbol_separable(cfp_plan_t plan, const double *cx_hat, const d
 /* General symbol: an explicit Diag vector of N complex values (copied into the plan).
  * diag_is_device != 0 means `diag` is a device pointer. */
 int cfp_plan_set_diag(cfp_plan_t plan, const double *diag, int diag_is_device);
+/* Counter bumped by every symbol setter above (set_symbol_*, set_diag), whoever calls it: a
+ * caller that cached "the plan holds the symbol I set" compares versions instead. */
+int cfp_plan_symbol_version(cfp_plan_t plan, uint64_t *version);
 /* Materialise the plan's current symbol as a full Diag vector (device). */
 int cfp_plan_get_diag(cfp_plan_t plan, double *diag_dev, void *stream);
 
@@ -84,6 +87,8 @@ int cfp_plan_apply_with_diag(cfp_plan_t plan, const double *diag_dev, const doub
                              void *stream);
 /* Host-buffer variant (PCIe-inclusive): stages b through the plan's device buffers. Synchronous. */
 int cfp_plan_apply_host(cfp_plan_t plan, const double *b_host, double *x_host);
+/* Same with a caller-owned device Diag (solve_3D on host Vecs with an explicit Diag). */
+int cfp_plan_apply_with_diag_host(cfp_plan_t plan, const double *diag_dev, const double *b_host, double *x_host);
 
 /* Unnormalised 3-D transforms: forward (e^{-}, MatMult) and backward (e^{+}, MatMultTranspose). */
 int cfp_plan_forward(cfp_plan_t plan, const double *in_dev, double *out_dev, void *stream);

@@ -21,8 +21,13 @@
  *     creates it, item 2);
  *   - FftTransportSolver/Fft3DSolver do not destroy the caller's FFT_MAT (item 6) and cache
  *     the symbol between calls with equal lambdas (item 9);
- *   - FFTPrecTransportContext has two extra trailing members: `plan` (owned by
- *     setup/destroy) and `remapBack` (the caller's, include/mesh_unstructured.h).
+ *   - none in the context's layout: FFTPrecTransportContext is the reference's 12 members in
+ *     the reference's order (src/PCSHELLFft_3D.hxx:8-21), so a translation unit compiled
+ *     against the reference header links against this library.  What this build adds per
+ *     context -- the Cartesian -> mesh `remapBack` (include/mesh_unstructured.h) -- lives in a
+ *     side table keyed by the context's address (FFTPrecTransportContextSetRemapBack), and
+ *     the HIP plan is reached through the FFT matrix (MatFFTHIPGetPlan(ctx->FFT_MAT, ...)).
+ *     (PetscInt is 64-bit in the stand-in PETSc, as a --with-64-bit-indices build.)
  */
 #ifndef CFP_PCSHELL_FFT3D_H
 #define CFP_PCSHELL_FFT3D_H
@@ -47,9 +52,6 @@ struct FFTPrecTransportContext {
   Vec Diag;
   Vec b_hat;
   Vec b_cartesien;
-  cfp_plan_t plan; /* extra: the HIP plan behind FFT_MAT (set up by setupFFTPrec3D) */
-  Mat remapBack;   /* extra: Cartesian -> mesh remap applied to the solve's result (NULL:
-                      x stays on the Cartesian grid, as the reference's apply leaves it) */
 };
 typedef struct FFTPrecTransportContext FFTPrecTransportContext;
 
@@ -104,6 +106,12 @@ PetscErrorCode MatFFTHIPGetPlan(Mat A, cfp_plan_t *plan);
  * (Diag untouched since setupFFTPrec3D materialised it: same object id and PetscObjectState,
  * symbol unchanged) and how many streamed the Diag they were given. */
 PetscErrorCode MatFFTHIPGetSolveCounts(Mat A, PetscInt *own_symbol, PetscInt *explicit_diag);
+/* Side table of this build's per-context additions (not in the struct, see above).
+ * remapBack: Cartesian -> mesh remap applied to the solve's result (NULL, the default: x stays
+ * on the Cartesian grid, as the reference's apply leaves it).  The Mat stays the caller's.
+ * getFFTPrec3DContext and FFTPrecTransportContextDestroy clear the entry of their ctx. */
+PetscErrorCode FFTPrecTransportContextSetRemapBack(FFTPrecTransportContext *ctx, Mat remapBack);
+PetscErrorCode FFTPrecTransportContextGetRemapBack(const FFTPrecTransportContext *ctx, Mat *remapBack);
 PetscErrorCode FFTPrecTransportContextCreate(FFTPrecTransportContext **ctx);
 PetscErrorCode FFTPrecTransportContextDestroy(FFTPrecTransportContext **ctx);
 

@@ -101,8 +101,9 @@ SIZES = [(16, 16, 16), (32, 32, 32), (64, 64, 64), (128, 128, 128), (32, 64, 128
          (1000, 3, 2), (3, 243, 5)]
 
 
-@pytest.mark.parametrize("n", SIZES)
-@pytest.mark.parametrize("lam", [(0.6, 0.15, 0.02), (55.6, 0.0, 0.0), (0.3 + 0.2j, -0.1j, 1.7)])
+@pytest.mark.parametrize("n", SIZES, ids=lambda n: "x".join(map(str, n)))
+@pytest.mark.parametrize("lam", [(0.6, 0.15, 0.02), (55.6, 0.0, 0.0), (0.3 + 0.2j, -0.1j, 1.7)],
+                         ids=["bench", "transport", "complex"])
 def test_vs_oracle(cp, oracle, n, lam):
     N = int(np.prod(n))
     b = oracle.c_fill_uniform(N, 20251017)
@@ -447,7 +448,7 @@ def test_three_pass_128_vs_oracle(cp, oracle, lam):
 
 # ------------------------------------------------------------------ plane schedule (n_x = n_y)
 @pytest.mark.parametrize("n", [(100, 100, 100), (64, 64, 64), (128, 128, 128), (100, 100, 7), (64, 64, 2),
-                               (128, 128, 10)])
+                               (128, 128, 10)], ids=lambda n: "x".join(map(str, n)))
 def test_plane_vs_oracle(cp, oracle, n):
     """x + y DFTs of whole z-planes | fused z | inverse planes: against the oracle (separable
     symbol and explicit Diag), in place, and against the 5-pass schedule."""

@@ -47,9 +47,9 @@ def test_pcshell_apply_on_mesh(mods, name, oracle_v):
     lam = (complex(ctx.lambda_x), complex(ctx.lambda_y), complex(ctx.lambda_z))
     np.testing.assert_allclose(lam, [ad * dt * 1.0 / k for ad in a], rtol=1e-15)  # a dt (max-min)/n
     if name.startswith("mesh_hexa"):  # cells already in Cartesian order: identity, no remap
-        assert not ctx.intersectionMatrix and not ctx.remapBack
+        assert not ctx.intersectionMatrix and not P.context_remap_back(ctx)
     else:
-        assert ctx.intersectionMatrix and ctx.remapBack
+        assert ctx.intersectionMatrix and P.context_remap_back(ctx)
     pc = P.PC.shell(ctx).setup()
     rng = np.random.default_rng(11)
     b = rng.standard_normal(n) + 1j * rng.standard_normal(n)
@@ -68,7 +68,7 @@ def test_pcshell_apply_on_mesh(mods, name, oracle_v):
     assert np.abs(tx.cpu().numpy() - (3.0 - 1.0j)).max() < 1e-12
     pc.destroy()
     M.destroy_remap(ctx)
-    assert not ctx.intersectionMatrix and not ctx.remapBack
+    assert not ctx.intersectionMatrix and not P.context_remap_back(ctx)
 
 
 def _one_step_reference(M, m, sign):

@@ -30,7 +30,7 @@ def test_pcshell_apply_golden(P, golden, name):
     ctx = P.make_context(n, _lam(c))
     pc = P.PC.shell(ctx)
     pc.setup()  # setupFFTPrec3D: FFT matrix, Diag, work vectors
-    assert ctx.FFT_MAT and ctx.Diag and ctx.b_hat and ctx.b_cartesien and ctx.plan
+    assert ctx.FFT_MAT and ctx.Diag and ctx.b_hat and ctx.b_cartesien and P.context_plan(ctx)
     tb, tx = _dev(c["b"]), torch.zeros(int(np.prod(n)), dtype=torch.complex128, device="cuda")
     b, x = P.Vec.from_tensor(tb), P.Vec.from_tensor(tx)
     pc.apply(b, x)  # PCApply -> applyFFT3DPrecTransport
@@ -245,3 +245,55 @@ def test_device_vec_kernels(P):
     assert abs(x.norm(P.NORM_INFINITY) - np.abs(a).max()) < 1e-12
     x.axpy(0.5j, y)
     np.testing.assert_allclose(x.array(), a + 0.5j * bb, rtol=1e-14)
+
+
+@pytest.mark.parametrize("explicit", [False, True], ids=["own_symbol", "explicit_diag"])
+def test_solve_3D_in_place_host_vec(P, oracle, explicit):
+    """solve_3D(FFT_MAT, X, Diag, X, ...) on a host (VECSEQ) Vec, in place: staged through the
+    plan's persistent device buffer with checked copies (no per-call allocation), for the
+    plan's own symbol and for an explicit (scaled) Diag."""
+    n, lam = (32, 16, 8), (0.6, 0.15, 0.02)
+    N = int(np.prod(n))
+    b = oracle.c_fill_uniform(N, 21)
+    d0 = oracle.c_build_diag_transport(n, lam)
+    ctx = P.make_context(n, lam)
+    pc = P.PC.shell(ctx).setup()
+    F = P.Mat(ctypes_handle(ctx.FFT_MAT), owned=False)
+    diag = P.Vec.borrow(ctx.Diag)
+    if explicit:
+        diag.scale(0.5 + 0.5j)
+    vx = P.Vec.seq(N).set_array(b)
+    for k in range(3):  # repeated in-place solves reuse the staging buffer
+        vx.set_array(b)
+        P.solve_3D(F, vx, diag, vx, None, N)
+        dref = d0 * (0.5 + 0.5j) if explicit else d0
+        assert oracle.rel_l2(vx.array(), oracle.c_solve_3d(dref, b, n)) < TOL
+    assert F.solve_counts() == ((0, 3) if explicit else (3, 0))
+    pc.destroy()
+
+
+def test_symbol_set_on_the_plan_directly_leaves_the_fast_path(P, oracle):
+    """A symbol set on the plan behind FFT_MAT (MatFFTHIPGetPlan + cfp_plan_set_*) bumps the
+    plan's own symbol version: solve_3D then divides by the Diag it is given, not by the new
+    register symbol."""
+    from circulantpreconditioner_amd._lib import check, lib
+    import ctypes
+    n, lam = (16, 16, 8), (0.6, 0.15, 0.02)
+    N = int(np.prod(n))
+    b = oracle.c_fill_uniform(N, 3)
+    d0 = oracle.c_build_diag_transport(n, lam)
+    ctx = P.make_context(n, lam)
+    pc = P.PC.shell(ctx).setup()
+    F = P.Mat(ctypes_handle(ctx.FFT_MAT), owned=False)
+    v0, v1 = ctypes.c_uint64(), ctypes.c_uint64()
+    check(lib().cfp_plan_symbol_version(ctypes.c_void_p(P.context_plan(ctx)), ctypes.byref(v0)))
+    lam2 = (ctypes.c_double * 6)(2.0, 0.0, 0.5, 0.0, 0.1, 0.0)
+    check(lib().cfp_plan_set_symbol_transport(ctypes.c_void_p(P.context_plan(ctx)), lam2))
+    check(lib().cfp_plan_symbol_version(ctypes.c_void_p(P.context_plan(ctx)), ctypes.byref(v1)))
+    assert v1.value > v0.value
+    tb, tx = _dev(b), torch.empty(N, dtype=torch.complex128, device="cuda")
+    pc.apply(P.Vec.from_tensor(tb), P.Vec.from_tensor(tx))
+    torch.cuda.synchronize()
+    assert oracle.rel_l2(tx.cpu().numpy(), oracle.c_solve_3d(d0, b, n)) < TOL
+    assert F.solve_counts() == (0, 1)
+    pc.destroy()
