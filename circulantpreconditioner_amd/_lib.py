@@ -118,6 +118,7 @@ def _parse_decls(path: str) -> list:
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     txt = re.sub(r"//[^\n]*", "", txt)
     out = []
+    txt = re.sub(r"^\s*typedef[^;]*;", "", txt, flags=re.M)  # function-pointer typedefs are not exports
     for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][\w]*\s*\**\s*([A-Za-z_]\w*)\s*\([^;{]*\)\s*;", txt, flags=re.M):
         name = m.group(1)
         if name not in ("if", "while", "return", "sizeof") and len(name) > 2:

@@ -116,6 +116,42 @@ def declare(L) -> None:
         "cfp_group_apply": ([vp, P(vp), P(vp)], c_int),
         "cfp_group_set_schedule": ([vp, c_int], c_int),
         "cfp_dist_plan_set_schedule": ([vp, c_int], c_int),
+        "cfp_slab_steps_count": ([i64, i64, i64, c_int, c_int, c_int, c_int, c_int, P(c_int)], c_int),
+        "cfp_slab_steps_get": ([i64, i64, i64, c_int, c_int, c_int, c_int, c_int, c_int, P(i64),
+                                P(ctypes.c_double)], c_int),
+        "cfp_dist_plan_create_with_comm": ([P(vp), i64, i64, i64, c_int, c_int, vp, c_int], c_int),
+        "cfp_dist_plan_set_exchange": ([vp, vp, vp], c_int),
+        "cfp_dist_plan_set_work_buffers": ([vp, dp, dp], c_int),
+        "cfp_dist_plan_num_steps": ([vp, P(c_int)], c_int),
+        "cfp_dist_plan_step": ([vp, c_int, P(i64)], c_int),
+        "cfp_dist_plan_run_step": ([vp, c_int, dp, dp, vp], c_int),
+        "cfp_dist_plan_set_diag": ([vp, dp, vp], c_int),
+        "cfp_dist_plan_clear_diag": ([vp], c_int),
+        "cfp_dist_plan_forward": ([vp, dp, dp, vp], c_int),
+        "cfp_dist_plan_backward": ([vp, dp, dp, vp], c_int),
+        "cfp_dist_plan_set_pieces": ([vp, c_int], c_int),
+        "cfp_dist_plan_pieces": ([vp, P(c_int)], c_int),
+        "cfp_group_set_pieces": ([vp, c_int], c_int),
+        "cfp_dist_plan_use_diag": ([vp, c_int], c_int),
+        # PETSc stand-in: communicators and distributed objects
+        "MPI_Comm_size": ([c_int, P(c_int)], c_int),
+        "MPI_Comm_rank": ([c_int, P(c_int)], c_int),
+        "PetscMiniCommCreate": ([c_int, c_int, vp, P(c_int)], c_int),
+        "PetscMiniCommCreateRCCL": ([c_int, c_int, ctypes.c_char_p, P(c_int)], c_int),
+        "PetscMiniCommDestroy": ([P(c_int)], c_int),
+        "PetscMiniSetCommWorld": ([c_int], c_int),
+        "PetscMiniCommResolve": ([c_int, P(c_int)], c_int),
+        "PetscMiniAllreduce": ([c_int, P(ctypes.c_double), i64, c_int], c_int),
+        "PetscMiniCommGetNCCL": ([c_int, P(vp)], c_int),
+        "VecCreateMPI": ([c_int, i64, i64, P(vp)], c_int),
+        "VecCreateMPIHIP": ([c_int, i64, i64, P(vp)], c_int),
+        "VecCreateMPIHIPWithArray": ([c_int, i64, i64, i64, vp, P(vp)], c_int),
+        "VecGetComm": ([vp, P(c_int)], c_int),
+        "VecGetLocalSize": ([vp, P(i64)], c_int),
+        "VecGetOwnershipRange": ([vp, P(i64), P(i64)], c_int),
+        "MatGetLocalSize": ([vp, P(i64), P(i64)], c_int),
+        "MatGetComm": ([vp, P(c_int)], c_int),
+        "MatFFTHIPGetDistPlan": ([vp, P(vp)], c_int),
         # PETSc stand-in
         "PetscErrorLastMessage": ([], cs),
         "VecMiniSetStream": ([vp], c_int),

@@ -12,6 +12,14 @@
 // object state recorded after the write (PetscObjectStateGet: every write access bumps it),
 // and the plan's symbol unchanged since -- the apply evaluates the symbol in registers
 // instead of streaming Diag from HBM; anything else takes the explicit-Diag apply.
+//
+// Several ranks (the reference's MATFFTW on PETSC_COMM_WORLD, src/PCSHELLFft_3D.cxx:34-37, and
+// its MPI direct-solve driver, tests/TransportEquationFFT_SphericalExplosion_impl_mpi.cxx:66,
+// 100,111): the FFT matrix is backed by the z-slab plan (include/circulant_fft_dist.h), every
+// Vec holds its rank's PETSC_DECIDE rows = its z-planes, and the exchanges go through the
+// communicator (RCCL, or the caller's collectives).  Whether solve_3D may use the register
+// symbol, and whether an explicit Diag must be moved into the z-pencil layout again, is
+// decided on every rank and agreed by one all-reduce, so all ranks run the same collectives.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -19,8 +27,10 @@
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
+#include <vector>
 
 #include "../../include/circulant_fft.h"
+#include "../../include/circulant_fft_dist.h"
 #include "../../include/pcshell_fft3d.h"
 #include "pcshell_common.h"
 
@@ -29,9 +39,58 @@ using namespace cfp_pc;
 
 const int kFFTMagic = 0x46465448;  // "FFTH"
 
+#ifdef CFP_WITH_PETSC
+// Exchange piece over a real MPI communicator (cfp_dist_exchange_fn): host-staged
+// MPI_Alltoall of the [size][count] pieces.
+struct MpiExchange {
+  MPI_Comm comm;
+  int size;
+  std::vector<char> hs, hr;
+};
+int mpi_exchange(void* user, const double* src, double* dst, int64_t chunk, int64_t off, int64_t count, void* stream) {
+  MpiExchange* m = (MpiExchange*)user;
+  const size_t bytes = 16 * (size_t)count, pitch = 16 * (size_t)chunk;
+  if (bytes > (size_t)INT32_MAX) return 1;
+  m->hs.resize(bytes * m->size);
+  m->hr.resize(bytes * m->size);
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemcpy2DAsync(m->hs.data(), bytes, src + 2 * off, pitch, bytes, m->size, hipMemcpyDeviceToHost, st) ||
+      hipStreamSynchronize(st))
+    return 1;
+  if (MPI_Alltoall(m->hs.data(), (int)bytes, MPI_BYTE, m->hr.data(), (int)bytes, MPI_BYTE, m->comm)) return 1;
+  if (hipMemcpy2DAsync(dst + 2 * off, pitch, m->hr.data(), bytes, bytes, m->size, hipMemcpyHostToDevice, st) ||
+      hipStreamSynchronize(st))
+    return 1;
+  return 0;
+}
+#endif
+
+// max over the ranks of the FFT matrix' communicator (one rank: itself)
+PetscErrorCode comm_max(MPI_Comm comm, int nranks, double* v, int n) {
+  if (nranks == 1) return PETSC_SUCCESS;
+#ifdef CFP_WITH_PETSC
+  PetscCallMPI(MPI_Allreduce(MPI_IN_PLACE, v, n, MPI_DOUBLE, MPI_MAX, comm));
+#else
+  PetscCall(PetscMiniAllreduce(comm, v, n, PETSCMINI_OP_MAX));
+#endif
+  return PETSC_SUCCESS;
+}
+
 struct FFTShell {
   int magic = kFFTMagic;
-  cfp_plan_t plan = nullptr;
+  cfp_plan_t plan = nullptr;        // one rank
+  cfp_dist_plan_t dplan = nullptr;  // several ranks: this rank's z slab
+  MPI_Comm comm = PETSC_COMM_SELF;
+  int nranks = 1, rank = 0;
+  PetscInt nlocal = 0;              // this rank's rows (= N on one rank)
+  uint64_t dist_version = 0;        // symbol version of dplan (its setters are called here only)
+  // the explicit Diag last moved into dplan's z-pencil layout (0 id: none)
+  PetscObjectId dt_id = 0;
+  PetscObjectState dt_state = 0;
+  void* stage = nullptr;            // in-place host-Vec staging of the slab path (nlocal values)
+#ifdef CFP_WITH_PETSC
+  MpiExchange* mx = nullptr;
+#endif
   PetscInt dims[3] = {1, 1, 1};  // n_x, n_y, n_z
   bool has_lam = false;
   double lam[6] = {0, 0, 0, 0, 0, 0};
@@ -57,18 +116,26 @@ PetscErrorCode fft_shell(Mat A, FFTShell** out) {
 }
 
 
+// MatMult / MatMultTranspose: the unnormalised 3-D DFT; several ranks: of the slab-distributed
+// grid, natural slab in and out (FFTW-MPI's non-transposed layout)
 PetscErrorCode fft_mult_impl(Mat A, Vec x, Vec y, bool backward) {
   FFTShell* s;
   PetscCall(fft_shell(A, &s));
-  const PetscInt N = s->dims[0] * s->dims[1] * s->dims[2];
-  PetscCall(check_size(x, N, "MatMult: x has the wrong size"));
-  PetscCall(check_size(y, N, "MatMult: y has the wrong size"));
+  const PetscInt n = s->nlocal;
+  PetscCall(check_size(x, n, "MatMult: x has the wrong size"));
+  PetscCall(check_size(y, n, "MatMult: y has the wrong size"));
+  PetscCheck(x != y || !s->dplan, PETSC_COMM_SELF, PETSC_ERR_ARG_IDN, "MatMult: x and y must differ");
   DevIn in;
   DevOut out;
-  PetscCall(in.get(x, N));
-  PetscCall(out.get(y, N));
-  int rc = backward ? cfp_plan_backward(s->plan, in.ptr(), out.ptr(), nullptr)
-                    : cfp_plan_forward(s->plan, in.ptr(), out.ptr(), nullptr);
+  PetscCall(in.get(x, n));
+  PetscCall(out.get(y, n));
+  int rc;
+  if (s->dplan)
+    rc = backward ? cfp_dist_plan_backward(s->dplan, in.ptr(), out.ptr(), nullptr)
+                  : cfp_dist_plan_forward(s->dplan, in.ptr(), out.ptr(), nullptr);
+  else
+    rc = backward ? cfp_plan_backward(s->plan, in.ptr(), out.ptr(), nullptr)
+                  : cfp_plan_forward(s->plan, in.ptr(), out.ptr(), nullptr);
   if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
   PetscCall(out.put());
   PetscCall(in.put());
@@ -80,7 +147,12 @@ PetscErrorCode fft_mult_transpose(Mat A, Vec x, Vec y) { return fft_mult_impl(A,
 PetscErrorCode fft_destroy(Mat A) {
   FFTShell* s;
   PetscCall(fft_shell(A, &s));
-  cfp_plan_destroy(s->plan);
+  if (s->plan) cfp_plan_destroy(s->plan);
+  if (s->dplan) cfp_dist_plan_destroy(s->dplan);
+  if (s->stage) hipFree(s->stage);
+#ifdef CFP_WITH_PETSC
+  delete s->mx;
+#endif
   s->magic = 0;
   delete s;
   return PETSC_SUCCESS;
@@ -95,7 +167,8 @@ void lam6(PetscScalar lx, PetscScalar ly, PetscScalar lz, double out[6]) {
 // Use (or refresh) the plan's separable transport symbol for these lambdas (App. A item 9:
 // the reference rebuilds Diag on every direct-solve call; equal lambdas reuse it here).
 PetscErrorCode symbol_version(FFTShell* s, uint64_t* v) {
-  CFPCALL(cfp_plan_symbol_version(s->plan, v));
+  if (s->dplan) *v = s->dist_version;
+  else CFPCALL(cfp_plan_symbol_version(s->plan, v));
   return PETSC_SUCCESS;
 }
 
@@ -103,7 +176,12 @@ PetscErrorCode ensure_transport_symbol(FFTShell* s, const double lam[6]) {
   uint64_t v;
   PetscCall(symbol_version(s, &v));
   if (s->has_lam && v == s->lam_version && std::memcmp(s->lam, lam, sizeof(s->lam)) == 0) return PETSC_SUCCESS;
-  CFPCALL(cfp_plan_set_symbol_transport(s->plan, lam));
+  if (s->dplan) {
+    CFPCALL(cfp_dist_plan_set_symbol_transport(s->dplan, lam));
+    ++s->dist_version;
+  } else {
+    CFPCALL(cfp_plan_set_symbol_transport(s->plan, lam));
+  }
   std::memcpy(s->lam, lam, sizeof(s->lam));
   s->has_lam = true;
   PetscCall(symbol_version(s, &s->lam_version));
@@ -157,32 +235,66 @@ extern "C" PetscErrorCode FFTPrecTransportContextGetRemapBack(const FFTPrecTrans
   return PETSC_SUCCESS;
 }
 
+// the z-slab plan of this rank, its exchanges over `comm`
+PetscErrorCode create_dist(FFTShell* s, MPI_Comm comm, int dev) {
+  int64_t lay[8];
+  CFPCALL(cfp_slab_layout(s->dims[0], s->dims[1], s->dims[2], s->nranks, s->rank, lay));
+  s->nlocal = lay[4];
+#ifdef CFP_WITH_PETSC
+  CFPCALL(cfp_dist_plan_create_external(&s->dplan, s->dims[0], s->dims[1], s->dims[2], s->nranks, s->rank, dev));
+  s->mx = new MpiExchange{comm, s->nranks, {}, {}};
+  CFPCALL(cfp_dist_plan_set_exchange(s->dplan, mpi_exchange, s->mx));
+#else
+  MPI_Comm c;
+  PetscCall(PetscMiniCommResolve(comm, &c));
+  void* nccl = nullptr;
+  PetscCall(PetscMiniCommGetNCCL(c, &nccl));
+  if (nccl) {  // an RCCL communicator: the plan's exchanges are grouped ncclSend / ncclRecv on it
+    CFPCALL(cfp_dist_plan_create_with_comm(&s->dplan, s->dims[0], s->dims[1], s->dims[2], s->nranks, s->rank, nccl,
+                                           dev));
+  } else {     // the caller's collectives, host-staged
+    CFPCALL(cfp_dist_plan_create_external(&s->dplan, s->dims[0], s->dims[1], s->dims[2], s->nranks, s->rank, dev));
+    CFPCALL(cfp_dist_plan_set_exchange(s->dplan, PetscMiniCommExchange, (void*)(intptr_t)c));
+  }
+  s->comm = c;
+#endif
+  return PETSC_SUCCESS;
+}
+
 // ------------------------------------------------------------------ FFT matrix
+// MatCreateFFT(comm, ndim, dims, MATFFTW) of the reference (src/PCSHELLFft_3D.cxx:34-35): one
+// rank -> the single-GPU plan; several -> this rank's z slab (needs nranks | n_z, n_y)
 extern "C" PetscErrorCode MatCreateFFTHIP(MPI_Comm comm, PetscInt ndim, const PetscInt dims[], Mat* A) {
   PetscCheck(ndim >= 1 && ndim <= 3, PETSC_COMM_SELF, PETSC_ERR_ARG_OUTOFRANGE, "ndim must be 1, 2 or 3");
   PetscCheck(dims && A, PETSC_COMM_SELF, PETSC_ERR_ARG_NULL, "NULL argument");
-#ifdef CFP_WITH_PETSC
-  // one rank per FFT matrix: the local size is the global size.  Several ranks use the slab
-  // plan (include/circulant_fft_dist.h) instead.
-  PetscMPIInt nranks = 1;
+  int nranks = 1, rank = 0;
   PetscCallMPI(MPI_Comm_size(comm, &nranks));
-  PetscCheck(nranks == 1, comm, PETSC_ERR_SUP,
-             "MatCreateFFTHIP: the communicator has more than one rank; use cfp_dist_plan_* (z slabs) instead");
-#else
-  (void)comm;  // the stand-in PETSc is single-process by construction
-#endif
+  PetscCallMPI(MPI_Comm_rank(comm, &rank));
   FFTShell* s = new FFTShell;
+  s->comm = comm;
+  s->nranks = nranks;
+  s->rank = rank;
   // dims are row-major {n_z, n_y, n_x} (src/PCSHELLFft_3D.cxx:34): last = fastest = x
   for (PetscInt d = 0; d < ndim; ++d) s->dims[d] = dims[ndim - 1 - d];
+  const PetscInt N = s->dims[0] * s->dims[1] * s->dims[2];
+  s->nlocal = N;
   int dev = 0;
   hipGetDevice(&dev);
-  int rc = cfp_plan_create(&s->plan, s->dims[0], s->dims[1], s->dims[2], dev);
-  if (rc) {
-    delete s;
-    return cfp_err(rc, "MatCreateFFTHIP");
+  if (nranks > 1) {
+    PetscErrorCode e = create_dist(s, comm, dev);
+    if (e) {
+      if (s->dplan) cfp_dist_plan_destroy(s->dplan);
+      delete s;
+      return e;
+    }
+  } else {
+    int rc = cfp_plan_create(&s->plan, s->dims[0], s->dims[1], s->dims[2], dev);
+    if (rc) {
+      delete s;
+      return cfp_err(rc, "MatCreateFFTHIP");
+    }
   }
-  const PetscInt N = s->dims[0] * s->dims[1] * s->dims[2];
-  PetscCall(MatCreateShell(comm, N, N, N, N, s, A));
+  PetscCall(MatCreateShell(comm, s->nlocal, s->nlocal, N, N, s, A));
   PetscCall(MatShellSetOperation(*A, MATOP_MULT, (void (*)(void))fft_mult));
   PetscCall(MatShellSetOperation(*A, MATOP_MULT_TRANSPOSE, (void (*)(void))fft_mult_transpose));
   PetscCall(MatShellSetOperation(*A, MATOP_DESTROY, (void (*)(void))fft_destroy));
@@ -193,6 +305,13 @@ extern "C" PetscErrorCode MatFFTHIPGetPlan(Mat A, cfp_plan_t* plan) {
   FFTShell* s;
   PetscCall(fft_shell(A, &s));
   *plan = s->plan;
+  return PETSC_SUCCESS;
+}
+
+extern "C" PetscErrorCode MatFFTHIPGetDistPlan(Mat A, cfp_dist_plan_t* plan) {
+  FFTShell* s;
+  PetscCall(fft_shell(A, &s));
+  *plan = s->dplan;
   return PETSC_SUCCESS;
 }
 
@@ -218,12 +337,28 @@ extern "C" PetscErrorCode build_transport_col(Vec c, PetscInt size) {
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
-// build_diag_mat_vec_3D, :136-164: one device sweep instead of ~4N VecSetValue calls
+// Diag[k] = 1 + lx cx[kx] + ly cy[ky] + lz cz[kz] on this rank's planes [z0, z0 + nzl) (one
+// device sweep; cx, cy, cz device arrays of the full axes)
+PetscErrorCode build_diag_rows(double* diag, const double* cx, const double* cy, const double* cz, PetscInt nx,
+                               PetscInt ny, PetscInt z0, PetscInt nzl, const double lam[6]) {
+  int rc = cfp_build_diag_3d(diag, cx, cy, cz + 2 * z0, nx, ny, nzl, lam, nullptr);
+  if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
+  CFPCALL(rc);
+  return PETSC_SUCCESS;
+}
+
+// build_diag_mat_vec_3D, :136-164: one device sweep instead of ~4N VecSetValue calls.  A
+// distributed Diag gets its rank's rows (whole z-planes); the 1-D vectors hold the full axes.
 extern "C" PetscErrorCode build_diag_mat_vec_3D(Vec Diag, Vec cx, Vec cy, Vec cz, PetscInt nx, PetscInt ny,
                                                 PetscInt nz, PetscScalar lx, PetscScalar ly, PetscScalar lz) {
   PetscFunctionBeginUser;
-  const PetscInt N = nx * ny * nz;
-  PetscCall(check_size(Diag, N, "build_diag_mat_vec_3D: Diag size != n_x n_y n_z"));
+  PetscInt Ng, nloc, lo, hi;
+  PetscCall(VecGetSize(Diag, &Ng));
+  PetscCall(VecGetLocalSize(Diag, &nloc));
+  PetscCall(VecGetOwnershipRange(Diag, &lo, &hi));
+  PetscCheck(Ng == nx * ny * nz, PETSC_COMM_SELF, PETSC_ERR_ARG_SIZ, "build_diag_mat_vec_3D: Diag size != n_x n_y n_z");
+  PetscCheck(lo % (nx * ny) == 0 && nloc % (nx * ny) == 0, PETSC_COMM_SELF, PETSC_ERR_ARG_SIZ,
+             "build_diag_mat_vec_3D: a distributed Diag must hold whole z-planes");
   PetscCall(check_size(cx, nx, "build_diag_mat_vec_3D: c_x_hat size != n_x"));
   PetscCall(check_size(cy, ny, "build_diag_mat_vec_3D: c_y_hat size != n_y"));
   PetscCall(check_size(cz, nz, "build_diag_mat_vec_3D: c_z_hat size != n_z"));
@@ -232,20 +367,74 @@ extern "C" PetscErrorCode build_diag_mat_vec_3D(Vec Diag, Vec cx, Vec cy, Vec cz
   PetscCall(a.get(cx, nx));
   PetscCall(b.get(cy, ny));
   PetscCall(c.get(cz, nz));
-  PetscCall(d.get(Diag, N));
+  PetscCall(d.get(Diag, nloc));
   double lam[6];
   lam6(lx, ly, lz, lam);
-  int rc = cfp_build_diag_3d(d.ptr(), a.ptr(), b.ptr(), c.ptr(), nx, ny, nz, lam, nullptr);
-  if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
+  PetscErrorCode e = build_diag_rows(d.ptr(), a.ptr(), b.ptr(), c.ptr(), nx, ny, lo / (nx * ny), nloc / (nx * ny), lam);
   PetscCall(d.put());  // a write access: Diag's state moves on, so no plan treats it as its own symbol
   PetscCall(c.put());
   PetscCall(b.put());
   PetscCall(a.put());
-  CFPCALL(rc);
+  PetscCall(e);
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
-// solve_3D, :166-190: X = (1/size) F^T( F(b) ./ Diag ), fused into one 5-launch apply.
+// One apply of FFT_MAT's plan, X = (1/N) IDFT(DFT(b) ./ symbol): the register symbol (own) or
+// the explicit Diag (single rank: streamed; slab plan: the z-pencil copy already set).  b may be
+// X (the direct solver's Un, Un).  Host Vecs are staged: single rank through the plan's own
+// persistent buffer (cfp_plan_apply_host), slab plan through the shell's.  Synchronous.
+PetscErrorCode shell_apply(FFTShell* s, Vec X, Vec b, bool own, Vec Diag) {
+  const PetscInt n = s->nlocal;
+  DevIn din;
+  if (!own && !s->dplan) PetscCall(din.get(Diag, n));
+  if (s->dplan) CFPCALL(cfp_dist_plan_use_diag(s->dplan, own ? 0 : 1));
+  auto dev_apply = [&](const double* in, double* out) -> int {
+    if (s->dplan) return cfp_dist_plan_apply(s->dplan, in, out, nullptr);
+    return own ? cfp_plan_apply(s->plan, in, out, nullptr) : cfp_plan_apply_with_diag(s->plan, din.ptr(), in, out, nullptr);
+  };
+  int rc;
+  int stage_err = 0;  // slab path: failed host staging (PETSC_ERR_MEM / PETSC_ERR_LIB)
+  if (b == X) {
+    // in-place direct solve (PetscFft3DTransportSolver(ctx, Un, Un)): read-write access
+    PetscScalar* arr;
+    PetscMemType mt;
+    PetscCall(VecGetArrayAndMemType(X, &arr, &mt));
+    double* p = (double*)arr;
+    if (mt == PETSC_MEMTYPE_HOST && !s->dplan) {
+      // staged through the plan's persistent device buffer; both copies are checked, so a
+      // failed copy returns PETSC_ERR_LIB instead of leaving stale data behind
+      rc = own ? cfp_plan_apply_host(s->plan, p, p) : cfp_plan_apply_with_diag_host(s->plan, din.ptr(), p, p);
+    } else if (mt == PETSC_MEMTYPE_HOST) {
+      const size_t bytes = sizeof(PetscScalar) * (size_t)n;
+      rc = CFP_SUCCESS;
+      if (!s->stage && hipMalloc(&s->stage, bytes) != hipSuccess) stage_err = PETSC_ERR_MEM;
+      if (!stage_err && hipMemcpy(s->stage, p, bytes, hipMemcpyHostToDevice) != hipSuccess) stage_err = PETSC_ERR_LIB;
+      if (!stage_err) rc = dev_apply((const double*)s->stage, (double*)s->stage);
+      if (!stage_err && !rc) rc = cfp_stream_sync(nullptr);
+      if (!stage_err && !rc && hipMemcpy(p, s->stage, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+        stage_err = PETSC_ERR_LIB;
+    } else {
+      rc = dev_apply(p, p);
+      if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
+    }
+    PetscCall(VecRestoreArrayAndMemType(X, &arr));
+  } else {
+    DevIn bin;
+    DevOut xout;
+    PetscCall(bin.get(b, n));
+    PetscCall(xout.get(X, n));
+    rc = dev_apply(bin.ptr(), xout.ptr());
+    if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
+    PetscCall(xout.put());
+    PetscCall(bin.put());
+  }
+  if (!own && !s->dplan) PetscCall(din.put());
+  PetscCheck(!stage_err, PETSC_COMM_SELF, stage_err, "solve: host staging of the slab failed");
+  CFPCALL(rc);
+  return PETSC_SUCCESS;
+}
+
+// solve_3D, :166-190: X = (1/size) F^T( F(b) ./ Diag ), fused into one 3- or 5-launch apply.
 // b_hat is the reference's scratch vector; the fused apply needs none and leaves it untouched.
 extern "C" PetscErrorCode solve_3D(Mat FFT_MAT, Vec X, Vec Diag, Vec b, Vec b_hat, PetscInt size) {
   PetscFunctionBeginUser;
@@ -254,43 +443,35 @@ extern "C" PetscErrorCode solve_3D(Mat FFT_MAT, Vec X, Vec Diag, Vec b, Vec b_ha
   PetscCall(fft_shell(FFT_MAT, &s));
   const PetscInt N = s->dims[0] * s->dims[1] * s->dims[2];
   PetscCheck(size == N, PETSC_COMM_SELF, PETSC_ERR_ARG_SIZ, "solve_3D: size != number of grid cells of FFT_MAT");
-  PetscCall(check_size(X, N, "solve_3D: X has the wrong size"));
-  PetscCall(check_size(b, N, "solve_3D: b has the wrong size"));
-  PetscCall(check_size(Diag, N, "solve_3D: Diag has the wrong size"));
+  PetscCall(check_size(X, s->nlocal, "solve_3D: X has the wrong size"));
+  PetscCall(check_size(b, s->nlocal, "solve_3D: b has the wrong size"));
+  PetscCall(check_size(Diag, s->nlocal, "solve_3D: Diag has the wrong size"));
   // the plan's own symbol, if Diag was materialised from it and nothing has written to it since
   bool own = false;
   PetscCall(diag_is_own_symbol(s, Diag, &own));
-  ++(own ? s->solves_own : s->solves_diag);
-  DevIn bin, din;
-  if (!own) PetscCall(din.get(Diag, N));
-  int rc;
-  if (b == X) {
-    // in-place direct solve (PetscFft3DTransportSolver(ctx, Un, Un)): read-write access
-    PetscScalar* arr;
-    PetscMemType mt;
-    PetscCall(VecGetArrayAndMemType(X, &arr, &mt));
-    double* p = (double*)arr;
-    if (mt == PETSC_MEMTYPE_HOST) {
-      // staged through the plan's persistent device buffer; both copies are checked, so a
-      // failed copy returns PETSC_ERR_LIB instead of leaving stale data behind
-      rc = own ? cfp_plan_apply_host(s->plan, p, p) : cfp_plan_apply_with_diag_host(s->plan, din.ptr(), p, p);
-    } else {
-      rc = own ? cfp_plan_apply(s->plan, p, p, nullptr) : cfp_plan_apply_with_diag(s->plan, din.ptr(), p, p, nullptr);
+  if (s->dplan) {
+    // every rank must take the same path (the apply holds collectives): agree on it, and on
+    // whether the explicit Diag has to be moved into the z-pencil layout again
+    PetscObjectId id;
+    PetscObjectState st;
+    PetscCall(PetscObjectGetId((PetscObject)Diag, &id));
+    PetscCall(PetscObjectStateGet((PetscObject)Diag, &st));
+    double f[2] = {own ? 0.0 : 1.0, (id == s->dt_id && st == s->dt_state) ? 0.0 : 1.0};
+    PetscCall(comm_max(s->comm, s->nranks, f, 2));
+    own = f[0] == 0.0;
+    if (!own && f[1] != 0.0) {
+      DevIn din;
+      PetscCall(din.get(Diag, s->nlocal));
+      int rc = cfp_dist_plan_set_diag(s->dplan, din.ptr(), nullptr);
       if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
+      PetscCall(din.put());
+      CFPCALL(rc);
+      s->dt_id = id;
+      s->dt_state = st;
     }
-    PetscCall(VecRestoreArrayAndMemType(X, &arr));
-  } else {
-    DevOut xout;
-    PetscCall(bin.get(b, N));
-    PetscCall(xout.get(X, N));
-    rc = own ? cfp_plan_apply(s->plan, bin.ptr(), xout.ptr(), nullptr)
-             : cfp_plan_apply_with_diag(s->plan, din.ptr(), bin.ptr(), xout.ptr(), nullptr);
-    if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
-    PetscCall(xout.put());
-    PetscCall(bin.put());
   }
-  if (!own) PetscCall(din.put());
-  CFPCALL(rc);
+  ++(own ? s->solves_own : s->solves_diag);
+  PetscCall(shell_apply(s, X, b, own, Diag));
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
@@ -309,31 +490,9 @@ extern "C" PetscErrorCode FftTransportSolver(PetscInt nx, PetscInt ny, PetscInt 
   double lam[6];
   lam6(lx, ly, lz, lam);
   PetscCall(ensure_transport_symbol(s, lam));
-  const PetscInt N = nx * ny * nz;
-  PetscCall(check_size(X, N, "FftTransportSolver: X has the wrong size"));
-  PetscCall(check_size(b, N, "FftTransportSolver: b has the wrong size"));
-  int rc;
-  if (b == X) {
-    PetscScalar* arr;
-    PetscMemType mt;
-    PetscCall(VecGetArrayAndMemType(X, &arr, &mt));
-    if (mt == PETSC_MEMTYPE_HOST) rc = cfp_plan_apply_host(s->plan, (const double*)arr, (double*)arr);
-    else {
-      rc = cfp_plan_apply(s->plan, (const double*)arr, (double*)arr, nullptr);
-      if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
-    }
-    PetscCall(VecRestoreArrayAndMemType(X, &arr));
-  } else {
-    DevIn bin;
-    DevOut xout;
-    PetscCall(bin.get(b, N));
-    PetscCall(xout.get(X, N));
-    rc = cfp_plan_apply(s->plan, bin.ptr(), xout.ptr(), nullptr);
-    if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
-    PetscCall(xout.put());
-    PetscCall(bin.put());
-  }
-  CFPCALL(rc);
+  PetscCall(check_size(X, s->nlocal, "FftTransportSolver: X has the wrong size"));
+  PetscCall(check_size(b, s->nlocal, "FftTransportSolver: b has the wrong size"));
+  PetscCall(shell_apply(s, X, b, true, nullptr));
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
@@ -413,13 +572,32 @@ extern "C" PetscErrorCode setupFFTPrec3D(PC pc) {
   double lam[6];
   lam6(ctx->lambda_x, ctx->lambda_y, ctx->lambda_z, lam);
   PetscCall(ensure_transport_symbol(s, lam));
-  const PetscInt N = ctx->n_x * ctx->n_y * ctx->n_z;
   DevOut d;
-  PetscCall(d.get(ctx->Diag, N));
-  int rc = cfp_plan_get_diag(s->plan, d.ptr(), nullptr);
-  if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
+  PetscCall(d.get(ctx->Diag, s->nlocal));
+  PetscErrorCode e = PETSC_SUCCESS;
+  if (s->dplan) {  // this rank's z-planes of the closed-form Diag
+    const PetscInt nx = ctx->n_x, ny = ctx->n_y, nz = ctx->n_z;
+    std::vector<double> h(2 * (size_t)(nx + ny + nz));
+    int rc = cfp_transport_symbol_1d(nx, h.data());
+    if (!rc) rc = cfp_transport_symbol_1d(ny, h.data() + 2 * nx);
+    if (!rc) rc = cfp_transport_symbol_1d(nz, h.data() + 2 * (nx + ny));
+    void* t = nullptr;
+    if (!rc && hipMalloc(&t, sizeof(double) * h.size()) != hipSuccess) rc = CFP_ERR_MEM;
+    if (!rc && hipMemcpy(t, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice) != hipSuccess) rc = CFP_ERR_LIB;
+    PetscInt lo;
+    PetscCall(VecGetOwnershipRange(ctx->Diag, &lo, NULL));
+    const double* td = (const double*)t;
+    if (!rc) e = build_diag_rows(d.ptr(), td, td + 2 * nx, td + 2 * (nx + ny), nx, ny, lo / (nx * ny),
+                                 s->nlocal / (nx * ny), lam);
+    if (t) hipFree(t);
+    if (rc) e = cfp_err(rc, "setupFFTPrec3D");
+  } else {
+    int rc = cfp_plan_get_diag(s->plan, d.ptr(), nullptr);
+    if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
+    e = cfp_err(rc, "setupFFTPrec3D");
+  }
   PetscCall(d.put());
-  CFPCALL(rc);
+  PetscCall(e);
   // remember which object and state hold the symbol (solve_3D's register-symbol fast path)
   PetscCall(PetscObjectGetId((PetscObject)ctx->Diag, &s->diag_id));
   PetscCall(PetscObjectStateGet((PetscObject)ctx->Diag, &s->diag_state));

@@ -7,8 +7,10 @@
 // compiled out when building against a real PETSc (-DCFP_WITH_PETSC).
 #ifndef CFP_WITH_PETSC
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <atomic>
+#include <mutex>
 #include <sys/time.h>
 
 #include <cmath>
@@ -44,6 +46,188 @@ extern "C" PetscErrorCode VecMiniSetStream(void* s) {
 }
 
 #define ERR(code, msg) PetscErrorSet((code), __func__, (msg))
+
+// ------------------------------------------------------------------ communicators
+// handle 0 = PETSC_COMM_WORLD (resolves to g_world), 1 = PETSC_COMM_SELF, >= 2 created ones
+struct CommRec {
+  bool live = false;
+  int size = 1, rank = 0;
+  PetscMiniCommOps ops{};
+  ncclComm_t nccl = nullptr;
+  double* dbuf = nullptr;           // RCCL all-reduce staging (device)
+  int64_t dbuf_n = 0;
+  void* hsend = nullptr;            // exchange staging (pinned host)
+  void* hrecv = nullptr;
+  size_t hbytes = 0;
+};
+static std::mutex g_comm_mu;
+static std::vector<CommRec> g_comms(2);
+static MPI_Comm g_world = PETSC_COMM_SELF;
+
+static CommRec* comm_rec(MPI_Comm c) {
+  if (c == PETSC_COMM_WORLD) c = g_world;
+  if (c < 1 || c >= (MPI_Comm)g_comms.size() || (c >= 2 && !g_comms[(size_t)c].live)) return nullptr;
+  return &g_comms[(size_t)c];
+}
+static MPI_Comm comm_resolve(MPI_Comm c) { return c == PETSC_COMM_WORLD ? g_world : c; }
+
+extern "C" int MPI_Comm_size(MPI_Comm c, int* size) {
+  CommRec* r = comm_rec(c);
+  if (!r || !size) return 1;
+  *size = r->size;
+  return MPI_SUCCESS;
+}
+extern "C" int MPI_Comm_rank(MPI_Comm c, int* rank) {
+  CommRec* r = comm_rec(c);
+  if (!r || !rank) return 1;
+  *rank = r->rank;
+  return MPI_SUCCESS;
+}
+
+static PetscErrorCode comm_new(CommRec rec, MPI_Comm* out) {
+  std::lock_guard<std::mutex> g(g_comm_mu);
+  rec.live = true;
+  for (size_t i = 2; i < g_comms.size(); ++i)
+    if (!g_comms[i].live) {
+      g_comms[i] = rec;
+      *out = (MPI_Comm)i;
+      return PETSC_SUCCESS;
+    }
+  g_comms.push_back(rec);
+  *out = (MPI_Comm)(g_comms.size() - 1);
+  return PETSC_SUCCESS;
+}
+
+extern "C" PetscErrorCode PetscMiniCommCreate(int size, int rank, const PetscMiniCommOps* ops, MPI_Comm* comm) {
+  if (!comm) return ERR(PETSC_ERR_ARG_NULL, "NULL output");
+  if (size < 1 || rank < 0 || rank >= size) return ERR(PETSC_ERR_ARG_OUTOFRANGE, "rank / size");
+  if (size > 1 && (!ops || !ops->alltoall || !ops->allreduce))
+    return ERR(PETSC_ERR_ARG_NULL, "a communicator of several ranks needs alltoall and allreduce");
+  CommRec r;
+  r.size = size;
+  r.rank = rank;
+  if (ops) r.ops = *ops;
+  return comm_new(r, comm);
+}
+
+extern "C" PetscErrorCode PetscMiniCommCreateRCCL(int size, int rank, const char* uid, MPI_Comm* comm) {
+  if (!comm || !uid) return ERR(PETSC_ERR_ARG_NULL, "NULL argument");
+  if (size < 1 || rank < 0 || rank >= size) return ERR(PETSC_ERR_ARG_OUTOFRANGE, "rank / size");
+  CommRec r;
+  r.size = size;
+  r.rank = rank;
+  ncclUniqueId id;
+  std::memcpy(&id, uid, sizeof(id));
+  ncclResult_t nr = ncclCommInitRank(&r.nccl, size, id, rank);
+  if (nr != ncclSuccess) return ERR(PETSC_ERR_LIB, ncclGetErrorString(nr));
+  return comm_new(r, comm);
+}
+
+extern "C" PetscErrorCode PetscMiniCommDestroy(MPI_Comm* comm) {
+  if (!comm || *comm < 2) return PETSC_SUCCESS;
+  std::lock_guard<std::mutex> g(g_comm_mu);
+  if (*comm >= (MPI_Comm)g_comms.size()) return ERR(PETSC_ERR_ARG_WRONG, "unknown communicator");
+  CommRec& r = g_comms[(size_t)*comm];
+  if (r.nccl) ncclCommDestroy(r.nccl);
+  if (r.dbuf) hipFree(r.dbuf);
+  if (r.hsend) hipHostFree(r.hsend);
+  if (r.hrecv) hipHostFree(r.hrecv);
+  if (g_world == *comm) g_world = PETSC_COMM_SELF;
+  r = CommRec();
+  *comm = PETSC_COMM_SELF;
+  return PETSC_SUCCESS;
+}
+
+extern "C" PetscErrorCode PetscMiniSetCommWorld(MPI_Comm comm) {
+  comm = comm_resolve(comm);
+  if (!comm_rec(comm)) return ERR(PETSC_ERR_ARG_WRONG, "unknown communicator");
+  g_world = comm;
+  return PETSC_SUCCESS;
+}
+
+extern "C" PetscErrorCode PetscMiniCommResolve(MPI_Comm comm, MPI_Comm* out) {
+  if (!out) return ERR(PETSC_ERR_ARG_NULL, "NULL output");
+  *out = comm_resolve(comm);
+  return PETSC_SUCCESS;
+}
+
+extern "C" PetscErrorCode PetscMiniCommGetNCCL(MPI_Comm comm, void** nccl) {
+  CommRec* r = comm_rec(comm);
+  if (!r || !nccl) return ERR(PETSC_ERR_ARG_WRONG, "unknown communicator");
+  *nccl = (void*)r->nccl;
+  return PETSC_SUCCESS;
+}
+
+extern "C" PetscErrorCode PetscMiniAllreduce(MPI_Comm comm, double* buf, int64_t count, int op) {
+  CommRec* r = comm_rec(comm);
+  if (!r) return ERR(PETSC_ERR_ARG_WRONG, "unknown communicator");
+  if (r->size == 1 || count <= 0) return PETSC_SUCCESS;
+  if (r->nccl) {
+    if (r->dbuf_n < count) {
+      if (r->dbuf) hipFree(r->dbuf);
+      r->dbuf = nullptr;
+      r->dbuf_n = 0;
+      if (hipMalloc(&r->dbuf, sizeof(double) * (size_t)count) != hipSuccess) return ERR(PETSC_ERR_MEM, "allreduce buffer");
+      r->dbuf_n = count;
+    }
+    if (hipMemcpyAsync(r->dbuf, buf, sizeof(double) * (size_t)count, hipMemcpyHostToDevice, g_stream) != hipSuccess)
+      return ERR(PETSC_ERR_LIB, "allreduce copy");
+    ncclResult_t nr = ncclAllReduce(r->dbuf, r->dbuf, (size_t)count, ncclDouble, op == PETSCMINI_OP_MAX ? ncclMax : ncclSum,
+                                    r->nccl, g_stream);
+    if (nr != ncclSuccess) return ERR(PETSC_ERR_LIB, ncclGetErrorString(nr));
+    if (hipMemcpyAsync(buf, r->dbuf, sizeof(double) * (size_t)count, hipMemcpyDeviceToHost, g_stream) != hipSuccess ||
+        hipStreamSynchronize(g_stream) != hipSuccess)
+      return ERR(PETSC_ERR_LIB, "allreduce copy back");
+    return PETSC_SUCCESS;
+  }
+  if (r->ops.allreduce(r->ops.user, buf, count, op)) return ERR(PETSC_ERR_LIB, "allreduce callback failed");
+  return PETSC_SUCCESS;
+}
+
+// one exchange piece of a slab plan (include/circulant_fft_dist.h, cfp_dist_exchange_fn)
+extern "C" int PetscMiniCommExchange(void* user, const double* src, double* dst, int64_t chunk, int64_t off,
+                                     int64_t count, void* stream) {
+  CommRec* r = comm_rec((MPI_Comm)(intptr_t)user);
+  if (!r) return PetscErrorSet(PETSC_ERR_ARG_WRONG, __func__, "unknown communicator");
+  hipStream_t st = (hipStream_t)stream;
+  const cd* s = (const cd*)src + off;
+  cd* d = (cd*)dst + off;
+  const size_t bytes = sizeof(cd) * (size_t)count, pitch = sizeof(cd) * (size_t)chunk;
+  if (r->nccl) {
+    if (hipMemcpyAsync(d + r->rank * chunk, s + r->rank * chunk, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+      return PetscErrorSet(PETSC_ERR_LIB, __func__, "self copy");
+    if (ncclGroupStart() != ncclSuccess) return PetscErrorSet(PETSC_ERR_LIB, __func__, "ncclGroupStart");
+    for (int q = 0; q < r->size; ++q) {
+      if (q == r->rank) continue;
+      if (ncclSend(s + q * chunk, 2 * (size_t)count, ncclDouble, q, r->nccl, st) != ncclSuccess ||
+          ncclRecv(d + q * chunk, 2 * (size_t)count, ncclDouble, q, r->nccl, st) != ncclSuccess)
+        return PetscErrorSet(PETSC_ERR_LIB, __func__, "ncclSend / ncclRecv");
+    }
+    if (ncclGroupEnd() != ncclSuccess) return PetscErrorSet(PETSC_ERR_LIB, __func__, "ncclGroupEnd");
+    return 0;
+  }
+  // callback communicator: [size][count] pieces through pinned host buffers
+  const size_t total = bytes * (size_t)r->size;
+  if (r->hbytes < total) {
+    if (r->hsend) hipHostFree(r->hsend);
+    if (r->hrecv) hipHostFree(r->hrecv);
+    r->hsend = r->hrecv = nullptr;
+    r->hbytes = 0;
+    if (hipHostMalloc(&r->hsend, total) != hipSuccess || hipHostMalloc(&r->hrecv, total) != hipSuccess)
+      return PetscErrorSet(PETSC_ERR_MEM, __func__, "pinned staging");
+    r->hbytes = total;
+  }
+  if (hipMemcpy2DAsync(r->hsend, bytes, s, pitch, bytes, (size_t)r->size, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return PetscErrorSet(PETSC_ERR_LIB, __func__, "device to host");
+  if (r->size == 1) std::memcpy(r->hrecv, r->hsend, bytes);
+  else if (r->ops.alltoall(r->ops.user, r->hsend, r->hrecv, (int64_t)bytes))
+    return PetscErrorSet(PETSC_ERR_LIB, __func__, "alltoall callback failed");
+  if (hipMemcpy2DAsync(d, pitch, r->hrecv, bytes, bytes, (size_t)r->size, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)  // the staging buffers are reused by the next piece
+    return PetscErrorSet(PETSC_ERR_LIB, __func__, "host to device");
+  return 0;
+}
 #define HCHK(expr)                                                      \
   do {                                                                  \
     hipError_t e__ = (expr);                                            \
@@ -58,7 +242,11 @@ static const int kVecMagic = 0x56656331;
 
 struct _p_Vec {
   int magic = kVecMagic;
-  PetscInt n = 0;
+  PetscInt n = 0;        // local size
+  PetscInt N = 0;        // global size
+  PetscInt rstart = 0;   // first global row of this rank
+  MPI_Comm comm = PETSC_COMM_SELF;
+  int nranks = 1;
   bool hip = false;
   cd* d = nullptr;
   cd* h = nullptr;
@@ -121,6 +309,7 @@ static PetscErrorCode vec_new(PetscInt n, bool hip, const PetscScalar* devarr, V
   Vec v = new _p_Vec;
   v->id = ++g_object_ids;
   v->n = n;
+  v->N = n;
   v->hip = hip;
   if (hip) {
     hipGetDevice(&v->device);
@@ -147,15 +336,78 @@ extern "C" PetscErrorCode VecCreateSeqHIP(MPI_Comm, PetscInt n, Vec* v) { return
 extern "C" PetscErrorCode VecCreateSeqHIPWithArray(MPI_Comm, PetscInt, PetscInt n, const PetscScalar* a, Vec* v) {
   return vec_new(n, true, a, v);
 }
-extern "C" PetscErrorCode VecCreateMPI(MPI_Comm, PetscInt nlocal, PetscInt N, Vec* v) {
-  // single process: the local part is everything
-  PetscInt n = N >= 0 ? N : nlocal;
-  if (nlocal >= 0 && N >= 0 && nlocal != N) return ERR(PETSC_ERR_ARG_SIZ, "one process: local size must equal N");
-  return vec_new(n, true, nullptr, v);
+// PETSC_DECIDE rows (PetscSplitOwnership): N / size each, the first N % size ranks one more;
+// with every local size given, N and the row start come from one all-reduce of the sizes
+static PetscErrorCode mpi_layout(MPI_Comm comm, PetscInt nlocal, PetscInt N, PetscInt* n, PetscInt* Ng, PetscInt* rstart) {
+  CommRec* r = comm_rec(comm);
+  if (!r) return ERR(PETSC_ERR_ARG_WRONG, "unknown communicator");
+  if (nlocal < 0 && N < 0) return ERR(PETSC_ERR_ARG_WRONG, "local or global size must be given");
+  const int P = r->size, k = r->rank;
+  if (nlocal < 0) {
+    *n = N / P + (k < N % P ? 1 : 0);
+    *Ng = N;
+    *rstart = k * (N / P) + (k < N % P ? k : N % P);
+    return PETSC_SUCCESS;
+  }
+  std::vector<double> sizes((size_t)P, 0.0);
+  sizes[(size_t)k] = (double)nlocal;
+  PetscCall(PetscMiniAllreduce(comm, sizes.data(), P, PETSCMINI_OP_SUM));
+  PetscInt tot = 0, start = 0;
+  for (int q = 0; q < P; ++q) {
+    if (q == k) start = tot;
+    tot += (PetscInt)sizes[(size_t)q];
+  }
+  if (N >= 0 && N != tot) return ERR(PETSC_ERR_ARG_SIZ, "the local sizes do not add up to N");
+  *n = nlocal;
+  *Ng = tot;
+  *rstart = start;
+  return PETSC_SUCCESS;
+}
+
+static PetscErrorCode vec_mpi(MPI_Comm comm, PetscInt nlocal, PetscInt N, bool hip, Vec* v,
+                              const PetscScalar* devarr = nullptr) {
+  comm = comm_resolve(comm);
+  PetscInt n, Ng, rs;
+  PetscCall(mpi_layout(comm, nlocal, N, &n, &Ng, &rs));
+  PetscCall(vec_new(n, hip, devarr, v));
+  (*v)->N = Ng;
+  (*v)->rstart = rs;
+  (*v)->comm = comm;
+  MPI_Comm_size(comm, &(*v)->nranks);
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode VecCreateMPI(MPI_Comm comm, PetscInt nlocal, PetscInt N, Vec* v) {
+  return vec_mpi(comm, nlocal, N, false, v);
+}
+extern "C" PetscErrorCode VecCreateMPIHIP(MPI_Comm comm, PetscInt nlocal, PetscInt N, Vec* v) {
+  return vec_mpi(comm, nlocal, N, true, v);
+}
+extern "C" PetscErrorCode VecCreateMPIHIPWithArray(MPI_Comm comm, PetscInt, PetscInt nlocal, PetscInt N,
+                                                   const PetscScalar* a, Vec* v) {
+  if (!a) return ERR(PETSC_ERR_ARG_NULL, "NULL array");
+  return vec_mpi(comm, nlocal, N, true, v, a);
+}
+extern "C" PetscErrorCode VecGetComm(Vec v, MPI_Comm* comm) {
+  VCHK(v);
+  *comm = v->comm;
+  return PETSC_SUCCESS;
+}
+static void vec_copy_layout(Vec from, Vec to) {
+  to->N = from->N;
+  to->rstart = from->rstart;
+  to->comm = from->comm;
+  to->nranks = from->nranks;
 }
 extern "C" PetscErrorCode VecDuplicate(Vec v, Vec* nv) {
   VCHK(v);
-  return vec_new(v->n, v->hip, nullptr, nv);
+  PetscCall(vec_new(v->n, v->hip, nullptr, nv));
+  vec_copy_layout(v, *nv);
+  return PETSC_SUCCESS;
+}
+// sum (or max) over the Vec's communicator; no-op on one rank
+static PetscErrorCode vec_reduce(Vec v, double* buf, int64_t count, int op) {
+  if (v->nranks == 1) return PETSC_SUCCESS;
+  return PetscMiniAllreduce(v->comm, buf, count, op);
 }
 extern "C" PetscErrorCode VecDestroy(Vec* pv) {
   if (!pv || !*pv) return PETSC_SUCCESS;
@@ -184,15 +436,15 @@ extern "C" PetscErrorCode PetscObjectGetId(PetscObject obj, PetscObjectId* id) {
 }
 extern "C" PetscErrorCode VecGetType(Vec v, VecType* t) {
   VCHK(v);
-  *t = v->hip ? VECSEQHIP : VECSEQ;
+  *t = v->nranks > 1 ? (v->hip ? VECMPIHIP : VECMPI) : (v->hip ? VECSEQHIP : VECSEQ);
   return PETSC_SUCCESS;
 }
-extern "C" PetscErrorCode VecGetSize(Vec v, PetscInt* n) { VCHK(v); *n = v->n; return PETSC_SUCCESS; }
+extern "C" PetscErrorCode VecGetSize(Vec v, PetscInt* n) { VCHK(v); *n = v->N; return PETSC_SUCCESS; }
 extern "C" PetscErrorCode VecGetLocalSize(Vec v, PetscInt* n) { VCHK(v); *n = v->n; return PETSC_SUCCESS; }
 extern "C" PetscErrorCode VecGetOwnershipRange(Vec v, PetscInt* lo, PetscInt* hi) {
   VCHK(v);
-  if (lo) *lo = 0;
-  if (hi) *hi = v->n;
+  if (lo) *lo = v->rstart;
+  if (hi) *hi = v->rstart + v->n;
   return PETSC_SUCCESS;
 }
 
@@ -358,10 +610,12 @@ extern "C" PetscErrorCode VecSetValues(Vec v, PetscInt n, const PetscInt* idx, c
   PetscCall(host_rw(v, &h));
   for (PetscInt k = 0; k < n; ++k) {
     if (idx[k] < 0) continue;
-    if (idx[k] >= v->n) return ERR(PETSC_ERR_ARG_OUTOFRANGE, "index out of range");
+    if (idx[k] >= v->N) return ERR(PETSC_ERR_ARG_OUTOFRANGE, "index out of range");
+    const PetscInt i = idx[k] - v->rstart;  // global row -> local; other ranks' rows are not kept
+    if (i < 0 || i >= v->n) continue;
     cd val = tocd(y[k]);
-    if (mode == ADD_VALUES) val = cfp::make_cd(h[idx[k]].x + val.x, h[idx[k]].y + val.y);
-    h[idx[k]] = val;
+    if (mode == ADD_VALUES) val = cfp::make_cd(h[i].x + val.x, h[i].y + val.y);
+    h[i] = val;
   }
   return PETSC_SUCCESS;
 }
@@ -370,8 +624,9 @@ extern "C" PetscErrorCode VecGetValues(Vec v, PetscInt n, const PetscInt* idx, P
   const cd* h;
   PetscCall(host_read(v, &h));
   for (PetscInt k = 0; k < n; ++k) {
-    if (idx[k] < 0 || idx[k] >= v->n) return ERR(PETSC_ERR_ARG_OUTOFRANGE, "index out of range");
-    y[k] = PetscScalar(h[idx[k]].x, h[idx[k]].y);
+    const PetscInt i = idx[k] - v->rstart;  // local rows only, as PETSc's VecGetValues
+    if (i < 0 || i >= v->n) return ERR(PETSC_ERR_ARG_OUTOFRANGE, "index not owned by this rank");
+    y[k] = PetscScalar(h[i].x, h[i].y);
   }
   return PETSC_SUCCESS;
 }
@@ -517,6 +772,9 @@ extern "C" PetscErrorCode VecDot(Vec x, Vec y, PetscScalar* val) {  // y^H x
     for (i64 i = 0; i < x->n; ++i) s += C(xh[i]) * std::conj(C(yh[i]));
     *val = s;
   }
+  double buf[2] = {val->real(), val->imag()};
+  PetscCall(vec_reduce(x, buf, 2, PETSCMINI_OP_SUM));
+  *val = PetscScalar(buf[0], buf[1]);
   return PETSC_SUCCESS;
 }
 extern "C" PetscErrorCode VecNorm(Vec x, NormType t, PetscReal* val) {
@@ -537,6 +795,11 @@ extern "C" PetscErrorCode VecNorm(Vec x, NormType t, PetscReal* val) {
     }
     *val = t == NORM_2 ? std::sqrt(s) : s;
   }
+  if (x->nranks > 1) {  // local norms -> the global one
+    double v = t == NORM_2 ? (*val) * (*val) : *val;
+    PetscCall(vec_reduce(x, &v, 1, t == NORM_INFINITY ? PETSCMINI_OP_MAX : PETSCMINI_OP_SUM));
+    *val = t == NORM_2 ? std::sqrt(v) : v;
+  }
   return PETSC_SUCCESS;
 }
 
@@ -556,6 +819,7 @@ extern "C" PetscErrorCode VecMDot(Vec x, PetscInt nv, const Vec y[], PetscScalar
     for (PetscInt j = 0; j < nv; ++j) PetscCall(dev_read(y[j], &ys[(size_t)j]));
     std::vector<cd> r((size_t)nv);
     HIPK(cfp::blas_mdot(xd, (int)nv, ys.data(), x->n, r.data(), g_stream));
+    PetscCall(vec_reduce(x, (double*)r.data(), 2 * nv, PETSCMINI_OP_SUM));  // one all-reduce for all nv
     for (PetscInt j = 0; j < nv; ++j) val[j] = PetscScalar(r[(size_t)j].x, r[(size_t)j].y);
     return PETSC_SUCCESS;
   }
@@ -620,7 +884,9 @@ typedef PetscErrorCode (*MatDestroyFn)(Mat);
 struct _p_Mat {
   int magic = kMatMagic;
   std::string type;
-  PetscInt m = 0, n = 0;
+  PetscInt m = 0, n = 0;    // global sizes
+  PetscInt lm = 0, ln = 0;  // local sizes
+  MPI_Comm comm = PETSC_COMM_SELF;
   void* ctx = nullptr;
   MatMultFn mult = nullptr, multT = nullptr;
   MatDestroyFn destroy = nullptr;
@@ -637,12 +903,15 @@ static PetscErrorCode mcheck(Mat A, const char* f) {
 }
 #define MCHK(A) PetscCall(mcheck((A), __func__))
 
-extern "C" PetscErrorCode MatCreateShell(MPI_Comm, PetscInt m, PetscInt n, PetscInt M, PetscInt N, void* ctx, Mat* A) {
+extern "C" PetscErrorCode MatCreateShell(MPI_Comm comm, PetscInt m, PetscInt n, PetscInt M, PetscInt N, void* ctx, Mat* A) {
   if (!A) return ERR(PETSC_ERR_ARG_NULL, "NULL output");
   Mat a = new _p_Mat;
   a->type = MATSHELL;
   a->m = M >= 0 ? M : m;
   a->n = N >= 0 ? N : n;
+  a->lm = m >= 0 ? m : a->m;
+  a->ln = n >= 0 ? n : a->n;
+  a->comm = comm_resolve(comm);
   a->ctx = ctx;
   *A = a;
   return PETSC_SUCCESS;
@@ -666,8 +935,8 @@ extern "C" PetscErrorCode MatCreateSeqAIJWithArrays(MPI_Comm, PetscInt m, PetscI
   if (!A || !i || !j || !a) return ERR(PETSC_ERR_ARG_NULL, "NULL argument");
   Mat M = new _p_Mat;
   M->type = MATSEQAIJ;
-  M->m = m;
-  M->n = n;
+  M->m = M->lm = m;
+  M->n = M->ln = n;
   const i64 nnz = i[m];
   M->h_rowptr.assign(i, i + m + 1);
   M->h_col.assign(j, j + nnz);
@@ -707,7 +976,19 @@ extern "C" PetscErrorCode MatGetSize(Mat A, PetscInt* m, PetscInt* n) {
   if (n) *n = A->n;
   return PETSC_SUCCESS;
 }
+extern "C" PetscErrorCode MatGetLocalSize(Mat A, PetscInt* m, PetscInt* n) {
+  MCHK(A);
+  if (m) *m = A->lm;
+  if (n) *n = A->ln;
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode MatGetComm(Mat A, MPI_Comm* comm) {
+  MCHK(A);
+  *comm = A->comm;
+  return PETSC_SUCCESS;
+}
 static PetscErrorCode aij_mult(Mat A, Vec x, Vec y) {
+  if (x->nranks > 1 || y->nranks > 1) return ERR(PETSC_ERR_SUP, "the stand-in AIJ matrix is sequential");
   if (x->n != A->n || y->n != A->m) return ERR(PETSC_ERR_ARG_SIZ, "MatMult sizes");
   if (x == y) return ERR(PETSC_ERR_ARG_IDN, "x and y must be different vectors");
   if (x->hip && y->hip) {
@@ -780,9 +1061,14 @@ extern "C" PetscErrorCode MatCreateFFT(MPI_Comm comm, PetscInt ndim, const Petsc
 }
 extern "C" PetscErrorCode MatCreateVecsFFTW(Mat A, Vec* x, Vec* y, Vec* z) {
   MCHK(A);
+  int P = 1;
+  MPI_Comm_size(A->comm, &P);
   Vec* outs[3] = {x, y, z};
-  for (Vec* o : outs)
-    if (o) PetscCall(VecCreateSeqHIP(PETSC_COMM_SELF, A->n, o));
+  for (Vec* o : outs) {
+    if (!o) continue;
+    if (P > 1) PetscCall(VecCreateMPIHIP(A->comm, A->ln, A->n, o));  // the matrix' slab rows
+    else PetscCall(VecCreateSeqHIP(PETSC_COMM_SELF, A->n, o));
+  }
   return PETSC_SUCCESS;
 }
 

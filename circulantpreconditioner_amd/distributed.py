@@ -38,20 +38,28 @@ def slab_layout(dims: Sequence[int], nranks: int, rank: int) -> dict:
 
 STEP_KEYS = ("kind", "src", "dst", "axis", "n", "mode", "ncols", "inner_n",
              "in_inner", "in_outer", "in_pt", "in_seg_len", "in_seg_stride",
-             "out_inner", "out_outer", "out_pt", "out_seg_len", "out_seg_stride")
+             "out_inner", "out_outer", "out_pt", "out_seg_len", "out_seg_stride",
+             "src_off", "dst_off", "ex_off", "ex_cnt", "chunk", "wait", "lnyl", "k1_off", "seg", "fused")
+STEP_KINDS = {0: "pass", 1: "exchange", 2: "three_sweep", 3: "repack"}
+STEP_LISTS = {"apply": 0, "apply_diag": 1, "forward": 2, "backward": 3, "diag": 4}
 
 
-def slab_steps(dims: Sequence[int], nranks: int, rank: int) -> list:
-    """Host-only: the steps rank `rank`'s cfp_dist_plan_apply runs, as dicts (STEP_KEYS + scale);
-    buffers 0 = b, 1 = x, 2 = work (include/circulant_fft_dist.h)."""
+def slab_steps(dims: Sequence[int], nranks: int, rank: int, schedule="five", pieces: int = 1,
+               list_: str = "apply") -> list:
+    """Host-only: the steps of rank `rank`'s slab plan as dicts (STEP_KEYS + scale): `schedule`
+    'auto' | 'five' | 'three', `pieces` 0 (AUTO) or K, `list_` 'apply' | 'apply_diag' | 'forward'
+    | 'backward' | 'diag' (cfp_slab_steps_get; buffers 0 = b, 1 = x, 2 = W, 3 = W2, 4 = the
+    z-pencil Diag).  The defaults are the round-2 list: five passes, one piece."""
     nx, ny, nz = (int(d) for d in dims)
+    sch, lst = _slab_schedule(schedule), STEP_LISTS[list_]
     n = ctypes.c_int()
-    check(lib().cfp_slab_num_steps(nx, ny, nz, int(nranks), int(rank), ctypes.byref(n)))
+    check(lib().cfp_slab_steps_count(nx, ny, nz, int(nranks), int(rank), sch, int(pieces), lst, ctypes.byref(n)))
     out = []
     for i in range(n.value):
-        desc = (ctypes.c_int64 * 18)()
+        desc = (ctypes.c_int64 * len(STEP_KEYS))()
         sc = ctypes.c_double()
-        check(lib().cfp_slab_step_info(nx, ny, nz, int(nranks), int(rank), i, desc, ctypes.byref(sc)))
+        check(lib().cfp_slab_steps_get(nx, ny, nz, int(nranks), int(rank), sch, int(pieces), lst, i, desc,
+                                       ctypes.byref(sc)))
         d = dict(zip(STEP_KEYS, list(desc)))
         d["scale"] = sc.value
         out.append(d)
@@ -95,7 +103,8 @@ class SlabPlan:
             check(lib().cfp_dist_plan_create_external(ctypes.byref(h), nx, ny, nz, self.world, self.rank,
                                                       self.device))
             self.work = torch.empty(self.local_size, dtype=torch.complex128, device=f"cuda:{self.device}")
-            check(lib().cfp_dist_plan_set_work_buffer(h, self.work.data_ptr()))
+            self.work2 = torch.empty_like(self.work)
+            check(lib().cfp_dist_plan_set_work_buffers(h, self.work.data_ptr(), self.work2.data_ptr()))
         else:
             raise ValueError("exchange must be 'rccl' or 'torch'")
         self._h = h
@@ -117,14 +126,53 @@ class SlabPlan:
         check(lib().cfp_dist_plan_set_schedule(self._h, _slab_schedule(schedule)))
         return self
 
-    def _all_to_all(self, dst: torch.Tensor, src: torch.Tensor) -> None:
+    def set_pieces(self, pieces: int) -> "SlabPlan":
+        """Pipeline depth: 0 = AUTO, K = each all-to-all in K pieces overlapped with the x/y passes."""
+        check(lib().cfp_dist_plan_set_pieces(self._h, int(pieces)))
+        return self
+
+    @property
+    def pieces(self) -> int:
+        k = ctypes.c_int()
+        check(lib().cfp_dist_plan_pieces(self._h, ctypes.byref(k)))
+        return k.value
+
+    def set_diag(self, diag: torch.Tensor, stream=None) -> "SlabPlan":
+        """Explicit Diag: this rank's natural slab (a collective; rccl exchange only)."""
+        if self.exchange != "rccl":
+            raise NotImplementedError("set_diag runs its exchange inside the library (exchange='rccl')")
+        check(lib().cfp_dist_plan_set_diag(self._h, _dev_ptr(diag, self.local_size, "diag", self.device),
+                                           _stream_handle(stream)))
+        return self
+
+    def steps(self) -> list:
+        """The apply's step list (dicts of STEP_KEYS)."""
+        n = ctypes.c_int()
+        check(lib().cfp_dist_plan_num_steps(self._h, ctypes.byref(n)))
+        out = []
+        for i in range(n.value):
+            desc = (ctypes.c_int64 * len(STEP_KEYS))()
+            check(lib().cfp_dist_plan_step(self._h, i, desc))
+            out.append(dict(zip(STEP_KEYS, list(desc))))
+        return out
+
+    def _buffers(self, b, x):
+        return {0: b, 1: x, 2: self.work, 3: self.work2}
+
+    def _exchange_piece(self, st: dict, bufs: dict) -> None:
+        """One all-to-all piece through torch.distributed: peer q gets src[q chunk + off, + cnt)
+        and stores it at dst[rank chunk + off] (gloo: staged through host memory)."""
         import torch.distributed as dist
-        if dist.get_backend(self.group) == "gloo":  # gloo exchanges host tensors only
-            h = torch.empty(dst.numel(), dtype=dst.dtype)
-            dist.all_to_all_single(h, src.cpu(), group=self.group)
-            dst.copy_(h)
-        else:
-            dist.all_to_all_single(dst, src, group=self.group)
+        c, off, cnt = st["chunk"], st["ex_off"], st["ex_cnt"]
+        src, dst = bufs[st["src"]], bufs[st["dst"]]
+        send = torch.cat([src[q * c + off:q * c + off + cnt] for q in range(self.world)])
+        gloo = dist.get_backend(self.group) == "gloo"
+        if gloo:
+            send = send.cpu()
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send, group=self.group)
+        for q in range(self.world):
+            dst[q * c + off:q * c + off + cnt].copy_(recv[q * cnt:(q + 1) * cnt])
 
     def apply(self, b: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
         if out is None:
@@ -135,29 +183,37 @@ class SlabPlan:
         if self.exchange == "rccl":
             check(lib().cfp_dist_plan_apply(self._h, bp, xp, sh))
             return out
-        # the segments run on `stream`; the collectives are ordered on torch's current stream,
-        # so make that the same stream for the whole apply
+        # the library's step list, one stream: kernel steps through cfp_dist_plan_run_step, the
+        # exchange pieces through torch.distributed (ordered on torch's current stream, so
+        # make that the apply's stream)
+        bufs = self._buffers(b, out)
         with (torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()):
-            check(lib().cfp_dist_plan_run_segment(self._h, 0, bp, xp, sh))
-            self._all_to_all(out, self.work)  # work chunks -> x chunks
-            check(lib().cfp_dist_plan_run_segment(self._h, 1, bp, xp, sh))
-            self._all_to_all(self.work, out)  # x chunks -> work chunks
-            check(lib().cfp_dist_plan_run_segment(self._h, 2, bp, xp, sh))
+            for i, st in enumerate(self.steps()):
+                if st["kind"] == 1:
+                    self._exchange_piece(st, bufs)
+                else:
+                    check(lib().cfp_dist_plan_run_step(self._h, i, bp, xp, sh))
         return out
 
     def phases(self) -> list:
-        """The apply's steps: axis passes and all-to-all exchanges, in order."""
-        nph = ctypes.c_int()
-        check(lib().cfp_dist_plan_num_phases(self._h, ctypes.byref(nph)))
+        """The apply's steps: axis passes (with the number of grid elements they sweep) and
+        all-to-all pieces (with the bytes each leaves this GPU with), in order."""
         out = []
-        for i in range(nph.value):
-            ex, ax, n, mode = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-            check(lib().cfp_dist_plan_phase_info(self._h, i, ctypes.byref(ex), ctypes.byref(ax), ctypes.byref(n),
-                                                 ctypes.byref(mode)))
-            if ex.value:
-                out.append({"kind": "all-to-all"})
+        nx, ny, nz = self.dims
+        for st in self.steps():
+            if st["kind"] == 1:
+                out.append({"kind": "all-to-all", "elements": st["ex_cnt"] * self.world,
+                            "bytes_out": 16 * st["ex_cnt"] * (self.world - 1)})
+                continue
+            if st["kind"] == 2:  # 3-sweep stage: P1/P3 over `ncols` local planes, P2 over the slab
+                el = self.local_size if st["axis"] == 1 else st["ncols"] * ny * nx
+                ax = {0: "xy", 1: "yz", 2: "xy"}[st["axis"]]
+            elif st["kind"] == 3:
+                el, ax = st["ncols"] * ny * nx, "-"
             else:
-                out.append({"kind": "pass", "axis": "xyz"[ax.value], "n": n.value, "mode": PASS_MODES[mode.value]})
+                el, ax = st["ncols"] * st["n"], "xyz"[st["axis"]]
+            out.append({"kind": "pass", "axis": ax, "n": st["n"], "mode": PASS_MODES.get(st["mode"], "repack"),
+                        "elements": el})
         return out
 
     def profile_begin(self, max_applies: int, every: int = 1) -> bool:
@@ -190,31 +246,23 @@ class SlabPlan:
         return list(ms)
 
     def _time_phases_torch(self, b, x, iters):
-        ph = self.phases()
+        steps = self.steps()
         n = self.local_size
         bp, xp = _dev_ptr(b, n, "b", self.device), _dev_ptr(x, n, "x", self.device)
         sh = _stream_handle()
-        acc = [0.0] * len(ph)
+        bufs = self._buffers(b, x)
+        acc = [0.0] * len(steps)
         for _ in range(iters):
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(ph) + 1)]
-            seg = 0
-            for i, p in enumerate(ph):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(steps) + 1)]
+            for i, st in enumerate(steps):
                 ev[i].record()
-                if p["kind"] == "all-to-all":
-                    if seg == 1:
-                        self._all_to_all(x, self.work)
-                    else:
-                        self._all_to_all(self.work, x)
-                    continue
-                # run this single pass: segments hold consecutive passes, so time per segment
-                # once (the first pass of a segment carries the whole segment)
-                first_of_seg = i == 0 or ph[i - 1]["kind"] == "all-to-all"
-                if first_of_seg:
-                    check(lib().cfp_dist_plan_run_segment(self._h, seg, bp, xp, sh))
-                    seg += 1
+                if st["kind"] == 1:
+                    self._exchange_piece(st, bufs)
+                else:
+                    check(lib().cfp_dist_plan_run_step(self._h, i, bp, xp, sh))
             ev[-1].record()
             torch.cuda.synchronize()
-            for i in range(len(ph)):
+            for i in range(len(steps)):
                 acc[i] += ev[i].elapsed_time(ev[i + 1])
         return [a / iters for a in acc]
 
@@ -254,6 +302,11 @@ class SlabGroup:
     def set_schedule(self, schedule: str | int) -> "SlabGroup":
         """Local passes per slab: 'auto' (3 sweeps at 256^3 with P | 32), 'five' or 'three'."""
         check(lib().cfp_group_set_schedule(self._h, _slab_schedule(schedule)))
+        return self
+
+    def set_pieces(self, pieces: int) -> "SlabGroup":
+        """Exchange pieces (0 = AUTO): the pipelined step list, run here in list order."""
+        check(lib().cfp_group_set_pieces(self._h, int(pieces)))
         return self
 
     def scatter(self, full: torch.Tensor) -> list:

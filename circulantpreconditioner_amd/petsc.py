@@ -66,6 +66,15 @@ class Vec:
         return cls(h, keep=t)
 
     @classmethod
+    def from_tensor_mpi(cls, t: torch.Tensor, N: int, comm: int = PETSC_COMM_WORLD) -> "Vec":
+        """VecCreateMPIHIPWithArray: this rank's rows of a distributed Vec, in t's memory."""
+        if t.dtype != torch.complex128 or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("need a contiguous complex128 device tensor")
+        h = ctypes.c_void_p()
+        PetscCall(lib().VecCreateMPIHIPWithArray(int(comm), 1, t.numel(), int(N), t.data_ptr(), ctypes.byref(h)))
+        return cls(h, keep=t)
+
+    @classmethod
     def seq_hip(cls, n: int) -> "Vec":
         h = ctypes.c_void_p()
         PetscCall(lib().VecCreateSeqHIP(PETSC_COMM_SELF, int(n), ctypes.byref(h)))
@@ -78,15 +87,42 @@ class Vec:
         PetscCall(lib().VecCreateSeq(PETSC_COMM_SELF, int(n), ctypes.byref(h)))
         return cls(h)
 
+    @classmethod
+    def mpi(cls, N: int, comm: int = PETSC_COMM_WORLD, nlocal: int = -1) -> "Vec":
+        """VecCreateMPI(comm, PETSC_DECIDE, N): this rank's block of rows, host memory."""
+        h = ctypes.c_void_p()
+        PetscCall(lib().VecCreateMPI(int(comm), int(nlocal), int(N), ctypes.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def mpi_hip(cls, N: int, comm: int = PETSC_COMM_WORLD, nlocal: int = -1) -> "Vec":
+        """VecCreateMPIHIP(comm, PETSC_DECIDE, N): this rank's block of rows on the device."""
+        h = ctypes.c_void_p()
+        PetscCall(lib().VecCreateMPIHIP(int(comm), int(nlocal), int(N), ctypes.byref(h)))
+        return cls(h)
+
     @property
     def size(self) -> int:
+        """Global size (VecGetSize)."""
         n = ctypes.c_int64()
         PetscCall(lib().VecGetSize(self.h, ctypes.byref(n)))
         return n.value
 
+    @property
+    def local_size(self) -> int:
+        n = ctypes.c_int64()
+        PetscCall(lib().VecGetLocalSize(self.h, ctypes.byref(n)))
+        return n.value
+
+    def ownership_range(self) -> tuple:
+        lo, hi = ctypes.c_int64(), ctypes.c_int64()
+        PetscCall(lib().VecGetOwnershipRange(self.h, ctypes.byref(lo), ctypes.byref(hi)))
+        return lo.value, hi.value
+
     def set_array(self, a) -> "Vec":
+        """Write this rank's rows (local size)."""
         a = np.ascontiguousarray(np.asarray(a, dtype=np.complex128).reshape(-1))
-        if a.size != self.size:
+        if a.size != self.local_size:
             raise ValueError("size mismatch")
         p = ctypes.c_void_p()
         PetscCall(lib().VecGetArray(self.h, ctypes.byref(p)))
@@ -95,7 +131,8 @@ class Vec:
         return self
 
     def array(self) -> np.ndarray:
-        n = self.size
+        """This rank's rows (local size)."""
+        n = self.local_size
         p = ctypes.c_void_p()
         PetscCall(lib().VecGetArrayRead(self.h, ctypes.byref(p)))
         out = np.empty(n, dtype=np.complex128)
@@ -156,6 +193,112 @@ class Vec:
             self.destroy()
         except Exception:
             pass
+
+
+class Comm:
+    """A communicator of several ranks for the stand-in PETSc (an int handle, as MPI_Comm).
+
+    ``Comm.torch(group)``: the collectives are torch.distributed's on `group` (under gloo the
+    library stages the exchange pieces through pinned host memory) -- several processes may
+    then share one GPU.  ``Comm.rccl(group)``: an RCCL communicator inside the library (one
+    process per GPU), its unique id broadcast over `group`.  ``set_world()`` makes it
+    PETSC_COMM_WORLD, the communicator setupFFTPrec3D builds its FFT matrix on
+    (src/PCSHELLFft_3D.cxx:34-35)."""
+
+    _A2A = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
+    _RED = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int64, ctypes.c_int)
+
+    class _Ops(ctypes.Structure):
+        pass
+
+    _Ops._fields_ = [("alltoall", _A2A), ("allreduce", _RED), ("user", ctypes.c_void_p)]
+
+    def __init__(self, handle: int, keep=()):
+        self.handle = int(handle)
+        self._keep = keep
+
+    @classmethod
+    def torch(cls, group=None) -> "Comm":
+        import torch.distributed as dist
+        size, rank = dist.get_world_size(group), dist.get_rank(group)
+
+        def alltoall(_user, send, recv, nbytes):
+            try:
+                n = size * nbytes // 8
+                s = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_double * n).from_address(send)))
+                r = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_double * n).from_address(recv)))
+                dist.all_to_all_single(r, s.clone(), group=group)
+                return 0
+            except Exception:  # reported to the library as a failed collective
+                return 1
+
+        def allreduce(_user, buf, count, op):
+            try:
+                a = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_double * count).from_address(
+                    ctypes.addressof(buf.contents))))
+                t = a.clone()
+                dist.all_reduce(t, op=dist.ReduceOp.MAX if op == 1 else dist.ReduceOp.SUM, group=group)
+                a.copy_(t)
+                return 0
+            except Exception:
+                return 1
+
+        a2a, red = cls._A2A(alltoall), cls._RED(allreduce)
+        ops = cls._Ops(a2a, red, None)
+        h = ctypes.c_int()
+        PetscCall(lib().PetscMiniCommCreate(size, rank, ctypes.byref(ops), ctypes.byref(h)))
+        return cls(h.value, keep=(a2a, red, ops))
+
+    @classmethod
+    def rccl(cls, group=None, device: int | None = None) -> "Comm":
+        import torch.distributed as dist
+        size, rank = dist.get_world_size(group), dist.get_rank(group)
+        nbytes = lib().cfp_dist_unique_id_bytes()
+        uid = ctypes.create_string_buffer(nbytes)
+        if rank == 0:
+            from ._lib import check
+            check(lib().cfp_dist_get_unique_id(uid))
+        t = torch.frombuffer(bytearray(uid.raw), dtype=torch.uint8).clone()
+        if dist.get_backend(group) == "nccl":
+            t = t.to(f"cuda:{torch.cuda.current_device() if device is None else device}")
+        dist.broadcast(t, src=0, group=group)
+        uid = ctypes.create_string_buffer(bytes(t.cpu().numpy().tobytes()), nbytes)
+        h = ctypes.c_int()
+        PetscCall(lib().PetscMiniCommCreateRCCL(size, rank, uid, ctypes.byref(h)))
+        return cls(h.value)
+
+    @property
+    def size(self) -> int:
+        v = ctypes.c_int()
+        lib().MPI_Comm_size(self.handle, ctypes.byref(v))
+        return v.value
+
+    @property
+    def rank(self) -> int:
+        v = ctypes.c_int()
+        lib().MPI_Comm_rank(self.handle, ctypes.byref(v))
+        return v.value
+
+    def set_world(self) -> "Comm":
+        PetscCall(lib().PetscMiniSetCommWorld(self.handle))
+        return self
+
+    def allreduce(self, values, op: int = 0) -> np.ndarray:
+        a = np.ascontiguousarray(np.asarray(values, dtype=np.float64).reshape(-1))
+        PetscCall(lib().PetscMiniAllreduce(self.handle, a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), a.size,
+                                           int(op)))
+        return a
+
+    def destroy(self) -> None:
+        if self.handle >= 2:
+            h = ctypes.c_int(self.handle)
+            PetscCall(lib().PetscMiniCommDestroy(ctypes.byref(h)))
+        self.handle = PETSC_COMM_SELF
+
+
+def set_comm_world(comm: "Comm | int") -> None:
+    """PETSC_COMM_WORLD := comm (PETSC_COMM_SELF: back to one rank)."""
+    PetscCall(lib().PetscMiniSetCommWorld(comm.handle if isinstance(comm, Comm) else int(comm)))
 
 
 class Mat:

@@ -102,6 +102,8 @@ PetscErrorCode build_transport_col(Vec c, PetscInt size);
 PetscErrorCode MatCreateFFTHIP(MPI_Comm comm, PetscInt ndim, const PetscInt dims[], Mat *A);
 /* the plan behind an FFT matrix made by MatCreateFFT/MatCreateFFTHIP (NULL otherwise) */
 PetscErrorCode MatFFTHIPGetPlan(Mat A, cfp_plan_t *plan);
+/* the z-slab plan behind an FFT matrix made on a communicator of several ranks (NULL on one) */
+PetscErrorCode MatFFTHIPGetDistPlan(Mat A, struct cfp_dist_plan_s **plan);
 /* How many solve_3D calls on this FFT matrix divided by the plan's own symbol in registers
  * (Diag untouched since setupFFTPrec3D materialised it: same object id and PetscObjectState,
  * symbol unchanged) and how many streamed the Diag they were given. */

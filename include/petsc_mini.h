@@ -8,7 +8,14 @@
  * <petscksp.h>; pcshell_fft3d.cpp only calls functions that exist there.  Deliberate
  * differences of the stand-in:
  *   - PetscInt is 64-bit (as a PETSc built --with-64-bit-indices);
- *   - MPI_Comm is an int tag (no MPI inside; only PETSC_COMM_SELF/WORLD of size 1);
+ *   - MPI_Comm is an int handle (no MPI library inside).  PETSC_COMM_SELF has one rank;
+ *     PETSC_COMM_WORLD has one rank until PetscMiniSetCommWorld points it at a communicator of
+ *     several ranks made by PetscMiniCommCreate (the caller's collectives: all-to-all and
+ *     all-reduce callbacks, e.g. torch.distributed) or PetscMiniCommCreateRCCL (an RCCL
+ *     communicator, one process per GPU).  Vecs made on such a communicator hold the
+ *     PETSC_DECIDE block of rows of their rank; VecDot / VecNorm / VecMDot reduce over it;
+ *     VecSetValues keeps the entries of the calling rank's rows only (PETSc would stash the
+ *     others for their owners);
  *   - Vec is either host-only (VECSEQ) or device-resident with a host mirror (VECSEQHIP),
  *     with PETSc's offload mask semantics for the Get/Restore pairs;
  *   - Mat supports MATSHELL (user operations), MATSEQAIJ (CSR, device SpMV) and the FFT
@@ -42,6 +49,7 @@ typedef enum { PETSC_FALSE = 0, PETSC_TRUE = 1 } PetscBool;
 typedef int MPI_Comm;
 #define PETSC_COMM_WORLD ((MPI_Comm)0)
 #define PETSC_COMM_SELF ((MPI_Comm)1)
+#define MPI_SUCCESS 0
 #define PETSC_DECIDE (-1)
 #define PETSC_DETERMINE (-1)
 #define PETSC_DEFAULT (-2)
@@ -75,6 +83,8 @@ typedef const char *PCType;
 typedef const char *VecType;
 #define VECSEQ "seq"
 #define VECSEQHIP "seqhip"
+#define VECMPI "mpi"
+#define VECMPIHIP "mpihip"
 #define MATSHELL "shell"
 #define MATSEQAIJ "seqaij"
 #define MATFFTW "fftw"
@@ -102,6 +112,44 @@ const char *PetscErrorLastMessage(void);
     if (!(cond)) return PetscErrorSet((code), __func__, (msg)); \
   } while (0)
 PetscErrorCode PetscTime(PetscLogDouble *t);
+#define PetscCallMPI(expr)                                                   \
+  do {                                                                       \
+    int mpierr__ = (expr);                                                   \
+    if (mpierr__) return PetscErrorSet(PETSC_ERR_LIB, __func__, "MPI error"); \
+  } while (0)
+
+/* ---- communicators (stand-in for the MPI subset the boundary uses) */
+int MPI_Comm_size(MPI_Comm comm, int *size);
+int MPI_Comm_rank(MPI_Comm comm, int *rank);
+/* the caller's collectives for a communicator of `size` ranks (host buffers):
+ *   alltoall: sendbuf holds `size` blocks of bytes_per_rank bytes, block q goes to rank q;
+ *             recvbuf block q is what rank q sent to this rank
+ *   allreduce: in place over `count` doubles, op PETSCMINI_OP_SUM or PETSCMINI_OP_MAX
+ * each returns 0 on success */
+#define PETSCMINI_OP_SUM 0
+#define PETSCMINI_OP_MAX 1
+typedef struct {
+  int (*alltoall)(void *user, const void *sendbuf, void *recvbuf, int64_t bytes_per_rank);
+  int (*allreduce)(void *user, double *buf, int64_t count, int op);
+  void *user;
+} PetscMiniCommOps;
+PetscErrorCode PetscMiniCommCreate(int size, int rank, const PetscMiniCommOps *ops, MPI_Comm *comm);
+/* an RCCL communicator (ncclCommInitRank on the current HIP device; unique_id = the 128 bytes
+ * of cfp_dist_get_unique_id, created on rank 0 and broadcast by the caller) */
+PetscErrorCode PetscMiniCommCreateRCCL(int size, int rank, const char *unique_id, MPI_Comm *comm);
+PetscErrorCode PetscMiniCommDestroy(MPI_Comm *comm);
+/* PETSC_COMM_WORLD resolves to comm from now on (PETSC_COMM_SELF: back to one rank) */
+PetscErrorCode PetscMiniSetCommWorld(MPI_Comm comm);
+/* the communicator PETSC_COMM_WORLD currently stands for (others: themselves) */
+PetscErrorCode PetscMiniCommResolve(MPI_Comm comm, MPI_Comm *resolved);
+PetscErrorCode PetscMiniAllreduce(MPI_Comm comm, double *buf, int64_t count, int op);
+/* the ncclComm_t behind an RCCL communicator (NULL for a callback communicator) */
+PetscErrorCode PetscMiniCommGetNCCL(MPI_Comm comm, void **nccl_comm);
+/* One exchange piece of a slab plan over a communicator (the cfp_dist_exchange_fn contract of
+ * include/circulant_fft_dist.h; user = (void *)(intptr_t)comm): device buffers, staged through
+ * pinned host memory for a callback communicator, grouped ncclSend/ncclRecv for RCCL. */
+int PetscMiniCommExchange(void *user, const double *src_dev, double *dst_dev, int64_t chunk, int64_t off,
+                          int64_t count, void *stream);
 
 /* Object state and id, as PETSc's: the state of a Vec increases on every write access (write
  * Get/RestoreArray, VecSet, VecScale, VecCopy into it, ...); the id is unique per object.
@@ -113,7 +161,13 @@ PetscErrorCode PetscObjectGetId(PetscObject obj, PetscObjectId *id);
 PetscErrorCode VecCreateSeq(MPI_Comm comm, PetscInt n, Vec *v);
 PetscErrorCode VecCreateSeqHIP(MPI_Comm comm, PetscInt n, Vec *v);
 PetscErrorCode VecCreateSeqHIPWithArray(MPI_Comm comm, PetscInt bs, PetscInt n, const PetscScalar *gpuarray, Vec *v);
+/* distributed: nlocal or N may be PETSC_DECIDE (N / size rows, the first N % size ranks one
+ * more); VECMPI lives in host memory, VECMPIHIP on the device */
 PetscErrorCode VecCreateMPI(MPI_Comm comm, PetscInt nlocal, PetscInt N, Vec *v);
+PetscErrorCode VecCreateMPIHIP(MPI_Comm comm, PetscInt nlocal, PetscInt N, Vec *v);
+PetscErrorCode VecCreateMPIHIPWithArray(MPI_Comm comm, PetscInt bs, PetscInt nlocal, PetscInt N,
+                                        const PetscScalar *gpuarray, Vec *v);
+PetscErrorCode VecGetComm(Vec v, MPI_Comm *comm); /* not in PETSc (PetscObjectGetComm) */
 PetscErrorCode VecDuplicate(Vec v, Vec *newv);
 PetscErrorCode VecDestroy(Vec *v);
 PetscErrorCode VecGetType(Vec v, VecType *type);
@@ -171,13 +225,17 @@ PetscErrorCode MatCreateSeqAIJWithArrays(MPI_Comm comm, PetscInt m, PetscInt n, 
                                          PetscScalar *a, Mat *A);
 PetscErrorCode MatGetType(Mat A, MatType *type);
 PetscErrorCode MatGetSize(Mat A, PetscInt *m, PetscInt *n);
+PetscErrorCode MatGetLocalSize(Mat A, PetscInt *m, PetscInt *n);
+PetscErrorCode MatGetComm(Mat A, MPI_Comm *comm); /* not in PETSc (PetscObjectGetComm) */
 PetscErrorCode MatMult(Mat A, Vec x, Vec y);
 PetscErrorCode MatMultTranspose(Mat A, Vec x, Vec y);
 PetscErrorCode MatShift(Mat A, PetscScalar a);
 PetscErrorCode MatDestroy(Mat *A);
 /* the FFT matrix: a MATSHELL around a cfp plan; dims = {n_z, n_y, n_x} for ndim = 3
  * (row-major, x fastest), {n_y, n_x} for 2, {n_x} for 1.  MatCreateFFT accepts only
- * MATFFTW as type and returns the HIP implementation. */
+ * MATFFTW as type and returns the HIP implementation.  On a communicator of several ranks the
+ * matrix is z-slab distributed (FFTW-MPI's local_n0 = PETSC_DECIDE rows) and
+ * MatCreateVecsFFTW gives VECMPIHIP vectors of the local slab. */
 PetscErrorCode MatCreateFFT(MPI_Comm comm, PetscInt ndim, const PetscInt dims[], MatType type, Mat *A);
 PetscErrorCode MatCreateVecsFFTW(Mat A, Vec *x, Vec *y, Vec *z);
 

@@ -40,14 +40,12 @@ def test_group_vs_oracle(dims, P, oracle):
     assert oracle.rel_l2(got, ref) < TOL
 
 
-def test_group_config5_512_in_8_slabs(oracle):
+def test_group_config5_512_in_8_slabs(oracle, case512):
     """BASELINE config 5's decomposition (512^3, z slabs of 64 planes, 8 ranks) on one device,
-    against the oracle's full-grid solve."""
+    against the oracle's full-grid solve (AUTO pieces: 4 per all-to-all at this size)."""
     from circulantpreconditioner_amd.distributed import SlabGroup
-    dims, P, lam = (512, 512, 512), 8, (0.6, 0.15, 0.02)
-    N = int(np.prod(dims))
-    b = oracle.c_fill_uniform(N, 512)
-    ref = oracle.c_solve_3d(oracle.c_build_diag_transport(dims, lam), b, dims)
+    dims, lam, b, ref = case512
+    P = 8
     with SlabGroup(dims, P) as g:
         g.set_transport_symbol(lam)
         bs = g.scatter(torch.from_numpy(b).cuda())
@@ -108,7 +106,64 @@ def _free_port():
     return p
 
 
-def _slab_rank(rank, world, port, dims, lam, seed, q):
+@pytest.fixture(scope="module")
+def case512(oracle):
+    dims, lam = (512, 512, 512), (0.6, 0.15, 0.02)
+    b = oracle.c_fill_uniform(512 ** 3, 512)
+    ref = oracle.c_solve_3d(oracle.c_build_diag_transport(dims, lam), b, dims)
+    return dims, lam, b, ref
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_group_pieces_512(P, case512):
+    """Config 5's grid with the pipelined exchange: the pieced step list (K = 1, 4, 8 pieces per
+    all-to-all) through the group executor, against the oracle (compared on the device)."""
+    from circulantpreconditioner_amd.distributed import SlabGroup
+    dims, lam, b, ref = case512
+    full = torch.from_numpy(b).cuda()
+    rd = torch.from_numpy(ref).cuda()
+    with SlabGroup(dims, P) as g:
+        g.set_transport_symbol(lam)
+        bs = g.scatter(full)
+        del full
+        for K in (1, 4, 8):
+            g.set_pieces(K)
+            xs = g.apply(bs)
+            got = torch.cat(xs)
+            del xs
+            err = float(torch.linalg.vector_norm(got - rd) / torch.linalg.vector_norm(rd))
+            del got
+            assert err < TOL, (P, K, err)
+        del bs
+    del rd
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("P", [2, 4, 8, 16])
+def test_group_pieces_256(P, case256):
+    """256^3 with pieces (K = 1, 4, 8 where K | 256 / P): the 3-sweep slab schedule (P <= 4, and
+    on request at 8 and 16) and the five-pass one, in place at K = 4."""
+    from circulantpreconditioner_amd.distributed import SlabGroup
+    dims, lam, b, ref = case256
+    rd = torch.from_numpy(ref).cuda()
+    with SlabGroup(dims, P) as g:
+        g.set_transport_symbol(lam)
+        bs = g.scatter(torch.from_numpy(b).cuda())
+        for sched in ("three", "five"):
+            g.set_schedule(sched)
+            for K in [k for k in (1, 4, 8) if (256 // P) % k == 0]:
+                g.set_pieces(K)
+                got = torch.cat(g.apply(bs))
+                err = float(torch.linalg.vector_norm(got - rd) / torch.linalg.vector_norm(rd))
+                assert err < TOL, (P, sched, K, err)
+        g.set_schedule("auto").set_pieces(4)
+        g.apply(bs, bs)  # in place, as the direct solver's (Un, Un)
+        got = torch.cat(bs)
+        assert float(torch.linalg.vector_norm(got - rd) / torch.linalg.vector_norm(rd)) < TOL
+        del bs
+
+
+def _slab_rank(rank, world, port, dims, lam, seed, q, pieces=1):
     """One rank of a SlabPlan in its own process (exchange through torch.distributed / gloo)."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -119,7 +174,7 @@ def _slab_rank(rank, world, port, dims, lam, seed, q):
         from circulantpreconditioner_amd.distributed import SlabPlan
         torch.cuda.set_device(0)
         plan = SlabPlan(dims, rank=rank, world=world, device=0, exchange="torch")
-        plan.set_transport_symbol(lam)
+        plan.set_transport_symbol(lam).set_pieces(pieces)
         b = torch.empty(plan.local_size, dtype=torch.complex128, device="cuda:0")
         cp.fill_uniform(b, seed, offset=plan.local_offset)
         x = plan.apply(b)
@@ -132,16 +187,20 @@ def _slab_rank(rank, world, port, dims, lam, seed, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dims,world", [((64, 32, 16), 2), ((128, 128, 128), 2), ((64, 64, 64), 4),
-                                        ((100, 20, 10), 2), ((256, 256, 256), 2)])
-def test_slab_plan_processes_vs_oracle(dims, world, oracle):
-    """`world` fresh processes, one SlabPlan rank each, on cuda:0; gathered x vs the oracle."""
+@pytest.mark.parametrize("dims,world,pieces", [((64, 32, 16), 2, 1), ((128, 128, 128), 2, 1), ((64, 64, 64), 4, 1),
+                                               ((100, 20, 10), 2, 1), ((256, 256, 256), 2, 1),
+                                               ((64, 32, 16), 2, 4), ((128, 128, 128), 2, 4),
+                                               ((256, 256, 256), 2, 4), ((64, 64, 64), 4, 2)])
+def test_slab_plan_processes_vs_oracle(dims, world, pieces, oracle):
+    """`world` fresh processes, one SlabPlan rank each, on cuda:0; gathered x vs the oracle.
+    pieces > 1: the pipelined step list, every piece through torch.distributed."""
     import torch.multiprocessing as mp
     lam, seed = (0.6, 0.15 - 0.1j, 0.02), 29
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_slab_rank, args=(r, world, port, dims, lam, seed, q)) for r in range(world)]
+    procs = [ctx.Process(target=_slab_rank, args=(r, world, port, dims, lam, seed, q, pieces))
+             for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -209,6 +268,67 @@ def test_rccl_single_rank(oracle):
         plan.set_transport_symbol(lam)
         assert [p.get("mode") for p in plan.phases()] == ["rows_fwd", None, "mid_fused", None, "rows_inv"]
         x = plan.apply(torch.from_numpy(b).cuda())
+        assert oracle.rel_l2(x.cpu().numpy(), ref) < TOL
+        # the pipelined apply: 4 pieces per exchange on the plan's exchange stream, ordered by
+        # events against the passes on the caller's stream (world 1: the pieces are self copies)
+        plan.set_pieces(4)
+        assert plan.pieces == 4 and sum(p["kind"] == "all-to-all" for p in plan.phases()) == 8
+        tb = torch.from_numpy(b).cuda()
+        for _ in range(3):
+            x = plan.apply(tb, out=x)
+        assert oracle.rel_l2(x.cpu().numpy(), ref) < TOL
+        plan.apply(tb, out=tb)  # in place
+        assert oracle.rel_l2(tb.cpu().numpy(), ref) < TOL
+        assert plan.profile_begin(4, every=1)
+        for _ in range(2):
+            plan.apply(torch.from_numpy(b).cuda(), out=x)
+        ms, napp = plan.profile_end()
+        assert napp == 2 and len(ms) == len(plan.phases()) and all(m >= 0.0 for m in ms)
+        plan.set_schedule("five")
+        x = plan.apply(torch.from_numpy(b).cuda())
+        assert oracle.rel_l2(x.cpu().numpy(), ref) < TOL
+        plan.close()
+    finally:
+        if created:
+            dist.destroy_process_group()
+
+
+def test_rccl_single_rank_transforms_and_diag(oracle):
+    """World 1 through the RCCL executor: the distributed MatMult / MatMultTranspose step lists
+    (natural slab in and out) against torch.fft, and the explicit-Diag apply (Diag moved into the
+    z-pencil layout once) against the oracle."""
+    import torch.distributed as dist
+    from circulantpreconditioner_amd._lib import check, lib
+    from circulantpreconditioner_amd.distributed import SlabPlan
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29532")
+    created = False
+    if not dist.is_initialized():
+        dist.init_process_group("gloo", rank=0, world_size=1)
+        created = True
+    try:
+        dims = (64, 32, 16)
+        N = int(np.prod(dims))
+        b = oracle.c_fill_uniform(N, 41)
+        tb = torch.from_numpy(b).cuda()
+        plan = SlabPlan(dims, rank=0, world=1, device=0)
+        out = torch.empty_like(tb)
+        check(lib().cfp_dist_plan_forward(plan._h, tb.data_ptr(), out.data_ptr(), None))
+        torch.cuda.synchronize()
+        f = torch.fft.fftn(tb.view(16, 32, 64)).reshape(-1)
+        assert float(torch.linalg.vector_norm(out - f) / torch.linalg.vector_norm(f)) < 1e-13
+        check(lib().cfp_dist_plan_backward(plan._h, tb.data_ptr(), out.data_ptr(), None))
+        torch.cuda.synchronize()
+        g = torch.fft.ifftn(tb.view(16, 32, 64)).reshape(-1) * N
+        assert float(torch.linalg.vector_norm(out - g) / torch.linalg.vector_norm(g)) < 1e-13
+        rng = np.random.default_rng(3)
+        d = 1.5 + rng.random(N) + 1j * rng.standard_normal(N)
+        ref = oracle.c_solve_3d(d, b, dims)
+        plan.set_diag(torch.from_numpy(d).cuda())
+        x = plan.apply(tb)
+        assert oracle.rel_l2(x.cpu().numpy(), ref) < TOL
+        plan.set_pieces(2)
+        x = plan.apply(tb)
         assert oracle.rel_l2(x.cpu().numpy(), ref) < TOL
         plan.close()
     finally:
