@@ -95,6 +95,77 @@ def cpu_model() -> str:
     return "unknown"
 
 
+FFTW_LIBS = ("libfftw3.so.3", "libfftw3.so")
+FFTW_OMP_LIBS = ("libfftw3_omp.so.3", "libfftw3_omp.so")
+
+
+def fftw_leg(grid, b, d, threads: int, budget_s: float):
+    """BASELINE.md §4 / SURVEY §8d(i): the reference's own arithmetic on FFTW when the box has
+    it -- fftw_plan_dft_3d(nz, ny, nx, FFTW_FORWARD / FFTW_BACKWARD, FFTW_ESTIMATE) (what PETSc's
+    MATFFTW uses, src/FftLinearSolver_3D.c:170-184), pointwise divide, 1/N -- on 1 thread and,
+    with libfftw3_omp, on `threads`.  Returns {"fftw": "not found", "probed": [...]} otherwise."""
+    import ctypes
+    import numpy as np
+    lib = None
+    for name in FFTW_LIBS:
+        try:
+            lib = ctypes.CDLL(name)
+            break
+        except OSError:
+            continue
+    if lib is None:
+        return {"fftw": "not found", "probed": list(FFTW_LIBS)}
+    omp = None
+    for name in FFTW_OMP_LIBS:
+        try:
+            omp = ctypes.CDLL(name)
+            break
+        except OSError:
+            continue
+    nx, ny, nz = grid
+    N = nx * ny * nz
+    vp = ctypes.c_void_p
+    lib.fftw_plan_dft_3d.restype = vp
+    lib.fftw_plan_dft_3d.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_uint]
+    lib.fftw_execute.argtypes = [vp]
+    lib.fftw_destroy_plan.argtypes = [vp]
+    FORWARD, BACKWARD, ESTIMATE = -1, 1, 1 << 6
+    x = np.empty(N, dtype=np.complex128)
+    bh = np.empty(N, dtype=np.complex128)
+
+    def legs_for(nthreads):
+        if omp is not None:
+            omp.fftw_init_threads()
+            omp.fftw_plan_with_nthreads(ctypes.c_int(nthreads))
+        fwd = lib.fftw_plan_dft_3d(nz, ny, nx, b.ctypes.data, bh.ctypes.data, FORWARD, ESTIMATE)
+        bwd = lib.fftw_plan_dft_3d(nz, ny, nx, bh.ctypes.data, x.ctypes.data, BACKWARD, ESTIMATE)
+
+        def apply():
+            lib.fftw_execute(fwd)
+            np.divide(bh, d, out=bh)
+            lib.fftw_execute(bwd)
+            np.multiply(x, 1.0 / N, out=x)
+
+        t0 = time.perf_counter()
+        apply()
+        first = time.perf_counter() - t0
+        reps = max(1, min(5, int(budget_s / max(first, 1e-3))))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            apply()
+        dt = (time.perf_counter() - t0) / reps
+        lib.fftw_destroy_plan(fwd)
+        lib.fftw_destroy_plan(bwd)
+        return {"threads": nthreads, "value": round(1.0 / dt, 4), "ms_per_apply": round(dt * 1e3, 1),
+                "sample": f"{reps} timed applies (+1 warm-up) of the full {nx}x{ny}x{nz} grid"}
+
+    legs = [legs_for(1)]
+    if omp is not None and threads > 1:
+        legs.append(legs_for(threads))
+    return {"fftw": "found", "kind": "reference", "legs": legs, "value": legs[-1]["value"], "unit": "PCApply/s",
+            "cores": legs[-1]["threads"], "omp": omp is not None}
+
+
 def cpu_baseline(grid, budget_s: float = 20.0):
     """The oracle's C restatement (test infrastructure; the checker, never the product), timed
     on 1 thread and on all of this process's host cores."""
@@ -124,7 +195,12 @@ def cpu_baseline(grid, budget_s: float = 20.0):
     out = {"value": top["value"], "unit": "PCApply/s", "cores": threads, "kind": "port",
            "sample": f"{top['sample']}, oracle/cfp_oracle.c restatement of solve_3D, OpenMP {threads} threads, "
                      f"{top['ms_per_apply']:.0f} ms/apply",
-           "legs": legs, "cpu_model": cpu_model()}
+           "legs": legs, "cpu_model": cpu_model(),
+           "cores_affinity": len(os.sched_getaffinity(0)), "cores_box": os.cpu_count()}
+    try:
+        out["fftw"] = fftw_leg(n, b, d, threads, budget_s * 0.5)
+    except Exception as e:  # report, never fake
+        out["fftw"] = {"fftw": "error", "error": str(e)}
     # an optimised-library proxy beside the port (FFTW is absent): scipy's
     # pocketfft, multithreaded, on the same grid and symbol -- fftn, divide, ifftn
     try:
@@ -416,15 +492,19 @@ def main() -> int:
         kern = [i for i, p in enumerate(passes_info) if p["kind"] == "pass"]
         k = max(kern, key=lambda i: ms[i])
         dom = passes_info[k]
-        alg = kernel_alg_bytes(dom["mode"], nloc, dom["n"])
+        alg = kernel_alg_bytes(dom["mode"], dom["elements"], dom["n"])
         achieved = alg / (ms[k] * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                 "kernel": f"phase{k}_{dom['axis']}_{dom['mode']} (rank 0 slab)", "alg_bytes_per_launch": alg,
                 "mean_ms": round(ms[k], 5), "timing": timing_src}
-        ex = [ms[i] for i, p in enumerate(passes_info) if p["kind"] == "all-to-all"]
-        sent = 16 * nloc * (world - 1) / world  # bytes leaving this GPU per all-to-all
-        moved = sum(kernel_alg_bytes(p["mode"], nloc, p["n"]) for p in passes_info if p["kind"] == "pass")
+        # exchange pieces (pieces > 1: on the exchange stream, overlapped with the passes), per
+        # direction: summed piece time and bytes leaving this GPU
+        exi = [i for i, p in enumerate(passes_info) if p["kind"] == "all-to-all"]
+        half = len(exi) // 2
+        ex = [sum(ms[i] for i in exi[:half]), sum(ms[i] for i in exi[half:])]
+        sent = sum(passes_info[i]["bytes_out"] for i in exi[:half])  # bytes leaving this GPU per all-to-all
+        moved = sum(kernel_alg_bytes(p["mode"], p["elements"], p["n"]) for p in passes_info if p["kind"] == "pass")
         roof_apply = {"moved_bytes_per_gpu": moved,
                       "frac_moved": round(moved / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                       "B_alg_bytes_per_gpu": 208 * nloc,
@@ -432,7 +512,10 @@ def main() -> int:
                       "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": round(208 * nloc / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                       "alltoall_ms": [round(e, 5) for e in ex],
-                      "alltoall_GBps_out_per_gpu": [round(sent / (e * 1e-3) / 1e9, 1) for e in ex]}
+                      "alltoall_GBps_out_per_gpu": [round(sent / (e * 1e-3) / 1e9, 1) if e > 0 else None for e in ex],
+                      "pieces": plan.pieces,
+                      "note": "alltoall_ms: summed piece times per direction, each piece timed on the "
+                              "stream it runs on (overlapped with the passes when pieces > 1)"}
 
     # row f4: the real-data variant on the same grid (real b, the same real lambda), reported
     # beside the headline; the headline stays the complex apply
@@ -489,8 +572,10 @@ def main() -> int:
             if world == 1:
                 mv = moved_bytes(plan.passes(), nl)
             else:
-                mv = sum(kernel_alg_bytes(p["mode"], nl, p["n"]) for p in plan.phases() if p["kind"] == "pass")
+                mv = sum(kernel_alg_bytes(p["mode"], p["elements"], p["n"]) for p in plan.phases()
+                         if p["kind"] == "pass")
             scaling = {"grid": sg, "value": round(k / el, 4), "unit": "PCApply/s", "n_gpus": world,
+                       "pieces": plan.pieces if world > 1 else 1,
                        "steps": k, "ms_per_step": round(el / k * 1e3, 4), "scaling": "strong",
                        "parallelism": par2,
                        "moved_bytes_per_gpu": mv,
