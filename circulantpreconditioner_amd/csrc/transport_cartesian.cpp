@@ -332,6 +332,9 @@ extern "C" PetscErrorCode TransportEquationFFTDirect(const cfp_transport_config*
   res->all_converged = 1;
   while (it < cfg->ntmax && time <= cfg->tmax && !stationary) {  // :106
     PetscCall(VecCopy(Un, dUn));
+    // the copy above is queued on the Vec stream (PETSc's host VecCopy returns when done): drain
+    // it, so that the clock brackets the solve only, as the reference's PetscTime pair (:110-112)
+    PetscCall(VecMiniSynchronize(dUn));
     const double v = wall();
     PetscCall(PetscFft3DTransportSolver(ctx, Un, Un));  // :111 (synchronous on return)
     const double w = wall();
