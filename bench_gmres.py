@@ -87,7 +87,9 @@ def main(argv=None) -> int:
                         "solve_s": r["solve_seconds"], "ms_per_solve": 1e3 * r["solve_seconds"] / max(1, r["steps"]),
                         "ms_per_iteration": 1e3 * r["solve_seconds"] / its,
                         "pc_calls": r["pc_calls"], "pc_s": r["pc_seconds"],
+                        "pc_ms_per_call": 1e3 * r["pc_seconds"] / max(1, r["pc_calls"]),
                         "pc_share": r["pc_seconds"] / r["solve_seconds"] if r["solve_seconds"] > 0 else None,
+                        "pc_timing": "HIP events around each PCApply on the Vec stream (device time)",
                         "setup_s": r["setup_seconds"], "wall_s": wall,
                     }
                     print(json.dumps(line), flush=True)

@@ -749,11 +749,19 @@ hipError_t launch_three_pass_real(int stage, const double* b, cd* H, cd* Q, doub
 
 
 template <int N1, int TN, int PER_CU>
+#ifndef CFP_TP_P1_INPLACE_FLAGS
+#define CFP_TP_P1_INPLACE_FLAGS 0
+#endif
+#ifndef CFP_TP_P1_FLAGS
+#define CFP_TP_P1_FLAGS F_NT_LD
+#endif
 static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
   constexpr int units = TN * (TN / N1);  // z-planes x y2
   const unsigned g = grid_of(units, PER_CU);
-  if (stage == 0)
-    hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units);
+  if (stage == 0 && in == out)  // EXPERIMENT r03: in place (the direct solver's Un, Un)
+    hipLaunchKernelGGL((k_tp_rows<false, CFP_TP_P1_INPLACE_FLAGS, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units);
+  else if (stage == 0)
+    hipLaunchKernelGGL((k_tp_rows<false, CFP_TP_P1_FLAGS, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units);
   else
     hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units);
 }

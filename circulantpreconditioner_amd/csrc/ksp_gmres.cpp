@@ -14,6 +14,7 @@
 // Written against the PETSc API only; compiled out with -DCFP_WITH_PETSC (real PETSc has
 // its own KSP).
 #ifndef CFP_WITH_PETSC
+#include <hip/hip_runtime.h>
 #include <sys/time.h>
 
 #include <cmath>
@@ -50,6 +51,10 @@ struct _p_KSP {
   PetscReal rnorm = 0.0;
   PetscInt pc_calls = 0;
   double pc_seconds = 0.0;
+  // PCApply's device time: an event pair around every call on the Vec stream (a device-Vec
+  // PCApply is stream-ordered there and returns at once; its time is read at the end of the solve)
+  std::vector<hipEvent_t> pc_ev;
+  size_t pc_ev_used = 0;
   // work space (sized for the current problem)
   PetscInt n = -1, nvec = 0;
   Vec* V = nullptr;  // restart + 1 basis vectors
@@ -61,6 +66,12 @@ static PetscErrorCode kcheck(KSP k, const char* f) {
   return PETSC_SUCCESS;
 }
 #define KCHK(k) PetscCall(kcheck((k), __func__))
+
+static void free_events(KSP k) {
+  for (auto& e : k->pc_ev) hipEventDestroy(e);
+  k->pc_ev.clear();
+  k->pc_ev_used = 0;
+}
 
 static void free_work(KSP k) {
   if (k->V) VecDestroyVecs(k->nvec, &k->V);
@@ -127,6 +138,7 @@ extern "C" PetscErrorCode KSPDestroy(KSP* pk) {
   KSP k = *pk;
   KCHK(k);
   free_work(k);
+  free_events(k);
   PetscErrorCode rc = PCDestroy(&k->pc);
   k->magic = 0;
   delete k;
@@ -152,12 +164,46 @@ extern "C" PetscErrorCode KSPMiniSetUpWork(KSP k, Vec v) {
 }
 
 static PetscErrorCode pc_apply(KSP k, Vec x, Vec y) {
-  // drain the MatMult queued just before, so pc_seconds holds only PCApply's own time
-  PetscCall(VecMiniSynchronize(x));
-  const double t0 = now();
+  void* st = nullptr;
+  PetscCall(VecMiniGetStream(&st));
+  bool events = k->pc_ev_used + 2 <= k->pc_ev.size();
+  if (!events) {
+    events = true;
+    for (int i = 0; i < 64 && events; ++i) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) events = false;
+      else k->pc_ev.push_back(e);
+    }
+  }
+  if (!events) {  // no HIP device (host Vecs on a CPU-only machine): the apply is synchronous
+    hipGetLastError();
+    const double t0 = now();
+    PetscCall(PCApply(k->pc, x, y));
+    k->pc_seconds += now() - t0;
+    k->pc_calls += 1;
+    return PETSC_SUCCESS;
+  }
+  // recorded in stream order: the first one after the MatMult queued before, the second after
+  // the apply (on the same stream, or completed on the host before it returned)
+  hipEventRecord(k->pc_ev[k->pc_ev_used], (hipStream_t)st);
   PetscCall(PCApply(k->pc, x, y));
-  k->pc_seconds += now() - t0;
+  hipEventRecord(k->pc_ev[k->pc_ev_used + 1], (hipStream_t)st);
+  k->pc_ev_used += 2;
   k->pc_calls += 1;
+  return PETSC_SUCCESS;
+}
+
+// add the recorded PCApply times to pc_seconds (waits for the last event)
+static PetscErrorCode pc_collect(KSP k) {
+  if (!k->pc_ev_used) return PETSC_SUCCESS;
+  if (hipEventSynchronize(k->pc_ev[k->pc_ev_used - 1]) != hipSuccess)
+    return PetscErrorSet(PETSC_ERR_LIB, __func__, "hipEventSynchronize");
+  for (size_t i = 0; i + 1 < k->pc_ev_used; i += 2) {
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, k->pc_ev[i], k->pc_ev[i + 1]);
+    k->pc_seconds += 1e-3 * (double)ms;
+  }
+  k->pc_ev_used = 0;
   return PETSC_SUCCESS;
 }
 
@@ -192,6 +238,7 @@ extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
   k->reason = KSP_CONVERGED_ITERATING;
   k->pc_calls = 0;
   k->pc_seconds = 0.0;
+  k->pc_ev_used = 0;
   // KSPSolve(ksp, Un, Un): PETSc copies the right-hand side when b == x
   if (b == x) {
     PetscCall(VecCopy(b, k->rhs));
@@ -201,7 +248,7 @@ extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
     PetscCall(pc_apply(k, b, x));
     k->its = 1;
     k->reason = KSP_CONVERGED_ITS;
-    return PETSC_SUCCESS;
+    return pc_collect(k);
   }
   bool x_zero = !k->guess_nonzero;
   if (x_zero) PetscCall(VecSet(x, 0.0));
@@ -296,6 +343,6 @@ extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
     }
     if (k->reason != KSP_CONVERGED_ITERATING) break;
   }
-  return PETSC_SUCCESS;
+  return pc_collect(k);
 }
 #endif  // CFP_WITH_PETSC

@@ -379,18 +379,42 @@ extern "C" PetscErrorCode build_diag_mat_vec_3D(Vec Diag, Vec cx, Vec cy, Vec cz
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
+// The stream a single-rank apply on device Vecs is ordered on, and whether it must be waited
+// for: the stand-in's Vec stream, stream-ordered like PETSc's VECHIP operations (the next Vec
+// operation, e.g. GMRES's VecMAXPY, queues behind the apply; a host read synchronises), so
+// PCApply costs no host round trip.  Built against a real PETSc: the default stream, waited for.
+void device_stream(void** st, bool* wait) {
+#ifdef CFP_WITH_PETSC
+  *st = nullptr;
+  *wait = true;
+#else
+  VecMiniGetStream(st);
+  *wait = false;
+#endif
+}
+
 // One apply of FFT_MAT's plan, X = (1/N) IDFT(DFT(b) ./ symbol): the register symbol (own) or
 // the explicit Diag (single rank: streamed; slab plan: the z-pencil copy already set).  b may be
 // X (the direct solver's Un, Un).  Host Vecs are staged: single rank through the plan's own
-// persistent buffer (cfp_plan_apply_host), slab plan through the shell's.  Synchronous.
+// persistent buffer (cfp_plan_apply_host), slab plan through the shell's; those applies, and
+// every slab apply (its exchanges are host-driven), return complete.  A single-rank apply on
+// device Vecs is ordered on the Vec stream (device_stream).
 PetscErrorCode shell_apply(FFTShell* s, Vec X, Vec b, bool own, Vec Diag) {
   const PetscInt n = s->nlocal;
   DevIn din;
   if (!own && !s->dplan) PetscCall(din.get(Diag, n));
   if (s->dplan) CFPCALL(cfp_dist_plan_use_diag(s->dplan, own ? 0 : 1));
+  void* vst = nullptr;
+  bool vwait = true;
+  if (!s->dplan) device_stream(&vst, &vwait);
   auto dev_apply = [&](const double* in, double* out) -> int {
     if (s->dplan) return cfp_dist_plan_apply(s->dplan, in, out, nullptr);
-    return own ? cfp_plan_apply(s->plan, in, out, nullptr) : cfp_plan_apply_with_diag(s->plan, din.ptr(), in, out, nullptr);
+    return own ? cfp_plan_apply(s->plan, in, out, vst) : cfp_plan_apply_with_diag(s->plan, din.ptr(), in, out, vst);
+  };
+  // device Vecs: wait only where the caller cannot rely on stream order
+  auto dev_sync = [&]() -> int {
+    if (s->dplan || vwait || din.tmp) return cfp_stream_sync(vst);  // din.tmp: a staged host Diag is freed below
+    return CFP_SUCCESS;
   };
   int rc;
   int stage_err = 0;  // slab path: failed host staging (PETSC_ERR_MEM / PETSC_ERR_LIB)
@@ -410,12 +434,12 @@ PetscErrorCode shell_apply(FFTShell* s, Vec X, Vec b, bool own, Vec Diag) {
       if (!s->stage && hipMalloc(&s->stage, bytes) != hipSuccess) stage_err = PETSC_ERR_MEM;
       if (!stage_err && hipMemcpy(s->stage, p, bytes, hipMemcpyHostToDevice) != hipSuccess) stage_err = PETSC_ERR_LIB;
       if (!stage_err) rc = dev_apply((const double*)s->stage, (double*)s->stage);
-      if (!stage_err && !rc) rc = cfp_stream_sync(nullptr);
+      if (!stage_err && !rc) rc = cfp_stream_sync(vst);
       if (!stage_err && !rc && hipMemcpy(p, s->stage, bytes, hipMemcpyDeviceToHost) != hipSuccess)
         stage_err = PETSC_ERR_LIB;
     } else {
       rc = dev_apply(p, p);
-      if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
+      if (rc == CFP_SUCCESS) rc = dev_sync();
     }
     PetscCall(VecRestoreArrayAndMemType(X, &arr));
   } else {
@@ -424,7 +448,8 @@ PetscErrorCode shell_apply(FFTShell* s, Vec X, Vec b, bool own, Vec Diag) {
     PetscCall(bin.get(b, n));
     PetscCall(xout.get(X, n));
     rc = dev_apply(bin.ptr(), xout.ptr());
-    if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
+    // a staged host side (DevIn/DevOut copies) needs the result now
+    if (rc == CFP_SUCCESS) rc = (bin.tmp || xout.tmp) ? cfp_stream_sync(vst) : dev_sync();
     PetscCall(xout.put());
     PetscCall(bin.put());
   }

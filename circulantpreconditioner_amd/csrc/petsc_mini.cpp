@@ -44,6 +44,11 @@ extern "C" PetscErrorCode VecMiniSetStream(void* s) {
   g_stream = (hipStream_t)s;
   return PETSC_SUCCESS;
 }
+extern "C" PetscErrorCode VecMiniGetStream(void** s) {
+  if (!s) return PetscErrorSet(PETSC_ERR_ARG_NULL, __func__, "NULL output");
+  *s = (void*)g_stream;
+  return PETSC_SUCCESS;
+}
 
 #define ERR(code, msg) PetscErrorSet((code), __func__, (msg))
 

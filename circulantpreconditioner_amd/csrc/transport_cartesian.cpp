@@ -336,7 +336,8 @@ extern "C" PetscErrorCode TransportEquationFFTDirect(const cfp_transport_config*
     // it, so that the clock brackets the solve only, as the reference's PetscTime pair (:110-112)
     PetscCall(VecMiniSynchronize(dUn));
     const double v = wall();
-    PetscCall(PetscFft3DTransportSolver(ctx, Un, Un));  // :111 (synchronous on return)
+    PetscCall(PetscFft3DTransportSolver(ctx, Un, Un));  // :111
+    PetscCall(VecMiniSynchronize(Un));  // a device-Vec solve is stream-ordered: time it to completion
     const double w = wall();
     PetscCall(VecAXPY(dUn, -1.0, Un));
     time += dt;

@@ -212,8 +212,11 @@ PetscErrorCode VecMDot(Vec x, PetscInt nv, const Vec y[], PetscScalar val[]); /*
 PetscErrorCode VecMAXPY(Vec y, PetscInt nv, const PetscScalar alpha[], Vec x[]); /* y += sum alpha_i x_i */
 PetscErrorCode VecDuplicateVecs(Vec v, PetscInt m, Vec *V[]);
 PetscErrorCode VecDestroyVecs(PetscInt m, Vec *V[]);
-/* stream the Vec kernels are enqueued on (hipStream_t, NULL = default); not in PETSc */
+/* stream the Vec kernels are enqueued on (hipStream_t, NULL = default); not in PETSc.  Like
+ * PETSc's VECHIP operations on its default device stream, work on device Vecs is stream-ordered
+ * on it and returns before completion; host reads (VecGetArray...) synchronise. */
 PetscErrorCode VecMiniSetStream(void *stream);
+PetscErrorCode VecMiniGetStream(void **stream);
 /* wait for the work queued on that stream if v is a device vector; not in PETSc */
 PetscErrorCode VecMiniSynchronize(Vec v);
 
@@ -285,7 +288,8 @@ PetscErrorCode KSPGetConvergedReason(KSP ksp, KSPConvergedReason *reason);
 PetscErrorCode KSPGetIterationNumber(KSP ksp, PetscInt *its);
 PetscErrorCode KSPGetResidualNorm(KSP ksp, PetscReal *rnorm);
 PetscErrorCode KSPDestroy(KSP *ksp);
-/* not in PETSc: seconds spent inside PCApply during the last KSPSolve, and its call count */
+/* not in PETSc: the device time of the PCApply calls of the last KSPSolve (HIP events around
+ * each call on the Vec stream; a device-Vec PCApply is stream-ordered there), and their count */
 PetscErrorCode KSPMiniGetPCApplyStats(KSP ksp, PetscInt *calls, PetscLogDouble *seconds);
 /* not in PETSc: allocate the GMRES work vectors now (duplicates of v) instead of in the first
  * KSPSolve, so a timed solve does not include their allocation */
