@@ -282,6 +282,8 @@ def main() -> int:
                     help="z-planes per chunk of the Infinity-Cache-resident x/y schedule (0 = off; default: plan's)")
     ap.add_argument("--graph", action="store_true",
                     help="single GPU: replay each apply as one captured HIP graph (cfp_plan_set_graph)")
+    ap.add_argument("--pieces", type=int, default=0,
+                    help="N > 1: exchange pieces per all-to-all (0 = the plan's AUTO: 4 on slabs of 64 MiB and more)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--settle-ms", type=float, default=300.0,
                     help="untimed applies for this long after the warm-up (clock ramp-up; 0 = off)")
@@ -357,6 +359,8 @@ def main() -> int:
             os.environ.get("CFP_EXCHANGE"), agree, warn=lambda m: log(f"rank {rank}: {m}"))
         exchange_used[0] = exchange
         plan.set_transport_symbol(LAM)
+        if args.pieces:
+            plan.set_pieces(args.pieces)
         b = torch.empty(plan.local_size, dtype=torch.complex128, device=dev)
         x = torch.empty_like(b)
         cp.fill_uniform(b, SEED, offset=plan.local_offset)
