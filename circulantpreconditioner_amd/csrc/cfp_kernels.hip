@@ -112,7 +112,7 @@ CFP_CFG(50, true, 1, 10, 5, 64, ST)
 CFP_CFG(50, true, 2, 10, 5, 64, LD)
 CFP_CFG(100, false, 0, 10, 10, 32, 0)
 CFP_CFG(100, false, 1, 10, 10, 32, ST)
-CFP_CFG(100, false, 2, 10, 10, 16, LD)
+CFP_CFG(100, false, 2, 10, 10, 16, LD)  // r03: T = 8, 32, 64 measured 1-3 % slower (profiles/r03l_t100.txt)
 CFP_CFG(100, true, 0, 10, 10, 32, LD)
 CFP_CFG(100, true, 1, 10, 10, 32, ST)
 CFP_CFG(100, true, 2, 10, 10, 32, LD)

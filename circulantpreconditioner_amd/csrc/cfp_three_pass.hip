@@ -749,19 +749,18 @@ hipError_t launch_three_pass_real(int stage, const double* b, cd* H, cd* Q, doub
 
 
 template <int N1, int TN, int PER_CU>
-#ifndef CFP_TP_P1_INPLACE_FLAGS
-#define CFP_TP_P1_INPLACE_FLAGS 0
-#endif
-#ifndef CFP_TP_P1_FLAGS
-#define CFP_TP_P1_FLAGS F_NT_LD
-#endif
+// P1 load policy (r03, profiles/r03f_p1_inplace_ab.jsonl, r03g_p1_out_of_place_ab.jsonl):
+// out of place, non-temporal loads (plain loads leave P2 at 153-160 us); in place (the direct
+// solver's Un, Un), plain loads -- with NT loads of the lines it then overwrites, P1's output
+// drops out of the Infinity Cache and P2 takes 143-145 us instead of 128.
+constexpr int kP1Flags = F_NT_LD, kP1InPlaceFlags = 0;
 static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
   constexpr int units = TN * (TN / N1);  // z-planes x y2
   const unsigned g = grid_of(units, PER_CU);
-  if (stage == 0 && in == out)  // EXPERIMENT r03: in place (the direct solver's Un, Un)
-    hipLaunchKernelGGL((k_tp_rows<false, CFP_TP_P1_INPLACE_FLAGS, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units);
+  if (stage == 0 && in == out)  // in place (the direct solver's Un, Un)
+    hipLaunchKernelGGL((k_tp_rows<false, kP1InPlaceFlags, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units);
   else if (stage == 0)
-    hipLaunchKernelGGL((k_tp_rows<false, CFP_TP_P1_FLAGS, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units);
+    hipLaunchKernelGGL((k_tp_rows<false, kP1Flags, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units);
   else
     hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units);
 }
