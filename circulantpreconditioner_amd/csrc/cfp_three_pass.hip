@@ -748,12 +748,13 @@ hipError_t launch_three_pass_real(int stage, const double* b, cd* H, cd* Q, doub
 }
 
 
-template <int N1, int TN, int PER_CU>
 // P1 load policy (r03, profiles/r03f_p1_inplace_ab.jsonl, r03g_p1_out_of_place_ab.jsonl):
 // out of place, non-temporal loads (plain loads leave P2 at 153-160 us); in place (the direct
 // solver's Un, Un), plain loads -- with NT loads of the lines it then overwrites, P1's output
 // drops out of the Infinity Cache and P2 takes 143-145 us instead of 128.
 constexpr int kP1Flags = F_NT_LD, kP1InPlaceFlags = 0;
+
+template <int N1, int TN, int PER_CU>
 static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
   constexpr int units = TN * (TN / N1);  // z-planes x y2
   const unsigned g = grid_of(units, PER_CU);
