@@ -342,7 +342,7 @@ def main() -> int:
             plan.set_schedule(args.schedule)
             if args.tp_shape:
                 n1, mid = args.tp_shape.split(",")
-                plan.set_three_pass_shape(int(n1), mid)
+                plan.set_three_pass_shape(int(n1), int(mid) if mid.isdigit() else mid)
             if args.graph:
                 plan.set_graph(True)
             return plan, b, x, (lambda: plan.apply(b, out=x)), "single GPU"

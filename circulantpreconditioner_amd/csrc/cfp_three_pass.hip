@@ -71,25 +71,31 @@ __device__ __forceinline__ int brev(int j) {
   return N2 == 4 ? ((j & 1) << 1) | (j >> 1) : ((j & 1) << 2) | (j & 2) | (j >> 2);
 }
 
+// first radix of an n-point FFT done as r0 x PTS x ... x PTS (n = r0 PTS^k, r0 <= PTS)
+constexpr int r0_of(int n, int pts) { return n > pts ? r0_of(n / pts, pts) : n; }
+
 }  // namespace
 
 // Persistent: a workgroup walks units blockIdx.x, + gridDim.x, ...  Prefetching the next unit
 // into VGPRs across LDS-only barriers was tried and lost: at 1024 threads the extra registers
-// spill (profiles/r01_schedule_sweep.txt).
-template <bool INV, int FLAGS, int N1, int TN>
-__global__ void __launch_bounds__(N1 * (TN / 16)) __attribute__((amdgpu_waves_per_eu(4)))
+// spill (profiles/r01_schedule_sweep.txt); at 128^3 with 8 points per thread it fits (104
+// VGPRs) and still lost, P1 20.7 -> 23.3 us with one workgroup per CU walking two units
+// (profiles/r03m_128_three_sweep.md).  PTS points per thread (16 or 8); XS = the LDS exchanges
+// split into real and imaginary halves (half the footprint, twice the barriers).
+template <bool INV, int FLAGS, int N1, int TN, int PTS = 16, bool XS = true>
+__global__ void __launch_bounds__(N1 * (TN / PTS)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
-  constexpr int N2 = TN / N1, TR = TN / 16, NT = N1 * TR, TY = N1 / 16;
+  constexpr int N2 = TN / N1, TR = TN / PTS, NT = N1 * TR, TY = N1 / PTS;
   constexpr int RS = TN + TN / 16;  // padded row stride of the row-mode LDS layout
-  constexpr int F = FLAGS | F_SPLIT_LDS | F_LDS_SYNC;
-  __shared__ __attribute__((aligned(16))) double lds[N1 * RS];  // both layouts fit
+  constexpr int F = FLAGS | (XS ? F_SPLIT_LDS : 0) | F_LDS_SYNC;
+  __shared__ __attribute__((aligned(16))) double lds[N1 * RS * (XS ? 1 : 2)];  // both layouts fit
   __shared__ cd tw_l[N1];  // W_N1 for phase A; phase C reads W_256 from global memory (L2 hits),
                            // which keeps it out of scratch (20 B/lane with the table in LDS)
   const int tid = threadIdx.x;
   for (int i = tid; i < N1; i += NT) tw_l[i] = a.tw[N2 * i];
   const int x0 = tid % TN, ty0 = tid / TN;  // phase A: column x, thread ty of TY
   const int r0 = tid / TR, tx0 = tid % TR;  // phase C: row r, thread tx of TR
-  // fresh (laundered) index copies at every use, as in k_tp_mid: nothing but the 16 points
+  // fresh (laundered) index copies at every use, as in k_tp_mid: nothing but the points
   // stays live across an FFT
   const auto idx = [](int i) {
     asm volatile("" : "+v"(i));
@@ -101,59 +107,78 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
   const auto crow = [&](int z, int y) -> i64 {
     return (i64)(y >> lnyl) * a.chunk + ((i64)z << lnyl) * TN + (i64)(y & (nyl - 1)) * TN;
   };
-  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
-    // unit u = (z, y2): rows y2 + N2 y1 of (local) plane z
-    cd v[16];
-    {
-      const int x = idx(x0), ty = idx(ty0);
-      if (INV) {  // chunked rows y2 + N2 ty + N2 TY m: per-thread part + uniform part (nyl >= N2 TY)
-        const cd* const src = in + crow(u / N2, u % N2 + N2 * ty) + x;
+  // unit u = (z, y2): rows y2 + N2 y1 of (local) plane z; thread (column x, ty) loads rows
+  // y2 + N2 (ty + TY m)
+  const auto load = [&](int u, cd* v) {
+    const int x = idx(x0), ty = idx(ty0);
+    if (INV) {  // chunked rows: per-thread part + uniform part (nyl >= N2 TY)
+      const cd* const src = in + crow(u / N2, u % N2 + N2 * ty) + x;
 #pragma unroll
-        for (int m = 0; m < 16; ++m) v[m] = gload<FLAGS>(src + crow(0, N2 * TY * m));
-        // all 16 loads go out before the first butterfly: with runtime strides the scheduler
-        // otherwise starts the DFT after 9 of them and issues the rest a memory latency later
-        // (P3 100 -> 93 us at 256^3)
-        __builtin_amdgcn_sched_barrier(0);
+      for (int m = 0; m < PTS; ++m) v[m] = gload<FLAGS>(src + crow(0, N2 * TY * m));
+    } else {
+      const cd* const src = in + (i64)(u / N2) * TN * TN + x + (i64)TN * (u % N2 + N2 * ty);  // + uniform
 #pragma unroll
-        for (int m = 0; m < 16; ++m) v[m] = cconj(v[m]);
-      } else {
-        const cd* const src = in + (i64)(u / N2) * TN * TN + x + (i64)TN * (u % N2 + N2 * ty);  // + uniform
-#pragma unroll
-        for (int m = 0; m < 16; ++m) v[m] = gload<FLAGS>(src + (i64)TN * N2 * TY * m);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      // phase A: N1-point DFT over y1 for every x (column mode, 256 columns x TY threads)
-      fft_stages<N1, 16, N1 / 16, false, TN, F>(v, lds, tw_l, x, ty, true);  // v[m]: k1 = ty + TY m
+      for (int m = 0; m < PTS; ++m) v[m] = gload<FLAGS>(src + (i64)TN * N2 * TY * m);
     }
-    // phase B: transpose to rows k1, thread (row r, tx) gets x = tx + 16 m
+    // all loads go out before the first butterfly: with runtime strides the scheduler
+    // otherwise starts the DFT after 9 of them and issues the rest a memory latency later
+    // (P3 100 -> 93 us at 256^3)
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+    cd v[PTS];
+    load(u, v);
+    if (INV) {
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
+    }
+    {
+      // phase A: N1-point DFT over y1 for every x (column mode, TN columns x TY threads)
+      const int x = idx(x0), ty = idx(ty0);
+      fft_stages<N1, PTS, r0_of(N1, PTS), false, TN, F>(v, lds, tw_l, x, ty, true);  // v[m]: k1 = ty + TY m
+    }
+    // phase B: transpose to rows k1, thread (row r, tx) gets x = tx + TR m
     lds_barrier();  // phase A's last LDS reads are done
     {
       const int x = idx(x0), ty = idx(ty0), r = idx(r0), tx = idx(tx0);
+      if constexpr (XS) {
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
+        for (int half = 0; half < 2; ++half) {
 #pragma unroll
-        for (int m = 0; m < 16; ++m) lds[(ty + TY * m) * RS + x + (x >> 4)] = half ? v[m].y : v[m].x;
+          for (int m = 0; m < PTS; ++m) lds[(ty + TY * m) * RS + x + (x >> 4)] = half ? v[m].y : v[m].x;
+          lds_barrier();
+#pragma unroll
+          for (int m = 0; m < PTS; ++m) {
+            const int xx = tx + TR * m;
+            const double val = lds[r * RS + xx + (xx >> 4)];
+            if (half) v[m].y = val; else v[m].x = val;
+          }
+          lds_barrier();
+        }
+      } else {
+        cd* const lc = reinterpret_cast<cd*>(lds);
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) lc[(ty + TY * m) * RS + x + (x >> 4)] = v[m];
         lds_barrier();
 #pragma unroll
-        for (int m = 0; m < 16; ++m) {
+        for (int m = 0; m < PTS; ++m) {
           const int xx = tx + TR * m;
-          const double val = lds[r * RS + xx + (xx >> 4)];
-          if (half) v[m].y = val; else v[m].x = val;
+          v[m] = lc[r * RS + xx + (xx >> 4)];
         }
         lds_barrier();
       }
     }
     {
-      // phase C: 256-point DFT along row r (row mode, N1 rows x 16 threads)
+      // phase C: TN-point DFT along row r (row mode, N1 rows x TR threads)
       const int r = idx(r0), tx = idx(tx0);
-      fft_stages<TN, 16, TN / 16, true, N1, F | F_TW_GLOBAL>(v, lds, a.tw, r, tx, true);  // v[m]: kx = tx + TR m
+      fft_stages<TN, PTS, r0_of(TN, PTS), true, N1, F | F_TW_GLOBAL>(v, lds, a.tw, r, tx, true);  // v[m]: kx = tx + TR m
     }
     {
       const int r = idx(r0), tx = idx(tx0);
       const double sc = a.scale, sy = INV ? -sc : sc;
       cd* dst = out + (INV ? (i64)(u / N2) * TN * TN + (i64)TN * (u % N2 + N2 * r) : crow(u / N2, u % N2 + N2 * r)) + tx;
 #pragma unroll
-      for (int m = 0; m < 16; ++m) gstore<FLAGS>(dst + TR * m, make_cd(v[m].x * sc, v[m].y * sy));
+      for (int m = 0; m < PTS; ++m) gstore<FLAGS>(dst + TR * m, make_cd(v[m].x * sc, v[m].y * sy));
     }
     lds_barrier();  // the next unit's first exchange overwrites LDS
   }
@@ -161,13 +186,13 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
 
 // Persistent over units u = (x-tile, k1); T columns per unit = T/N2 x values times N2 y2.
 // Barriers wait for LDS only, so one unit's stores drain while the next unit loads.
-template <int FLAGS, int T, int N2, int TN>
-__global__ void __launch_bounds__(T * (TN / 16)) __attribute__((amdgpu_waves_per_eu(4)))
+template <int FLAGS, int T, int N2, int TN, int PTS = 16, bool XS = true>
+__global__ void __launch_bounds__(T * (TN / PTS)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid(cd* data, TPArgs a, int nunits) {
-  constexpr int N1 = TN / N2, TZ = TN / 16, NT = T * TZ, XT = T / N2, NXT = TN / XT;
-  constexpr int F = FLAGS | F_SPLIT_LDS | F_LDS_SYNC;
+  constexpr int N1 = TN / N2, TZ = TN / PTS, NT = T * TZ, XT = T / N2, NXT = TN / XT;
+  constexpr int F = FLAGS | (XS ? F_SPLIT_LDS : 0) | F_LDS_SYNC;
   static_assert(N2 == 4 || N2 == 8, "the y2 DFT runs across 4 or 8 lanes");
-  __shared__ __attribute__((aligned(16))) double lds[T * TN];  // split exchange
+  __shared__ __attribute__((aligned(16))) double lds[T * TN * (XS ? 1 : 2)];
   __shared__ cd tw_l[TN];
   const int tid = threadIdx.x;
   for (int i = tid; i < TN; i += NT) tw_l[i] = a.tw[i];
@@ -177,7 +202,7 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
   // it is used: 128 VGPRs hold the points plus one radix-16 stage's twiddles, and an address,
   // twiddle or index kept live across the FFTs (or hoisted out of the unit loop) spills.
   struct Col {
-    cd* col;  // this thread's first point; slot m adds the uniform zs * 16 m
+    cd* col;  // this thread's first point; slot m adds the uniform zs * TZ m
     int y2, xk;
     cd w, w8;  // W_256^{y2 k1}; W_8^(y2 & 3) (N2 = 8)
   };
@@ -194,15 +219,15 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
     return q;
   };
   for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
-    cd v[16];
+    cd v[PTS];
     {
       const Col q = column(u);
 #pragma unroll
-      for (int m = 0; m < 16; ++m) {
+      for (int m = 0; m < PTS; ++m) {
         v[m] = gload<FLAGS>(q.col + zs * TZ * m);
       }
 #pragma unroll
-      for (int m = 0; m < 16; ++m) {  // the lane DFT in two sweeps over the slots: fewer live temporaries
+      for (int m = 0; m < PTS; ++m) {  // the lane DFT in two sweeps over the slots: fewer live temporaries
         v[m] = cmul(v[m], q.w);
         if constexpr (N2 == 8) {  // dft8_dif's first stage
           const cd p = lane_xor4(v[m]);
@@ -210,12 +235,12 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
         }
       }
 #pragma unroll
-      for (int m = 0; m < 16; ++m) v[m] = dft4_dif(v[m], q.y2 & 3);  // the lane now holds k2
+      for (int m = 0; m < PTS; ++m) v[m] = dft4_dif(v[m], q.y2 & 3);  // the lane now holds k2
     }
     {
       int c = c0, tz = tz0;
       asm volatile("" : "+v"(c), "+v"(tz));
-      fft_stages<TN, 16, TN / 16, false, T, F>(v, lds, tw_l, c, tz, true);  // kz = tz + 16 m
+      fft_stages<TN, PTS, r0_of(TN, PTS), false, T, F>(v, lds, tw_l, c, tz, true);  // kz = tz + TZ m
     }
     {
       int c = c0, tz = tz0;
@@ -223,18 +248,18 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
       const int k1 = u / NXT, y2 = c & (N2 - 1);
       const cd cs = a.colsym[(u % NXT) * XT + c / N2 + (i64)TN * (k1 + N1 * brev<N2>(y2))];
 #pragma unroll
-      for (int m = 0; m < 16; ++m) {
+      for (int m = 0; m < PTS; ++m) {
         const cd d = cadd(cadd(cs, a.axsym[tz + TZ * m]), make_cd(1.0, 0.0));
         v[m] = cconj(cdiv_sym(v[m], d));
       }
-      fft_stages<TN, 16, TN / 16, false, T, F>(v, lds, tw_l, c, tz, false);
+      fft_stages<TN, PTS, r0_of(TN, PTS), false, T, F>(v, lds, tw_l, c, tz, false);
     }
     {
       const Col q = column(u);
 #pragma unroll
-      for (int m = 0; m < 16; ++m) v[m] = dft4_dit(v[m], q.y2 & 3);
+      for (int m = 0; m < PTS; ++m) v[m] = dft4_dit(v[m], q.y2 & 3);
 #pragma unroll
-      for (int m = 0; m < 16; ++m) {
+      for (int m = 0; m < PTS; ++m) {
         if constexpr (N2 == 8) {  // dft8_dit's last stage
           const cd u = (q.y2 & 4) ? cmul(v[m], q.w8) : v[m];
           const cd p = lane_xor4(u);
@@ -243,7 +268,7 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
         v[m] = cmul(v[m], q.w);
       }
 #pragma unroll
-      for (int m = 0; m < 16; ++m) gstore<FLAGS>(q.col + zs * TZ * m, cconj(v[m]));
+      for (int m = 0; m < PTS; ++m) gstore<FLAGS>(q.col + zs * TZ * m, cconj(v[m]));
     }
     lds_barrier();  // the next unit's first exchange overwrites LDS
   }
@@ -754,23 +779,24 @@ hipError_t launch_three_pass_real(int stage, const double* b, cd* H, cd* Q, doub
 // drops out of the Infinity Cache and P2 takes 143-145 us instead of 128.
 constexpr int kP1Flags = F_NT_LD, kP1InPlaceFlags = 0;
 
-template <int N1, int TN, int PER_CU>
+template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true>
 static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
   constexpr int units = TN * (TN / N1);  // z-planes x y2
   const unsigned g = grid_of(units, PER_CU);
+  const dim3 blk(N1 * (TN / PTS));
   if (stage == 0 && in == out)  // in place (the direct solver's Un, Un)
-    hipLaunchKernelGGL((k_tp_rows<false, kP1InPlaceFlags, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units);
+    hipLaunchKernelGGL((k_tp_rows<false, kP1InPlaceFlags, N1, TN, PTS, XS>), dim3(g), blk, 0, s, in, out, a, units);
   else if (stage == 0)
-    hipLaunchKernelGGL((k_tp_rows<false, kP1Flags, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units);
+    hipLaunchKernelGGL((k_tp_rows<false, kP1Flags, N1, TN, PTS, XS>), dim3(g), blk, 0, s, in, out, a, units);
   else
-    hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST, N1, TN>), dim3(g), dim3(N1 * (TN / 16)), 0, s, in, out, a, units);
+    hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST, N1, TN, PTS, XS>), dim3(g), blk, 0, s, in, out, a, units);
 }
 
-template <int T, int N2, int TN, int PER_CU>
+template <int T, int N2, int TN, int PER_CU, int PTS = 16, bool XS = true>
 static void launch_mid(cd* data, const TPArgs& a, hipStream_t s) {
   constexpr int units = (TN / (T / N2)) * (TN / N2);  // x-tiles x k1
-  hipLaunchKernelGGL((k_tp_mid<0, T, N2, TN>), dim3(grid_of(units, PER_CU)), dim3(T * (TN / 16)), 0, s, data, a,
-                     units);
+  hipLaunchKernelGGL((k_tp_mid<0, T, N2, TN, PTS, XS>), dim3(grid_of(units, PER_CU)), dim3(T * (TN / PTS)), 0, s, data,
+                     a, units);
 }
 
 template <int N2, int TN, bool PF = false>
@@ -811,10 +837,19 @@ bool three_pass_shape_valid(int n1, int mid) {
 hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, TPShape shape,
                              hipStream_t s) {
   if (n == 128) {
-    // 128^3: N1 = 32 x N2 = 4; P1/P3 256 threads and 35 KiB of LDS (4 per CU), P2 64 columns =
-    // 16 x 4 y2 (256-byte runs), 512 threads and 66 KiB (2 per CU)
-    if (stage == 1) launch_mid<64, 4, 128, 2>(out, a, s);
-    else launch_rows<32, 128, 4>(stage, in, out, a, s);
+    // 128^3 (N1 = 32 x N2 = 4; AUTO since r03m), 8 points per thread and whole-complex LDS
+    // exchanges (one barrier pair per exchange instead of two): P1/P3 512 threads, 69 KiB (2 per
+    // CU); P2 32 columns = 8 x times 4 y2 (128-byte runs), 512 threads, 64 KiB (2 per CU).
+    // shape.mid = lane64 keeps the round-2 kernels (16 points per thread, split exchanges, P2
+    // 64 columns) for A/B: 15.9k against 18.4k applies/s, the 5-pass schedule 17.3k
+    // (profiles/r03m_128_three_sweep.md).
+    if (shape.mid == TP_MID_LANE64) {
+      if (stage == 1) launch_mid<64, 4, 128, 2>(out, a, s);
+      else launch_rows<32, 128, 4>(stage, in, out, a, s);
+    } else {
+      if (stage == 1) launch_mid<32, 4, 128, 2, 8, false>(out, a, s);
+      else launch_rows<32, 128, 2, 8, false>(stage, in, out, a, s);
+    }
     return hipGetLastError();
   }
   // 256^3.  Default shape = the measured best: N1 = 32, P2 tiles of 64 columns (8 x times 8 y2,

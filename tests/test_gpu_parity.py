@@ -427,15 +427,17 @@ def test_three_pass_schedule_rules(cp):
         assert len(plan.passes()) == 5
 
 
+@pytest.mark.parametrize("mid", ["default", "lane64"])
 @pytest.mark.parametrize("lam", [(0.6, 0.15, 0.02), (0.3 + 0.2j, 1.1, 0.7 - 0.4j)], ids=["bench", "complex"])
-def test_three_pass_128_vs_oracle(cp, oracle, lam):
-    """The 3-sweep schedule at 128^3 (N1 = 32 x N2 = 4): against the oracle, in place, and
-    against the 5-pass schedule."""
+def test_three_pass_128_vs_oracle(cp, oracle, lam, mid):
+    """The 3-sweep schedule at 128^3 (N1 = 32 x N2 = 4; AUTO there): the default kernels (8
+    points per thread, whole-complex exchanges) and the round-2 ones (lane64): against the
+    oracle, in place, and against the 5-pass schedule."""
     n = (128, 128, 128)
     b = oracle.c_fill_uniform(128 ** 3, 31)
     ref = oracle.c_solve_3d(oracle.c_build_diag_transport(n, lam), b, n)
     with cp.CirculantPlan(n) as plan:
-        plan.set_transport_symbol(lam).set_schedule("three")
+        plan.set_transport_symbol(lam).set_schedule("three").set_three_pass_shape(0, mid)
         assert [p["mode"] for p in plan.passes()] == ["rows_fwd", "mid_fused", "rows_inv"]
         x = plan.apply(_dev(b))
         assert _rel(x, ref) < TOL
@@ -486,7 +488,10 @@ def test_plane_schedule_rules(cp):
     with cp.CirculantPlan((64, 64, 64)) as plan:  # AUTO: planes for 64^2 too
         plan.set_transport_symbol((0.5, 0.5, 0.5))
         assert len(plan.passes()) == 3
-    with cp.CirculantPlan((128, 128, 128)) as plan:  # ... but not for 128^2 (slower there)
+    with cp.CirculantPlan((128, 128, 128)) as plan:  # ... but not for 128^3: 3 sweeps there (r03m)
+        plan.set_transport_symbol((0.5, 0.5, 0.5))
+        assert [p["mode"] for p in plan.passes()] == ["rows_fwd", "mid_fused", "rows_inv"]
+    with cp.CirculantPlan((128, 128, 64)) as plan:  # 128^2 planes, another n_z: 5 passes
         plan.set_transport_symbol((0.5, 0.5, 0.5))
         assert len(plan.passes()) == 5
 
