@@ -253,6 +253,7 @@ def declare(L) -> None:
         "cfp_wave_plan_destroy": ([vp], c_int),
         "cfp_wave_plan_set_symbol": ([vp, P(ctypes.c_double), ctypes.c_double], c_int),
         "cfp_wave_plan_apply": ([vp, dp, dp, vp], c_int),
+        "cfp_wave_plan_set_schedule": ([vp, c_int], c_int),
         "cfp_wave_plan_forward": ([vp, dp, dp, vp], c_int),
         "cfp_wave_plan_backward": ([vp, dp, dp, vp], c_int),
         "cfp_wave_plan_num_passes": ([vp, P(c_int)], c_int),

@@ -41,4 +41,15 @@ hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs
 hipError_t launch_three_pass_real(int stage, const double* b, cd* H, cd* Q, double* x, const TPArgs& a,
                                   hipStream_t s);
 
+// wave-system plan (cfp_wave_three.hip): the 3-sweep apply of the interleaved 4-component field
+// (idx = 4 cell + comp) on a 128^3 grid, y split 16 x 8.  stage 0 P1w (in -> out), 1 P2w (out in
+// place), 2 P3w (in -> out, x a.scale).  a.tw = W_128; a.wave: the (p, q) tables and c0^2.
+struct WTPArgs {
+  const cd* tw;
+  WaveSym wave;
+  double scale;
+};
+bool wave_three_pass_supported(const i64 n[3], int ncomp);
+hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArgs& a, hipStream_t s);
+
 }  // namespace cfp

@@ -21,27 +21,12 @@
 // 1024-thread workgroup per CU; T = 32: two of 512); its global runs are T/N2 x 16 bytes.
 //
 #include "cfp_fft_device.h"
+#include "cfp_lane.h"
 #include "cfp_three_pass.h"
 
 namespace cfp {
 
 namespace {
-
-// DPP controls: quad_perm lane ^ 1, ^ 2, ^ 3; row_half_mirror (lane ^ 7 within 8 lanes)
-constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_XOR3 = 0x1B, DPP_HALF_MIRROR = 0x141;
-
-template <int M>
-__device__ __forceinline__ double dpp_d(double v) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffll), M, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), M, 0xf, 0xf, false);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-template <int M>
-__device__ __forceinline__ cd dpp_c(cd v) { return make_cd(dpp_d<M>(v.x), dpp_d<M>(v.y)); }
-// lane ^ 4: mirror within 8 lanes (7 - j), then reverse within the quad (^ 3)
-__device__ __forceinline__ cd lane_xor4(cd v) { return dpp_c<DPP_XOR3>(dpp_c<DPP_HALF_MIRROR>(v)); }
-__device__ __forceinline__ cd mul_mi(cd v) { return make_cd(v.y, -v.x); }  // x W_4 = x (-i)
 
 // Radix-2 butterflies across lanes.  The DIF forms take points in natural lane order and
 // leave the frequencies bit-reversed; the DIT forms are the forward transform from that order

@@ -25,6 +25,7 @@
 #include "../../include/wave_system.h"
 #include "cfp_host.h"
 #include "cfp_internal.h"
+#include "cfp_three_pass.h"
 
 using namespace cfp;
 
@@ -46,6 +47,7 @@ struct cfp_wave_plan_s {
   double c0 = 0.0;
   std::vector<int> axes;
   int fused = 0;
+  int schedule = CFP_SCHEDULE_AUTO;  // AUTO: 3 sweeps where cfp_wave_three.hip serves the grid
 };
 
 namespace {
@@ -116,10 +118,19 @@ int launch(cfp_wave_plan_s* p, const PassDesc& d, const cd* in, cd* out, hipStre
 struct WStep {
   int axis, mode;
   bool from_b, scale;
+  int tp = -1;  // >= 0: stage of the 3-sweep apply (cfp_wave_three.hip)
 };
+
+bool use_three(const cfp_wave_plan_s* p) {
+  return p->schedule != CFP_SCHEDULE_FIVE_PASS && p->dim == 3 && wave_three_pass_supported(p->n, p->ncomp);
+}
 
 std::vector<WStep> wave_steps(const cfp_wave_plan_s* p) {
   std::vector<WStep> st;
+  if (use_three(p)) {
+    for (int k = 0; k < 3; ++k) st.push_back({k == 1 ? 2 : 0, PASS_FUSED_WAVE, k == 0, k == 2, k});
+    return st;
+  }
   const std::vector<int>& A = p->axes;
   if (A.empty()) {
     st.push_back({0, PASS_FUSED_WAVE, true, true});
@@ -138,6 +149,16 @@ int run_wave(cfp_wave_plan_s* p, const cd* b, cd* x, hipStream_t s, std::vector<
   for (size_t i = 0; i < st.size(); ++i) {
     const WStep& q = st[i];
     if (ev) HIPCHK(hipEventRecord((*ev)[i], s));
+    if (q.tp >= 0) {
+      WTPArgs a;
+      a.tw = p->tw[128];
+      a.wave = wave_pass(p, 2, PASS_FUSED_WAVE, 1.0).wave;
+      a.wave.fused = 2;
+      a.scale = q.scale ? invN : 1.0;
+      hipError_t e = launch_wave_three_pass(q.tp, q.from_b ? b : x, x, a, s);
+      if (e != hipSuccess) return hip_error(e, "wave 3-sweep launch");
+      continue;
+    }
     int rc = launch(p, wave_pass(p, q.axis, q.mode, q.scale ? invN : 1.0), q.from_b ? b : x, x, s);
     if (rc) return rc;
   }
@@ -246,6 +267,17 @@ extern "C" int cfp_wave_plan_backward(cfp_wave_plan_t p, const double* in, doubl
   if (!p || !in || !out) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
   Guard g(p->device);
   return run_transform(p, true, (const cd*)in, (cd*)out, (hipStream_t)stream);
+}
+
+extern "C" int cfp_wave_plan_set_schedule(cfp_wave_plan_t p, int schedule) {
+  if (!p) return set_error(CFP_ERR_ARG_NULL, "plan is NULL");
+  if (schedule != CFP_SCHEDULE_AUTO && schedule != CFP_SCHEDULE_FIVE_PASS && schedule != CFP_SCHEDULE_THREE_PASS)
+    return set_error(CFP_ERR_ARG_OUTOFRANGE, "wave plan schedule must be AUTO, FIVE_PASS or THREE_PASS (got %d)",
+                     schedule);
+  if (schedule == CFP_SCHEDULE_THREE_PASS && !(p->dim == 3 && wave_three_pass_supported(p->n, p->ncomp)))
+    return set_error(CFP_ERR_SUP, "the wave 3-sweep schedule needs a 3-D 128^3 grid");
+  p->schedule = schedule;
+  return CFP_SUCCESS;
 }
 
 extern "C" int cfp_wave_plan_num_passes(cfp_wave_plan_t p, int* passes) {

@@ -1,0 +1,286 @@
+// cfp_wave_three.hip -- the 3-sweep apply of the wave-system block-circulant plan on a 128^3
+// grid (config 4; cfp_wave.hip's 5-sweep schedule serves every other grid).  The field is the
+// reference's interleaved layout idx = 4 cell + comp (src/WaveSystem.cxx:112-113), 64 bytes per
+// cell.  As in the scalar 3-sweep (cfp_three_pass.hip) the y transform is split four-step,
+// here ny = N1 N2 = 16 x 8, y = y2 + 8 y1, ky = k1 + 16 k2:
+//
+//   P1w k_wtp_rows<fwd>: one z-plane's rows y2 + 8 y1 (16 rows x 128 cells x 4 comps = 128 KiB).
+//       Column mode, one thread per column 4 x + comp: the 16-point y1 DFT in registers; LDS
+//       transpose to 64 rows (k1, comp) with the 4 comps of a cell in adjacent lanes; the
+//       128-point x DFT along each row.  Every intermediate stays in its slot (y1 <-> k1).
+//   P2w k_wtp_mid: 2 cells x 4 comps x 8 y2 (64 columns, lane = comp + 4 y2 + 32 x) x 128 z of
+//       one k1: twiddle W_128^{y2 k1}, 8-point y2 DFT across lane bits 2..4 (DPP lane ^ 4, ^ 8,
+//       ds_swizzle lane ^ 16), 128-point z DFT, the arrowhead solve S(k)^-1 per frequency with
+//       the 4 comps gathered from the lane quad (wave_point, cfp_fft_device.h), then the same
+//       transforms on the conjugate (inverse).
+//   P3w k_wtp_rows<inv>: P1w on the conjugate, x 1/N.
+//
+// An apply moves 3 x (read + write) x 64 bytes per cell instead of the 5-sweep schedule's 5 x.
+#include "cfp_fft_device.h"
+#include "cfp_lane.h"
+#include "cfp_three_pass.h"
+
+namespace cfp {
+
+namespace {
+
+constexpr int WNX = 128, WNC = 4, WW = WNX * WNC;  // cells per row, comps, values per row
+constexpr int WN1 = 16, WN2 = 8;                   // y = y2 + WN2 y1
+constexpr i64 WPLANE = (i64)WNX * WW;              // values per z-plane
+
+__device__ __forceinline__ int launder(int i) {
+  asm volatile("" : "+v"(i));
+  return i;
+}
+
+// first radix of an n-point FFT done as r0 x PTS x ... x PTS (n = r0 PTS^k, r0 <= PTS)
+constexpr int wr0_of(int n, int pts) { return n > pts ? wr0_of(n / pts, pts) : n; }
+
+}  // namespace
+
+// P1w / P3w.  512 threads, 16 points each; one unit = (z, y2); persistent over the units.
+// FLAGS: the global load / store policy (F_NT_LD, F_NT_ST).
+template <bool INV, int FLAGS>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+k_wtp_rows(const cd* in, cd* out, WTPArgs a, int nunits) {
+  constexpr int PTS = 16, TR = WNX / PTS;  // row mode: 8 threads per (row, comp)
+  constexpr int NROW = WN1 * WNC;          // 64 row-mode rows (k1, comp)
+  constexpr int CS = WW + WW / 16;         // padded stride of the column-mode transpose rows
+  constexpr int RS = WNX + WNX / 16;       // fft_stages' row-mode stride
+  constexpr int F = F_SPLIT_LDS | F_LDS_SYNC | F_TW_GLOBAL;
+  constexpr int LDS_D = WN1 * CS > NROW * RS ? WN1 * CS : NROW * RS;
+  static_assert(WN1 == PTS, "the y1 DFT runs in registers");
+  __shared__ __attribute__((aligned(16))) double lds[LDS_D];
+  const int tid = threadIdx.x;
+  const int c0 = tid;  // column mode: column 4 x + comp
+  const int comp0 = tid & 3, tx0 = (tid >> 2) & (TR - 1), k0 = tid >> 5;  // row mode
+  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+    const int z = u / WN2, y2 = u % WN2;
+    cd v[PTS];
+    {
+      const int c = launder(c0);
+      const cd* src = in + z * WPLANE + (i64)y2 * WW + c;
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) v[m] = gload<FLAGS>(src + (i64)WN2 * WW * m);  // rows y2 + 8 m
+      __builtin_amdgcn_sched_barrier(0);  // every load out before the first butterfly
+      if (INV) {
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
+      }
+      dft_any<PTS>(v);  // v[m]: k1 = m (forward) / y1 = m (inverse)
+    }
+    {
+      // transpose: (slot m, column c) -> row m's comp of cell x = tx + TR t
+      const int c = launder(c0), comp = launder(comp0), tx = launder(tx0), k = launder(k0);
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) lds[m * CS + c + (c >> 4)] = half ? v[m].y : v[m].x;
+        lds_barrier();
+#pragma unroll
+        for (int t = 0; t < PTS; ++t) {
+          const int cc = WNC * (tx + TR * t) + comp;
+          const double val = lds[k * CS + cc + (cc >> 4)];
+          if (half) v[t].y = val; else v[t].x = val;
+        }
+        lds_barrier();
+      }
+    }
+    {
+      const int comp = launder(comp0), tx = launder(tx0), k = launder(k0);
+      fft_stages<WNX, PTS, wr0_of(WNX, PTS), true, NROW, F>(v, lds, a.tw, k * WNC + comp, tx, true);  // v[t]: kx = tx + TR t
+    }
+    {
+      const int comp = launder(comp0), tx = launder(tx0), k = launder(k0);
+      const double sc = a.scale, sy = INV ? -sc : sc;
+      cd* dst = out + z * WPLANE + (i64)(y2 + WN2 * k) * WW + WNC * tx + comp;
+#pragma unroll
+      for (int t = 0; t < PTS; ++t) gstore<FLAGS>(dst + WNC * TR * t, make_cd(v[t].x * sc, v[t].y * sy));
+    }
+    lds_barrier();  // the next unit's first exchange overwrites LDS
+  }
+}
+
+// P2w.  512 threads = 8 z-groups x 64 columns (one wave per z-group); 16 points per thread.
+// PROBE != 0 only in tools/kexp (wave_probe.hip, built with CFP_KEXP): timing probes that drop
+// a part of the work (output invalid); the product library instantiates PROBE = 0 only.
+enum { WPR_NO_Y2 = 1, WPR_NO_SOLVE = 2, WPR_NO_LOAD = 4, WPR_NO_STORE = 8 };
+template <bool XS, int PROBE = 0>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+k_wtp_mid(cd* data, WTPArgs a, int nunits) {
+#ifndef CFP_KEXP
+  static_assert(PROBE == 0, "timing probes are built in tools/kexp only");
+#endif
+  constexpr int XT = 2, T = WNC * WN2 * XT;  // 64 columns: lane = comp + 4 y2 + 32 xl
+  constexpr int PTS = 16, TZ = WNX / PTS;    // 8 z-groups, kz = tz + 8 m
+  constexpr int NXT = WNX / XT;              // x tiles
+  constexpr int F = (XS ? F_SPLIT_LDS : 0) | F_LDS_SYNC;
+  __shared__ __attribute__((aligned(16))) double lds[T * WNX * (XS ? 1 : 2)];
+  __shared__ cd tw_l[WNX];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < WNX; i += T * TZ) tw_l[i] = a.tw[i];
+  const int c0 = tid & (T - 1), tz0 = tid / T;
+  const i64 zs = WPLANE;
+  const double c0sq = a.wave.c0sq;
+  // the thread's first point and its y twiddles (rebuilt where used: nothing but the points
+  // stays live across an FFT)
+  struct Col {
+    cd* p;
+    int y2;
+    cd w, w8;  // W_128^{y2 k1}; W_8^(y2 & 3)
+  };
+  const auto column = [&](int u) {
+    const int c = launder(c0), tz = launder(tz0);
+    Col q;
+    const int xt = u % NXT, k1 = u / NXT;
+    const int comp = c & 3, xl = c >> 5;
+    q.y2 = (c >> 2) & (WN2 - 1);
+    q.p = data + (i64)(q.y2 + WN2 * k1) * WW + (xt * XT + xl) * WNC + comp + zs * tz;
+    q.w = a.tw[(q.y2 * k1) & (WNX - 1)];
+    q.w8 = a.tw[(WNX / 8) * (q.y2 & 3)];
+    return q;
+  };
+  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+    cd v[PTS];
+    {
+      const Col q = column(u);
+      if constexpr (PROBE & WPR_NO_LOAD) {
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) v[m] = make_cd((double)m, (double)q.y2);
+      } else {
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) v[m] = q.p[zs * TZ * m];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // 8-point DIF over y2 = lane bits 2..4; lane y2 ends with frequency k2 = brev3(y2).
+      // Each radix-2 stage is branch-free: the upper lane forms partner - own as fma(-1, own,
+      // partner), the lower own + partner; the upper lanes' twiddle W_8^(y2 & 3) is 1 below.
+      const double s4 = q.y2 & 4 ? -1.0 : 1.0, s2 = q.y2 & 2 ? -1.0 : 1.0, s1 = q.y2 & 1 ? -1.0 : 1.0;
+      const bool mi = (q.y2 & 3) == 3;
+      const cd w8 = q.y2 & 4 ? q.w8 : make_cd(1.0, 0.0);
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) {
+        v[m] = cmul(v[m], q.w);
+        if constexpr (PROBE & WPR_NO_Y2) continue;
+        const cd p = lane_xor16(v[m]);
+        v[m] = cmul(make_cd(fma(s4, v[m].x, p.x), fma(s4, v[m].y, p.y)), w8);
+      }
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) {
+        if constexpr (PROBE & WPR_NO_Y2) continue;
+        const cd p = lane_xor8(v[m]);
+        cd t = make_cd(fma(s2, v[m].x, p.x), fma(s2, v[m].y, p.y));
+        t = mi ? mul_mi(t) : t;
+        const cd r = lane_xor4(t);
+        v[m] = make_cd(fma(s1, t.x, r.x), fma(s1, t.y, r.y));
+      }
+    }
+    {
+      const int c = launder(c0), tz = launder(tz0);
+      fft_stages<WNX, PTS, wr0_of(WNX, PTS), false, T, F>(v, lds, tw_l, c, tz, true);  // v[m]: kz = tz + TZ m
+    }
+    {
+      const int c = launder(c0), tz = launder(tz0);
+      const int xt = u % NXT, k1 = u / NXT;
+      const int comp = c & 3, xl = c >> 5, y2 = (c >> 2) & (WN2 - 1);
+      const int k2 = ((y2 & 1) << 2) | (y2 & 2) | (y2 >> 2);
+      double2 pq[3];
+      pq[0] = a.wave.tab[0][xt * XT + xl];
+      pq[1] = a.wave.tab[1][k1 + WN1 * k2];
+      pq[2] = make_double2(0.0, 0.0);
+      const WaveCol wc = wave_col(pq, 2, comp, c0sq);
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) {
+        if constexpr (PROBE & WPR_NO_SOLVE) {
+          v[m] = cconj(v[m]);
+          continue;
+        }
+        cd r[4];
+        r[0] = make_cd(quad_bcast<0>(v[m].x), quad_bcast<0>(v[m].y));
+        r[1] = make_cd(quad_bcast<1>(v[m].x), quad_bcast<1>(v[m].y));
+        r[2] = make_cd(quad_bcast<2>(v[m].x), quad_bcast<2>(v[m].y));
+        r[3] = make_cd(quad_bcast<3>(v[m].x), quad_bcast<3>(v[m].y));
+        v[m] = cconj(wave_point(r, comp, 2, wc, a.wave.tab[2][tz + TZ * m], c0sq));
+      }
+    }
+    {
+      const int c = launder(c0), tz = launder(tz0);
+      fft_stages<WNX, PTS, wr0_of(WNX, PTS), false, T, F>(v, lds, tw_l, c, tz, false);
+    }
+    {
+      const Col q = column(u);
+      // forward DFT from the bit-reversed order back to natural (the inverse by conjugation),
+      // branch-free as above
+      const double s4 = q.y2 & 4 ? -1.0 : 1.0, s2 = q.y2 & 2 ? -1.0 : 1.0, s1 = q.y2 & 1 ? -1.0 : 1.0;
+      const bool mi = (q.y2 & 3) == 3;
+      const cd w8 = q.y2 & 4 ? q.w8 : make_cd(1.0, 0.0);
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) {
+        if constexpr (PROBE & WPR_NO_Y2) continue;
+        const cd r = lane_xor4(v[m]);
+        cd t = make_cd(fma(s1, v[m].x, r.x), fma(s1, v[m].y, r.y));
+        t = mi ? mul_mi(t) : t;
+        const cd p = lane_xor8(t);
+        v[m] = make_cd(fma(s2, t.x, p.x), fma(s2, t.y, p.y));
+      }
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) {
+        if constexpr (PROBE & WPR_NO_Y2) {
+          v[m] = cmul(v[m], q.w);
+          continue;
+        }
+        const cd t = cmul(v[m], w8);
+        const cd p = lane_xor16(t);
+        v[m] = cmul(make_cd(fma(s4, t.x, p.x), fma(s4, t.y, p.y)), q.w);
+      }
+      if constexpr (PROBE & WPR_NO_STORE) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) acc += v[m].x + v[m].y;
+        if (acc == 1.2345e300) q.p[0] = make_cd(acc, 0.0);  // keeps the work live, never true
+      } else {
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) q.p[zs * TZ * m] = cconj(v[m]);
+      }
+    }
+    lds_barrier();  // the next unit's first exchange overwrites LDS
+  }
+}
+
+bool wave_three_pass_supported(const i64 n[3], int ncomp) {
+  return ncomp == WNC && n[0] == WNX && n[1] == WNX && n[2] == WNX;
+}
+
+static int wcu_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+      cus = 256;
+  }
+  return cus;
+}
+
+hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArgs& a, hipStream_t s) {
+  // persistent grids, two 512-thread workgroups per CU (70 / 64 KiB of LDS each)
+  const int g = 2 * wcu_count();
+  if (stage == 1) {
+    const int units = (WNX / 2) * WN1;  // x tiles x k1
+    hipLaunchKernelGGL((k_wtp_mid<true>), dim3(units < g ? units : g), dim3(512), 0, s, out, a, units);
+  } else {
+    const int units = WNX * WN2;  // z-planes x y2
+    // P1w out of place: non-temporal loads keep b out of the 256 MB Infinity Cache, which then
+    // still holds much of P1w's output for P2w (the scalar 3-sweep's policy, cfp_three_pass.hip)
+    const dim3 gg(units < g ? units : g);
+    if (stage == 0 && in != out)
+      hipLaunchKernelGGL((k_wtp_rows<false, F_NT_LD>), gg, dim3(512), 0, s, in, out, a, units);
+    else if (stage == 0)
+      hipLaunchKernelGGL((k_wtp_rows<false, 0>), gg, dim3(512), 0, s, in, out, a, units);
+    else
+      hipLaunchKernelGGL((k_wtp_rows<true, F_NT_ST>), gg, dim3(512), 0, s, in, out, a, units);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace cfp

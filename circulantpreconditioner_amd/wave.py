@@ -54,6 +54,14 @@ class WavePlan:
         check(lib().cfp_wave_plan_set_symbol(self._h, _d3(kappa), float(c0)))
         return self
 
+    SCHEDULES = {"auto": 0, "five": 1, "three": 2}
+
+    def set_schedule(self, schedule: str | int = "auto") -> "WavePlan":
+        """'auto' (3 sweeps on a 3-D 128^3 grid, else 5), 'five', or 'three' (3-D 128^3 only)."""
+        v = self.SCHEDULES[schedule] if isinstance(schedule, str) else int(schedule)
+        check(lib().cfp_wave_plan_set_schedule(self._h, v))
+        return self
+
     def apply(self, b: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
         if out is None:
             out = torch.empty_like(b)

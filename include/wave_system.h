@@ -45,6 +45,9 @@ int cfp_wave_plan_apply(cfp_wave_plan_t plan, const double *b, double *x, void *
 /* unnormalised forward / backward 3-D DFT of each component (tests and tools) */
 int cfp_wave_plan_forward(cfp_wave_plan_t plan, const double *in, double *out, void *stream);
 int cfp_wave_plan_backward(cfp_wave_plan_t plan, const double *in, double *out, void *stream);
+/* CFP_SCHEDULE_AUTO (default: the 3-sweep apply on a 3-D 128^3 grid, else 5 sweeps),
+   CFP_SCHEDULE_FIVE_PASS, or CFP_SCHEDULE_THREE_PASS (3-D 128^3 only; CFP_ERR_SUP otherwise) */
+int cfp_wave_plan_set_schedule(cfp_wave_plan_t plan, int schedule);
 int cfp_wave_plan_num_passes(cfp_wave_plan_t plan, int *passes);
 int cfp_wave_plan_time_passes(cfp_wave_plan_t plan, const double *b, double *x, int iters, double *ms_out,
                               void *stream);

@@ -24,6 +24,7 @@ PRIORITY = [
     ("test_transport.py", "test_driver_fft_pc_matches_oracle", ""),   # config 1 (32^3 GMRES + PCSHELL)
     ("test_transport.py", "test_config3_256_converges_and_solves", ""),  # config 3
     ("test_wave.py", "test_wave_plan_128_inverts_periodic_operator", ""),  # config 4
+    ("test_wave.py", "test_wave_plan_128_three_sweep_matches_oracle", ""),  # config 4, 3 sweeps
     ("test_dist_gpu.py", "test_group_config5_512_in_8_slabs", ""),    # config 5 (HIP path, 8 slabs)
     ("test_dist_gpu.py", "test_slab_plan_processes_vs_oracle", ""),   # config 5 pieces, several processes
     ("test_pcshell_mpi_gpu.py", "", ""),                              # PCSHELL on a 2-rank communicator

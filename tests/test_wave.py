@@ -276,6 +276,38 @@ def test_wave_plan_128_inverts_periodic_operator():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kappa", [(0.079, 0.079, 0.079), (0.31, 0.05, 0.11)], ids=["config4", "anisotropic"])
+def test_wave_plan_128_three_sweep_matches_oracle(kappa):
+    """The 3-sweep wave apply (cfp_wave_three.hip, AUTO at 128^3): against the oracle's block
+    solve, against the 5-sweep schedule, in place; schedule rules."""
+    import torch
+    dims = (128, 128, 128)
+    m = 4 * 128 ** 3
+    b = _rand(m, 5)
+    xo = OW.block_solve(dims, kappa, b)
+    plan = W.WavePlan(dims).set_symbol(kappa)
+    assert plan.num_passes() == 3
+    bd = torch.from_numpy(b).cuda()
+    x3 = plan.apply(bd)
+    assert np.linalg.norm(x3.cpu().numpy() - xo) <= 1e-12 * np.linalg.norm(xo)
+    t = bd.clone()
+    plan.apply(t, out=t)
+    assert torch.equal(t, x3)
+    plan.set_schedule("five")
+    assert plan.num_passes() == 5
+    x5 = plan.apply(bd)
+    assert float(torch.linalg.vector_norm(x5 - x3) / torch.linalg.vector_norm(x5)) < 1e-13
+    plan.set_schedule("three")
+    assert plan.num_passes() == 3
+    small = W.WavePlan((64, 64, 64))
+    assert small.set_symbol(kappa).num_passes() == 5
+    with pytest.raises(Exception):
+        small.set_schedule("three")
+    with pytest.raises(Exception):
+        W.WavePlan((128, 128), dim=2).set_schedule("three")
+
+
+@pytest.mark.gpu
 def test_wave_plan_errors():
     import torch
     plan = W.WavePlan((8, 8, 8))
