@@ -15,7 +15,9 @@ hipError_t blas_waxpy(cd* w, cd a, const cd* x, const cd* y, i64 n, hipStream_t 
 hipError_t blas_pmult(cd* w, const cd* x, const cd* y, i64 n, hipStream_t s);
 // y += sum_j a[j] xs[j]   (a, xs: host arrays of k coefficients / device pointers)
 hipError_t blas_maxpy(cd* y, int k, const cd* a, const cd* const* xs, i64 n, hipStream_t s);
-hipError_t blas_csr_spmv(i64 m, const i64* rowptr, const i64* col, const cd* val, const cd* x, cd* y, hipStream_t s);
+// y = A x for a CSR matrix of m rows and nnz nonzeros (nnz picks the lanes per row)
+hipError_t blas_csr_spmv(i64 m, i64 nnz, const i64* rowptr, const i64* col, const cd* val, const cd* x, cd* y,
+                         hipStream_t s);
 // synchronous reductions, PETSc conventions: dot = y^H x; norm type 0 = NORM_1 (sum |re|+|im|),
 // 1 = NORM_2, 3 = NORM_INFINITY (max modulus)
 hipError_t blas_dot(const cd* x, const cd* y, i64 n, cd* val, hipStream_t s);

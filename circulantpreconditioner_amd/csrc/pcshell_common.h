@@ -18,6 +18,20 @@ inline PetscErrorCode cfp_err(int rc, const char* where) {
 #endif
 }
 
+// The stream an apply on device Vecs is ordered on, and whether it must be waited for: the
+// stand-in's Vec stream, stream-ordered like PETSc's VECHIP operations (the next Vec operation,
+// e.g. GMRES's VecMAXPY, queues behind the apply; a host read synchronises), so PCApply costs no
+// host round trip.  Built against a real PETSc: the default stream, waited for.
+inline void device_stream(void** st, bool* wait) {
+#ifdef CFP_WITH_PETSC
+  *st = nullptr;
+  *wait = true;
+#else
+  VecMiniGetStream(st);
+  *wait = false;
+#endif
+}
+
 // Device view of a Vec for the duration of one solve: device arrays are used in place,
 // host arrays are staged through a temporary device buffer (PCIe-inclusive path).
 struct DevIn {

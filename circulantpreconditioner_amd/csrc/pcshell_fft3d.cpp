@@ -379,26 +379,12 @@ extern "C" PetscErrorCode build_diag_mat_vec_3D(Vec Diag, Vec cx, Vec cy, Vec cz
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
-// The stream a single-rank apply on device Vecs is ordered on, and whether it must be waited
-// for: the stand-in's Vec stream, stream-ordered like PETSc's VECHIP operations (the next Vec
-// operation, e.g. GMRES's VecMAXPY, queues behind the apply; a host read synchronises), so
-// PCApply costs no host round trip.  Built against a real PETSc: the default stream, waited for.
-void device_stream(void** st, bool* wait) {
-#ifdef CFP_WITH_PETSC
-  *st = nullptr;
-  *wait = true;
-#else
-  VecMiniGetStream(st);
-  *wait = false;
-#endif
-}
-
 // One apply of FFT_MAT's plan, X = (1/N) IDFT(DFT(b) ./ symbol): the register symbol (own) or
 // the explicit Diag (single rank: streamed; slab plan: the z-pencil copy already set).  b may be
 // X (the direct solver's Un, Un).  Host Vecs are staged: single rank through the plan's own
 // persistent buffer (cfp_plan_apply_host), slab plan through the shell's; those applies, and
 // every slab apply (its exchanges are host-driven), return complete.  A single-rank apply on
-// device Vecs is ordered on the Vec stream (device_stream).
+// device Vecs is ordered on the Vec stream (cfp_pc::device_stream).
 PetscErrorCode shell_apply(FFTShell* s, Vec X, Vec b, bool own, Vec Diag) {
   const PetscInt n = s->nlocal;
   DevIn din;
@@ -406,7 +392,7 @@ PetscErrorCode shell_apply(FFTShell* s, Vec X, Vec b, bool own, Vec Diag) {
   if (s->dplan) CFPCALL(cfp_dist_plan_use_diag(s->dplan, own ? 0 : 1));
   void* vst = nullptr;
   bool vwait = true;
-  if (!s->dplan) device_stream(&vst, &vwait);
+  if (!s->dplan) cfp_pc::device_stream(&vst, &vwait);
   auto dev_apply = [&](const double* in, double* out) -> int {
     if (s->dplan) return cfp_dist_plan_apply(s->dplan, in, out, nullptr);
     return own ? cfp_plan_apply(s->plan, in, out, vst) : cfp_plan_apply_with_diag(s->plan, din.ptr(), in, out, vst);

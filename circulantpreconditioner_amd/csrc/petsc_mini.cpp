@@ -1002,7 +1002,7 @@ static PetscErrorCode aij_mult(Mat A, Vec x, Vec y) {
     PetscCall(dev_read(x, &xd));
     cd* yd;
     PetscCall(dev_rw(y, &yd));
-    HIPK(cfp::blas_csr_spmv(A->m, A->rowptr, A->col, A->val, xd, yd, g_stream));
+    HIPK(cfp::blas_csr_spmv(A->m, (i64)A->h_col.size(), A->rowptr, A->col, A->val, xd, yd, g_stream));
   } else {
     const cd* xh;
     PetscCall(host_read(x, &xh));

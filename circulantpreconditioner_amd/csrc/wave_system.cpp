@@ -229,8 +229,13 @@ extern "C" PetscErrorCode applyFFT3DPrecWave(PC pc, Vec b, Vec x) {
   DevOut out;
   PetscCall(in.get(b, M));
   PetscCall(out.get(x, M));
-  int rc = cfp_wave_plan_apply(ctx->plan, in.ptr(), out.ptr(), nullptr);
-  if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
+  // device Vecs: ordered on the Vec stream without a host round trip (cfp_pc::device_stream);
+  // a staged host Vec is waited for (its buffers are copied back / freed below)
+  void* st = nullptr;
+  bool wait = true;
+  if (!in.tmp && !out.tmp) device_stream(&st, &wait);
+  int rc = cfp_wave_plan_apply(ctx->plan, in.ptr(), out.ptr(), st);
+  if (rc == CFP_SUCCESS && (wait || in.tmp || out.tmp)) rc = cfp_stream_sync(st);
   PetscCall(out.put());
   PetscCall(in.put());
   CFPCALL(rc);

@@ -234,6 +234,30 @@ def test_intersection_matrix_remap(P, oracle):
     pc.destroy()
 
 
+@pytest.mark.parametrize("mean", [1, 2, 3, 7, 13, 40])
+def test_aij_device_spmv_row_lengths(P, mean):
+    """MatMult of the stand-in AIJ on device Vecs (cfp::blas_csr_spmv: one thread per row up to
+    ~1 nonzero per row, 2 / 4 / 8 / 16 lanes per row above) against scipy, with empty rows, rows
+    far longer than the lanes and unsorted columns."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(mean)
+    m, n = 4099, 3001
+    lens = rng.integers(0, 2 * mean + 1, m)
+    lens[::17] = 0
+    lens[5] = 5 * mean + 37
+    rowptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    nnz = int(rowptr[-1])
+    col = rng.integers(0, n, nnz).astype(np.int64)
+    val = rng.standard_normal(nnz) + 1j * rng.standard_normal(nnz)
+    A = P.Mat.aij(rowptr, col, val, (m, n))
+    xs = rng.standard_normal(n) + 1j * rng.standard_normal(n)
+    ty = torch.empty(m, dtype=torch.complex128, device="cuda")
+    A.mult(P.Vec.from_tensor(_dev(xs)), P.Vec.from_tensor(ty))
+    ref = sp.csr_matrix((val, col, rowptr), shape=(m, n)) @ xs
+    assert np.linalg.norm(ty.cpu().numpy() - ref) <= 1e-13 * np.linalg.norm(ref)
+    A.destroy()
+
+
 def test_device_vec_kernels(P):
     rng = np.random.default_rng(1)
     a = rng.standard_normal(3000) + 1j * rng.standard_normal(3000)

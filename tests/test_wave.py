@@ -326,9 +326,11 @@ def test_wave_driver_pcnone_device_equals_host():
     dims = (8, 8, 8)
     rh, Uh = W.run(W.config(dims, pc="none", device=False), return_field=True)
     rd, Ud = W.run(W.config(dims, pc="none", device=True), return_field=True)
-    assert rd["total_its"] == rh["total_its"]
-    # ten rtol = 1e-5 solves in a row (c0^2 = 4.9e5 couples pressure and momentum): the two
-    # rounding paths agree to the solver tolerance, not to rounding
+    # the device SpMV sums a row's nonzeros in lane-strided partial sums (cfp::blas_csr_spmv),
+    # the host loop in order: ten unpreconditioned rtol = 1e-5 solves in a row (c0^2 = 4.9e5
+    # couples pressure and momentum) may then stop an iteration apart, and the two rounding
+    # paths agree to the solver tolerance, not to rounding
+    assert abs(rd["total_its"] - rh["total_its"]) <= 2, (rd["total_its"], rh["total_its"])
     np.testing.assert_allclose(Ud, Uh, rtol=0, atol=1e-5 * np.abs(Uh).max())
 
 
