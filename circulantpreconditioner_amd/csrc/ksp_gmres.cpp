@@ -146,6 +146,20 @@ extern "C" PetscErrorCode KSPDestroy(KSP* pk) {
   return rc;
 }
 
+// 64 more PCApply timing events (32 applies); false without a HIP device.  Creating them costs
+// ~25 us each, so KSPMiniSetUpWork makes the first batch outside the timed solves.
+static bool grow_events(KSP k) {
+  for (int i = 0; i < 64; ++i) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) {
+      hipGetLastError();
+      return false;
+    }
+    k->pc_ev.push_back(e);
+  }
+  return true;
+}
+
 extern "C" PetscErrorCode KSPMiniSetUpWork(KSP k, Vec v) {
   KCHK(k);
   PetscInt n;
@@ -160,6 +174,7 @@ extern "C" PetscErrorCode KSPMiniSetUpWork(KSP k, Vec v) {
     PetscCall(VecDuplicate(v, &k->rhs));
     k->n = n;
   }
+  if (k->pc_ev.empty()) grow_events(k);  // no device: the applies are timed on the host
   return PETSC_SUCCESS;
 }
 
@@ -167,14 +182,7 @@ static PetscErrorCode pc_apply(KSP k, Vec x, Vec y) {
   void* st = nullptr;
   PetscCall(VecMiniGetStream(&st));
   bool events = k->pc_ev_used + 2 <= k->pc_ev.size();
-  if (!events) {
-    events = true;
-    for (int i = 0; i < 64 && events; ++i) {
-      hipEvent_t e;
-      if (hipEventCreate(&e) != hipSuccess) events = false;
-      else k->pc_ev.push_back(e);
-    }
-  }
+  if (!events) events = grow_events(k);
   if (!events) {  // no HIP device (host Vecs on a CPU-only machine): the apply is synchronous
     hipGetLastError();
     const double t0 = now();
