@@ -149,13 +149,15 @@ struct cfp_rplan_s {
   bool has_sym = false;
   hipStream_t side = nullptr;  // the Nyquist grid's passes overlap the half-spectrum passes
   hipEvent_t fork = nullptr, join = nullptr;
-  // 3-sweep schedule at 256^3 (cfp_three_pass.hip): separable symbol of the half spectrum
+  // 3-sweep schedule at 128^3 / 256^3 (cfp_three_pass.hip): separable symbol of the half spectrum
   int schedule = CFP_RSCHEDULE_AUTO;
   cd* colsym3 = nullptr;  // [kx + M ky], kx < M
   cd* axsym3 = nullptr;   // [kz]
 };
 
-static bool three_ok(const cfp_rplan_s* p) { return p->n[0] == 256 && p->n[1] == 256 && p->n[2] == 256; }
+static bool three_ok(const cfp_rplan_s* p) {
+  return p->n[0] == p->n[1] && p->n[1] == p->n[2] && (p->n[0] == 128 || p->n[0] == 256);
+}
 static bool use_three(const cfp_rplan_s* p) { return three_ok(p) && p->schedule != CFP_RSCHEDULE_FIVE; }
 
 namespace {
@@ -186,25 +188,26 @@ void free_rplan(cfp_rplan_s* p) {
   delete p;
 }
 
-// 3 sweeps at 256^3: P1r (r2c rows + y1, Nyquist column to Q) | P2 on the half spectrum |
-// P3r (y1 inverse + c2r rows).  The Nyquist column's own y/z plan runs in between; it cannot
-// overlap P2 (P2's workgroups fill every CU), so it simply follows P1r on the same stream.
+// 3 sweeps at 128^3 and 256^3: P1r (r2c rows + y1, Nyquist column to Q) | P2 on the half spectrum |
+// P3r (y1 inverse + c2r rows).  The Nyquist column's own y/z plan runs in between, on the same
+// stream: at 256^3 P2's workgroups fill every CU; at 128^3 there is room beside P2, but the
+// side-stream handshake costs more than the column's launches (20,800 -> 15,400 PCApply/s, r03t).
 int run_real_three(cfp_rplan_s* p, const double* b, double* x, hipStream_t s, std::vector<hipEvent_t>* ev) {
   TPArgs a;
-  a.tw = p->twn;  // W_256: nx = ny = nz = 256
+  a.tw = p->twn;  // W_n: nx = ny = nz = n
   a.colsym = p->colsym3;
   a.axsym = p->axsym3;
   a.scale = 2.0 / (double)(p->n[0] * p->n[1] * p->n[2]);
   if (ev) HIPCHK(hipEventRecord((*ev)[0], s));
-  hipError_t e = launch_three_pass_real(0, b, p->H, p->Q, nullptr, a, s);
+  hipError_t e = launch_three_pass_real(0, (int)p->n[0], b, p->H, p->Q, nullptr, a, s);
   if (e != hipSuccess) return hip_error(e, "r2c rows + y1 pass");
   if (ev) HIPCHK(hipEventRecord((*ev)[1], s));
-  e = launch_three_pass_real(1, nullptr, p->H, nullptr, nullptr, a, s);
+  e = launch_three_pass_real(1, (int)p->n[0], nullptr, p->H, nullptr, nullptr, a, s);
   if (e != hipSuccess) return hip_error(e, "half-spectrum y2/z pass");
   if (ev) HIPCHK(hipEventRecord((*ev)[2], s));
   CFPCHK(cfp_plan_apply(p->nyq, (const double*)p->Q, (double*)p->Q, s));
   if (ev) HIPCHK(hipEventRecord((*ev)[3], s));
-  e = launch_three_pass_real(2, nullptr, p->H, p->Q, x, a, s);
+  e = launch_three_pass_real(2, (int)p->n[0], nullptr, p->H, p->Q, x, a, s);
   if (e != hipSuccess) return hip_error(e, "y1 inverse + c2r rows pass");
   if (ev) HIPCHK(hipEventRecord((*ev)[4], s));
   return CFP_SUCCESS;
@@ -320,7 +323,7 @@ extern "C" int cfp_rplan_set_schedule(cfp_rplan_t p, int schedule) {
   if (schedule != CFP_RSCHEDULE_AUTO && schedule != CFP_RSCHEDULE_FIVE && schedule != CFP_RSCHEDULE_THREE)
     return set_error(CFP_ERR_ARG_OUTOFRANGE, "unknown real-plan schedule %d", schedule);
   if (schedule == CFP_RSCHEDULE_THREE && !three_ok(p))
-    return set_error(CFP_ERR_SUP, "the 3-sweep real schedule needs a 256^3 grid");
+    return set_error(CFP_ERR_SUP, "the 3-sweep real schedule needs a 128^3 or 256^3 grid");
   p->schedule = schedule;
   return CFP_SUCCESS;
 }

@@ -35,10 +35,11 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
 // the default shape (N1 = 32, permlane P2 with prefetch)
 bool three_pass_slab_supported(const i64 n[3], int P);
 hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs& a, int nzl, hipStream_t s);
-// real-data plan at 256^3 (cfp_real.hip): stage 0 P1r (b -> H, Q), 1 P2 on H (128 x 256 x 256,
-// in place), 2 P3r (H, Q -> x, x a.scale); a.tw = W_256, a.colsym = [kx + 128 ky], a.axsym = [kz].
-// Q (256 x 256, the Nyquist column kx = 128) takes its own y/z plan between P1r and P3r.
-hipError_t launch_three_pass_real(int stage, const double* b, cd* H, cd* Q, double* x, const TPArgs& a,
+// real-data plan at n^3, n = 128 or 256 (cfp_real.hip): stage 0 P1r (b -> H, Q), 1 P2 on H
+// (n/2 x n x n, in place), 2 P3r (H, Q -> x, x a.scale); a.tw = W_n, a.colsym = [kx + (n/2) ky],
+// a.axsym = [kz].  Q (n x n, the Nyquist column kx = n/2) takes its own y/z plan between P1r
+// and P3r.
+hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* Q, double* x, const TPArgs& a,
                                   hipStream_t s);
 
 // wave-system plan (cfp_wave_three.hip): the 3-sweep apply of the interleaved 4-component field

@@ -171,10 +171,10 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
 
 // Persistent over units u = (x-tile, k1); T columns per unit = T/N2 x values times N2 y2.
 // Barriers wait for LDS only, so one unit's stores drain while the next unit loads.
-template <int FLAGS, int T, int N2, int TN, int PTS = 16, bool XS = true>
+template <int FLAGS, int T, int N2, int TN, int PTS = 16, bool XS = true, int NX = TN>
 __global__ void __launch_bounds__(T * (TN / PTS)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid(cd* data, TPArgs a, int nunits) {
-  constexpr int N1 = TN / N2, TZ = TN / PTS, NT = T * TZ, XT = T / N2, NXT = TN / XT;
+  constexpr int N1 = TN / N2, TZ = TN / PTS, NT = T * TZ, XT = T / N2, NXT = NX / XT;
   constexpr int F = FLAGS | (XS ? F_SPLIT_LDS : 0) | F_LDS_SYNC;
   static_assert(N2 == 4 || N2 == 8, "the y2 DFT runs across 4 or 8 lanes");
   __shared__ __attribute__((aligned(16))) double lds[T * TN * (XS ? 1 : 2)];
@@ -182,7 +182,7 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
   const int tid = threadIdx.x;
   for (int i = tid; i < TN; i += NT) tw_l[i] = a.tw[i];
   const int c0 = tid & (T - 1), tz0 = tid / T;
-  const i64 zs = (i64)TN * TN;
+  const i64 zs = (i64)NX * TN;  // NX: row length (TN; the real plan's half spectrum: TN / 2)
   // Everything but the 16 points is rebuilt from laundered copies of the thread indices where
   // it is used: 128 VGPRs hold the points plus one radix-16 stage's twiddles, and an address,
   // twiddle or index kept live across the FFTs (or hoisted out of the unit loop) spills.
@@ -198,7 +198,7 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
     const int xt = u % NXT, k1 = u / NXT;
     q.y2 = c & (N2 - 1);
     q.xk = xt * XT + c / N2;
-    q.col = data + q.xk + (i64)TN * (q.y2 + N2 * k1) + zs * tz;
+    q.col = data + q.xk + (i64)NX * (q.y2 + N2 * k1) + zs * tz;
     q.w = a.tw[(q.y2 * k1) & (TN - 1)];
     q.w8 = a.tw[(TN / 8) * (q.y2 & 3)];
     return q;
@@ -231,7 +231,7 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
       int c = c0, tz = tz0;
       asm volatile("" : "+v"(c), "+v"(tz));
       const int k1 = u / NXT, y2 = c & (N2 - 1);
-      const cd cs = a.colsym[(u % NXT) * XT + c / N2 + (i64)TN * (k1 + N1 * brev<N2>(y2))];
+      const cd cs = a.colsym[(u % NXT) * XT + c / N2 + (i64)NX * (k1 + N1 * brev<N2>(y2))];
 #pragma unroll
       for (int m = 0; m < PTS; ++m) {
         const cd d = cadd(cadd(cs, a.axsym[tz + TZ * m]), make_cd(1.0, 0.0));
@@ -611,21 +611,23 @@ static unsigned grid_of(int units, int per_cu) {
 // units on 256 CUs take a third round, P2 70 -> 89 us.)
 // 8 points per thread (512 threads): the even/odd split needs every point and its mirror live
 // at once, which at 16 points per thread spills.
-template <bool INV>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+// At 128^3 (r03, AUTO there too): M = 64, y = y2 + 4 y1 (N1 = 32, N2 = 4), 256 threads; P2 is
+// the lane-DFT k_tp_mid on the 64-wide half spectrum (NX = 64).
+template <bool INV, int M = 128, int N1 = 32, int N2 = 8, int NY = 256>
+__global__ void __launch_bounds__(N1 * (M / 8)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nunits) {
-  constexpr int M = 128, N1 = 32, N2 = 8, NY = 256, PTS = 8;
-  constexpr int TPC = M / PTS;  // 16 threads per row (row mode)
+  constexpr int PTS = 8;
+  constexpr int TPC = M / PTS;  // threads per row (row mode)
   constexpr int TY = N1 / PTS;  // 4 threads per column (column mode)
-  constexpr int NT = N1 * TPC;  // 512
+  constexpr int NT = N1 * TPC;
   constexpr int RS = M + M / 16;
   constexpr int F = F_SPLIT_LDS | F_LDS_SYNC;
   __shared__ __attribute__((aligned(16))) double lds[N1 * RS];  // row layout; the column layout (N1 x M) fits
-  __shared__ cd tw_m[M];   // W_128 (row FFT)
-  __shared__ cd tw_1[N1];  // W_32 (y1 DFT)
+  __shared__ cd tw_m[M];   // W_M (row FFT)
+  __shared__ cd tw_1[N1];  // W_N1 (y1 DFT)
   const int tid = threadIdx.x;
   for (int i = tid; i < M; i += NT) tw_m[i] = a.tw[2 * i];
-  for (int i = tid; i < N1; i += NT) tw_1[i] = a.tw[8 * i];
+  for (int i = tid; i < N1; i += NT) tw_1[i] = a.tw[(2 * M / N1) * i];
   const int r0 = tid / TPC, tpc0 = tid % TPC;  // row mode: row r (= y1), thread tpc
   const int x0 = tid % M, ty0 = tid / M;       // column mode: column kx, thread ty
   const auto idx = [](int i) {
@@ -705,12 +707,12 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
 #pragma unroll
         for (int t = 0; t < PTS; ++t) v[t] = src[TPC * t];
         __builtin_amdgcn_sched_barrier(0);  // all loads out before the first butterfly
-        fft_stages<M, PTS, 2, true, N1, F>(v, lds, tw_m, r, tpc, true);  // 128 = 2 x 8 x 8; v[t] = Z[tpc + TPC t]
+        fft_stages<M, PTS, r0_of(M, PTS), true, N1, F>(v, lds, tw_m, r, tpc, true);  // 128 = 2 x 8 x 8; v[t] = Z[tpc + TPC t]
       }
       to_columns_r2c(v, z, y2);
       {
         const int x = idx(x0), ty = idx(ty0);
-        fft_stages<N1, PTS, 4, false, M, F>(v, lds, tw_1, x, ty, true);  // 32 = 4 x 8; v[m]: k1 = ty + TY m
+        fft_stages<N1, PTS, r0_of(N1, PTS), false, M, F>(v, lds, tw_1, x, ty, true);  // 32 = 4 x 8; v[m]: k1 = ty + TY m
         cd* dst = H + ((i64)z * NY + y2 + N2 * ty) * M + x;
 #pragma unroll
         for (int m = 0; m < PTS; ++m) dst[(i64)N2 * TY * M * m] = v[m];
@@ -724,12 +726,12 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
         __builtin_amdgcn_sched_barrier(0);  // all loads out before the first butterfly (measured neutral here)
 #pragma unroll
         for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
-        fft_stages<N1, PTS, 4, false, M, F>(v, lds, tw_1, x, ty, true);  // v[m]: y1 = ty + TY m
+        fft_stages<N1, PTS, r0_of(N1, PTS), false, M, F>(v, lds, tw_1, x, ty, true);  // v[m]: y1 = ty + TY m
       }
       to_rows_c2r(v, z, y2);
       {
         const int r = idx(r0), tpc = idx(tpc0);
-        fft_stages<M, PTS, 2, true, N1, F>(v, lds, tw_m, r, tpc, true);
+        fft_stages<M, PTS, r0_of(M, PTS), true, N1, F>(v, lds, tw_m, r, tpc, true);
         const double sc = a.scale;
         cd* dst = reinterpret_cast<cd*>(out_r) + ((i64)z * NY + y2 + N2 * r) * M + tpc;
 #pragma unroll
@@ -740,8 +742,25 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
   }
 }
 
-hipError_t launch_three_pass_real(int stage, const double* b, cd* H, cd* Q, double* x, const TPArgs& a,
+hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* Q, double* x, const TPArgs& a,
                                   hipStream_t s) {
+  if (n == 128) {
+    if (stage == 1) {  // x tiles of the 64-wide half spectrum (8 x times 4 y2) x k1
+      constexpr int units = (64 / 8) * 32;
+      hipLaunchKernelGGL((k_tp_mid<0, 32, 4, 128, 8, false, 64>), dim3(grid_of(units, 2)), dim3(512), 0, s, H, a,
+                         units);
+    } else {
+      constexpr int units = 128 * 4;  // z-planes x y2
+      const unsigned g = grid_of(units, 4);
+      if (stage == 0)
+        hipLaunchKernelGGL((k_tp_rows_r2c<false, 64, 32, 4, 128>), dim3(g), dim3(256), 0, s, b, H, Q, nullptr, a,
+                           units);
+      else
+        hipLaunchKernelGGL((k_tp_rows_r2c<true, 64, 32, 4, 128>), dim3(g), dim3(256), 0, s, nullptr, H, Q, x, a,
+                           units);
+    }
+    return hipGetLastError();
+  }
   if (stage == 1) {
     constexpr int units = (128 / 8) * 32;  // x tiles of the half spectrum x k1
     hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true, 128>), dim3(grid_of(units, 1)), dim3(1024), 0, s, H, a,

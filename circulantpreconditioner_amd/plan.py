@@ -296,8 +296,8 @@ class RealPlan:
     SCHEDULES = {"auto": 0, "five": 1, "three": 2}
 
     def set_schedule(self, schedule: str | int) -> "RealPlan":
-        """'auto' (3 sweeps at 256^3), 'five' (r2c + 3 half-spectrum passes + c2r) or 'three'
-        (256^3 only)."""
+        """'auto' (3 sweeps at 128^3 and 256^3), 'five' (r2c + 3 half-spectrum passes + c2r) or 'three'
+        (128^3 and 256^3 only)."""
         v = self.SCHEDULES[schedule] if isinstance(schedule, str) else int(schedule)
         check(lib().cfp_rplan_set_schedule(self._h, v))
         return self

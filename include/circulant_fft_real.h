@@ -34,8 +34,8 @@ int cfp_rplan_destroy(cfp_rplan_t plan);
 int cfp_rplan_set_symbol_transport(cfp_rplan_t plan, const double lam[3]);
 /* x = C^{-1} b for real b (nx*ny*nz doubles on the device); x may alias b */
 int cfp_rplan_apply(cfp_rplan_t plan, const double *b, double *x, void *stream);
-/* schedule: CFP_RSCHEDULE_AUTO (3 sweeps at 256^3, else r2c + 3 half-spectrum passes + c2r),
- * CFP_RSCHEDULE_FIVE (always the latter) or CFP_RSCHEDULE_THREE (256^3 only, else CFP_ERR_SUP) */
+/* schedule: CFP_RSCHEDULE_AUTO (3 sweeps at 128^3 and 256^3, else r2c + 3 half-spectrum passes + c2r),
+ * CFP_RSCHEDULE_FIVE (always the latter) or CFP_RSCHEDULE_THREE (128^3 and 256^3 only, else CFP_ERR_SUP) */
 #define CFP_RSCHEDULE_AUTO 0
 #define CFP_RSCHEDULE_FIVE 1
 #define CFP_RSCHEDULE_THREE 2

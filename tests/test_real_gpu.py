@@ -50,17 +50,19 @@ def test_real_plan_matches_complex_plan_256(cp):
         assert len(ms) == 4 and all(m > 0 for m in ms)
 
 
+@pytest.mark.parametrize("side", [256, 128])
 @pytest.mark.parametrize("lam", [(0.6, 0.15, 0.02), (55.6, 0.0, 0.0), (1.3, 0.0, 2.5)], ids=["bench", "transport", "xz"])
-def test_real_three_sweep_256_vs_oracle(cp, oracle, lam):
+def test_real_three_sweep_256_vs_oracle(cp, oracle, lam, side):
     """The 3-sweep real schedule (r2c rows + y1 | half-spectrum y2/z | y1 inverse + c2r rows) at
-    256^3 against the oracle, in place, and against the r2c + 3 half-spectrum passes schedule."""
-    n = (256, 256, 256)
-    N = 256 ** 3
+    256^3 and 128^3 against the oracle, in place, and against the r2c + 3 half-spectrum passes
+    schedule."""
+    n = (side, side, side)
+    N = side ** 3
     b = oracle.c_fill_uniform(N, 41).real.copy()
     ref = oracle.c_solve_3d(oracle.c_build_diag_transport(n, lam), b.astype(np.complex128), n).real
     with cp.RealPlan(n) as plan:
         plan.set_transport_symbol(lam)
-        assert plan.three_sweep  # AUTO at 256^3
+        assert plan.three_sweep  # AUTO at 128^3 and 256^3
         x = plan.apply(torch.from_numpy(b).cuda())
         assert np.linalg.norm(x.cpu().numpy() - ref) <= TOL * np.linalg.norm(ref)
         t = torch.from_numpy(b).cuda()
@@ -81,7 +83,7 @@ def test_real_plan_errors(cp):
         cp.RealPlan((64, 1, 1))  # ny * nz == 1
     with cp.RealPlan((32, 4, 4)) as plan:
         with pytest.raises(cp.CirculantError):
-            plan.set_schedule("three")  # 256^3 only
+            plan.set_schedule("three")  # 128^3 and 256^3 only
         with pytest.raises(cp.CirculantError):
             plan.set_schedule(7)
         assert not plan.three_sweep
