@@ -349,7 +349,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 // NX: x extent (row length in points) of the grid P2 runs on: TN for the complex apply, TN / 2
 // for the real-data plan's half spectrum (cfp_real.hip); y and z are TN long.
-template <int T, int N2, int TN, int PROBE = 0, bool PF = false, int NX = TN>
+template <int T, int N2, int TN, int PROBE = 0, bool PF = false, int NX = TN, int ST = 0>
 __global__ void __launch_bounds__(T * (TN / 16)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
 #ifndef CFP_KEXP
@@ -568,7 +568,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
         if (acc == 1.2345e300) dst[0] = make_cd(acc, 0.0);  // keeps the work live, never true
       } else {
 #pragma unroll
-        for (int m = 0; m < 16; ++m) dst[zs * TZ * m] = cconj(cmul(v[m], w));
+        for (int m = 0; m < 16; ++m) gstore<ST>(dst + zs * TZ * m, cconj(cmul(v[m], w)));  // ST: store policy
       }
     }
     if constexpr (!PF) lds_barrier();  // the next unit's first exchange overwrites LDS
@@ -782,6 +782,11 @@ hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* 
 // solver's Un, Un), plain loads -- with NT loads of the lines it then overwrites, P1's output
 // drops out of the Infinity Cache and P2 takes 143-145 us instead of 128.
 constexpr int kP1Flags = F_NT_LD, kP1InPlaceFlags = 0;
+// P3 store policy: non-temporal.  r03v A/B of all 24 P1 / P2 / P3 cache policies in the apply
+// chain (tools/kexp/tp_chain.hip, profiles/r03v_tp_chain.txt): plain P3 stores 310 us against
+// 314 us there, but +0.3-0.8 % in bench.py and -2 % inside GMRES (0.387 vs 0.379 ms per PCApply),
+// so the measured policy stays.
+constexpr int kP3Flags = F_NT_ST;
 
 template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true>
 static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
@@ -793,7 +798,7 @@ static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipSt
   else if (stage == 0)
     hipLaunchKernelGGL((k_tp_rows<false, kP1Flags, N1, TN, PTS, XS>), dim3(g), blk, 0, s, in, out, a, units);
   else
-    hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST, N1, TN, PTS, XS>), dim3(g), blk, 0, s, in, out, a, units);
+    hipLaunchKernelGGL((k_tp_rows<true, kP3Flags, N1, TN, PTS, XS>), dim3(g), blk, 0, s, in, out, a, units);
 }
 
 template <int T, int N2, int TN, int PER_CU, int PTS = 16, bool XS = true>
