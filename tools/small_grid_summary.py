@@ -80,7 +80,9 @@ def main():
                 if line.startswith("{"):
                     d = json.loads(line)
                     keep = {k: d[k] for k in d if k in ("pc", "gmres_its", "ms_per_solve", "apply_ms", "applies_per_s",
-                                                         "GBps", "frac_hbm", "pass_ms")}
+                                                         "GBps", "frac_hbm", "pass_ms", "pcapply_per_s",
+                                                         "ms_per_apply", "sweeps", "passes_ms",
+                                                         "five_sweep_ms_per_apply")}
                     print("- " + json.dumps(keep))
         print("\n| kernel | calls | mean us |\n|---|---|---|")
         for name, (calls, us) in sorted(st.items(), key=lambda t: -t[1][1] * t[1][0])[:12]:
