@@ -227,6 +227,26 @@ def moved_bytes(passes, N: int) -> int:
     return int(sum(kernel_alg_bytes(p["mode"], N, p["n"]) for p in passes))
 
 
+def event_ms(fn, iters: int, settle_ms: float = 150.0) -> float:
+    """Mean ms of fn() over iters back-to-back calls (HIP events on the current stream) after
+    settle_ms of untimed ones (the clocks ramp between legs, as before the headline's region)."""
+    import torch
+    t0 = time.perf_counter()
+    while True:
+        for _ in range(8):
+            fn()
+        torch.cuda.synchronize()
+        if (time.perf_counter() - t0) * 1e3 >= settle_ms:
+            break
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
 def choose_slab_plan(create, requested, agree, warn=None):
     """Pick the N > 1 exchange.  create(exchange) builds this rank's SlabPlan (raises on
     failure); agree(ok) -> True when every rank's creation succeeded.  RCCL unless the
@@ -288,6 +308,8 @@ def main() -> int:
     ap.add_argument("--settle-ms", type=float, default=300.0,
                     help="untimed applies for this long after the warm-up (clock ramp-up; 0 = off)")
     ap.add_argument("--no-real", action="store_true", help="skip the real-data variant line item")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the other BASELINE configs' line items (128^3, the wave system, 100^3)")
     ap.add_argument("--scaling-grid", type=int, nargs="+", default=[512],
                     help="grid of the scaling_512 line item (BASELINE config 5; 0 = skip)")
     ap.add_argument("--scaling-steps", type=int, default=20)
@@ -552,6 +574,54 @@ def main() -> int:
         except Exception as e:  # unsupported grid or failure: report, never fake
             real_variant = {"error": str(e)}
 
+    # the other single-GPU BASELINE configs, measured after the headline on the same box: config 2
+    # (128^3 complex apply), config 4's block preconditioner (wave system 128^3) and the
+    # reference's default mesh (100^3); each with its own output check
+    other_configs = None
+    if world == 1 and not args.no_configs:
+        other_configs = {}
+        for key, g3 in (("config2_128", [128, 128, 128]), ("reference_mesh_100", [100, 100, 100])):
+            try:
+                with cp.CirculantPlan(g3, device=local_rank) as p3:
+                    p3.set_transport_symbol(LAM)
+                    b3 = torch.empty(g3[0] * g3[1] * g3[2], dtype=torch.complex128, device=dev)
+                    cp.fill_uniform(b3, SEED)
+                    x3 = torch.empty_like(b3)
+                    ms3 = event_ms(lambda: p3.apply(b3, out=x3), 2000)
+                    r3 = transport_residual(b3, x3, g3, LAM, 0, 1, dev)
+                    other_configs[key] = {"value": round(1e3 / ms3, 1), "unit": "PCApply/s",
+                                          "ms_per_apply": round(ms3, 5),
+                                          "schedule": " | ".join(f"{q['axis']}:{q['mode']}" for q in p3.passes()),
+                                          "check": {"residual": r3, "tol": RES_TOL, "ok": r3 < RES_TOL}}
+                    if not r3 < RES_TOL:
+                        check["ok"] = False
+                    del b3, x3
+            except Exception as e:  # report, never fake
+                other_configs[key] = {"error": str(e)}
+        try:
+            from circulantpreconditioner_amd import wave as W
+            wg = (128, 128, 128)
+            wp = W.WavePlan(wg, device=local_rank).set_symbol((0.079, 0.079, 0.079))
+            bw = torch.empty(4 * 128 ** 3, dtype=torch.complex128, device=dev)
+            cp.fill_uniform(bw, SEED)
+            xw = torch.empty_like(bw)
+            msw = event_ms(lambda: wp.apply(bw, out=xw), 1000)
+            sweeps = wp.num_passes()
+            wp.set_schedule("five")
+            x5 = wp.apply(bw)
+            dw = float(torch.linalg.vector_norm(x5 - xw) / torch.linalg.vector_norm(x5))
+            other_configs["config4_wave128"] = {
+                "value": round(1e3 / msw, 1), "unit": "block PCApply/s", "ms_per_apply": round(msw, 5),
+                "sweeps": sweeps, "dtype": "c128, 4 interleaved unknowns per cell",
+                "check": {"what": "rel. difference to the 5-sweep schedule", "value": dw, "ok": dw < 1e-12}}
+            if not dw < 1e-12:
+                check["ok"] = False
+            wp.close()
+            del bw, xw, x5
+        except Exception as e:  # report, never fake
+            other_configs["config4_wave128"] = {"error": str(e)}
+        torch.cuda.empty_cache()
+
     # north_star's scaling curve: the same apply on the 512^3 grid (BASELINE config 5), at every
     # N the driver launches, reported beside the 256^3 headline (strong scaling, whole job)
     scaling = None
@@ -629,6 +699,8 @@ def main() -> int:
         }
         if real_variant is not None:
             out["real_variant"] = real_variant
+        if other_configs is not None:
+            out["other_configs"] = other_configs
         if scaling is not None:
             out["scaling_512"] = scaling
         if passes_info is not None:
