@@ -578,14 +578,7 @@ def main() -> int:
     # (128^3 complex apply), config 4's block preconditioner (wave system 128^3) and the
     # reference's default mesh (100^3); each with its own output check
     other_configs = None
-    released = False
     if world == 1 and not args.no_configs:
-        # the headline's two 268 MB vectors go first: with them still held, the 32 MiB 128^3
-        # buffers measured 17.1k applies/s against 18.4-19.0k in a process of their own
-        plan.close()
-        del plan, b, x, run
-        torch.cuda.empty_cache()
-        released = True
         other_configs = {}
         for key, g3 in (("config2_128", [128, 128, 128]), ("reference_mesh_100", [100, 100, 100])):
             try:
@@ -635,12 +628,11 @@ def main() -> int:
     sg = [int(v) for v in args.scaling_grid]
     sg = sg * 3 if len(sg) == 1 else sg
     if len(sg) == 3 and min(sg) > 0 and sg != grid:
-        if not released:
-            if world > 1:
-                plan.close()  # one library RCCL communicator at a time
-                dist.barrier()
-            del plan, b, x, run
-            torch.cuda.empty_cache()
+        if world > 1:
+            plan.close()  # one library RCCL communicator at a time
+            dist.barrier()
+        del plan, b, x, run
+        torch.cuda.empty_cache()
         try:
             plan, b, x, run, par2 = make(sg)
             k = max(1, args.scaling_steps)

@@ -56,6 +56,34 @@ __device__ __forceinline__ int brev(int j) {
   return N2 == 4 ? ((j & 1) << 1) | (j >> 1) : ((j & 1) << 2) | (j & 2) | (j >> 2);
 }
 
+// (a, b) -> lanes with bit B clear: (a[L], a[L ^ 2^B]); set: (b[L ^ 2^B], b[L])
+template <int B>
+__device__ __forceinline__ void swap32(unsigned& a, unsigned& b) {
+  if constexpr (B == 5) {
+    const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+    a = r[0];
+    b = r[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+    a = r[0];
+    b = r[1];
+  }
+}
+template <int B>
+__device__ __forceinline__ void swap_d(double& a, double& b) {
+  unsigned long long ua = (unsigned long long)__double_as_longlong(a),
+                     ub = (unsigned long long)__double_as_longlong(b);
+  unsigned al = (unsigned)ua, ah = (unsigned)(ua >> 32), bl = (unsigned)ub, bh = (unsigned)(ub >> 32);
+  swap32<B>(al, bl);
+  swap32<B>(ah, bh);
+  a = __longlong_as_double((long long)(((unsigned long long)ah << 32) | al));
+  b = __longlong_as_double((long long)(((unsigned long long)bh << 32) | bl));
+}
+template <int B>
+__device__ __forceinline__ void swap_c(cd& a, cd& b) {
+  swap_d<B>(a.x, b.x);
+  swap_d<B>(a.y, b.y);
+}
 // first radix of an n-point FFT done as r0 x PTS x ... x PTS (n = r0 PTS^k, r0 <= PTS)
 constexpr int r0_of(int n, int pts) { return n > pts ? r0_of(n / pts, pts) : n; }
 
@@ -67,10 +95,19 @@ constexpr int r0_of(int n, int pts) { return n > pts ? r0_of(n / pts, pts) : n; 
 // VGPRs) and still lost, P1 20.7 -> 23.3 us with one workgroup per CU walking two units
 // (profiles/r03m_128_three_sweep.md).  PTS points per thread (16 or 8); XS = the LDS exchanges
 // split into real and imaginary halves (half the footprint, twice the barriers).
-template <bool INV, int FLAGS, int N1, int TN, int PTS = 16, bool XS = true>
+//
+// LP (lane pair, N1 = 2 PTS): the two threads of a column x are lanes L and L + 32 of one wave
+// (x = lane % 32 + 32 wave), so phase A's 32-point DFT is a 16-point DFT per lane (even / odd
+// y1), the twiddle W_32^k on the odd lane, and a radix-2 across lane bit 5 on permlane32 swaps:
+// no LDS exchange and no barrier pair in phase A.  Slot m then holds k1 = m % 8 + 8 ty + 16 (m / 8).
+//
+// TWY: the four-step twiddle W_TN^{y2 k1} rides here (P1: on the y1 DFT's output; P3: on the
+// loaded, conjugated points) instead of in P2 (k_tp_mid_sw<.., TWY = false>).
+template <bool INV, int FLAGS, int N1, int TN, int PTS = 16, bool XS = true, bool LP = false, bool TWY = false>
 __global__ void __launch_bounds__(N1 * (TN / PTS)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
   constexpr int N2 = TN / N1, TR = TN / PTS, NT = N1 * TR, TY = N1 / PTS;
+  static_assert(!LP || (TY == 2 && TN % 32 == 0), "lane pairs: two threads per column, 32 columns per wave");
   constexpr int RS = TN + TN / 16;  // padded row stride of the row-mode LDS layout
   constexpr int F = FLAGS | (XS ? F_SPLIT_LDS : 0) | F_LDS_SYNC;
   __shared__ __attribute__((aligned(16))) double lds[N1 * RS * (XS ? 1 : 2)];  // both layouts fit
@@ -78,7 +115,9 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
                            // which keeps it out of scratch (20 B/lane with the table in LDS)
   const int tid = threadIdx.x;
   for (int i = tid; i < N1; i += NT) tw_l[i] = a.tw[N2 * i];
-  const int x0 = tid % TN, ty0 = tid / TN;  // phase A: column x, thread ty of TY
+  if constexpr (LP) __syncthreads();  // phase A reads tw_l before any barrier
+  // phase A: column x, thread ty of TY
+  const int x0 = LP ? (tid & 31) + 32 * (tid >> 6) : tid % TN, ty0 = LP ? (tid >> 5) & 1 : tid / TN;
   const int r0 = tid / TR, tx0 = tid % TR;  // phase C: row r, thread tx of TR
   // fresh (laundered) index copies at every use, as in k_tp_mid: nothing but the points
   // stays live across an FFT
@@ -116,21 +155,51 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
     if (INV) {
 #pragma unroll
       for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
+      if constexpr (TWY) {  // slot m = row y2 + N2 k1, k1 = ty + TY m
+        const int ty = idx(ty0), y2 = u % N2;
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) v[m] = cmul(v[m], a.tw[(y2 * (ty + TY * m)) & (TN - 1)]);
+      }
     }
-    {
+    const auto k1_of = [](int m, int ty) {
+      return LP ? (m & (PTS / 2 - 1)) + (PTS / 2) * ty + PTS * (m / (PTS / 2)) : ty + TY * m;
+    };
+    if constexpr (LP) {
+      // phase A on lane pairs: E / O = the 16-point DFTs of the even / odd y1 (lanes ty = 0 / 1)
+      dft_reg<PTS>(v);
+      {
+        const int ty = idx(ty0);
+#pragma unroll
+        for (int k = 1; k < PTS; ++k) v[k] = cmul(v[k], tw_l[k * ty]);  // W_32^k on the odd lane
+      }
+      // lane ty = 0 takes (E[k], W^k O[k]), lane ty = 1 (E[k+8], W^(k+8) O[k+8]) -> X[k], X[k+16]
+#pragma unroll
+      for (int k = 0; k < PTS / 2; ++k) swap_c<5>(v[k], v[k + PTS / 2]);
+#pragma unroll
+      for (int k = 0; k < PTS / 2; ++k) {
+        const cd p = v[k], q = v[k + PTS / 2];
+        v[k] = cadd(p, q);
+        v[k + PTS / 2] = csub(p, q);
+      }
+    } else {
       // phase A: N1-point DFT over y1 for every x (column mode, TN columns x TY threads)
       const int x = idx(x0), ty = idx(ty0);
       fft_stages<N1, PTS, r0_of(N1, PTS), false, TN, F>(v, lds, tw_l, x, ty, true);  // v[m]: k1 = ty + TY m
+      lds_barrier();  // phase A's last LDS reads are done
+    }
+    if constexpr (TWY && !INV) {
+      const int ty = idx(ty0), y2 = u % N2;
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) v[m] = cmul(v[m], a.tw[(y2 * k1_of(m, ty)) & (TN - 1)]);
     }
     // phase B: transpose to rows k1, thread (row r, tx) gets x = tx + TR m
-    lds_barrier();  // phase A's last LDS reads are done
     {
       const int x = idx(x0), ty = idx(ty0), r = idx(r0), tx = idx(tx0);
       if constexpr (XS) {
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
 #pragma unroll
-          for (int m = 0; m < PTS; ++m) lds[(ty + TY * m) * RS + x + (x >> 4)] = half ? v[m].y : v[m].x;
+          for (int m = 0; m < PTS; ++m) lds[k1_of(m, ty) * RS + x + (x >> 4)] = half ? v[m].y : v[m].x;
           lds_barrier();
 #pragma unroll
           for (int m = 0; m < PTS; ++m) {
@@ -143,7 +212,7 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
       } else {
         cd* const lc = reinterpret_cast<cd*>(lds);
 #pragma unroll
-        for (int m = 0; m < PTS; ++m) lc[(ty + TY * m) * RS + x + (x >> 4)] = v[m];
+        for (int m = 0; m < PTS; ++m) lc[k1_of(m, ty) * RS + x + (x >> 4)] = v[m];
         lds_barrier();
 #pragma unroll
         for (int m = 0; m < PTS; ++m) {
@@ -277,34 +346,6 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
 // the bit-reversed order back to natural, same register map, so the second exchange lands in
 // the load layout.
 namespace {
-// (a, b) -> lanes with bit B clear: (a[L], a[L ^ 2^B]); set: (b[L ^ 2^B], b[L])
-template <int B>
-__device__ __forceinline__ void swap32(unsigned& a, unsigned& b) {
-  if constexpr (B == 5) {
-    const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
-    a = r[0];
-    b = r[1];
-  } else {
-    const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
-    a = r[0];
-    b = r[1];
-  }
-}
-template <int B>
-__device__ __forceinline__ void swap_d(double& a, double& b) {
-  unsigned long long ua = (unsigned long long)__double_as_longlong(a),
-                     ub = (unsigned long long)__double_as_longlong(b);
-  unsigned al = (unsigned)ua, ah = (unsigned)(ua >> 32), bl = (unsigned)ub, bh = (unsigned)(ub >> 32);
-  swap32<B>(al, bl);
-  swap32<B>(ah, bh);
-  a = __longlong_as_double((long long)(((unsigned long long)ah << 32) | al));
-  b = __longlong_as_double((long long)(((unsigned long long)bh << 32) | bl));
-}
-template <int B>
-__device__ __forceinline__ void swap_c(cd& a, cd& b) {
-  swap_d<B>(a.x, b.x);
-  swap_d<B>(a.y, b.y);
-}
 // partner across lane bit 3 (row_ror:8 inside each 16-lane row)
 __device__ __forceinline__ double ror8_d(double v) {
   const long long b = __double_as_longlong(v);
@@ -349,7 +390,10 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 // NX: x extent (row length in points) of the grid P2 runs on: TN for the complex apply, TN / 2
 // for the real-data plan's half spectrum (cfp_real.hip); y and z are TN long.
-template <int T, int N2, int TN, int PROBE = 0, bool PF = false, int NX = TN, int ST = 0>
+// TWY = false: the four-step twiddle W_TN^{y2 k1} is applied by P1 on its way out and by P3 on its
+// way in (k_tp_rows<.., TWY>), where k1 is a register slot; P2 then skips 32 complex multiplies
+// per lane and unit.
+template <int T, int N2, int TN, int PROBE = 0, bool PF = false, int NX = TN, int ST = 0, bool TWY = true>
 __global__ void __launch_bounds__(T * (TN / 16)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
 #ifndef CFP_KEXP
@@ -447,7 +491,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
         for (int m = 0; m < NPF; ++m) v[m] = fromv(*reinterpret_cast<const dv2*>(lds + (wv * NPF + m) * 128 + 2 * c));
       }
     }
-    {
+    if constexpr (TWY) {
       const int c = idx(c0);
       const cd w = tw_y(u, c);
 #pragma unroll
@@ -568,7 +612,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
         if (acc == 1.2345e300) dst[0] = make_cd(acc, 0.0);  // keeps the work live, never true
       } else {
 #pragma unroll
-        for (int m = 0; m < 16; ++m) gstore<ST>(dst + zs * TZ * m, cconj(cmul(v[m], w)));  // ST: store policy
+        for (int m = 0; m < 16; ++m) gstore<ST>(dst + zs * TZ * m, cconj(TWY ? cmul(v[m], w) : v[m]));  // ST: store policy
       }
     }
     if constexpr (!PF) lds_barrier();  // the next unit's first exchange overwrites LDS
@@ -787,18 +831,26 @@ constexpr int kP1Flags = F_NT_LD, kP1InPlaceFlags = 0;
 // 314 us there, but +0.3-0.8 % in bench.py and -2 % inside GMRES (0.387 vs 0.379 ms per PCApply),
 // so the measured policy stays.
 constexpr int kP3Flags = F_NT_ST;
+// 256^3, N1 = 32 (r03z, tools/kexp/run_tp_lp.py, profiles/r03z_tp_lp.txt, 3-sweep chain):
+// P1 / P3 with the lane-pair phase A (no LDS exchange there): 310.8 -> 303.0 us.  Moving the
+// four-step twiddle W_256^{y2 k1} from the swap P2 kernel into P1 / P3 lost (313.1 us; P1 +9 us
+// for its 16 table loads per thread, P2 -1 us), so the switch stays off.  Every executor (one GPU,
+// slabs, pieces) runs the same pair.
+constexpr bool kRowsLP = true;
+constexpr bool kTwyInRows = false;
 
-template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true>
+template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true, bool LP = false, bool TWY = false>
 static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
   constexpr int units = TN * (TN / N1);  // z-planes x y2
   const unsigned g = grid_of(units, PER_CU);
   const dim3 blk(N1 * (TN / PTS));
   if (stage == 0 && in == out)  // in place (the direct solver's Un, Un)
-    hipLaunchKernelGGL((k_tp_rows<false, kP1InPlaceFlags, N1, TN, PTS, XS>), dim3(g), blk, 0, s, in, out, a, units);
+    hipLaunchKernelGGL((k_tp_rows<false, kP1InPlaceFlags, N1, TN, PTS, XS, LP, TWY>), dim3(g), blk, 0, s, in, out, a,
+                       units);
   else if (stage == 0)
-    hipLaunchKernelGGL((k_tp_rows<false, kP1Flags, N1, TN, PTS, XS>), dim3(g), blk, 0, s, in, out, a, units);
+    hipLaunchKernelGGL((k_tp_rows<false, kP1Flags, N1, TN, PTS, XS, LP, TWY>), dim3(g), blk, 0, s, in, out, a, units);
   else
-    hipLaunchKernelGGL((k_tp_rows<true, kP3Flags, N1, TN, PTS, XS>), dim3(g), blk, 0, s, in, out, a, units);
+    hipLaunchKernelGGL((k_tp_rows<true, kP3Flags, N1, TN, PTS, XS, LP, TWY>), dim3(g), blk, 0, s, in, out, a, units);
 }
 
 template <int T, int N2, int TN, int PER_CU, int PTS = 16, bool XS = true>
@@ -808,11 +860,11 @@ static void launch_mid(cd* data, const TPArgs& a, hipStream_t s) {
                      a, units);
 }
 
-template <int N2, int TN, bool PF = false>
+template <int N2, int TN, bool PF = false, bool TWY = true>
 static void launch_mid_sw(cd* data, const TPArgs& a, hipStream_t s) {
   constexpr int units = (TN / (64 / N2)) * (TN / N2);
-  hipLaunchKernelGGL((k_tp_mid_sw<64, N2, TN, 0, PF>), dim3(grid_of(units, 1)), dim3(64 * (TN / 16)), 0, s, data, a,
-                     units);
+  hipLaunchKernelGGL((k_tp_mid_sw<64, N2, TN, 0, PF, TN, 0, TWY>), dim3(grid_of(units, 1)), dim3(64 * (TN / 16)), 0, s,
+                     data, a, units);
 }
 
 bool three_pass_slab_supported(const i64 n[3], int P) {
@@ -824,17 +876,22 @@ hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs
   if (stage == 1) {
     const int nk1 = a.lnyl ? (1 << a.lnyl) / 8 : 32;  // local k1 values: nyl / N2
     const int units = 32 * nk1;                        // x tiles x local k1
+    constexpr bool TWY = !kTwyInRows;
     if (((uintptr_t)out & 15) == 0)  // the LDS-DMA prefetch needs 16-byte addresses
-      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true>), dim3(grid_of(units, 1)), dim3(1024), 0, s, out, a, units);
+      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true, 256, 0, TWY>), dim3(grid_of(units, 1)), dim3(1024), 0, s,
+                         out, a, units);
     else
-      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, false>), dim3(grid_of(units, 1)), dim3(1024), 0, s, out, a, units);
+      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, false, 256, 0, TWY>), dim3(grid_of(units, 1)), dim3(1024), 0, s,
+                         out, a, units);
   } else {
     const int units = nzl * 8;  // local z-planes x y2
     const unsigned g = grid_of(units, 2);
     if (stage == 0)
-      hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD, 32, 256>), dim3(g), dim3(512), 0, s, in, out, a, units);
+      hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD, 32, 256, 16, true, kRowsLP, kTwyInRows>), dim3(g), dim3(512), 0, s,
+                         in, out, a, units);
     else
-      hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST, 32, 256>), dim3(g), dim3(512), 0, s, in, out, a, units);
+      hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST, 32, 256, 16, true, kRowsLP, kTwyInRows>), dim3(g), dim3(512), 0, s,
+                         in, out, a, units);
   }
   return hipGetLastError();
 }
@@ -871,13 +928,15 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
   // the LDS-DMA prefetch (global_load_lds_dwordx4) takes 16-byte aligned addresses: a buffer that
   // is only 8-byte aligned runs the same kernel without it
   const bool pf_ok = ((uintptr_t)out & 15) == 0;
+  // the swap P2 kernels at N1 = 32 leave the y2 k1 twiddle to P1 / P3 (kTwyInRows)
+  const bool swap = shape.mid == TP_MID_SWAP64 || shape.mid == TP_MID_SWAP64_PF || shape.mid == TP_MID_DEFAULT;
   if (stage == 1) {
     if ((shape.mid == TP_MID_SWAP64_PF || shape.mid == TP_MID_DEFAULT) && pf_ok) {
       if (n1 == 64) launch_mid_sw<4, 256, true>(out, a, s);
-      else launch_mid_sw<8, 256, true>(out, a, s);
-    } else if (shape.mid == TP_MID_SWAP64 || shape.mid == TP_MID_SWAP64_PF || shape.mid == TP_MID_DEFAULT) {
+      else launch_mid_sw<8, 256, true, !kTwyInRows>(out, a, s);
+    } else if (swap) {
       if (n1 == 64) launch_mid_sw<4, 256>(out, a, s);
-      else launch_mid_sw<8, 256>(out, a, s);
+      else launch_mid_sw<8, 256, false, !kTwyInRows>(out, a, s);
     } else if (n1 == 64) {
       if (t32) launch_mid<32, 4, 256, 2>(out, a, s);
       else launch_mid<64, 4, 256, 1>(out, a, s);
@@ -888,8 +947,10 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
     }
   } else if (n1 == 64) {
     launch_rows<64, 256, 1>(stage, in, out, a, s);
+  } else if (swap) {
+    launch_rows<32, 256, 2, 16, true, kRowsLP, kTwyInRows>(stage, in, out, a, s);
   } else {
-    launch_rows<32, 256, 2>(stage, in, out, a, s);
+    launch_rows<32, 256, 2, 16, true, kRowsLP>(stage, in, out, a, s);
   }
   return hipGetLastError();
 }
