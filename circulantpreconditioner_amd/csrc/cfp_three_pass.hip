@@ -361,13 +361,13 @@ __device__ __forceinline__ cd bfly_l3(cd v, double sgn) {
 
 // DIF stage over register pairs (k, k + D) after a swap on lane bit B: a + b, (a - b) w
 // (TW = false: no twiddle)
-template <int B, int D, bool TW = true>
+template <int B, int D, bool TW = true, int NR = 16>
 __device__ __forceinline__ void dif_pairs(cd* v, cd w) {
 #pragma unroll
-  for (int k = 0; k < 16; ++k)
+  for (int k = 0; k < NR; ++k)
     if ((k & D) == 0) swap_c<B>(v[k], v[k + D]);
 #pragma unroll
-  for (int k = 0; k < 16; ++k)
+  for (int k = 0; k < NR; ++k)
     if ((k & D) == 0) {
       const cd a = v[k], b = v[k + D];
       v[k] = cadd(a, b);
@@ -618,6 +618,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
     if constexpr (!PF) lds_barrier();  // the next unit's first exchange overwrites LDS
   }
 }
+
 
 bool three_pass_supported(const i64 n[3]) {
   return n[0] == n[1] && n[1] == n[2] && (n[0] == 128 || n[0] == 256);
