@@ -933,7 +933,7 @@ extern "C" int cfp_dist_plan_profile_begin(cfp_dist_plan_t p, int max_applies, i
   p->prof_stride = 2 * apply_list(p).size();
   p->prof_ev.resize(p->prof_stride * (size_t)max_applies, nullptr);
   for (auto& e : p->prof_ev) {
-    hipError_t r = hipEventCreate(&e);
+    hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
     if (r != hipSuccess) {
       dist_profile_free(p);
       return hip_error(r, "hipEventCreate");
@@ -980,7 +980,7 @@ extern "C" int cfp_dist_plan_time_phases(cfp_dist_plan_t p, const double* b, dou
   const std::vector<Step>& steps = apply_list(p);
   const size_t np = steps.size();
   std::vector<hipEvent_t> ev(2 * np);
-  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  for (auto& e : ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
   std::vector<double> acc(np, 0.0);
   int rc = CFP_SUCCESS;
   for (int it = 0; it < iters && !rc; ++it) {

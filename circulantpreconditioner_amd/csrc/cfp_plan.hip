@@ -765,7 +765,7 @@ extern "C" int cfp_plan_profile_begin(cfp_plan_t p, int max_applies, int every) 
   p->prof_stride = apply_steps(p).size() + 1;
   p->prof_ev.resize(p->prof_stride * (size_t)max_applies, nullptr);
   for (auto& e : p->prof_ev) {
-    hipError_t r = hipEventCreate(&e);
+    hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
     if (r != hipSuccess) {
       profile_free(p);
       return hip_error(r, "hipEventCreate");
@@ -957,7 +957,7 @@ extern "C" int cfp_plan_time_passes(cfp_plan_t p, const double* b, double* x, in
   const size_t np = apply_steps(p).size();
   std::vector<double> acc(np, 0.0);
   std::vector<hipEvent_t> ev(np + 1);
-  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  for (auto& e : ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
   int rc = CFP_SUCCESS;
   for (int it = 0; it < iters && rc == CFP_SUCCESS; ++it) {
     rc = run_apply(p, nullptr, (const cd*)b, (cd*)x, s, &ev);

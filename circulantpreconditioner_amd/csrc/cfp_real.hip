@@ -353,7 +353,7 @@ extern "C" int cfp_rplan_time_passes(cfp_rplan_t p, const double* b, double* x, 
   RGuard g(p->device);
   hipStream_t s = (hipStream_t)stream;
   std::vector<hipEvent_t> ev(5);
-  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  for (auto& e : ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
   double acc[4] = {0, 0, 0, 0};
   int rc = CFP_SUCCESS;
   for (int it = 0; it < iters && rc == CFP_SUCCESS; ++it) {

@@ -295,7 +295,7 @@ extern "C" int cfp_wave_plan_time_passes(cfp_wave_plan_t p, const double* b, dou
   const size_t np = wave_steps(p).size();
   std::vector<double> acc(np, 0.0);
   std::vector<hipEvent_t> ev(np + 1);
-  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  for (auto& e : ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
   int rc = CFP_SUCCESS;
   for (int it = 0; it < iters && rc == CFP_SUCCESS; ++it) {
     rc = run_wave(p, (const cd*)b, (cd*)x, s, &ev);

@@ -151,7 +151,7 @@ extern "C" PetscErrorCode KSPDestroy(KSP* pk) {
 static bool grow_events(KSP k) {
   for (int i = 0; i < 64; ++i) {
     hipEvent_t e;
-    if (hipEventCreate(&e) != hipSuccess) {
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) {
       hipGetLastError();
       return false;
     }
