@@ -12,6 +12,16 @@ namespace cfp {
 typedef double2 cd;
 typedef long long i64;
 
+// Per-launch profiling of the apply (cfp_plan_profile_begin / cfp_plan_time_passes): while
+// `start` is set, the 3-sweep launch sites (cfp_three_pass.hip) stamp their dispatch itself with
+// hipExtLaunchKernel's start / stop events, i.e. the kernel's own execution as rocprofv3 sees
+// it.  Separate event packets between back-to-back kernels leave the device idle for ~4-5 us
+// each, which inflated every measured pass by that much (profiles/r03z_256_kernel_stats.md).
+struct LaunchStamp {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+extern thread_local LaunchStamp g_stamp;
+
 // How the points of one FFT column are addressed on one side (input or output) of an
 // axis pass.  Column g (0 <= g < ncols) starts at
 //     base(g) = (g % inner_n) * inner_stride + (g / inner_n) * outer_stride

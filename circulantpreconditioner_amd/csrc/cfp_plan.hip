@@ -161,6 +161,10 @@ struct cfp_plan_s {
   size_t prof_every = 1, prof_calls = 0;  // record every prof_every-th apply (sampling)
 };
 
+namespace cfp {
+thread_local LaunchStamp g_stamp;  // cfp_internal.h
+}  // namespace cfp
+
 namespace {
 
 struct DeviceGuard {
@@ -372,6 +376,8 @@ int step_mode(const cfp_plan_s* p, const Step& q, bool diag_override) {
   return (diag_override || p->sym_kind == 2) ? PASS_FUSED_DIAG : PASS_FUSED_SEP;
 }
 
+// ev (profiling): 2 events per step, (*ev)[2 i] / [2 i + 1] = start / end of step i -- the 3-sweep
+// kernels' own dispatch stamps, else events recorded around the step's launches
 int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStream_t s, std::vector<hipEvent_t>* ev) {
   if (!diag_override && p->sym_kind == 0)
     return set_error(CFP_ERR_ARG_WRONGSTATE, "no symbol set on plan (call cfp_plan_set_symbol_* first)");
@@ -388,8 +394,9 @@ int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStr
       a.colsym = p->colsym;
       a.axsym = p->axsym;
       a.scale = q.scale ? invN : 1.0;
-      if (ev) HIPCHK(hipEventRecord((*ev)[i], s));
+      if (ev) g_stamp = LaunchStamp{(*ev)[2 * i], (*ev)[2 * i + 1]};  // one kernel: stamp its dispatch
       hipError_t e = launch_three_pass(q.tp, tn, q.from_b ? b : x, x, a, p->tp_shape, s);
+      g_stamp = LaunchStamp{};
       if (e != hipSuccess) return hip_error(e, "3-sweep launch");
       continue;
     }
@@ -397,17 +404,19 @@ int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStr
       const int pn = (int)p->n[0];
       int prc = ensure_tw(p, pn);
       if (prc) return prc;
-      if (ev) HIPCHK(hipEventRecord((*ev)[i], s));
+      if (ev) HIPCHK(hipEventRecord((*ev)[2 * i], s));
       hipError_t e = launch_plane_pass(q.mode == PASS_PLANE_INV, pn, p->n[2], q.from_b ? b : x, x, p->tw[pn],
                                        q.scale ? invN : 1.0, s);
       if (e != hipSuccess) return hip_error(e, "plane pass launch");
+      if (ev) HIPCHK(hipEventRecord((*ev)[2 * i + 1], s));
       continue;
     }
     if (q.sub == 3) {
-      if (ev) HIPCHK(hipEventRecord((*ev)[i], s));
+      if (ev) HIPCHK(hipEventRecord((*ev)[2 * i], s));
       hipError_t e = launch_sym_divide_positions(x, p->possym[0], p->possym[1], p->possym[2], p->n[0], p->n[1],
                                                  p->n[2], s);
       if (e != hipSuccess) return hip_error(e, "symbol divide");
+      if (ev) HIPCHK(hipEventRecord((*ev)[2 * i + 1], s));
       continue;
     }
     i64 off = 0;
@@ -415,11 +424,11 @@ int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStr
     if (diag_override) d.diag = diag_override;
     int rc = ensure_tw(p, d.n);
     if (rc) return rc;
-    if (ev) HIPCHK(hipEventRecord((*ev)[i], s));
+    if (ev) HIPCHK(hipEventRecord((*ev)[2 * i], s));
     hipError_t e = launch_axis_pass(d, (q.from_b ? b : x) + off, x + off, p->tw[d.n], s);
     if (e != hipSuccess) return hip_error(e, "axis pass launch");
+    if (ev) HIPCHK(hipEventRecord((*ev)[2 * i + 1], s));
   }
-  if (ev) HIPCHK(hipEventRecord((*ev)[st.size()], s));
   return CFP_SUCCESS;
 }
 
@@ -737,7 +746,7 @@ extern "C" int cfp_plan_apply(cfp_plan_t p, const double* b, double* x, void* st
   DeviceGuard dg(p->device);
   // profiling: this apply's own event slot (skipped if the schedule changed since begin)
   const bool sample = p->prof_cap && (p->prof_calls++ % p->prof_every) == 0;
-  if (sample && p->prof_used < p->prof_cap && apply_steps(p).size() + 1 == p->prof_stride) {
+  if (sample && p->prof_used < p->prof_cap && 2 * apply_steps(p).size() == p->prof_stride) {
     std::vector<hipEvent_t> ev(p->prof_ev.begin() + (long)(p->prof_used * p->prof_stride),
                                p->prof_ev.begin() + (long)((p->prof_used + 1) * p->prof_stride));
     ++p->prof_used;
@@ -762,7 +771,7 @@ extern "C" int cfp_plan_profile_begin(cfp_plan_t p, int max_applies, int every) 
   if (every < 1) return set_error(CFP_ERR_ARG_OUTOFRANGE, "every must be >= 1");
   DeviceGuard dg(p->device);
   profile_free(p);
-  p->prof_stride = apply_steps(p).size() + 1;
+  p->prof_stride = 2 * apply_steps(p).size();
   p->prof_ev.resize(p->prof_stride * (size_t)max_applies, nullptr);
   for (auto& e : p->prof_ev) {
     hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
@@ -784,7 +793,7 @@ extern "C" int cfp_plan_profile_end(cfp_plan_t p, double* ms_out, int* applies) 
   if (!p || !ms_out || !applies) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
   if (!p->prof_cap) return set_error(CFP_ERR_ARG_WRONGSTATE, "profiling was not started");
   DeviceGuard dg(p->device);
-  const size_t np = p->prof_stride - 1, used = p->prof_used;
+  const size_t np = p->prof_stride / 2, used = p->prof_used;
   std::vector<double> acc(np, 0.0);
   int rc = CFP_SUCCESS;
   if (used > 0) {
@@ -794,7 +803,7 @@ extern "C" int cfp_plan_profile_end(cfp_plan_t p, double* ms_out, int* applies) 
   for (size_t a = 0; a < used && !rc; ++a)
     for (size_t i = 0; i < np; ++i) {
       float ms = 0.f;
-      hipEventElapsedTime(&ms, p->prof_ev[a * p->prof_stride + i], p->prof_ev[a * p->prof_stride + i + 1]);
+      hipEventElapsedTime(&ms, p->prof_ev[a * p->prof_stride + 2 * i], p->prof_ev[a * p->prof_stride + 2 * i + 1]);
       acc[i] += ms;
     }
   for (size_t i = 0; i < np; ++i) ms_out[i] = used ? acc[i] / (double)used : 0.0;
@@ -956,17 +965,17 @@ extern "C" int cfp_plan_time_passes(cfp_plan_t p, const double* b, double* x, in
   hipStream_t s = (hipStream_t)stream;
   const size_t np = apply_steps(p).size();
   std::vector<double> acc(np, 0.0);
-  std::vector<hipEvent_t> ev(np + 1);
+  std::vector<hipEvent_t> ev(2 * np);
   for (auto& e : ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
   int rc = CFP_SUCCESS;
   for (int it = 0; it < iters && rc == CFP_SUCCESS; ++it) {
     rc = run_apply(p, nullptr, (const cd*)b, (cd*)x, s, &ev);
     if (rc) break;
-    hipError_t e = hipEventSynchronize(ev[np]);
+    hipError_t e = hipEventSynchronize(ev[2 * np - 1]);
     if (e != hipSuccess) { rc = hip_error(e, "event sync"); break; }
     for (size_t i = 0; i < np; ++i) {
       float ms = 0.f;
-      hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+      hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]);
       acc[i] += ms;
     }
   }

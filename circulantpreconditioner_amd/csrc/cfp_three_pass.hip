@@ -24,6 +24,17 @@
 #include "cfp_lane.h"
 #include "cfp_three_pass.h"
 
+#include <hip/hip_ext.h>
+
+// a launch that stamps its own dispatch while per-launch profiling is on (cfp_internal.h)
+#define TP_LAUNCH(K, G, B, S, ...)                                                                    \
+  do {                                                                                                \
+    if (g_stamp.start)                                                                                \
+      hipExtLaunchKernelGGL(K, G, B, 0, S, g_stamp.start, g_stamp.stop, 0, __VA_ARGS__);              \
+    else                                                                                              \
+      hipLaunchKernelGGL(K, G, B, 0, S, __VA_ARGS__);                                                 \
+  } while (0)
+
 namespace cfp {
 
 namespace {
@@ -846,26 +857,24 @@ static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipSt
   const unsigned g = grid_of(units, PER_CU);
   const dim3 blk(N1 * (TN / PTS));
   if (stage == 0 && in == out)  // in place (the direct solver's Un, Un)
-    hipLaunchKernelGGL((k_tp_rows<false, kP1InPlaceFlags, N1, TN, PTS, XS, LP, TWY>), dim3(g), blk, 0, s, in, out, a,
-                       units);
+    TP_LAUNCH((k_tp_rows<false, kP1InPlaceFlags, N1, TN, PTS, XS, LP, TWY>), dim3(g), blk, s, in, out, a, units);
   else if (stage == 0)
-    hipLaunchKernelGGL((k_tp_rows<false, kP1Flags, N1, TN, PTS, XS, LP, TWY>), dim3(g), blk, 0, s, in, out, a, units);
+    TP_LAUNCH((k_tp_rows<false, kP1Flags, N1, TN, PTS, XS, LP, TWY>), dim3(g), blk, s, in, out, a, units);
   else
-    hipLaunchKernelGGL((k_tp_rows<true, kP3Flags, N1, TN, PTS, XS, LP, TWY>), dim3(g), blk, 0, s, in, out, a, units);
+    TP_LAUNCH((k_tp_rows<true, kP3Flags, N1, TN, PTS, XS, LP, TWY>), dim3(g), blk, s, in, out, a, units);
 }
 
 template <int T, int N2, int TN, int PER_CU, int PTS = 16, bool XS = true>
 static void launch_mid(cd* data, const TPArgs& a, hipStream_t s) {
   constexpr int units = (TN / (T / N2)) * (TN / N2);  // x-tiles x k1
-  hipLaunchKernelGGL((k_tp_mid<0, T, N2, TN, PTS, XS>), dim3(grid_of(units, PER_CU)), dim3(T * (TN / PTS)), 0, s, data,
-                     a, units);
+  TP_LAUNCH((k_tp_mid<0, T, N2, TN, PTS, XS>), dim3(grid_of(units, PER_CU)), dim3(T * (TN / PTS)), s, data, a, units);
 }
 
 template <int N2, int TN, bool PF = false, bool TWY = true>
 static void launch_mid_sw(cd* data, const TPArgs& a, hipStream_t s) {
   constexpr int units = (TN / (64 / N2)) * (TN / N2);
-  hipLaunchKernelGGL((k_tp_mid_sw<64, N2, TN, 0, PF, TN, 0, TWY>), dim3(grid_of(units, 1)), dim3(64 * (TN / 16)), 0, s,
-                     data, a, units);
+  TP_LAUNCH((k_tp_mid_sw<64, N2, TN, 0, PF, TN, 0, TWY>), dim3(grid_of(units, 1)), dim3(64 * (TN / 16)), s, data, a,
+            units);
 }
 
 bool three_pass_slab_supported(const i64 n[3], int P) {
