@@ -111,10 +111,7 @@ constexpr int r0_of(int n, int pts) { return n > pts ? r0_of(n / pts, pts) : n; 
 // (x = lane % 32 + 32 wave), so phase A's 32-point DFT is a 16-point DFT per lane (even / odd
 // y1), the twiddle W_32^k on the odd lane, and a radix-2 across lane bit 5 on permlane32 swaps:
 // no LDS exchange and no barrier pair in phase A.  Slot m then holds k1 = m % 8 + 8 ty + 16 (m / 8).
-//
-// TWY: the four-step twiddle W_TN^{y2 k1} rides here (P1: on the y1 DFT's output; P3: on the
-// loaded, conjugated points) instead of in P2 (k_tp_mid_sw<.., TWY = false>).
-template <bool INV, int FLAGS, int N1, int TN, int PTS = 16, bool XS = true, bool LP = false, bool TWY = false>
+template <bool INV, int FLAGS, int N1, int TN, int PTS = 16, bool XS = true, bool LP = false>
 __global__ void __launch_bounds__(N1 * (TN / PTS)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
   constexpr int N2 = TN / N1, TR = TN / PTS, NT = N1 * TR, TY = N1 / PTS;
@@ -166,11 +163,6 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
     if (INV) {
 #pragma unroll
       for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
-      if constexpr (TWY) {  // slot m = row y2 + N2 k1, k1 = ty + TY m
-        const int ty = idx(ty0), y2 = u % N2;
-#pragma unroll
-        for (int m = 0; m < PTS; ++m) v[m] = cmul(v[m], a.tw[(y2 * (ty + TY * m)) & (TN - 1)]);
-      }
     }
     const auto k1_of = [](int m, int ty) {
       return LP ? (m & (PTS / 2 - 1)) + (PTS / 2) * ty + PTS * (m / (PTS / 2)) : ty + TY * m;
@@ -197,11 +189,6 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
       const int x = idx(x0), ty = idx(ty0);
       fft_stages<N1, PTS, r0_of(N1, PTS), false, TN, F>(v, lds, tw_l, x, ty, true);  // v[m]: k1 = ty + TY m
       lds_barrier();  // phase A's last LDS reads are done
-    }
-    if constexpr (TWY && !INV) {
-      const int ty = idx(ty0), y2 = u % N2;
-#pragma unroll
-      for (int m = 0; m < PTS; ++m) v[m] = cmul(v[m], a.tw[(y2 * k1_of(m, ty)) & (TN - 1)]);
     }
     // phase B: transpose to rows k1, thread (row r, tx) gets x = tx + TR m
     {
@@ -401,10 +388,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 // NX: x extent (row length in points) of the grid P2 runs on: TN for the complex apply, TN / 2
 // for the real-data plan's half spectrum (cfp_real.hip); y and z are TN long.
-// TWY = false: the four-step twiddle W_TN^{y2 k1} is applied by P1 on its way out and by P3 on its
-// way in (k_tp_rows<.., TWY>), where k1 is a register slot; P2 then skips 32 complex multiplies
-// per lane and unit.
-template <int T, int N2, int TN, int PROBE = 0, bool PF = false, int NX = TN, int ST = 0, bool TWY = true>
+template <int T, int N2, int TN, int PROBE = 0, bool PF = false, int NX = TN, int ST = 0>
 __global__ void __launch_bounds__(T * (TN / 16)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
 #ifndef CFP_KEXP
@@ -502,7 +486,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
         for (int m = 0; m < NPF; ++m) v[m] = fromv(*reinterpret_cast<const dv2*>(lds + (wv * NPF + m) * 128 + 2 * c));
       }
     }
-    if constexpr (TWY) {
+    {
       const int c = idx(c0);
       const cd w = tw_y(u, c);
 #pragma unroll
@@ -623,7 +607,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
         if (acc == 1.2345e300) dst[0] = make_cd(acc, 0.0);  // keeps the work live, never true
       } else {
 #pragma unroll
-        for (int m = 0; m < 16; ++m) gstore<ST>(dst + zs * TZ * m, cconj(TWY ? cmul(v[m], w) : v[m]));  // ST: store policy
+        for (int m = 0; m < 16; ++m) gstore<ST>(dst + zs * TZ * m, cconj(cmul(v[m], w)));  // ST: store policy
       }
     }
     if constexpr (!PF) lds_barrier();  // the next unit's first exchange overwrites LDS
@@ -844,24 +828,22 @@ constexpr int kP1Flags = F_NT_LD, kP1InPlaceFlags = 0;
 // so the measured policy stays.
 constexpr int kP3Flags = F_NT_ST;
 // 256^3, N1 = 32 (r03z, tools/kexp/run_tp_lp.py, profiles/r03z_tp_lp.txt, 3-sweep chain):
-// P1 / P3 with the lane-pair phase A (no LDS exchange there): 310.8 -> 303.0 us.  Moving the
-// four-step twiddle W_256^{y2 k1} from the swap P2 kernel into P1 / P3 lost (313.1 us; P1 +9 us
-// for its 16 table loads per thread, P2 -1 us), so the switch stays off.  Every executor (one GPU,
-// slabs, pieces) runs the same pair.
+// P1 / P3 with the lane-pair phase A (no LDS exchange there): 310.8 -> 303.0 us.  Every executor
+// (one GPU, slabs, pieces) runs it.  (Moving the four-step twiddle W_256^{y2 k1} from P2 into
+// P1 / P3 lost: 313.1 us, P1 +9 us for its table loads, P2 -1 us; DESIGN.md.)
 constexpr bool kRowsLP = true;
-constexpr bool kTwyInRows = false;
 
-template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true, bool LP = false, bool TWY = false>
+template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true, bool LP = false>
 static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
   constexpr int units = TN * (TN / N1);  // z-planes x y2
   const unsigned g = grid_of(units, PER_CU);
   const dim3 blk(N1 * (TN / PTS));
   if (stage == 0 && in == out)  // in place (the direct solver's Un, Un)
-    TP_LAUNCH((k_tp_rows<false, kP1InPlaceFlags, N1, TN, PTS, XS, LP, TWY>), dim3(g), blk, s, in, out, a, units);
+    TP_LAUNCH((k_tp_rows<false, kP1InPlaceFlags, N1, TN, PTS, XS, LP>), dim3(g), blk, s, in, out, a, units);
   else if (stage == 0)
-    TP_LAUNCH((k_tp_rows<false, kP1Flags, N1, TN, PTS, XS, LP, TWY>), dim3(g), blk, s, in, out, a, units);
+    TP_LAUNCH((k_tp_rows<false, kP1Flags, N1, TN, PTS, XS, LP>), dim3(g), blk, s, in, out, a, units);
   else
-    TP_LAUNCH((k_tp_rows<true, kP3Flags, N1, TN, PTS, XS, LP, TWY>), dim3(g), blk, s, in, out, a, units);
+    TP_LAUNCH((k_tp_rows<true, kP3Flags, N1, TN, PTS, XS, LP>), dim3(g), blk, s, in, out, a, units);
 }
 
 template <int T, int N2, int TN, int PER_CU, int PTS = 16, bool XS = true>
@@ -870,10 +852,10 @@ static void launch_mid(cd* data, const TPArgs& a, hipStream_t s) {
   TP_LAUNCH((k_tp_mid<0, T, N2, TN, PTS, XS>), dim3(grid_of(units, PER_CU)), dim3(T * (TN / PTS)), s, data, a, units);
 }
 
-template <int N2, int TN, bool PF = false, bool TWY = true>
+template <int N2, int TN, bool PF = false>
 static void launch_mid_sw(cd* data, const TPArgs& a, hipStream_t s) {
   constexpr int units = (TN / (64 / N2)) * (TN / N2);
-  TP_LAUNCH((k_tp_mid_sw<64, N2, TN, 0, PF, TN, 0, TWY>), dim3(grid_of(units, 1)), dim3(64 * (TN / 16)), s, data, a,
+  TP_LAUNCH((k_tp_mid_sw<64, N2, TN, 0, PF>), dim3(grid_of(units, 1)), dim3(64 * (TN / 16)), s, data, a,
             units);
 }
 
@@ -886,21 +868,20 @@ hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs
   if (stage == 1) {
     const int nk1 = a.lnyl ? (1 << a.lnyl) / 8 : 32;  // local k1 values: nyl / N2
     const int units = 32 * nk1;                        // x tiles x local k1
-    constexpr bool TWY = !kTwyInRows;
     if (((uintptr_t)out & 15) == 0)  // the LDS-DMA prefetch needs 16-byte addresses
-      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true, 256, 0, TWY>), dim3(grid_of(units, 1)), dim3(1024), 0, s,
+      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true>), dim3(grid_of(units, 1)), dim3(1024), 0, s,
                          out, a, units);
     else
-      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, false, 256, 0, TWY>), dim3(grid_of(units, 1)), dim3(1024), 0, s,
+      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, false>), dim3(grid_of(units, 1)), dim3(1024), 0, s,
                          out, a, units);
   } else {
     const int units = nzl * 8;  // local z-planes x y2
     const unsigned g = grid_of(units, 2);
     if (stage == 0)
-      hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD, 32, 256, 16, true, kRowsLP, kTwyInRows>), dim3(g), dim3(512), 0, s,
+      hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD, 32, 256, 16, true, kRowsLP>), dim3(g), dim3(512), 0, s,
                          in, out, a, units);
     else
-      hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST, 32, 256, 16, true, kRowsLP, kTwyInRows>), dim3(g), dim3(512), 0, s,
+      hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST, 32, 256, 16, true, kRowsLP>), dim3(g), dim3(512), 0, s,
                          in, out, a, units);
   }
   return hipGetLastError();
@@ -938,15 +919,13 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
   // the LDS-DMA prefetch (global_load_lds_dwordx4) takes 16-byte aligned addresses: a buffer that
   // is only 8-byte aligned runs the same kernel without it
   const bool pf_ok = ((uintptr_t)out & 15) == 0;
-  // the swap P2 kernels at N1 = 32 leave the y2 k1 twiddle to P1 / P3 (kTwyInRows)
-  const bool swap = shape.mid == TP_MID_SWAP64 || shape.mid == TP_MID_SWAP64_PF || shape.mid == TP_MID_DEFAULT;
   if (stage == 1) {
     if ((shape.mid == TP_MID_SWAP64_PF || shape.mid == TP_MID_DEFAULT) && pf_ok) {
       if (n1 == 64) launch_mid_sw<4, 256, true>(out, a, s);
-      else launch_mid_sw<8, 256, true, !kTwyInRows>(out, a, s);
-    } else if (swap) {
+      else launch_mid_sw<8, 256, true>(out, a, s);
+    } else if (shape.mid == TP_MID_SWAP64 || shape.mid == TP_MID_SWAP64_PF || shape.mid == TP_MID_DEFAULT) {
       if (n1 == 64) launch_mid_sw<4, 256>(out, a, s);
-      else launch_mid_sw<8, 256, false, !kTwyInRows>(out, a, s);
+      else launch_mid_sw<8, 256>(out, a, s);
     } else if (n1 == 64) {
       if (t32) launch_mid<32, 4, 256, 2>(out, a, s);
       else launch_mid<64, 4, 256, 1>(out, a, s);
@@ -957,8 +936,6 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
     }
   } else if (n1 == 64) {
     launch_rows<64, 256, 1>(stage, in, out, a, s);
-  } else if (swap) {
-    launch_rows<32, 256, 2, 16, true, kRowsLP, kTwyInRows>(stage, in, out, a, s);
   } else {
     launch_rows<32, 256, 2, 16, true, kRowsLP>(stage, in, out, a, s);
   }

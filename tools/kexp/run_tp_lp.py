@@ -16,7 +16,7 @@ x = torch.empty_like(b)
 tw = torch.from_numpy(np.exp(-2j * np.pi * np.arange(n) / n)).to("cuda")
 cs = torch.full((n * n,), 0.5 + 0.1j, dtype=torch.complex128, device="cuda")
 ax = torch.full((n,), 0.25, dtype=torch.complex128, device="cuda")
-cases = {"lds phase A (product)": 0, "lane-pair phase A": 64, "lane pair + twiddle in P1/P3": 128 + 64}
+cases = {"lds phase A": 0, "lane-pair phase A (product)": 64}
 outs = {}
 for name, c in cases.items():
     ms = ctypes.c_float()
@@ -24,7 +24,7 @@ for name, c in cases.items():
                       ctypes.byref(ms)) == 0
     torch.cuda.synchronize()
     outs[name] = x.clone()
-ref = outs["lds phase A (product)"]
+ref = outs["lds phase A"]
 for name, o in outs.items():
     print(f"{name:30s} max |x - x_product| / max |x_product| = {float((o - ref).abs().max() / ref.abs().max()):.3e}", flush=True)
 res = {c: [] for c in cases.values()}

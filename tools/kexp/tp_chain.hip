@@ -4,7 +4,8 @@
 //   p1: 0 NT loads (product), 1 plain, 2 NT loads + NT stores, 3 NT stores
 //   p2: 0 plain stores (product), 1 NT stores
 //   p3: 0 NT stores (product), 1 NT loads + NT stores, 2 plain
-//   + 64: P1 and P3 with the lane-pair phase A; + 128: and the y2 k1 twiddle moved from P2 to P1 / P3
+//   + 64: P1 and P3 with the lane-pair phase A
+//   (+ 128, the y2 k1 twiddle moved from P2 to P1 / P3, was measured in r03z and removed)
 //   + 256 * w: P2 = k_tp_mid_w8 (8 waves, 32 points per thread), w = 1: no register prefetch, 2: 8 slots, 3: 16
 #define CFP_KEXP 1
 #include "cfp_three_pass.hip"
@@ -264,21 +265,16 @@ k_tp_mid_w8(cd* data, TPArgs a, int nunits) {
 using namespace cfp;
 
 static bool g_lp = false;  // which bit 6: P1 / P3 with the lane-pair phase A (k_tp_rows<.., LP>)
-static bool g_twy = false;  // which bit 7: the y2 k1 twiddle in P1 / P3 (k_tp_rows<.., TWY>), not in P2
 template <int F>
 static void p1(const cd* b, cd* x, const TPArgs& a) {
-  if (g_twy)
-    hipLaunchKernelGGL((k_tp_rows<false, F, 32, 256, 16, true, true, true>), dim3(512), dim3(512), 0, 0, b, x, a, 2048);
-  else if (g_lp)
+  if (g_lp)
     hipLaunchKernelGGL((k_tp_rows<false, F, 32, 256, 16, true, true>), dim3(512), dim3(512), 0, 0, b, x, a, 2048);
   else
     hipLaunchKernelGGL((k_tp_rows<false, F, 32, 256>), dim3(512), dim3(512), 0, 0, b, x, a, 2048);
 }
 template <int F>
 static void p3(cd* x, const TPArgs& a) {
-  if (g_twy)
-    hipLaunchKernelGGL((k_tp_rows<true, F, 32, 256, 16, true, true, true>), dim3(512), dim3(512), 0, 0, x, x, a, 2048);
-  else if (g_lp)
+  if (g_lp)
     hipLaunchKernelGGL((k_tp_rows<true, F, 32, 256, 16, true, true>), dim3(512), dim3(512), 0, 0, x, x, a, 2048);
   else
     hipLaunchKernelGGL((k_tp_rows<true, F, 32, 256>), dim3(512), dim3(512), 0, 0, x, x, a, 2048);
@@ -292,8 +288,6 @@ static void p2(cd* x, const TPArgs& a) {
     hipLaunchKernelGGL((k_tp_mid_w8<true, 8>), dim3(256), dim3(512), 0, 0, x, a, 1024);
   else if (g_w8 == 3)
     hipLaunchKernelGGL((k_tp_mid_w8<true, 16>), dim3(256), dim3(512), 0, 0, x, a, 1024);
-  else if (g_twy)
-    hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true, 256, ST, false>), dim3(256), dim3(1024), 0, 0, x, a, 1024);
   else
     hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true, 256, ST>), dim3(256), dim3(1024), 0, 0, x, a, 1024);
 }
@@ -307,7 +301,6 @@ extern "C" int tp_chain(int which, const void* b, void* x, const void* tw, const
   a.scale = 1.0 / (256.0 * 256.0 * 256.0);
   const int q1 = which & 3, q2 = (which >> 2) & 3, q3 = (which >> 4) & 3;
   g_lp = (which >> 6) & 1;
-  g_twy = (which >> 7) & 1;
   g_w8 = (which >> 8) & 3;
   const cd* bb = (const cd*)b;
   cd* xx = (cd*)x;
