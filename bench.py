@@ -469,8 +469,9 @@ def main() -> int:
         passes_info = plan.passes()
         if timed_region_ms is not None:
             ms = timed_region_ms
-            timing_src = (f"HIP events around every launch of {live_applies} of the {args.steps} timed applies "
-                          f"(every {max(1, args.event_every)}th, launch stream)")
+            timing_src = (f"start / stop HIP events of every launch in {live_applies} of the {args.steps} timed "
+                          f"applies (every {max(1, args.event_every)}th; the 3-sweep kernels stamp their own "
+                          f"dispatch, hipExtLaunchKernelGGL; launch stream)")
         else:
             ms = plan.time_passes(b, x, iters=max(10, min(50, args.steps)))
             timing_src = "HIP events, separate applies after the timed region (launch stream)"
