@@ -147,7 +147,10 @@ struct cfp_rplan_s {
   cd* Q = nullptr;
   cd* twn = nullptr;  // W_nx
   bool has_sym = false;
-  hipStream_t side = nullptr;  // the Nyquist grid's passes overlap the half-spectrum passes
+  // the Nyquist grid's passes overlap the half-spectrum passes (5-pass schedule only; created on
+  // first use: a process holding an extra stream ran the 128^3 apply on the default stream 9 %
+  // slower afterwards, 17.1k against 18.8k applies/s in bench.py, r03z)
+  hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
   // 3-sweep schedule at 128^3 / 256^3 (cfp_three_pass.hip): separable symbol of the half spectrum
   int schedule = CFP_RSCHEDULE_AUTO;
@@ -230,6 +233,11 @@ int run_real(cfp_rplan_s* p, const double* b, double* x, hipStream_t s, std::vec
     CFPCHK(cfp_plan_apply(p->nyq, (const double*)p->Q, (double*)p->Q, s));
     if (ev) HIPCHK(hipEventRecord((*ev)[3], s));
   } else {  // Nyquist grid on the side stream, concurrently with the half spectrum
+    if (!p->side) {  // created on first use: the 3-sweep grids never need it
+      HIPCHK(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&p->fork, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&p->join, hipEventDisableTiming));
+    }
     HIPCHK(hipEventRecord(p->fork, s));
     HIPCHK(hipStreamWaitEvent(p->side, p->fork, 0));
     CFPCHK(cfp_plan_apply(p->nyq, (const double*)p->Q, (double*)p->Q, p->side));
@@ -272,9 +280,6 @@ extern "C" int cfp_rplan_create(cfp_rplan_t* plan, int64_t nx, int64_t ny, int64
   if (e == hipSuccess) e = hipMalloc(&p->Q, sizeof(cd) * (size_t)(ny * nz));
   if (e == hipSuccess) e = hipMalloc(&p->twn, sizeof(cd) * (size_t)nx);
   if (e == hipSuccess) e = hipMemcpy(p->twn, tw.data(), sizeof(cd) * (size_t)nx, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&p->fork, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&p->join, hipEventDisableTiming);
   if (e != hipSuccess) {
     free_rplan(p);
     return hip_error(e, "real plan buffers");
