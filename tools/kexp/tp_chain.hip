@@ -9,6 +9,9 @@
 //   + 256 * w: P2 = k_tp_mid_w8 (8 waves, 32 points per thread), w = 1: no register prefetch, 2: 8 slots, 3: 16
 #define CFP_KEXP 1
 #include "cfp_three_pass.hip"
+namespace cfp {
+thread_local LaunchStamp g_stamp;  // defined in cfp_plan.hip in the library
+}  // namespace cfp
 
 namespace cfp {
 

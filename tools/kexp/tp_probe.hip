@@ -7,6 +7,9 @@
 //   which += 1000: one workgroup per unit instead of the persistent grid
 #define CFP_KEXP 1
 #include "cfp_three_pass.hip"
+namespace cfp {
+thread_local LaunchStamp g_stamp;  // defined in cfp_plan.hip in the library
+}  // namespace cfp
 
 using namespace cfp;
 
