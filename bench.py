@@ -552,17 +552,9 @@ def main() -> int:
             rp = cp.RealPlan(grid, device=local_rank).set_transport_symbol([float(v) for v in LAM])
             br = b.real.contiguous()
             xr = torch.empty_like(br)
-            for _ in range(5):
-                rp.apply(br, out=xr)
-            torch.cuda.synchronize()
-            its = max(10, min(args.steps, 200))
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(its):
-                rp.apply(br, out=xr)
-            e1.record()
-            torch.cuda.synchronize()
-            rms = e0.elapsed_time(e1) / its
+            # 200 applies after a 150 ms settle whatever --steps is: with the driver's 20 steps the
+            # leg measured the clock ramp (4,576 against 4,930 PCApply/s, profiles/r03z_final_bench*.json)
+            rms = event_ms(lambda: rp.apply(br, out=xr), 200)
             real_variant = {"value": round(1e3 / rms, 3), "unit": "PCApply/s", "ms_per_apply": round(rms, 5),
                             "dtype": "f64 real b and x (r2c / half spectrum / c2r)",
                             "stage_ms": [round(v, 5) for v in rp.time_passes(br, xr, iters=10)],
