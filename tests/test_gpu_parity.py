@@ -610,6 +610,35 @@ def test_profile_mode_records_the_callers_applies(cp, oracle):
             plan.profile_end()  # not started
 
 
+def test_profile_mode_stamps_the_three_sweep_dispatches(cp):
+    """At 256^3 the profile mode stamps each 3-sweep kernel's own dispatch
+    (hipExtLaunchKernelGGL start / stop events, r03z): three positive times whose sum matches the
+    apply's own duration (kernels back to back), where separate event packets added ~5 us each."""
+    g = (256, 256, 256)
+    N = g[0] * g[1] * g[2]
+    b = torch.empty(N, dtype=torch.complex128, device="cuda")
+    cp.fill_uniform(b, 7)
+    x = torch.empty_like(b)
+    with cp.CirculantPlan(g) as plan:
+        plan.set_transport_symbol((0.6, 0.15, 0.02))
+        assert [q["mode"] for q in plan.passes()] == ["rows_fwd", "mid_fused", "rows_inv"]
+        for _ in range(20):
+            plan.apply(b, out=x)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(40):
+            plan.apply(b, out=x)
+        e1.record()
+        torch.cuda.synchronize()
+        apply_ms = e0.elapsed_time(e1) / 40
+        plan.profile_begin(20, every=2)
+        for _ in range(40):
+            plan.apply(b, out=x)
+        ms, napp = plan.profile_end()
+    assert napp == 20 and len(ms) == 3 and all(m > 0 for m in ms)
+    assert 0.85 < sum(ms) / apply_ms < 1.05, (ms, apply_ms)
+
+
 # ------------------------------------------------------------------ HIP-graph replay
 @pytest.mark.parametrize("n", [(32, 32, 32), (100, 100, 100), (64, 32, 16), (256, 256, 256)])
 def test_graph_replay_vs_oracle(cp, oracle, n):
