@@ -89,7 +89,7 @@ def main(argv=None) -> int:
                         "pc_calls": r["pc_calls"], "pc_s": r["pc_seconds"],
                         "pc_ms_per_call": 1e3 * r["pc_seconds"] / max(1, r["pc_calls"]),
                         "pc_share": r["pc_seconds"] / r["solve_seconds"] if r["solve_seconds"] > 0 else None,
-                        "pc_timing": "HIP events around each PCApply on the Vec stream (device time)",
+                        "pc_timing": "device time of each PCApply on the Vec stream: the 3-sweep apply's own first-kernel start to last-kernel end (dispatch stamps), else HIP events around it",
                         "setup_s": r["setup_seconds"], "wall_s": wall,
                     }
                     print(json.dumps(line), flush=True)

@@ -21,6 +21,14 @@ struct LaunchStamp {
   hipEvent_t start = nullptr, stop = nullptr;
 };
 extern thread_local LaunchStamp g_stamp;
+// The stand-in KSP's PCApply timing (ksp_gmres.cpp): while set, an apply whose steps are all
+// 3-sweep kernels stamps its first kernel's start into `start` and its last kernel's end into
+// `stop` (hits = 2): the apply's device time without event packets around it.
+struct ApplyStamp {
+  hipEvent_t start = nullptr, stop = nullptr;
+  int hits = 0;
+};
+extern thread_local ApplyStamp g_apply_stamp;
 
 // How the points of one FFT column are addressed on one side (input or output) of an
 // axis pass.  Column g (0 <= g < ncols) starts at

@@ -29,7 +29,7 @@
 // a launch that stamps its own dispatch while per-launch profiling is on (cfp_internal.h)
 #define TP_LAUNCH(K, G, B, S, ...)                                                                    \
   do {                                                                                                \
-    if (g_stamp.start)                                                                                \
+    if (g_stamp.start || g_stamp.stop)                                                                \
       hipExtLaunchKernelGGL(K, G, B, 0, S, g_stamp.start, g_stamp.stop, 0, __VA_ARGS__);              \
     else                                                                                              \
       hipLaunchKernelGGL(K, G, B, 0, S, __VA_ARGS__);                                                 \

@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "../../include/petsc_mini.h"
+#include "cfp_internal.h"
 
 namespace {
 const int kKSPMagic = 0x4b535031;
@@ -53,8 +54,9 @@ struct _p_KSP {
   double pc_seconds = 0.0;
   // PCApply's device time: an event pair around every call on the Vec stream (a device-Vec
   // PCApply is stream-ordered there and returns at once; its time is read at the end of the solve)
-  std::vector<hipEvent_t> pc_ev;
+  std::vector<hipEvent_t> pc_ev;  // 4 per PCApply: events around it, then the apply's own stamps
   size_t pc_ev_used = 0;
+  std::vector<char> pc_stamped;  // per recorded PCApply: the stamps were set (3-sweep apply)
   // work space (sized for the current problem)
   PetscInt n = -1, nvec = 0;
   Vec* V = nullptr;  // restart + 1 basis vectors
@@ -71,6 +73,7 @@ static void free_events(KSP k) {
   for (auto& e : k->pc_ev) hipEventDestroy(e);
   k->pc_ev.clear();
   k->pc_ev_used = 0;
+  k->pc_stamped.clear();
 }
 
 static void free_work(KSP k) {
@@ -146,7 +149,7 @@ extern "C" PetscErrorCode KSPDestroy(KSP* pk) {
   return rc;
 }
 
-// 64 more PCApply timing events (32 applies); false without a HIP device.  Creating them costs
+// 64 more PCApply timing events (16 applies); false without a HIP device.  Creating them costs
 // ~25 us each, so KSPMiniSetUpWork makes the first batch outside the timed solves.
 static bool grow_events(KSP k) {
   for (int i = 0; i < 64; ++i) {
@@ -181,7 +184,7 @@ extern "C" PetscErrorCode KSPMiniSetUpWork(KSP k, Vec v) {
 static PetscErrorCode pc_apply(KSP k, Vec x, Vec y) {
   void* st = nullptr;
   PetscCall(VecMiniGetStream(&st));
-  bool events = k->pc_ev_used + 2 <= k->pc_ev.size();
+  bool events = k->pc_ev_used + 4 <= k->pc_ev.size();
   if (!events) events = grow_events(k);
   if (!events) {  // no HIP device (host Vecs on a CPU-only machine): the apply is synchronous
     hipGetLastError();
@@ -192,11 +195,19 @@ static PetscErrorCode pc_apply(KSP k, Vec x, Vec y) {
     return PETSC_SUCCESS;
   }
   // recorded in stream order: the first one after the MatMult queued before, the second after
-  // the apply (on the same stream, or completed on the host before it returned)
-  hipEventRecord(k->pc_ev[k->pc_ev_used], (hipStream_t)st);
-  PetscCall(PCApply(k->pc, x, y));
-  hipEventRecord(k->pc_ev[k->pc_ev_used + 1], (hipStream_t)st);
-  k->pc_ev_used += 2;
+  // the apply (on the same stream, or completed on the host before it returned).  A 3-sweep
+  // apply also stamps its own first and last kernel (cfp::g_apply_stamp): the event packets
+  // themselves idle the device ~5 us each and read ~35 us high at 256^3 (GMRES).
+  const size_t i0 = k->pc_ev_used;
+  hipEventRecord(k->pc_ev[i0], (hipStream_t)st);
+  cfp::g_apply_stamp = cfp::ApplyStamp{k->pc_ev[i0 + 2], k->pc_ev[i0 + 3], 0};
+  const PetscErrorCode rc = PCApply(k->pc, x, y);
+  const bool stamped = cfp::g_apply_stamp.hits == 2;
+  cfp::g_apply_stamp = cfp::ApplyStamp{};
+  PetscCall(rc);
+  hipEventRecord(k->pc_ev[i0 + 1], (hipStream_t)st);
+  k->pc_ev_used += 4;
+  k->pc_stamped.push_back(stamped ? 1 : 0);
   k->pc_calls += 1;
   return PETSC_SUCCESS;
 }
@@ -204,14 +215,16 @@ static PetscErrorCode pc_apply(KSP k, Vec x, Vec y) {
 // add the recorded PCApply times to pc_seconds (waits for the last event)
 static PetscErrorCode pc_collect(KSP k) {
   if (!k->pc_ev_used) return PETSC_SUCCESS;
-  if (hipEventSynchronize(k->pc_ev[k->pc_ev_used - 1]) != hipSuccess)
+  if (hipEventSynchronize(k->pc_ev[k->pc_ev_used - 3]) != hipSuccess)  // the last apply's closing event
     return PetscErrorSet(PETSC_ERR_LIB, __func__, "hipEventSynchronize");
-  for (size_t i = 0; i + 1 < k->pc_ev_used; i += 2) {
+  for (size_t a = 0; 4 * a + 3 < k->pc_ev_used; ++a) {
+    const size_t i = 4 * a + (k->pc_stamped[a] ? 2 : 0);  // the stamps, else the events around it
     float ms = 0.f;
     hipEventElapsedTime(&ms, k->pc_ev[i], k->pc_ev[i + 1]);
     k->pc_seconds += 1e-3 * (double)ms;
   }
   k->pc_ev_used = 0;
+  k->pc_stamped.clear();
   return PETSC_SUCCESS;
 }
 
