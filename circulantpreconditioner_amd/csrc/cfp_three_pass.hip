@@ -388,7 +388,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 // NX: x extent (row length in points) of the grid P2 runs on: TN for the complex apply, TN / 2
 // for the real-data plan's half spectrum (cfp_real.hip); y and z are TN long.
-template <int T, int N2, int TN, int PROBE = 0, bool PF = false, int NX = TN, int ST = 0>
+template <int T, int N2, int TN, int PROBE = 0, bool PF = false, int NX = TN, int ST = 0, int LD = 0>
 __global__ void __launch_bounds__(T * (TN / 16)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
 #ifndef CFP_KEXP
@@ -426,7 +426,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
 #pragma unroll
     for (int m = 0; m < NPF; ++m)
       __builtin_amdgcn_global_load_lds((glb_void_t*)(src + zs * TZ * m), (lds_void_t*)(lds + (wv * NPF + m) * 128),
-                                       16, 0, 0);
+                                       16, 0, (LD & F_NT_LD) ? 2 : 0);
   };
   static_assert(!PF || 16 * NPF * 128 <= T * TN, "the prefetch fits the exchange buffer");
   if constexpr (PF) {
@@ -479,7 +479,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
       const int c = idx(c0), tz = idx(tz0);
       const cd* src = col_ptr(u, c, tz);
 #pragma unroll
-      for (int m = NPF; m < 16; ++m) v[m] = src[zs * TZ * m];
+      for (int m = NPF; m < 16; ++m) v[m] = gload<LD>(src + zs * TZ * m);  // LD: load policy
       if constexpr (PF) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA (and loads) landed
 #pragma unroll
@@ -832,6 +832,9 @@ constexpr int kP3Flags = F_NT_ST;
 // (one GPU, slabs, pieces) runs it.  (Moving the four-step twiddle W_256^{y2 k1} from P2 into
 // P1 / P3 lost: 313.1 us, P1 +9 us for its table loads, P2 -1 us; DESIGN.md.)
 constexpr bool kRowsLP = true;
+// P2 load policy (r03z, profiles/r03z_tp_p2nt.txt): non-temporal loads and LDS-DMA of its input,
+// which nothing reads after it: chain 304.4 -> 300.7 us
+constexpr int kP2LoadFlags = F_NT_LD;
 
 template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true, bool LP = false>
 static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
@@ -855,8 +858,8 @@ static void launch_mid(cd* data, const TPArgs& a, hipStream_t s) {
 template <int N2, int TN, bool PF = false>
 static void launch_mid_sw(cd* data, const TPArgs& a, hipStream_t s) {
   constexpr int units = (TN / (64 / N2)) * (TN / N2);
-  TP_LAUNCH((k_tp_mid_sw<64, N2, TN, 0, PF>), dim3(grid_of(units, 1)), dim3(64 * (TN / 16)), s, data, a,
-            units);
+  TP_LAUNCH((k_tp_mid_sw<64, N2, TN, 0, PF, TN, 0, kP2LoadFlags>), dim3(grid_of(units, 1)), dim3(64 * (TN / 16)), s,
+            data, a, units);
 }
 
 bool three_pass_slab_supported(const i64 n[3], int P) {
@@ -869,10 +872,10 @@ hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs
     const int nk1 = a.lnyl ? (1 << a.lnyl) / 8 : 32;  // local k1 values: nyl / N2
     const int units = 32 * nk1;                        // x tiles x local k1
     if (((uintptr_t)out & 15) == 0)  // the LDS-DMA prefetch needs 16-byte addresses
-      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true>), dim3(grid_of(units, 1)), dim3(1024), 0, s,
+      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true, 256, 0, kP2LoadFlags>), dim3(grid_of(units, 1)), dim3(1024), 0, s,
                          out, a, units);
     else
-      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, false>), dim3(grid_of(units, 1)), dim3(1024), 0, s,
+      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, false, 256, 0, kP2LoadFlags>), dim3(grid_of(units, 1)), dim3(1024), 0, s,
                          out, a, units);
   } else {
     const int units = nzl * 8;  // local z-planes x y2

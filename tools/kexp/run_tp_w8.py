@@ -3,6 +3,7 @@
 lane-pair phase A (which + 64), product cache policies, interleaved rounds, plus an output
 comparison of the two chains on the same input."""
 import ctypes
+import sys
 import os
 
 import numpy as np
@@ -17,6 +18,9 @@ tw = torch.from_numpy(np.exp(-2j * np.pi * np.arange(n) / n)).to("cuda")
 cs = torch.full((n * n,), 0.5 + 0.1j, dtype=torch.complex128, device="cuda")
 ax = torch.full((n,), 0.25, dtype=torch.complex128, device="cuda")
 cases = {"product (LP rows, sw P2)": 64, "w8 P2, VPF 0": 64 + 256, "w8 P2, VPF 8": 64 + 512, "w8 P2, VPF 16 (spills)": 64 + 768}
+if len(sys.argv) > 1:  # name=which pairs against the product
+    cases = {"product (LP rows, sw P2)": 64}
+    cases.update({kv.split("=")[0]: int(kv.split("=")[1]) for kv in sys.argv[1:]})
 outs = {}
 for name, c in cases.items():
     ms = ctypes.c_float()

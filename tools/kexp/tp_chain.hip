@@ -6,6 +6,7 @@
 //   p3: 0 NT stores (product), 1 NT loads + NT stores, 2 plain
 //   + 64: P1 and P3 with the lane-pair phase A
 //   (+ 128, the y2 k1 twiddle moved from P2 to P1 / P3, was measured in r03z and removed)
+//   + 4096: P2 loads non-temporally (its input is read once)
 //   + 256 * w: P2 = k_tp_mid_w8 (8 waves, 32 points per thread), w = 1: no register prefetch, 2: 8 slots, 3: 16
 #define CFP_KEXP 1
 #include "cfp_three_pass.hip"
@@ -282,10 +283,13 @@ static void p3(cd* x, const TPArgs& a) {
   else
     hipLaunchKernelGGL((k_tp_rows<true, F, 32, 256>), dim3(512), dim3(512), 0, 0, x, x, a, 2048);
 }
+static bool g_p2nt = false;  // which bit 12: P2 with non-temporal loads (and LDS-DMA)
 static int g_w8 = 0;  // which bits 8..9: P2 = k_tp_mid_w8 with 1: VPF 0, 2: VPF 8, 3: VPF 16
 template <int ST>
 static void p2(cd* x, const TPArgs& a) {
-  if (g_w8 == 1)
+  if (g_p2nt)
+    hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true, 256, ST, F_NT_LD>), dim3(256), dim3(1024), 0, 0, x, a, 1024);
+  else if (g_w8 == 1)
     hipLaunchKernelGGL((k_tp_mid_w8<true, 0>), dim3(256), dim3(512), 0, 0, x, a, 1024);
   else if (g_w8 == 2)
     hipLaunchKernelGGL((k_tp_mid_w8<true, 8>), dim3(256), dim3(512), 0, 0, x, a, 1024);
@@ -305,6 +309,7 @@ extern "C" int tp_chain(int which, const void* b, void* x, const void* tw, const
   const int q1 = which & 3, q2 = (which >> 2) & 3, q3 = (which >> 4) & 3;
   g_lp = (which >> 6) & 1;
   g_w8 = (which >> 8) & 3;
+  g_p2nt = (which >> 12) & 1;
   const cd* bb = (const cd*)b;
   cd* xx = (cd*)x;
   auto go = [&]() {
