@@ -17,7 +17,9 @@ ax = torch.full((n,), 0.25, dtype=torch.complex128, device="cuda")
 P1 = ["nt-ld", "plain", "nt-ld+st", "nt-st"]
 P2 = ["plain", "nt-st"]
 P3 = ["nt-st", "nt-ld+st", "plain"]
-cases = [64 + q1 + 4 * q2 + 16 * q3 for q3 in range(3) for q2 in range(2) for q1 in range(4)]
+import sys
+BASE = int(sys.argv[1]) if len(sys.argv) > 1 else 64  # 64: lane-pair rows; + 4096: P2 NT loads
+cases = [BASE + q1 + 4 * q2 + 16 * q3 for q3 in range(3) for q2 in range(2) for q1 in range(4)]
 res = {c: [] for c in cases}
 for rnd in range(3):
     for c in cases:
