@@ -169,6 +169,8 @@ def declare(L) -> None:
         "VecHIPRestoreArray": ([vp, P(vp)], c_int),
         "VecSet": ([vp, S], c_int),
         "VecSetValue": ([vp, i64, S, c_int], c_int),
+        "VecAssemblyBegin": ([vp], c_int),
+        "VecAssemblyEnd": ([vp], c_int),
         "VecCopy": ([vp, vp], c_int),
         "VecScale": ([vp, S], c_int),
         "VecShift": ([vp, S], c_int),

@@ -165,6 +165,7 @@ namespace cfp {
 thread_local LaunchStamp g_stamp;  // cfp_internal.h
 thread_local ApplyStamp g_apply_stamp;
 }  // namespace cfp
+extern "C" void cfp_apply_stamp_clear(void) { cfp::g_apply_stamp.start = cfp::g_apply_stamp.stop = nullptr; }
 
 namespace {
 
@@ -382,6 +383,14 @@ int step_mode(const cfp_plan_s* p, const Step& q, bool diag_override) {
 int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStream_t s, std::vector<hipEvent_t>* ev) {
   if (!diag_override && p->sym_kind == 0)
     return set_error(CFP_ERR_ARG_WRONGSTATE, "no symbol set on plan (call cfp_plan_set_symbol_* first)");
+  // no dispatch stamps into a graph being captured: a replay would record into events that
+  // belong to other applies by then (the caller then times the apply by its own events)
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  const bool capturing = hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
+  if (capturing) {
+    ev = nullptr;
+    g_apply_stamp.start = g_apply_stamp.stop = nullptr;
+  }
   std::vector<Step> st = apply_steps(p, diag_override != nullptr);
   const double invN = p->external_x ? 1.0 : 1.0 / (double)p->N;
   for (size_t i = 0; i < st.size(); ++i) {

@@ -111,11 +111,18 @@ constexpr int r0_of(int n, int pts) { return n > pts ? r0_of(n / pts, pts) : n; 
 // (x = lane % 32 + 32 wave), so phase A's 32-point DFT is a 16-point DFT per lane (even / odd
 // y1), the twiddle W_32^k on the odd lane, and a radix-2 across lane bit 5 on permlane32 swaps:
 // no LDS exchange and no barrier pair in phase A.  Slot m then holds k1 = m % 8 + 8 ty + 16 (m / 8).
-template <bool INV, int FLAGS, int N1, int TN, int PTS = 16, bool XS = true, bool LP = false>
+//
+// BL (blocked intermediate layout, r04): the N2 rows y2 + N2 k1 of one k1 (contiguous in every
+// layout) hold [x / BX][y2][x % BX] with BX = 64 / N2 instead of [y2][x], so a P2 unit's 64
+// columns (BX x times N2 y2) are one 1 KiB run per z; P1's stores and P3's loads become BX x 16 B
+// runs instead.  Only the intermediate between the sweeps changes; b and x stay natural.
+template <bool INV, int FLAGS, int N1, int TN, int PTS = 16, bool XS = true, bool LP = false, bool BL = false>
 __global__ void __launch_bounds__(N1 * (TN / PTS)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
   constexpr int N2 = TN / N1, TR = TN / PTS, NT = N1 * TR, TY = N1 / PTS;
+  constexpr int BX = 64 / N2;  // x per block column of the blocked layout
   static_assert(!LP || (TY == 2 && TN % 32 == 0), "lane pairs: two threads per column, 32 columns per wave");
+  static_assert(!BL || (N2 == 8 && TR % BX == 0), "blocked layout: 8 x times 8 y2 per block column");
   constexpr int RS = TN + TN / 16;  // padded row stride of the row-mode LDS layout
   constexpr int F = FLAGS | (XS ? F_SPLIT_LDS : 0) | F_LDS_SYNC;
   __shared__ __attribute__((aligned(16))) double lds[N1 * RS * (XS ? 1 : 2)];  // both layouts fit
@@ -144,7 +151,8 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
   const auto load = [&](int u, cd* v) {
     const int x = idx(x0), ty = idx(ty0);
     if (INV) {  // chunked rows: per-thread part + uniform part (nyl >= N2 TY)
-      const cd* const src = in + crow(u / N2, u % N2 + N2 * ty) + x;
+      const cd* const src = BL ? in + crow(u / N2, N2 * ty) + (u % N2) * BX + (x / BX) * 64 + x % BX
+                               : in + crow(u / N2, u % N2 + N2 * ty) + x;
 #pragma unroll
       for (int m = 0; m < PTS; ++m) v[m] = gload<FLAGS>(src + crow(0, N2 * TY * m));
     } else {
@@ -228,9 +236,15 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
     {
       const int r = idx(r0), tx = idx(tx0);
       const double sc = a.scale, sy = INV ? -sc : sc;
-      cd* dst = out + (INV ? (i64)(u / N2) * TN * TN + (i64)TN * (u % N2 + N2 * r) : crow(u / N2, u % N2 + N2 * r)) + tx;
+      if (BL && !INV) {  // blocked: kx = tx + TR m at (kx / BX) 64 + y2 BX + kx % BX of row block r
+        cd* dst = out + crow(u / N2, N2 * r) + (u % N2) * BX + (tx / BX) * 64 + tx % BX;
 #pragma unroll
-      for (int m = 0; m < PTS; ++m) gstore<FLAGS>(dst + TR * m, make_cd(v[m].x * sc, v[m].y * sy));
+        for (int m = 0; m < PTS; ++m) gstore<FLAGS>(dst + TR * N2 * m, make_cd(v[m].x * sc, v[m].y * sy));
+      } else {
+        cd* dst = out + (INV ? (i64)(u / N2) * TN * TN + (i64)TN * (u % N2 + N2 * r) : crow(u / N2, u % N2 + N2 * r)) + tx;
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) gstore<FLAGS>(dst + TR * m, make_cd(v[m].x * sc, v[m].y * sy));
+      }
     }
     lds_barrier();  // the next unit's first exchange overwrites LDS
   }
@@ -388,7 +402,9 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 // NX: x extent (row length in points) of the grid P2 runs on: TN for the complex apply, TN / 2
 // for the real-data plan's half spectrum (cfp_real.hip); y and z are TN long.
-template <int T, int N2, int TN, int PROBE = 0, bool PF = false, int NX = TN, int ST = 0, int LD = 0>
+// BL: the blocked intermediate layout of k_tp_rows<.., BL>: a unit's 64 columns c = x + XT y2 are
+// the 1 KiB run at block column xt of row block k1, for every z.
+template <int T, int N2, int TN, int PROBE = 0, bool PF = false, int NX = TN, int ST = 0, int LD = 0, bool BL = false>
 __global__ void __launch_bounds__(T * (TN / 16)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
 #ifndef CFP_KEXP
@@ -400,6 +416,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
   constexpr int N1 = TN / N2, TZ = TN / 16, NT = T * TZ, XT = T / N2, NXT = NX / XT;
   constexpr int XB = ilog2(XT);  // lane bits of x
   static_assert(NX % XT == 0, "whole x tiles");
+  static_assert(!BL || (NX == TN && N2 == 8), "blocked layout: complex grid, 8 x times 8 y2");
   __shared__ __attribute__((aligned(16))) double lds[T * TN];  // split exchange
   __shared__ cd tw_l[TN];
   const int tid = threadIdx.x;
@@ -415,6 +432,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
   // this lane's first point and the twiddle W_TN^{y2 k1} (natural layout: x = c % XT, y2 = c / XT)
   const auto col_ptr = [&](int u, int c, int tz) {
     const int xt = u % NXT, k1 = u / NXT;
+    if constexpr (BL) return data + (i64)NX * N2 * k1 + xt * T + c + zs * tz;
     return data + xt * XT + (c & (XT - 1)) + (i64)NX * ((c >> XB) + N2 * k1) + zs * tz;
   };
   const auto tw_y = [&](int u, int c) { return tw_l[((c >> XB) * (a.k1_off + u / NXT)) & (TN - 1)]; };
@@ -836,17 +854,17 @@ constexpr bool kRowsLP = true;
 // which nothing reads after it: chain 304.4 -> 300.7 us
 constexpr int kP2LoadFlags = F_NT_LD;
 
-template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true, bool LP = false>
+template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true, bool LP = false, bool BL = false>
 static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
   constexpr int units = TN * (TN / N1);  // z-planes x y2
   const unsigned g = grid_of(units, PER_CU);
   const dim3 blk(N1 * (TN / PTS));
   if (stage == 0 && in == out)  // in place (the direct solver's Un, Un)
-    TP_LAUNCH((k_tp_rows<false, kP1InPlaceFlags, N1, TN, PTS, XS, LP>), dim3(g), blk, s, in, out, a, units);
+    TP_LAUNCH((k_tp_rows<false, kP1InPlaceFlags, N1, TN, PTS, XS, LP, BL>), dim3(g), blk, s, in, out, a, units);
   else if (stage == 0)
-    TP_LAUNCH((k_tp_rows<false, kP1Flags, N1, TN, PTS, XS, LP>), dim3(g), blk, s, in, out, a, units);
+    TP_LAUNCH((k_tp_rows<false, kP1Flags, N1, TN, PTS, XS, LP, BL>), dim3(g), blk, s, in, out, a, units);
   else
-    TP_LAUNCH((k_tp_rows<true, kP3Flags, N1, TN, PTS, XS, LP>), dim3(g), blk, s, in, out, a, units);
+    TP_LAUNCH((k_tp_rows<true, kP3Flags, N1, TN, PTS, XS, LP, BL>), dim3(g), blk, s, in, out, a, units);
 }
 
 template <int T, int N2, int TN, int PER_CU, int PTS = 16, bool XS = true>
@@ -855,11 +873,11 @@ static void launch_mid(cd* data, const TPArgs& a, hipStream_t s) {
   TP_LAUNCH((k_tp_mid<0, T, N2, TN, PTS, XS>), dim3(grid_of(units, PER_CU)), dim3(T * (TN / PTS)), s, data, a, units);
 }
 
-template <int N2, int TN, bool PF = false>
+template <int N2, int TN, bool PF = false, bool BL = false>
 static void launch_mid_sw(cd* data, const TPArgs& a, hipStream_t s) {
   constexpr int units = (TN / (64 / N2)) * (TN / N2);
-  TP_LAUNCH((k_tp_mid_sw<64, N2, TN, 0, PF, TN, 0, kP2LoadFlags>), dim3(grid_of(units, 1)), dim3(64 * (TN / 16)), s,
-            data, a, units);
+  TP_LAUNCH((k_tp_mid_sw<64, N2, TN, 0, PF, TN, 0, kP2LoadFlags, BL>), dim3(grid_of(units, 1)), dim3(64 * (TN / 16)),
+            s, data, a, units);
 }
 
 bool three_pass_slab_supported(const i64 n[3], int P) {
@@ -891,7 +909,8 @@ hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs
 }
 
 bool three_pass_shape_valid(int n1, int mid) {
-  return (n1 == 0 || n1 == 32 || n1 == 64) && (mid >= 0 && mid <= TP_MID_SWAP64_PF);
+  return (n1 == 0 || n1 == 32 || n1 == 64) && (mid >= 0 && mid <= TP_MID_BLOCKED) &&
+         !(mid == TP_MID_BLOCKED && n1 == 64);
 }
 
 hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, TPShape shape,
@@ -922,6 +941,12 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
   // the LDS-DMA prefetch (global_load_lds_dwordx4) takes 16-byte aligned addresses: a buffer that
   // is only 8-byte aligned runs the same kernel without it
   const bool pf_ok = ((uintptr_t)out & 15) == 0;
+  if (shape.mid == TP_MID_BLOCKED) {  // N1 = 32, blocked intermediate layout (k_tp_rows<.., BL>)
+    if (stage != 1) launch_rows<32, 256, 2, 16, true, kRowsLP, true>(stage, in, out, a, s);
+    else if (pf_ok) launch_mid_sw<8, 256, true, true>(out, a, s);
+    else launch_mid_sw<8, 256, false, true>(out, a, s);
+    return hipGetLastError();
+  }
   if (stage == 1) {
     if ((shape.mid == TP_MID_SWAP64_PF || shape.mid == TP_MID_DEFAULT) && pf_ok) {
       if (n1 == 64) launch_mid_sw<4, 256, true>(out, a, s);

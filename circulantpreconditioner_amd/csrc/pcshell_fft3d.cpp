@@ -37,6 +37,9 @@
 namespace {
 using namespace cfp_pc;
 
+// cfp_plan.hip (internal): stop the current PCApply's dispatch stamping (cfp::g_apply_stamp)
+extern "C" void cfp_apply_stamp_clear(void);
+
 const int kFFTMagic = 0x46465448;  // "FFTH"
 
 #ifdef CFP_WITH_PETSC
@@ -129,14 +132,19 @@ PetscErrorCode fft_mult_impl(Mat A, Vec x, Vec y, bool backward) {
   DevOut out;
   PetscCall(in.get(x, n));
   PetscCall(out.get(y, n));
+  // on the Vec stream, behind the Vec kernels that produced x (a non-blocking stream does not
+  // order against the null stream), then waited for: the transforms return complete
+  void* vst = nullptr;
+  bool vwait = true;
+  cfp_pc::device_stream(&vst, &vwait);
   int rc;
   if (s->dplan)
-    rc = backward ? cfp_dist_plan_backward(s->dplan, in.ptr(), out.ptr(), nullptr)
-                  : cfp_dist_plan_forward(s->dplan, in.ptr(), out.ptr(), nullptr);
+    rc = backward ? cfp_dist_plan_backward(s->dplan, in.ptr(), out.ptr(), vst)
+                  : cfp_dist_plan_forward(s->dplan, in.ptr(), out.ptr(), vst);
   else
-    rc = backward ? cfp_plan_backward(s->plan, in.ptr(), out.ptr(), nullptr)
-                  : cfp_plan_forward(s->plan, in.ptr(), out.ptr(), nullptr);
-  if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
+    rc = backward ? cfp_plan_backward(s->plan, in.ptr(), out.ptr(), vst)
+                  : cfp_plan_forward(s->plan, in.ptr(), out.ptr(), vst);
+  if (rc == CFP_SUCCESS) rc = cfp_stream_sync(vst);
   PetscCall(out.put());
   PetscCall(in.put());
   CFPCALL(rc);
@@ -148,7 +156,12 @@ PetscErrorCode fft_destroy(Mat A) {
   FFTShell* s;
   PetscCall(fft_shell(A, &s));
   if (s->plan) cfp_plan_destroy(s->plan);
-  if (s->dplan) cfp_dist_plan_destroy(s->dplan);
+  if (s->dplan) {
+    cfp_dist_plan_destroy(s->dplan);
+#ifndef CFP_WITH_PETSC
+    PetscMiniCommRelease(s->comm);
+#endif
+  }
   if (s->stage) hipFree(s->stage);
 #ifdef CFP_WITH_PETSC
   delete s->mx;
@@ -256,6 +269,7 @@ PetscErrorCode create_dist(FFTShell* s, MPI_Comm comm, int dev) {
     CFPCALL(cfp_dist_plan_create_external(&s->dplan, s->dims[0], s->dims[1], s->dims[2], s->nranks, s->rank, dev));
     CFPCALL(cfp_dist_plan_set_exchange(s->dplan, PetscMiniCommExchange, (void*)(intptr_t)c));
   }
+  PetscCall(PetscMiniCommRetain(c));  // PetscMiniCommDestroy refuses until fft_destroy releases it
   s->comm = c;
 #endif
   return PETSC_SUCCESS;
@@ -390,11 +404,13 @@ PetscErrorCode shell_apply(FFTShell* s, Vec X, Vec b, bool own, Vec Diag) {
   DevIn din;
   if (!own && !s->dplan) PetscCall(din.get(Diag, n));
   if (s->dplan) CFPCALL(cfp_dist_plan_use_diag(s->dplan, own ? 0 : 1));
+  // device Vecs: on the Vec stream, behind the Vec kernels that produced b (the slab apply too,
+  // which then waits: its exchanges are host-driven)
   void* vst = nullptr;
   bool vwait = true;
-  if (!s->dplan) cfp_pc::device_stream(&vst, &vwait);
+  cfp_pc::device_stream(&vst, &vwait);
   auto dev_apply = [&](const double* in, double* out) -> int {
-    if (s->dplan) return cfp_dist_plan_apply(s->dplan, in, out, nullptr);
+    if (s->dplan) return cfp_dist_plan_apply(s->dplan, in, out, vst);
     return own ? cfp_plan_apply(s->plan, in, out, vst) : cfp_plan_apply_with_diag(s->plan, din.ptr(), in, out, vst);
   };
   // device Vecs: wait only where the caller cannot rely on stream order
@@ -473,8 +489,11 @@ extern "C" PetscErrorCode solve_3D(Mat FFT_MAT, Vec X, Vec Diag, Vec b, Vec b_ha
     if (!own && f[1] != 0.0) {
       DevIn din;
       PetscCall(din.get(Diag, s->nlocal));
-      int rc = cfp_dist_plan_set_diag(s->dplan, din.ptr(), nullptr);
-      if (rc == CFP_SUCCESS) rc = cfp_stream_sync(nullptr);
+      void* vst = nullptr;
+      bool vwait = true;
+      cfp_pc::device_stream(&vst, &vwait);
+      int rc = cfp_dist_plan_set_diag(s->dplan, din.ptr(), vst);
+      if (rc == CFP_SUCCESS) rc = cfp_stream_sync(vst);
       PetscCall(din.put());
       CFPCALL(rc);
       s->dt_id = id;
@@ -549,6 +568,9 @@ extern "C" PetscErrorCode applyFFT3DPrecTransport(PC pc, Vec b, Vec x) {
              "applyFFT3DPrecTransport: setupFFTPrec3D has not run");
   const PetscInt N = ctx->n_x * ctx->n_y * ctx->n_z;
   Vec src = b;
+  // the stand-in KSP times a PCApply by the plan's first and last kernel only when the plan
+  // apply is the whole PCApply: not with remaps around it
+  if (ctx->intersectionMatrix || ctx_remap_back(ctx)) cfp_apply_stamp_clear();
   if (ctx->intersectionMatrix) {  // mesh -> Cartesian remap (identity when NULL)
     PetscCall(MatMult(ctx->intersectionMatrix, b, ctx->b_cartesien));
     src = ctx->b_cartesien;

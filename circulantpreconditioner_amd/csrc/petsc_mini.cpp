@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <atomic>
 #include <mutex>
 #include <sys/time.h>
@@ -64,6 +65,7 @@ struct CommRec {
   void* hsend = nullptr;            // exchange staging (pinned host)
   void* hrecv = nullptr;
   size_t hbytes = 0;
+  int refs = 0;                     // FFT matrices (slab plans) built on this communicator
 };
 static std::mutex g_comm_mu;
 static std::vector<CommRec> g_comms(2);
@@ -133,6 +135,8 @@ extern "C" PetscErrorCode PetscMiniCommDestroy(MPI_Comm* comm) {
   std::lock_guard<std::mutex> g(g_comm_mu);
   if (*comm >= (MPI_Comm)g_comms.size()) return ERR(PETSC_ERR_ARG_WRONG, "unknown communicator");
   CommRec& r = g_comms[(size_t)*comm];
+  if (r.refs > 0)  // a slab plan still sends over it (its ncclComm_t, or the callbacks)
+    return ERR(PETSC_ERR_ARG_WRONGSTATE, "communicator still used by FFT matrices: destroy them first");
   if (r.nccl) ncclCommDestroy(r.nccl);
   if (r.dbuf) hipFree(r.dbuf);
   if (r.hsend) hipHostFree(r.hsend);
@@ -140,6 +144,21 @@ extern "C" PetscErrorCode PetscMiniCommDestroy(MPI_Comm* comm) {
   if (g_world == *comm) g_world = PETSC_COMM_SELF;
   r = CommRec();
   *comm = PETSC_COMM_SELF;
+  return PETSC_SUCCESS;
+}
+
+extern "C" PetscErrorCode PetscMiniCommRetain(MPI_Comm comm) {
+  std::lock_guard<std::mutex> g(g_comm_mu);
+  CommRec* r = comm_rec(comm);
+  if (!r) return ERR(PETSC_ERR_ARG_WRONG, "unknown communicator");
+  ++r->refs;
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode PetscMiniCommRelease(MPI_Comm comm) {
+  std::lock_guard<std::mutex> g(g_comm_mu);
+  CommRec* r = comm_rec(comm);
+  if (!r) return ERR(PETSC_ERR_ARG_WRONG, "unknown communicator");
+  if (r->refs > 0) --r->refs;
   return PETSC_SUCCESS;
 }
 
@@ -187,6 +206,37 @@ extern "C" PetscErrorCode PetscMiniAllreduce(MPI_Comm comm, double* buf, int64_t
   }
   if (r->ops.allreduce(r->ops.user, buf, count, op)) return ERR(PETSC_ERR_LIB, "allreduce callback failed");
   return PETSC_SUCCESS;
+}
+
+// host all-to-all of `per_peer` bytes from every rank to every rank ([size][per_peer] in and
+// out): the caller's callback, or RCCL through device staging
+static PetscErrorCode comm_alltoall_host(CommRec* r, const void* send, void* recv, size_t per_peer) {
+  const size_t total = per_peer * (size_t)r->size;
+  if (r->size == 1 || per_peer == 0) {
+    std::memcpy(recv, send, total);
+    return PETSC_SUCCESS;
+  }
+  if (!r->nccl) {
+    if (r->ops.alltoall(r->ops.user, send, recv, (int64_t)per_peer)) return ERR(PETSC_ERR_LIB, "alltoall callback failed");
+    return PETSC_SUCCESS;
+  }
+  char* d = nullptr;
+  if (hipMalloc(&d, 2 * total) != hipSuccess) return ERR(PETSC_ERR_MEM, "alltoall staging");
+  PetscErrorCode rc = PETSC_SUCCESS;
+  if (hipMemcpyAsync(d, send, total, hipMemcpyHostToDevice, g_stream) != hipSuccess) rc = ERR(PETSC_ERR_LIB, "alltoall copy");
+  if (!rc && ncclGroupStart() != ncclSuccess) rc = ERR(PETSC_ERR_LIB, "ncclGroupStart");
+  if (!rc) {
+    for (int q = 0; q < r->size && !rc; ++q)
+      if (ncclSend(d + q * per_peer, per_peer, ncclChar, q, r->nccl, g_stream) != ncclSuccess ||
+          ncclRecv(d + total + q * per_peer, per_peer, ncclChar, q, r->nccl, g_stream) != ncclSuccess)
+        rc = ERR(PETSC_ERR_LIB, "ncclSend / ncclRecv");
+    if (ncclGroupEnd() != ncclSuccess && !rc) rc = ERR(PETSC_ERR_LIB, "ncclGroupEnd");
+  }
+  if (!rc && (hipMemcpyAsync(recv, d + total, total, hipMemcpyDeviceToHost, g_stream) != hipSuccess ||
+              hipStreamSynchronize(g_stream) != hipSuccess))
+    rc = ERR(PETSC_ERR_LIB, "alltoall copy back");
+  hipFree(d);
+  return rc;
 }
 
 // one exchange piece of a slab plan (include/circulant_fft_dist.h, cfp_dist_exchange_fn)
@@ -260,6 +310,10 @@ struct _p_Vec {
   int device = 0;
   PetscObjectId id = 0;
   PetscObjectState state = 0;  // bumped by every write access (PetscObjectStateGet)
+  // VecSetValues entries of rows owned by other ranks, delivered by VecAssemblyBegin/End
+  std::vector<PetscInt> st_idx;
+  std::vector<cd> st_val;
+  std::vector<char> st_add;
 };
 
 static std::atomic<int64_t> g_object_ids{0};
@@ -616,8 +670,13 @@ extern "C" PetscErrorCode VecSetValues(Vec v, PetscInt n, const PetscInt* idx, c
   for (PetscInt k = 0; k < n; ++k) {
     if (idx[k] < 0) continue;
     if (idx[k] >= v->N) return ERR(PETSC_ERR_ARG_OUTOFRANGE, "index out of range");
-    const PetscInt i = idx[k] - v->rstart;  // global row -> local; other ranks' rows are not kept
-    if (i < 0 || i >= v->n) continue;
+    const PetscInt i = idx[k] - v->rstart;  // global row -> local
+    if (i < 0 || i >= v->n) {  // another rank's row: stashed until VecAssemblyBegin/End
+      v->st_idx.push_back(idx[k]);
+      v->st_val.push_back(tocd(y[k]));
+      v->st_add.push_back(mode == ADD_VALUES);
+      continue;
+    }
     cd val = tocd(y[k]);
     if (mode == ADD_VALUES) val = cfp::make_cd(h[i].x + val.x, h[i].y + val.y);
     h[i] = val;
@@ -635,7 +694,57 @@ extern "C" PetscErrorCode VecGetValues(Vec v, PetscInt n, const PetscInt* idx, P
   }
   return PETSC_SUCCESS;
 }
-extern "C" PetscErrorCode VecAssemblyBegin(Vec v) { VCHK(v); return PETSC_SUCCESS; }
+// Collective, as in PETSc: every rank's stashed entries travel to their owners (one all-reduce of
+// the largest per-peer count, one all-to-all of 32-byte records [row, re, im, add]) and are
+// applied there in rank order.  Begin does the whole exchange; End only completes the pair.
+extern "C" PetscErrorCode VecAssemblyBegin(Vec v) {
+  VCHK(v);
+  if (v->nranks == 1) {
+    v->st_idx.clear(), v->st_val.clear(), v->st_add.clear();
+    return PETSC_SUCCESS;
+  }
+  CommRec* r = comm_rec(v->comm);
+  if (!r) return ERR(PETSC_ERR_ARG_WRONG, "unknown communicator");
+  const int P = r->size;
+  // owner of a global row: the Vec's layout, gathered from every rank's start (one all-reduce)
+  std::vector<double> starts((size_t)P, 0.0);
+  starts[(size_t)r->rank] = (double)v->rstart;
+  PetscCall(PetscMiniAllreduce(v->comm, starts.data(), P, PETSCMINI_OP_SUM));
+  const auto owner = [&](PetscInt g) {
+    int q = (int)(std::upper_bound(starts.begin(), starts.end(), (double)g) - starts.begin()) - 1;
+    return q < 0 ? 0 : q;
+  };
+  std::vector<std::vector<size_t>> to((size_t)P);
+  for (size_t k = 0; k < v->st_idx.size(); ++k) to[(size_t)owner(v->st_idx[k])].push_back(k);
+  double mx = 0.0;
+  for (const auto& t : to) mx = std::max(mx, (double)t.size());
+  PetscCall(PetscMiniAllreduce(v->comm, &mx, 1, PETSCMINI_OP_MAX));
+  const size_t M = (size_t)mx;
+  if (M) {
+    std::vector<double> send((size_t)P * M * 4, -1.0), recv((size_t)P * M * 4);
+    for (int q = 0; q < P; ++q)
+      for (size_t j = 0; j < to[(size_t)q].size(); ++j) {
+        const size_t k = to[(size_t)q][j];
+        double* rec = &send[((size_t)q * M + j) * 4];
+        rec[0] = (double)v->st_idx[k];  // exact: rows < 2^53
+        rec[1] = v->st_val[k].x;
+        rec[2] = v->st_val[k].y;
+        rec[3] = v->st_add[k] ? 1.0 : 0.0;
+      }
+    PetscCall(comm_alltoall_host(r, send.data(), recv.data(), M * 4 * sizeof(double)));
+    cd* h;
+    PetscCall(host_rw(v, &h));
+    for (size_t e = 0; e < (size_t)P * M; ++e) {
+      const double* rec = &recv[e * 4];
+      if (rec[0] < 0) continue;  // padding
+      const PetscInt i = (PetscInt)rec[0] - v->rstart;
+      if (i < 0 || i >= v->n) return ERR(PETSC_ERR_PLIB, "stashed entry delivered to the wrong rank");
+      h[i] = rec[3] != 0.0 ? cfp::make_cd(h[i].x + rec[1], h[i].y + rec[2]) : cfp::make_cd(rec[1], rec[2]);
+    }
+  }
+  v->st_idx.clear(), v->st_val.clear(), v->st_add.clear();
+  return PETSC_SUCCESS;
+}
 extern "C" PetscErrorCode VecAssemblyEnd(Vec v) { VCHK(v); return PETSC_SUCCESS; }
 
 extern "C" PetscErrorCode VecCopy(Vec x, Vec y) {

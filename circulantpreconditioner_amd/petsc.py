@@ -213,9 +213,14 @@ class Comm:
 
     _Ops._fields_ = [("alltoall", _A2A), ("allreduce", _RED), ("user", ctypes.c_void_p)]
 
+    # the ctypes callbacks of live communicators, by handle: the library calls them for as long
+    # as the communicator exists, whether or not this Python object is still referenced
+    _REGISTRY: dict = {}
+
     def __init__(self, handle: int, keep=()):
         self.handle = int(handle)
-        self._keep = keep
+        if keep:
+            Comm._REGISTRY[self.handle] = keep
 
     @classmethod
     def torch(cls, group=None) -> "Comm":
@@ -290,9 +295,11 @@ class Comm:
         return a
 
     def destroy(self) -> None:
+        """PetscMiniCommDestroy; refused (PetscError) while FFT matrices built on it exist."""
         if self.handle >= 2:
             h = ctypes.c_int(self.handle)
             PetscCall(lib().PetscMiniCommDestroy(ctypes.byref(h)))
+            Comm._REGISTRY.pop(self.handle, None)
         self.handle = PETSC_COMM_SELF
 
 

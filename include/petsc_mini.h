@@ -137,7 +137,11 @@ PetscErrorCode PetscMiniCommCreate(int size, int rank, const PetscMiniCommOps *o
 /* an RCCL communicator (ncclCommInitRank on the current HIP device; unique_id = the 128 bytes
  * of cfp_dist_get_unique_id, created on rank 0 and broadcast by the caller) */
 PetscErrorCode PetscMiniCommCreateRCCL(int size, int rank, const char *unique_id, MPI_Comm *comm);
+/* refused (PETSC_ERR_ARG_WRONGSTATE) while FFT matrices built on the communicator still exist */
 PetscErrorCode PetscMiniCommDestroy(MPI_Comm *comm);
+/* reference count of the objects that use a communicator (FFT matrices of several ranks) */
+PetscErrorCode PetscMiniCommRetain(MPI_Comm comm);
+PetscErrorCode PetscMiniCommRelease(MPI_Comm comm);
 /* PETSC_COMM_WORLD resolves to comm from now on (PETSC_COMM_SELF: back to one rank) */
 PetscErrorCode PetscMiniSetCommWorld(MPI_Comm comm);
 /* the communicator PETSC_COMM_WORLD currently stands for (others: themselves) */

@@ -504,7 +504,8 @@ def tp_case(oracle):
 
 
 @pytest.mark.parametrize("n1,mid", [(64, "lane64"), (64, "lane32"), (32, "lane64"), (32, "lane32"), (0, "default"),
-                                    (32, "swap64"), (64, "swap64"), (32, "swap64pf"), (64, "swap64pf")])
+                                    (32, "swap64"), (64, "swap64"), (32, "swap64pf"), (64, "swap64pf"),
+                                    (0, "blocked"), (32, "blocked")])
 def test_three_pass_variants(cp, tp_case, n1, mid):
     """Both y splits (64 x 4 with a 4-lane y2 DFT, 32 x 8 with an 8-lane one) and both P2 tile
     widths, selected per plan through cfp_plan_set_three_pass_shape."""
@@ -518,14 +519,15 @@ def test_three_pass_variants(cp, tp_case, n1, mid):
         assert torch.equal(t_, x)
 
 
-def test_three_pass_8_byte_aligned(cp, tp_case):
+@pytest.mark.parametrize("mid", ["default", "blocked"])
+def test_three_pass_8_byte_aligned(cp, tp_case, mid):
     """The 3-sweep apply on buffers that are 8- but not 16-byte aligned (the LDS-DMA prefetch of
     the middle kernel needs 16-byte addresses; such buffers run it without the prefetch)."""
     n, lam, b, ref = tp_case
     N = 256 ** 3
     raw = torch.empty(2 * N + 1, dtype=torch.float64, device="cuda")  # raw[1:] starts 8 bytes past a 16-byte boundary
     with cp.CirculantPlan(n) as plan:
-        plan.set_transport_symbol(lam)
+        plan.set_transport_symbol(lam).set_three_pass_shape(0, mid)
         bd = _dev(b)
         x = plan.apply(bd)
         assert _rel(x, ref) < TOL

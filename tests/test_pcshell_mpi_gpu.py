@@ -92,6 +92,11 @@ def _rank(rank, world, port, dims, lam, pieces, q):
         out["fwd"] = ty.cpu().numpy()
         F.mult_transpose(vb, vy)
         out["bwd"] = ty.cpu().numpy()
+        try:  # the slab plan behind FFT_MAT still uses the communicator: destroy is refused
+            comm.destroy()
+            out["destroy_refused"] = False
+        except P.PetscError:
+            out["destroy_refused"] = True
         pc.destroy()
         P.set_comm_world(P.PETSC_COMM_SELF)
         comm.destroy()
@@ -140,6 +145,7 @@ def test_pcshell_and_direct_solver_on_several_ranks(dims, world, pieces, oracle)
     assert oracle.rel_l2(gather("pc_2diag"), oracle.c_solve_3d(2 * d0, b, dims)) < TOL
     for r in range(world):
         assert parts[r]["counts"] == (1, 1)  # own symbol once, then the changed Diag
+        assert parts[r]["destroy_refused"]  # PetscMiniCommDestroy while FFT_MAT's slab plan uses it
     bz = b.reshape(nz, ny, nx)
     f = np.fft.fftn(bz).reshape(-1)
     g = (np.fft.ifftn(bz) * N).reshape(-1)

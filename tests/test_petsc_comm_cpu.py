@@ -47,6 +47,22 @@ def _worker(rank, P, port, N, q):
         for i in range(N):
             Pm.PetscCall(Pm.lib().VecSetValue(vc.h, i, Pm._S(complex(i, -i)), Pm.INSERT_VALUES))
         out["setvalues"] = np.array_equal(vc.array(), np.arange(lo, hi) * (1 - 1j))
+        # the reference MPI driver's pattern (TransportEquationFFT_SphericalExplosion_impl_mpi.cxx:
+        # 69-92): rank 0 alone sets every global row, VecAssemblyBegin/End ships them to their owners
+        ve = Pm.Vec.mpi(N).set(0.0)
+        if rank == 0:
+            for i in range(N):
+                Pm.PetscCall(Pm.lib().VecSetValue(ve.h, i, Pm._S(complex(2 * i, 1)), Pm.INSERT_VALUES))
+        Pm.PetscCall(Pm.lib().VecAssemblyBegin(ve.h))
+        Pm.PetscCall(Pm.lib().VecAssemblyEnd(ve.h))
+        out["rank0_fill"] = np.array_equal(ve.array(), 2 * np.arange(lo, hi) + 1j)
+        # ADD_VALUES from every rank to every row (own rows at once, the others at assembly)
+        vf = Pm.Vec.mpi(N).set(0.5)
+        for i in range(N):
+            Pm.PetscCall(Pm.lib().VecSetValue(vf.h, i, Pm._S(complex(rank + 1, 0)), Pm.ADD_VALUES))
+        Pm.PetscCall(Pm.lib().VecAssemblyBegin(vf.h))
+        Pm.PetscCall(Pm.lib().VecAssemblyEnd(vf.h))
+        out["add_all"] = np.array_equal(vf.array(), np.full(hi - lo, 0.5 + P * (P + 1) / 2))
         out["max"] = comm.allreduce([rank, -rank], op=1).tolist()
         # the local sizes given, N determined (PETSC_DETERMINE) and the row start from them
         vd = Pm.Vec.mpi(-1, nlocal=rank + 1)
@@ -84,6 +100,7 @@ def test_comm_vec_reductions(P, N):
         assert res[r]["n1"] == pytest.approx(np.abs(a.real).sum() + np.abs(a.imag).sum(), rel=1e-13)
         assert res[r]["ninf"] == pytest.approx(np.abs(a).max(), rel=1e-13)
         assert res[r]["setvalues"]
+        assert res[r]["rank0_fill"] and res[r]["add_all"]
         assert res[r]["max"] == [P - 1, 0]
         tot = P * (P + 1) // 2
         assert res[r]["determine"] == (tot, (r * (r + 1) // 2, r * (r + 1) // 2 + r + 1))

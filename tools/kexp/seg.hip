@@ -82,3 +82,87 @@ extern "C" int seg_run(int kind, int tx, int nr, int xcd, const void* in, void* 
   hipEventDestroy(e1);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+// ---------------------------------------------------------------------------------------------
+// r04: the 3-sweep chain's three patterns as pure copies, natural against the
+// blocked intermediate layout (k_tp_rows<.., BL>): within the 8 rows y2 + 8 k1 of one k1 the
+// blocked layout holds [x / 8][y2][x % 8].  P1: rows y2 + 8 y1 of a plane (32 x 4 KiB runs) ->
+// rows k1 (natural: 4 KiB runs; blocked: 128-byte runs); P2 (in place): 8 x times 8 y2 times 256 z
+// (natural: 8 runs of 128 B per z; blocked: one 1 KiB run per z); P3 (in place): P1's pattern
+// reversed.  Thread maps as in the kernels: P1/P3 512 threads = (tx 16, row 32), 16 slots x = tx +
+// 16 m; P2 1024 threads = (column 64, tz 16), slots z = tz + 16 m.
+template <bool BL, bool REV>
+__global__ void __launch_bounds__(512) k_chain_rows(const cd* __restrict__ in, cd* __restrict__ out) {
+  const int tid = threadIdx.x, tx = tid % 16, r = tid / 16;
+  const int z = blockIdx.x / 8, y2 = blockIdx.x % 8;
+  const long long plane = (long long)n * n * z;
+  const long long nat = plane + (long long)n * (y2 + 8 * r) + tx;                  // row y2 + 8 r, natural
+  const long long blk = plane + 2048LL * r + 8 * y2 + (tx / 8) * 64 + tx % 8;       // row block r, blocked
+  const long long src = REV && BL ? blk : nat, dst = !REV && BL ? blk : nat;
+  const int ss = REV && BL ? 128 : 16, ds = !REV && BL ? 128 : 16;
+  cd v[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) v[m] = in[src + ss * m];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) out[dst + ds * m] = v[m];
+}
+template <bool BL>
+__global__ void __launch_bounds__(1024) k_chain_mid(const cd* __restrict__ in, cd* __restrict__ out) {
+  const int tid = threadIdx.x, c = tid % 64, tz = tid / 64;
+  const int xt = blockIdx.x % 32, k1 = blockIdx.x / 32;
+  const long long col = BL ? 2048LL * k1 + 64 * xt + c : (long long)n * (c / 8 + 8 * k1) + 8 * xt + c % 8;
+  cd v[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) v[m] = in[col + (long long)n * n * (tz + 16 * m)];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) out[col + (long long)n * n * (tz + 16 * m)] = v[m];
+}
+
+// chain b -> x (P1), x -> x (P2), x -> x (P3), iters times; us[0..2] = mean per-kernel time
+// (events between the kernels), us[3] = mean chain time without them
+extern "C" int seg_chain(int blocked, const void* b, void* x, int iters, double* us) {
+  hipEvent_t e[4];
+  for (auto& q : e) hipEventCreate(&q);
+  float acc[3] = {0, 0, 0};
+  const cd* bb = (const cd*)b;
+  cd* xx = (cd*)x;
+  for (int it = -1; it < iters; ++it) {
+    hipEventRecord(e[0], 0);
+    if (blocked) hipLaunchKernelGGL((k_chain_rows<true, false>), dim3(2048), dim3(512), 0, 0, bb, xx);
+    else hipLaunchKernelGGL((k_chain_rows<false, false>), dim3(2048), dim3(512), 0, 0, bb, xx);
+    hipEventRecord(e[1], 0);
+    if (blocked) hipLaunchKernelGGL((k_chain_mid<true>), dim3(1024), dim3(1024), 0, 0, xx, xx);
+    else hipLaunchKernelGGL((k_chain_mid<false>), dim3(1024), dim3(1024), 0, 0, xx, xx);
+    hipEventRecord(e[2], 0);
+    if (blocked) hipLaunchKernelGGL((k_chain_rows<true, true>), dim3(2048), dim3(512), 0, 0, xx, xx);
+    else hipLaunchKernelGGL((k_chain_rows<false, true>), dim3(2048), dim3(512), 0, 0, xx, xx);
+    hipEventRecord(e[3], 0);
+    hipEventSynchronize(e[3]);
+    if (it < 0) continue;
+    for (int k = 0; k < 3; ++k) {
+      float t = 0;
+      hipEventElapsedTime(&t, e[k], e[k + 1]);
+      acc[k] += t;
+    }
+  }
+  for (int k = 0; k < 3; ++k) us[k] = 1e3 * acc[k] / iters;
+  hipEventRecord(e[0], 0);
+  for (int it = 0; it < iters; ++it) {
+    if (blocked) {
+      hipLaunchKernelGGL((k_chain_rows<true, false>), dim3(2048), dim3(512), 0, 0, bb, xx);
+      hipLaunchKernelGGL((k_chain_mid<true>), dim3(1024), dim3(1024), 0, 0, xx, xx);
+      hipLaunchKernelGGL((k_chain_rows<true, true>), dim3(2048), dim3(512), 0, 0, xx, xx);
+    } else {
+      hipLaunchKernelGGL((k_chain_rows<false, false>), dim3(2048), dim3(512), 0, 0, bb, xx);
+      hipLaunchKernelGGL((k_chain_mid<false>), dim3(1024), dim3(1024), 0, 0, xx, xx);
+      hipLaunchKernelGGL((k_chain_rows<false, true>), dim3(2048), dim3(512), 0, 0, xx, xx);
+    }
+  }
+  hipEventRecord(e[1], 0);
+  hipEventSynchronize(e[1]);
+  float t = 0;
+  hipEventElapsedTime(&t, e[0], e[1]);
+  us[3] = 1e3 * t / iters;
+  for (auto& q : e) hipEventDestroy(q);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
