@@ -94,6 +94,7 @@ def declare(L) -> None:
         "cfp_dist_get_unique_id": ([ctypes.c_char_p], c_int),
         "cfp_dist_unique_id_bytes": ([], c_int),
         "cfp_slab_layout": ([i64, i64, i64, c_int, c_int, P(i64)], c_int),
+        "cfp_slab_work_size": ([i64, i64, i64, c_int, c_int, P(i64)], c_int),
         "cfp_slab_num_steps": ([i64, i64, i64, c_int, c_int, P(c_int)], c_int),
         "cfp_slab_step_info": ([i64, i64, i64, c_int, c_int, c_int, P(i64), P(ctypes.c_double)], c_int),
         "cfp_dist_plan_create": ([P(vp), i64, i64, i64, c_int, c_int, ctypes.c_char_p, c_int], c_int),

@@ -15,6 +15,10 @@ hipError_t blas_waxpy(cd* w, cd a, const cd* x, const cd* y, i64 n, hipStream_t 
 hipError_t blas_pmult(cd* w, const cd* x, const cd* y, i64 n, hipStream_t s);
 // y += sum_j a[j] xs[j]   (a, xs: host arrays of k coefficients / device pointers)
 hipError_t blas_maxpy(cd* y, int k, const cd* a, const cd* const* xs, i64 n, hipStream_t s);
+// y = (overwrite ? 0 : y) + sum_j a[j] xs[j]; norm2 != nullptr: also sum |y|^2 of the result,
+// accumulated in the same sweep (synchronous then, like the reductions below)
+hipError_t blas_maxpy_norm(cd* y, int k, const cd* a, const cd* const* xs, i64 n, bool overwrite, double* norm2,
+                           hipStream_t s);
 // y = A x for a CSR matrix of m rows and nnz nonzeros (nnz picks the lanes per row)
 hipError_t blas_csr_spmv(i64 m, i64 nnz, const i64* rowptr, const i64* col, const cd* val, const cd* x, cd* y,
                          hipStream_t s);

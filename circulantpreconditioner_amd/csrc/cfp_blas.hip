@@ -116,6 +116,29 @@ __global__ void k_mdot(const cd* x, int k, MVPtrs ys, i64 n, double* partial) {
   }
 }
 
+// y = (OW ? 0 : y) + sum_j a_j x_j, with NRM: per-block sums of |y|^2 of the result (one sweep)
+template <bool OW, bool NRM>
+__global__ void __launch_bounds__(BLAS_THREADS) k_maxpy_nrm(cd* y, int k, MVCoef a, MVPtrs xs, i64 n, double* partial) {
+  double s2 = 0.0;
+  GRID_LOOP(i, n) {
+    cd acc = OW ? make_cd(0.0, 0.0) : y[i];
+    for (int j = 0; j < k; ++j) acc = bcadd(acc, bcmul(a.a[j], xs.p[j][i]));
+    y[i] = acc;
+    if (NRM) s2 += acc.x * acc.x + acc.y * acc.y;
+  }
+  if constexpr (NRM) {
+    __shared__ double sm[BLAS_THREADS / 64];
+    s2 = wave_sum(s2);
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s2;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int q = 0; q < BLAS_THREADS / 64; ++q) t += sm[q];
+      partial[blockIdx.x] = t;
+    }
+  }
+}
+
 // CSR y = A x, one thread per row (rows of about one nonzero)
 __global__ void k_csr_spmv(i64 m, const i64* rowptr, const i64* col, const cd* val, const cd* x, cd* y) {
   GRID_LOOP(r, m) {
@@ -230,6 +253,54 @@ static hipError_t reduce(const cd* x, const cd* y, i64 n, int kind, double out[2
   }
   out[0] = a;
   out[1] = b;
+  return hipSuccess;
+}
+
+hipError_t blas_maxpy_norm(cd* y, int k, const cd* a, const cd* const* xs, i64 n, bool overwrite, double* norm2,
+                           hipStream_t s) {
+  static thread_local double* partial = nullptr;
+  static thread_local double* hpart = nullptr;
+  if (norm2 && !partial) {
+    hipError_t e = hipMalloc(&partial, sizeof(double) * RED_BLOCKS);
+    if (e != hipSuccess) return e;
+    e = hipHostMalloc(&hpart, sizeof(double) * RED_BLOCKS);
+    if (e != hipSuccess) return e;
+  }
+  unsigned nb = nblocks(n);
+  if (nb > RED_BLOCKS) nb = RED_BLOCKS;
+  if (k <= 0 && !overwrite) {
+    if (!norm2) return hipSuccess;
+    double v = 0.0;
+    const hipError_t e = blas_norm(y, n, 1, &v, s);
+    *norm2 = v * v;
+    return e;
+  }
+  for (int j0 = 0; j0 < (k > 0 ? k : 1); j0 += MV_MAX) {
+    const int kk = k - j0 < MV_MAX ? (k - j0 > 0 ? k - j0 : 0) : MV_MAX;
+    MVCoef c;
+    MVPtrs p;
+    for (int j = 0; j < kk; ++j) { c.a[j] = a[j0 + j]; p.p[j] = xs[j0 + j]; }
+    const bool ow = overwrite && j0 == 0, last = j0 + MV_MAX >= k, nrm = norm2 && last;
+    if (n <= 0) break;
+    const dim3 g(nb), blk(BLAS_THREADS);
+    if (ow && nrm) hipLaunchKernelGGL((k_maxpy_nrm<true, true>), g, blk, 0, s, y, kk, c, p, n, partial);
+    else if (ow) hipLaunchKernelGGL((k_maxpy_nrm<true, false>), g, blk, 0, s, y, kk, c, p, n, partial);
+    else if (nrm) hipLaunchKernelGGL((k_maxpy_nrm<false, true>), g, blk, 0, s, y, kk, c, p, n, partial);
+    else hipLaunchKernelGGL((k_maxpy_nrm<false, false>), g, blk, 0, s, y, kk, c, p, n, partial);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !norm2) return e;
+  if (n <= 0) {
+    *norm2 = 0.0;
+    return hipSuccess;
+  }
+  e = hipMemcpyAsync(hpart, partial, sizeof(double) * nb, hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) return e;
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return e;
+  double t = 0.0;
+  for (unsigned q = 0; q < nb; ++q) t += hpart[q];
+  *norm2 = t;
   return hipSuccess;
 }
 

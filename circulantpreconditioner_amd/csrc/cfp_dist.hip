@@ -3,11 +3,11 @@
 // Replaces the FFTW-MPI slab transposes that PETSc's MATFFTW performs inside MatMult /
 // MatMultTranspose when size > 1 (src/FftLinearSolver_3D.c:170,180).
 // The y passes read/write the exchange chunks directly (no pack/unpack kernels): the
-// forward y pass writes point ky of a column to chunk ky / nyl, the inverse y pass reads
+// forward y pass writes point ky of a column to chunk ky / nyp, the inverse y pass reads
 // it back from there, so an all-to-all is a set of contiguous peer messages.
 //
 // Pipelining (pieces K > 1).  A block of B = nzl / K local z-planes is a contiguous sub-block
-// of every per-peer chunk ([nzl][nyl][nx]), so the forward all-to-all splits into K pieces:
+// of every per-peer chunk ([nzl][nyp][nx]), so the forward all-to-all splits into K pieces:
 // piece k carries block k of every chunk and can leave as soon as block k's x and y passes are
 // done, while block k + 1's passes run.  The backward all-to-all mirrors it: block k's inverse
 // y and x passes start when piece k has arrived.  The exchanges run on a second stream, ordered
@@ -16,7 +16,7 @@
 // K > 1 the exchanges land in a second work buffer W2, so that no pass writes memory a piece is
 // still reading or receiving:
 //   x fwd  b -> x (block k, natural)       y fwd  x -> W (block k of every chunk)
-//   piece  W -> W2                         z      W2 -> W2 (fused symbol, [nz][nyl][nx])
+//   piece  W -> W2                         z      W2 -> W2 (fused symbol, [nz][nyp][nx])
 //   piece  W2 -> W                         y inv  W -> x (block k),  x inv  x -> x (1/N)
 // K = 1 keeps the round-2 layout (exchanges into x, one work buffer).
 #include <hip/hip_runtime.h>
@@ -49,24 +49,37 @@ using namespace cfp;
 
 namespace {
 
+// Rank r holds z-planes [r nzl, (r + 1) nzl) in natural order (PETSC_DECIDE rows; P | nz) and,
+// after the forward all-to-all, y rows [y0, y0 + nyl) of every plane (the z-pencil block).  The
+// y rows are split as FFTW-MPI splits its transposed dimension: blocks of nyp = ceil(ny / P), so
+// with P not dividing ny the last ranks hold fewer rows (possibly none).  Every per-peer chunk is
+// nzl x nyp x nx (the rows past a peer's count are padding, never read), so the segment
+// addressing of the y passes stays uniform and the z-pencil buffer is [nz][nyp][nx].
 struct SlabLayout {
   i64 nx, ny, nz;
   int P, r;
   i64 nzl, nyl, z0, y0, local, chunk, offset;
+  i64 nyp;   // y rows per chunk (ceil(ny / P)); nyl = this rank's valid rows <= nyp
+  i64 work;  // elements of a work buffer: max(local, P chunk)
+  bool padded() const { return nyp * P != ny; }
 };
 
 int make_layout(i64 nx, i64 ny, i64 nz, int P, int r, SlabLayout* L) {
   if (nx < 1 || ny < 1 || nz < 1) return set_error(CFP_ERR_ARG_OUTOFRANGE, "grid sizes must be >= 1");
   if (P < 1 || r < 0 || r >= P) return set_error(CFP_ERR_ARG_OUTOFRANGE, "rank %d of %d", r, P);
-  if (nz % P || ny % P)
-    return set_error(CFP_ERR_ARG_SIZ, "slab decomposition needs nranks | nz and nranks | ny (nz=%lld ny=%lld P=%d)",
-                     (long long)nz, (long long)ny, P);
+  if (nz % P)
+    return set_error(CFP_ERR_ARG_SIZ, "slab decomposition needs nranks | nz (whole z-planes per rank; nz=%lld P=%d)",
+                     (long long)nz, P);
   if (nx > 4096 || ny > 4096 || nz > 4096) return set_error(CFP_ERR_SUP, "axis lengths above 4096 unsupported");
   L->nx = nx; L->ny = ny; L->nz = nz; L->P = P; L->r = r;
-  L->nzl = nz / P; L->nyl = ny / P;
-  L->z0 = r * L->nzl; L->y0 = r * L->nyl;
+  L->nzl = nz / P;
+  L->nyp = (ny + P - 1) / P;
+  L->z0 = r * L->nzl;
+  L->y0 = r * L->nyp;
+  L->nyl = ny - L->y0 < 0 ? 0 : (ny - L->y0 < L->nyp ? ny - L->y0 : L->nyp);
   L->local = L->nzl * ny * nx;
-  L->chunk = L->nzl * L->nyl * nx;
+  L->chunk = L->nzl * L->nyp * nx;
+  L->work = L->local > P * L->chunk ? L->local : P * L->chunk;
   L->offset = L->z0 * ny * nx;
   return CFP_SUCCESS;
 }
@@ -134,12 +147,15 @@ int pieces_valid(const SlabLayout& L, int K) { return K >= 1 && K <= L.nzl && L.
 
 std::vector<Step> slab_steps(const SlabLayout& L, int schedule, int K, int list) {
   std::vector<Step> st;
-  const i64 nx = L.nx, ny = L.ny, nz = L.nz, nzl = L.nzl, nyl = L.nyl;
+  // nyp: rows per chunk; nyl: the z-pencil rows this rank transforms (nyl <= nyp, padded layouts)
+  const i64 nx = L.nx, ny = L.ny, nz = L.nz, nzl = L.nzl, nyl = L.nyl, nyp = L.nyp;
   const double invN = 1.0 / (double)(nx * ny * nz);
   const bool apply = list == L_APPLY_SEP || list == L_APPLY_DIAG;
   if (!apply) K = 1;
   const i64 B = nzl / K;  // planes per block
-  const int M = K == 1 ? B_X : B_W2;  // where the forward exchange lands (z-pencil buffer)
+  // where the forward exchange lands (z-pencil buffer [nz][nyp][nx]): x if it fits (one piece,
+  // no padding), else W2
+  const int M = (K == 1 && !L.padded()) ? B_X : B_W2;
   int seg = 0;
   auto push = [&](Step s) {
     s.seg = seg;
@@ -149,7 +165,7 @@ std::vector<Step> slab_steps(const SlabLayout& L, int schedule, int K, int list)
   auto exch = [&](int src, int dst, i64 k, int wait) {
     Step s;
     s.kind = K_EXCH; s.src = src; s.dst = dst;
-    s.ex_off = k * B * nyl * nx; s.ex_cnt = B * nyl * nx;
+    s.ex_off = k * B * nyp * nx; s.ex_cnt = B * nyp * nx;
     s.wait = wait;
     return push(s);
   };
@@ -165,8 +181,9 @@ std::vector<Step> slab_steps(const SlabLayout& L, int schedule, int K, int list)
   };
   const Side xs = side(0, nx, 1, nx, 0);                    // x rows of the local slab
   const Side ynat = side(1, nx * ny, nx, ny, 0);            // y columns, natural [nzl][ny][nx]
-  const Side ysplit = side(1, nyl * nx, nx, nyl, L.chunk);  // y columns in per-peer chunks
-  const Side zs = side(1, 0, nx * nyl, nz, 0);              // z columns of [nz][nyl][nx]
+  const Side ysplit = side(1, nyp * nx, nx, nyp, L.chunk);  // y columns in per-peer chunks
+  const Side zs = side(1, 0, nx * nyp, nz, 0);              // z columns of [nz][nyp][nx]: the first nyl rows
+  const i64 zcols_inner = nyl > 0 ? nx * nyl : 1;           // (no columns on a rank without rows)
 
   if (list == L_DIAG_T) {  // natural Diag slab -> chunks (W) -> exchange -> z-pencil copy (B_D)
     Step r;
@@ -185,7 +202,7 @@ std::vector<Step> slab_steps(const SlabLayout& L, int schedule, int K, int list)
     int y = pass(1, (int)ny, nx * nzl, nx, ynat, ysplit, mode, cur, 0, B_W, 0, 0, 1.0, -1);
     seg = 1;
     int e = exch(B_W, B_W2, 0, y);
-    int z = pass(2, (int)nz, nx * nyl, nx * nyl, zs, zs, mode, B_W2, 0, B_W2, 0, 0, 1.0, e);
+    int z = pass(2, (int)nz, nx * nyl, zcols_inner, zs, zs, mode, B_W2, 0, B_W2, 0, 0, 1.0, e);
     seg = 2;
     e = exch(B_W2, B_W, 0, z);
     Step r;
@@ -210,7 +227,7 @@ std::vector<Step> slab_steps(const SlabLayout& L, int schedule, int K, int list)
       return push(s);
     };
     std::vector<int> p1(K);
-    for (i64 k = 0; k < K; ++k) p1[k] = tp(0, B_IN, k * B * ny * nx, B_W, k * B * nyl * nx, (int)B, -1);
+    for (i64 k = 0; k < K; ++k) p1[k] = tp(0, B_IN, k * B * ny * nx, B_W, k * B * nyp * nx, (int)B, -1);
     seg = 1;
     int last = -1;
     for (i64 k = 0; k < K; ++k) last = exch(B_W, M, k, p1[k]);
@@ -218,7 +235,7 @@ std::vector<Step> slab_steps(const SlabLayout& L, int schedule, int K, int list)
     seg = 2;
     for (i64 k = 0; k < K; ++k) {
       const int e = exch(M, B_W, k, mid);
-      tp(2, B_W, k * B * nyl * nx, B_X, k * B * ny * nx, (int)B, e);
+      tp(2, B_W, k * B * nyp * nx, B_X, k * B * ny * nx, (int)B, e);
     }
     return st;
   }
@@ -229,32 +246,32 @@ std::vector<Step> slab_steps(const SlabLayout& L, int schedule, int K, int list)
     const i64 nat = k * B * ny * nx;
     int cur = B_IN;
     if (nx > 1) { pass(0, (int)nx, B * ny, 1, xs, xs, PASS_FWD, B_IN, nat, B_X, nat, 0, 1.0, -1); cur = B_X; }
-    yk[k] = pass(1, (int)ny, nx * B, nx, ynat, ysplit, PASS_FWD, cur, nat, B_W, k * B * nyl * nx, 0, 1.0, -1);
+    yk[k] = pass(1, (int)ny, nx * B, nx, ynat, ysplit, PASS_FWD, cur, nat, B_W, k * B * nyp * nx, 0, 1.0, -1);
   }
   seg = 1;
   int last = -1;
   for (i64 k = 0; k < K; ++k) last = exch(B_W, M, k, yk[k]);
-  const int z = pass(2, (int)nz, nx * nyl, nx * nyl, zs, zs, zmode, M, 0, M, 0, fused, 1.0, last);
+  const int z = pass(2, (int)nz, nx * nyl, zcols_inner, zs, zs, zmode, M, 0, M, 0, fused, 1.0, last);
   seg = 2;
   for (i64 k = 0; k < K; ++k) {
     const i64 nat = k * B * ny * nx;
     const int e = exch(M, B_W, k, z);
     // 1/N on the block's last launch
-    pass(1, (int)ny, nx * B, nx, ysplit, ynat, PASS_INV, B_W, k * B * nyl * nx, B_X, nat, 0, nx > 1 ? 1.0 : invN, e);
+    pass(1, (int)ny, nx * B, nx, ysplit, ynat, PASS_INV, B_W, k * B * nyp * nx, B_X, nat, 0, nx > 1 ? 1.0 : invN, e);
     if (nx > 1) pass(0, (int)nx, B * ny, 1, xs, xs, PASS_INV, B_X, nat, B_X, nat, 0, invN, -1);
   }
   return st;
 }
 
 // natural planes [planes][ny][nx] <-> per-peer chunks: element (z, y, x) of the slab sits at
-// (z ny + y) nx + x naturally and at (y / nyl) chunk + (z nyl + y % nyl) nx + x in the chunks.
+// (z ny + y) nx + x naturally and at (y / nyp) chunk + (z nyp + y % nyp) nx + x in the chunks.
 // One thread per element; consecutive threads walk x, so both sides are coalesced.
-__global__ void k_slab_repack(const cd* __restrict__ in, cd* __restrict__ out, i64 total, i64 nx, i64 ny, i64 nyl,
+__global__ void k_slab_repack(const cd* __restrict__ in, cd* __restrict__ out, i64 total, i64 nx, i64 ny, i64 nyp,
                               i64 chunk, int to_chunks) {
   for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (i64)gridDim.x * blockDim.x) {
     const i64 x = i % nx, row = i / nx;
     const i64 y = row % ny, z = row / ny;
-    const i64 c = (y / nyl) * chunk + (z * nyl + y % nyl) * nx + x;
+    const i64 c = (y / nyp) * chunk + (z * nyp + y % nyp) * nx + x;
     if (to_chunks) out[c] = in[i];
     else out[i] = in[c];
   }
@@ -265,7 +282,7 @@ hipError_t launch_repack(const cd* in, cd* out, const SlabLayout& L, i64 planes,
   if (total <= 0) return hipSuccess;
   const i64 want = (total + 255) / 256;
   const unsigned g = (unsigned)(want < 4096 ? want : 4096);
-  hipLaunchKernelGGL(k_slab_repack, dim3(g), dim3(256), 0, s, in, out, total, L.nx, L.ny, L.nyl, L.chunk, to_chunks);
+  hipLaunchKernelGGL(k_slab_repack, dim3(g), dim3(256), 0, s, in, out, total, L.nx, L.ny, L.nyp, L.chunk, to_chunks);
   return hipGetLastError();
 }
 
@@ -294,7 +311,7 @@ struct SlabRank {
     device = dev;
     int rc = set_steps(CFP_SCHEDULE_AUTO, 0);
     if (rc) return rc;
-    HIPCHK(hipMalloc(&work, sizeof(cd) * (size_t)L.local));
+    HIPCHK(hipMalloc(&work, sizeof(cd) * (size_t)L.work));
     return CFP_SUCCESS;
   }
   int pieces() const { return pieces_req ? pieces_req : auto_pieces(L); }
@@ -310,7 +327,7 @@ struct SlabRank {
   }
   int ensure_work2() {
     if (!work2) {
-      HIPCHK(hipMalloc(&work2, sizeof(cd) * (size_t)L.local));
+      HIPCHK(hipMalloc(&work2, sizeof(cd) * (size_t)L.work));
       own_work2 = true;
     }
     return CFP_SUCCESS;
@@ -352,13 +369,13 @@ struct SlabRank {
         s[a][k] = make_cd(cr * lr - ci * li, cr * li + ci * lr);
       }
     }
-    const i64 ncols = L.nx * L.nyl;
-    std::vector<cd> col((size_t)ncols);
+    const i64 ncols = L.nx * L.nyl;  // 0 on a rank past the last y row (padded layouts)
+    std::vector<cd> col((size_t)(ncols > 0 ? ncols : 1));
     for (i64 g = 0; g < ncols; ++g) {
       const i64 ix = g % L.nx, ky = L.y0 + g / L.nx;
       col[(size_t)g] = make_cd(s[0][ix].x + s[1][ky].x, s[0][ix].y + s[1][ky].y);
     }
-    if (!colsym) HIPCHK(hipMalloc(&colsym, sizeof(cd) * (size_t)ncols));
+    if (!colsym) HIPCHK(hipMalloc(&colsym, sizeof(cd) * (size_t)(ncols > 0 ? ncols : 1)));
     if (!axsym) HIPCHK(hipMalloc(&axsym, sizeof(cd) * (size_t)L.nz));
     HIPCHK(hipMemcpy(colsym, col.data(), sizeof(cd) * (size_t)ncols, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(axsym, s[2].data(), sizeof(cd) * (size_t)L.nz, hipMemcpyHostToDevice));
@@ -399,9 +416,9 @@ struct SlabRank {
       a.colsym = colsym3;
       a.axsym = axsym;
       a.scale = s.pass.scale;
-      a.lnyl = ilog2_exact(L.nyl);
+      a.lnyl = ilog2_exact(L.nyp);  // (the 3-sweep slab schedule is never padded: P | 32)
       a.chunk = L.chunk;
-      a.k1_off = (int)(L.r * (L.nyl / 8));  // N2 = 8 rows per k1
+      a.k1_off = (int)(L.r * (L.nyp / 8));  // N2 = 8 rows per k1
       hipError_t e = launch_three_pass_slab(s.tp, in, out, a, s.planes, st);
       return e == hipSuccess ? CFP_SUCCESS : hip_error(e, "slab 3-sweep launch");
     }
@@ -410,6 +427,7 @@ struct SlabRank {
       return e == hipSuccess ? CFP_SUCCESS : hip_error(e, "slab repack");
     }
     PassDesc p = s.pass;
+    if (p.ncols == 0) return CFP_SUCCESS;  // a rank without z-pencil rows (padded layouts)
     if (s.fused == 1) { p.colsym = colsym; p.axsym = axsym; }
     if (s.fused == 2) p.diag = diag_t;  // the z-pencil Diag, addressed like the pass input
     hipError_t e = launch_axis_pass(p, in, out, tw.at(p.n), st);
@@ -445,6 +463,15 @@ struct cfp_group_s {
 };
 
 // ------------------------------------------------------------------ host-only descriptions
+extern "C" int cfp_slab_work_size(int64_t nx, int64_t ny, int64_t nz, int P, int r, int64_t* n) {
+  if (!n) return set_error(CFP_ERR_ARG_NULL, "n is NULL");
+  SlabLayout L;
+  int rc = make_layout(nx, ny, nz, P, r, &L);
+  if (rc) return rc;
+  *n = L.work;
+  return CFP_SUCCESS;
+}
+
 extern "C" int cfp_slab_layout(int64_t nx, int64_t ny, int64_t nz, int P, int r, int64_t* out) {
   if (!out) return set_error(CFP_ERR_ARG_NULL, "out is NULL");
   SlabLayout L;
@@ -497,7 +524,7 @@ static void describe(const SlabLayout& L, const Step& s, int64_t* desc, double* 
       ps ? p.out.inner_stride : 0, ps ? p.out.outer_stride : 0, ps ? p.out.pt_stride : 0, ps ? p.out.seg_len : 0,
       ps ? p.out.seg_stride : 0,
       s.src_off, s.dst_off, s.ex_off, s.ex_cnt, L.chunk, s.wait,
-      s.kind == K_TP ? ilog2_exact(L.nyl) : 0, s.kind == K_TP ? (int64_t)(L.r * (L.nyl / 8)) : 0, s.seg, s.fused};
+      s.kind == K_TP ? ilog2_exact(L.nyp) : 0, s.kind == K_TP ? (int64_t)(L.r * (L.nyp / 8)) : 0, s.seg, s.fused};
   std::memcpy(desc, v, sizeof(v));
   *scale = (ps || s.kind == K_TP) ? p.scale : 1.0;
 }
@@ -615,7 +642,7 @@ extern "C" int cfp_dist_plan_work_buffer(cfp_dist_plan_t p, double** work) {
   return CFP_SUCCESS;
 }
 
-// use a caller-owned work buffer (local_size complex values) instead of the plan's own
+// use a caller-owned work buffer (cfp_slab_work_size complex values) instead of the plan's own
 extern "C" int cfp_dist_plan_set_work_buffer(cfp_dist_plan_t p, double* work) {
   return cfp_dist_plan_set_work_buffers(p, work, nullptr);
 }
@@ -833,7 +860,7 @@ extern "C" int cfp_dist_plan_set_diag(cfp_dist_plan_t p, const double* diag_loca
   if (!p || !diag_local) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
   HIPCHK(hipSetDevice(p->R.device));
   SlabRank& R = p->R;
-  if (!R.diag_t) HIPCHK(hipMalloc(&R.diag_t, sizeof(cd) * (size_t)R.L.local));
+  if (!R.diag_t) HIPCHK(hipMalloc(&R.diag_t, sizeof(cd) * (size_t)R.L.work));
   const std::vector<Step> st = slab_steps(R.L, R.schedule, 1, L_DIAG_T);
   int rc = dist_run(p, st, (const cd*)diag_local, nullptr, (hipStream_t)stream, nullptr);
   if (rc) return rc;

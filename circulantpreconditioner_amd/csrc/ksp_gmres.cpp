@@ -236,10 +236,13 @@ static void converged(KSP k, PetscReal rnorm0) {
   else if (k->its > 0 && k->rnorm >= k->dtol * rnorm0) k->reason = KSP_DIVERGED_DTOL;
 }
 
-// preconditioned residual into z (left: z = B (b - A x); right: z = b - A x)
+// preconditioned residual into z (left: z = B (b - A x); right: z = b - A x).  x = 0: left,
+// z = B b straight from b (no copy of b); right, z = a copy of b.
 static PetscErrorCode residual(KSP k, Vec b, Vec x, bool x_zero, Vec z) {
   Vec r = k->side == PC_LEFT ? k->t : z;
-  if (x_zero) {
+  if (x_zero && k->side == PC_LEFT) {
+    r = b;
+  } else if (x_zero) {
     PetscCall(VecCopy(b, r));
   } else {
     PetscCall(MatMult(k->A, x, k->t2));
@@ -260,24 +263,38 @@ extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
   k->pc_calls = 0;
   k->pc_seconds = 0.0;
   k->pc_ev_used = 0;
-  // KSPSolve(ksp, Un, Un): PETSc copies the right-hand side when b == x
-  if (b == x) {
-    PetscCall(VecCopy(b, k->rhs));
-    b = k->rhs;
-  }
   if (k->type == KSPPREONLY) {
+    if (b == x) {  // PCApply needs x != y
+      PetscCall(VecCopy(b, k->rhs));
+      b = k->rhs;
+    }
     PetscCall(pc_apply(k, b, x));
     k->its = 1;
     k->reason = KSP_CONVERGED_ITS;
     return pc_collect(k);
   }
-  bool x_zero = !k->guess_nonzero;
-  if (x_zero) PetscCall(VecSet(x, 0.0));
+  // KSPSolve(ksp, Un, Un): PETSc copies the right-hand side when b == x.  Here b is read from x
+  // until x is first written (the end of the first cycle), and copied only if a restart follows.
+  bool b_in_x = b == x;
+  // x = 0 initially: not set here; the first solution update overwrites x (VecMiniMAXPYNorm)
+  bool x_zero = !k->guess_nonzero, x_unset = x_zero;
 
   std::vector<C> H((size_t)(m + 1) * m), cc((size_t)m), ss((size_t)m), rs((size_t)m + 1), y((size_t)m);
   auto h = [&](PetscInt i, PetscInt j) -> C& { return H[(size_t)j * (m + 1) + i]; };
   PetscReal rnorm0 = -1.0;
   Vec* V = k->V;
+  // The basis is kept unnormalised: v_i = sg[i] u_i with u_i = V[i].  The normalisations are
+  // folded into the Gram-Schmidt coefficients (h_ij = sg_i sg_j u_i^H w' for w' = B A u_j, and
+  // w'' = w' - sum sg_i^2 (u_i^H w') u_i = w / sg_j), the norm rides in the orthogonalisation
+  // sweep, so no VecScale sweep of a basis vector remains.  Same iterates as PETSc's
+  // KSPGMRESCycle up to rounding.
+  std::vector<double> sg((size_t)m + 1, 1.0);
+  const auto renormalise = [&](PetscInt i) -> PetscErrorCode {  // keep |u_i| within range
+    if (sg[(size_t)i] > 1e-150 && sg[(size_t)i] < 1e150) return PETSC_SUCCESS;
+    PetscCall(VecScale(V[i], sg[(size_t)i]));
+    sg[(size_t)i] = 1.0;
+    return PETSC_SUCCESS;
+  };
 
   while (true) {
     PetscCall(residual(k, b, x, x_zero, V[0]));
@@ -289,13 +306,14 @@ extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
     converged(k, rnorm0);
     if (k->reason != KSP_CONVERGED_ITERATING) break;
     if (k->its >= k->maxits) { k->reason = KSP_DIVERGED_ITS; break; }
-    PetscCall(VecScale(V[0], 1.0 / beta));
+    sg[0] = 1.0 / beta;
+    PetscCall(renormalise(0));
     std::fill(rs.begin(), rs.end(), C(0.0));
     rs[0] = beta;
     PetscInt j = 0;
     bool happy = false;
     for (; j < m && k->reason == KSP_CONVERGED_ITERATING && k->its < k->maxits; ++j) {
-      // w = B A v_j (left) or A B v_j (right), written into V[j+1]
+      // w' = B A u_j (left) or A B u_j (right), written into V[j+1]; w = sg_j w'
       if (k->side == PC_LEFT) {
         PetscCall(MatMult(k->A, V[j], k->t));
         PetscCall(pc_apply(k, k->t, V[j + 1]));
@@ -303,22 +321,25 @@ extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
         PetscCall(pc_apply(k, V[j], k->t));
         PetscCall(MatMult(k->A, k->t, V[j + 1]));
       }
-      // classical Gram-Schmidt: h_ij = v_i^H w, w -= sum h_ij v_i
+      // classical Gram-Schmidt: h_ij = v_i^H w, w -= sum h_ij v_i, and |w|, in two sweeps
       std::vector<PetscScalar> hv((size_t)j + 1);
       PetscCall(VecMDot(V[j + 1], j + 1, V, hv.data()));
       std::vector<PetscScalar> neg((size_t)j + 1);
       for (PetscInt i = 0; i <= j; ++i) {
-        h(i, j) = hv[(size_t)i];
-        neg[(size_t)i] = -hv[(size_t)i];
+        h(i, j) = sg[(size_t)i] * sg[(size_t)j] * hv[(size_t)i];
+        neg[(size_t)i] = -(sg[(size_t)i] * sg[(size_t)i]) * hv[(size_t)i];
       }
-      PetscCall(VecMAXPY(V[j + 1], j + 1, neg.data(), V));
       PetscReal hn;
-      PetscCall(VecNorm(V[j + 1], NORM_2, &hn));
+      PetscCall(VecMiniMAXPYNorm(V[j + 1], j + 1, neg.data(), V, PETSC_FALSE, &hn));
+      hn *= sg[(size_t)j];  // |w| = sg_j |w''|
       h(j + 1, j) = hn;
       // happy breakdown test of KSPGMRESCycle: hn < min(hn / |rs_j|, haptol = 1e-30)
       const double hapbnd = std::fmin(hn / std::abs(rs[(size_t)j]), 1e-30);
       happy = hn < hapbnd;
-      if (!happy) PetscCall(VecScale(V[j + 1], 1.0 / hn));
+      if (!happy) {
+        sg[(size_t)j + 1] = sg[(size_t)j] / hn;  // v_{j+1} = w / hn = (sg_j / hn) w''
+        PetscCall(renormalise(j + 1));
+      }
       // KSPGMRESUpdateHessenberg: previous rotations, then a new one
       for (PetscInt i = 0; i < j; ++i) {
         const C tt = h(i, j);
@@ -351,19 +372,31 @@ extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
       for (PetscInt q = i + 1; q < kk; ++q) s -= h(i, q) * y[(size_t)q];
       y[(size_t)i] = s / h(i, i);
     }
+    // a restart follows: keep b before x (which holds it) is written
+    if (b_in_x && k->reason == KSP_CONVERGED_ITERATING) {
+      PetscCall(VecCopy(x, k->rhs));
+      b = k->rhs;
+      b_in_x = false;
+    }
     if (kk > 0) {
-      std::vector<PetscScalar> yy(y.begin(), y.begin() + kk);
+      std::vector<PetscScalar> yy((size_t)kk);
+      for (PetscInt i = 0; i < kk; ++i) yy[(size_t)i] = y[(size_t)i] * sg[(size_t)i];  // v_i = sg_i u_i
       if (k->side == PC_LEFT) {
-        PetscCall(VecMAXPY(x, kk, yy.data(), V));
+        PetscCall(VecMiniMAXPYNorm(x, kk, yy.data(), V, x_unset ? PETSC_TRUE : PETSC_FALSE, nullptr));
       } else {
-        PetscCall(VecSet(k->t2, 0.0));
-        PetscCall(VecMAXPY(k->t2, kk, yy.data(), V));
-        PetscCall(pc_apply(k, k->t2, k->t));
-        PetscCall(VecAXPY(x, 1.0, k->t));
+        PetscCall(VecMiniMAXPYNorm(k->t2, kk, yy.data(), V, PETSC_TRUE, nullptr));
+        if (x_unset) {
+          PetscCall(pc_apply(k, k->t2, x));
+        } else {
+          PetscCall(pc_apply(k, k->t2, k->t));
+          PetscCall(VecAXPY(x, 1.0, k->t));
+        }
       }
+      x_unset = false;
     }
     if (k->reason != KSP_CONVERGED_ITERATING) break;
   }
+  if (x_unset) PetscCall(VecSet(x, 0.0));  // converged before any update (b = 0): x = 0
   return pc_collect(k);
 }
 #endif  // CFP_WITH_PETSC

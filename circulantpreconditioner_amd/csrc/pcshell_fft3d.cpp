@@ -277,7 +277,8 @@ PetscErrorCode create_dist(FFTShell* s, MPI_Comm comm, int dev) {
 
 // ------------------------------------------------------------------ FFT matrix
 // MatCreateFFT(comm, ndim, dims, MATFFTW) of the reference (src/PCSHELLFft_3D.cxx:34-35): one
-// rank -> the single-GPU plan; several -> this rank's z slab (needs nranks | n_z, n_y)
+// rank -> the single-GPU plan; several -> this rank's z slab (needs nranks | n_z; n_y is split
+// in FFTW-MPI's blocks of ceil(n_y / nranks) rows, any n_y)
 extern "C" PetscErrorCode MatCreateFFTHIP(MPI_Comm comm, PetscInt ndim, const PetscInt dims[], Mat* A) {
   PetscCheck(ndim >= 1 && ndim <= 3, PETSC_COMM_SELF, PETSC_ERR_ARG_OUTOFRANGE, "ndim must be 1, 2 or 3");
   PetscCheck(dims && A, PETSC_COMM_SELF, PETSC_ERR_ARG_NULL, "NULL argument");

@@ -966,6 +966,44 @@ extern "C" PetscErrorCode VecMAXPY(Vec y, PetscInt nv, const PetscScalar alpha[]
   return PETSC_SUCCESS;
 }
 
+extern "C" PetscErrorCode VecMiniMAXPYNorm(Vec y, PetscInt nv, const PetscScalar alpha[], Vec x[], PetscBool overwrite,
+                                            PetscReal* norm) {
+  VCHK(y);
+  bool dev = y->hip;
+  for (PetscInt j = 0; j < nv; ++j) {
+    VCHK(x[j]);
+    PetscCall(same_size(y, x[j]));
+    dev = dev && x[j]->hip;
+  }
+  if (!dev) {  // host: the unfused operations
+    if (overwrite) PetscCall(VecSet(y, 0.0));
+    if (nv > 0) PetscCall(VecMAXPY(y, nv, alpha, x));
+    if (norm) PetscCall(VecNorm(y, NORM_2, norm));
+    return PETSC_SUCCESS;
+  }
+  std::vector<const cd*> xs((size_t)(nv > 0 ? nv : 1));
+  std::vector<cd> a((size_t)(nv > 0 ? nv : 1));
+  for (PetscInt j = 0; j < nv; ++j) {
+    PetscCall(dev_read(x[j], &xs[(size_t)j]));
+    a[(size_t)j] = tocd(alpha[j]);
+  }
+  cd* yd;
+  if (overwrite) {  // no read of y: nothing to bring to the device first
+    touch(y);
+    y->mask = MASK_GPU;
+    yd = y->d;
+  } else {
+    PetscCall(dev_rw(y, &yd));
+  }
+  double s2 = 0.0;
+  HIPK(cfp::blas_maxpy_norm(yd, (int)nv, a.data(), xs.data(), y->n, overwrite, norm ? &s2 : nullptr, g_stream));
+  if (norm) {
+    PetscCall(vec_reduce(y, &s2, 1, PETSCMINI_OP_SUM));
+    *norm = std::sqrt(s2);
+  }
+  return PETSC_SUCCESS;
+}
+
 extern "C" PetscErrorCode VecDuplicateVecs(Vec v, PetscInt m, Vec* V[]) {
   VCHK(v);
   if (!V) return ERR(PETSC_ERR_ARG_NULL, "NULL output");

@@ -28,12 +28,19 @@ def _slab_schedule(schedule) -> int:
 
 
 def slab_layout(dims: Sequence[int], nranks: int, rank: int) -> dict:
-    """Host-only layout query (no GPU needed)."""
+    """Host-only layout query (no GPU needed).  ny_local: this rank's z-pencil rows (blocks of
+    ny_chunk = ceil(ny / nranks), FFTW-MPI's split; the last ranks may hold fewer);
+    work_size: elements of one work buffer (max(local_size, nranks * chunk))."""
     nx, ny, nz = (int(d) for d in dims)
     out = (ctypes.c_int64 * 8)()
     check(lib().cfp_slab_layout(nx, ny, nz, int(nranks), int(rank), out))
     keys = ("nz_local", "ny_local", "z0", "y0", "local_size", "chunk", "local_offset", "nranks")
-    return dict(zip(keys, list(out)))
+    d = dict(zip(keys, list(out)))
+    w = ctypes.c_int64()
+    check(lib().cfp_slab_work_size(nx, ny, nz, int(nranks), int(rank), ctypes.byref(w)))
+    d["work_size"] = w.value
+    d["ny_chunk"] = d["chunk"] // (d["nz_local"] * nx)
+    return d
 
 
 STEP_KEYS = ("kind", "src", "dst", "axis", "n", "mode", "ncols", "inner_n",
@@ -102,7 +109,7 @@ class SlabPlan:
         elif exchange == "torch":
             check(lib().cfp_dist_plan_create_external(ctypes.byref(h), nx, ny, nz, self.world, self.rank,
                                                       self.device))
-            self.work = torch.empty(self.local_size, dtype=torch.complex128, device=f"cuda:{self.device}")
+            self.work = torch.empty(self.layout["work_size"], dtype=torch.complex128, device=f"cuda:{self.device}")
             self.work2 = torch.empty_like(self.work)
             check(lib().cfp_dist_plan_set_work_buffers(h, self.work.data_ptr(), self.work2.data_ptr()))
         else:

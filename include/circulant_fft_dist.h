@@ -4,8 +4,9 @@
  * Layout: rank r of P owns the z-planes [r*nz/P, (r+1)*nz/P) of the
  * x-fastest grid, i.e. the contiguous rows [r*N/P, (r+1)*N/P) -- exactly PETSc's
  * PETSC_DECIDE distribution of VecCreateMPI (tests/TransportEquationFFT_..._mpi.cxx:66) and
- * FFTW-MPI's local_n0 slabs of MATFFTW (src/PCSHELLFft_3D.cxx:34-35).  Requires P | nz and
- * P | ny.
+ * FFTW-MPI's local_n0 slabs of MATFFTW (src/PCSHELLFft_3D.cxx:34-35).  Requires P | nz; ny
+ * is split into blocks of ceil(ny / P) rows for the z pass, as FFTW-MPI splits its transposed
+ * dimension (cfp_slab_layout), so P need not divide ny.
  *
  * One apply = x-fwd, y-fwd (written straight into per-peer send chunks), all-to-all,
  * z: DFT ./Diag IDFT, all-to-all back, y-inv (read straight from the received chunks),
@@ -40,8 +41,14 @@ typedef struct cfp_group_s *cfp_group_t;
 
 /* host-only layout query: out[0..8) = {nz_local, ny_local, z0, y0, local_size,
  * chunk (elements per peer message), local_offset (global index of the first local element),
- * nranks} */
+ * nranks}.  nranks must divide nz (whole z-planes: PETSC_DECIDE rows); ny is split as FFTW-MPI
+ * splits its transposed dimension, in blocks of ceil(ny / nranks) rows: rank r transforms the
+ * z-pencil rows [y0, y0 + ny_local) with y0 = r ceil(ny / nranks), and the last ranks may hold
+ * fewer rows (or none).  chunk = nz_local * ceil(ny / nranks) * nx (padded rows included). */
 int cfp_slab_layout(int64_t nx, int64_t ny, int64_t nz, int nranks, int rank, int64_t *out);
+/* elements of one work buffer of the slab plan: max(local_size, nranks * chunk) (they differ
+ * when nranks does not divide ny); cfp_dist_plan_set_work_buffers takes buffers of this size */
+int cfp_slab_work_size(int64_t nx, int64_t ny, int64_t nz, int nranks, int rank, int64_t *n);
 
 /* Host-only description of rank `rank`'s step list (no GPU needed; tests replay it on the CPU
  * across processes).  schedule: CFP_SCHEDULE_AUTO / _FIVE_PASS / _THREE_PASS (AUTO resolves as
@@ -105,9 +112,9 @@ typedef int (*cfp_dist_exchange_fn)(void *user, const double *src_dev, double *d
                                     int64_t count, void *stream);
 int cfp_dist_plan_set_exchange(cfp_dist_plan_t plan, cfp_dist_exchange_fn fn, void *user);
 int cfp_dist_plan_work_buffer(cfp_dist_plan_t plan, double **work_dev);
-int cfp_dist_plan_set_work_buffer(cfp_dist_plan_t plan, double *work_dev); /* caller-owned, local_size values */
-/* both work buffers (W, W2: the second is used by pieces > 1 and the transforms; NULL keeps the
- * plan's own, allocated on first use) */
+int cfp_dist_plan_set_work_buffer(cfp_dist_plan_t plan, double *work_dev); /* caller-owned, cfp_slab_work_size values */
+/* both work buffers (W, W2: the second is used by pieces > 1, padded layouts and the transforms;
+ * NULL keeps the plan's own, allocated on first use), cfp_slab_work_size complex values each */
 int cfp_dist_plan_set_work_buffers(cfp_dist_plan_t plan, double *work_dev, double *work2_dev);
 int cfp_dist_plan_run_segment(cfp_dist_plan_t plan, int segment, const double *b_dev, double *x_dev, void *stream);
 int cfp_dist_plan_num_steps(cfp_dist_plan_t plan, int *nsteps);

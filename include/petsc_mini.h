@@ -223,6 +223,11 @@ PetscErrorCode VecMiniSetStream(void *stream);
 PetscErrorCode VecMiniGetStream(void **stream);
 /* wait for the work queued on that stream if v is a device vector; not in PETSc */
 PetscErrorCode VecMiniSynchronize(Vec v);
+/* y = (overwrite ? 0 : y) + sum alpha_i x_i and, if norm != NULL, ||y||_2 over the Vec's ranks,
+ * in one sweep of y (the stand-in GMRES's orthogonalisation + norm, and its solution update
+ * into a zero x without a VecSet); not in PETSc */
+PetscErrorCode VecMiniMAXPYNorm(Vec y, PetscInt nv, const PetscScalar alpha[], Vec x[], PetscBool overwrite,
+                                PetscReal *norm);
 
 /* ---- Mat */
 PetscErrorCode MatCreateShell(MPI_Comm comm, PetscInt m, PetscInt n, PetscInt M, PetscInt N, void *ctx, Mat *A);

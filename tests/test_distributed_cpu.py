@@ -62,11 +62,11 @@ def _replay_pass(st, bufs, L, dims, lam):
 def _replay_repack(st, bufs, L, dims):
     """natural planes [planes][ny][nx] <-> per-peer chunks (circulant_fft_dist.h, kind 3)"""
     nx, ny, _ = dims
-    nyl, c = L["ny_local"], L["chunk"]
+    nyp, c = L["ny_chunk"], L["chunk"]
     i = np.arange(st["ncols"] * ny * nx)
     x, row = i % nx, i // nx
     y, z = row % ny, row // ny
-    ci = (y // nyl) * c + (z * nyl + y % nyl) * nx + x
+    ci = (y // nyp) * c + (z * nyp + y % nyp) * nx + x
     src, dst = bufs[st["src"]], bufs[st["dst"]]
     if st["axis"]:  # to chunks
         dst[st["dst_off"] + ci] = src[st["src_off"] + i]
@@ -116,7 +116,8 @@ def _worker(rank, P, port, dims, lam, pieces, lists, q):
             steps = slab_steps(dims, P, rank, schedule="five", pieces=pieces, list_=lst)
             nex = [s["kind"] for s in steps].count(1)
             assert nex == (2 * pieces if lst == "apply" else 2), (lst, nex)
-            bufs = {0: b.copy(), 1: np.full(n, np.nan + 0j), 2: np.full(n, np.nan + 0j), 3: np.full(n, np.nan + 0j)}
+            w = L["work_size"]
+            bufs = {0: b.copy(), 1: np.full(n, np.nan + 0j), 2: np.full(w, np.nan + 0j), 3: np.full(w, np.nan + 0j)}
             _replay(steps, bufs, L, dims, lam, P)
             out[lst] = (bufs[1].copy(), np.array_equal(bufs[0], b))
         q.put((rank, L["local_offset"], out))
@@ -151,7 +152,10 @@ def _run(P, dims, lam, pieces, lists):
 @pytest.mark.parametrize("P,dims,pieces", [(2, (16, 8, 12), 1), (2, (10, 6, 4), 1), (4, (8, 16, 8), 1),
                                            (2, (1, 4, 6), 1), (2, (16, 8, 12), 2), (2, (16, 8, 12), 3),
                                            (2, (16, 8, 12), 6), (4, (8, 16, 8), 2), (2, (10, 6, 8), 4),
-                                           (2, (1, 4, 6), 3)])
+                                           (2, (1, 4, 6), 3),
+                                           # P does not divide ny (FFTW-MPI's ceil(ny / P) row blocks)
+                                           (2, (8, 7, 6), 1), (4, (16, 10, 8), 1), (4, (16, 10, 8), 2),
+                                           (4, (6, 3, 8), 1), (3, (5, 7, 9), 3), (4, (64, 30, 32), 1)])
 def test_slab_schedule_gloo(P, dims, pieces, oracle):
     """The library's apply step list (five passes, `pieces` exchange pieces), replayed across
     P gloo processes, against the oracle's full-grid solve."""

@@ -60,6 +60,22 @@ def test_slab_layout(dims, P):
     assert tot == nx * ny * nz
 
 
+@pytest.mark.parametrize("dims,P,rows", [((64, 30, 32), 4, [8, 8, 8, 6]), ((8, 3, 8), 4, [1, 1, 1, 0]),
+                                         ((256, 100, 256), 8, [13] * 7 + [9]), ((64, 40, 32), 4, [10] * 4)])
+def test_slab_layout_uneven_y(dims, P, rows):
+    """P need not divide ny: FFTW-MPI's blocks of ceil(ny / P) z-pencil rows, padded chunks."""
+    from circulantpreconditioner_amd.distributed import slab_layout
+    nx, ny, nz = dims
+    nyp = -(-ny // P)
+    for r in range(P):
+        L = slab_layout(dims, P, r)
+        assert L["ny_local"] == rows[r] and L["y0"] == r * nyp and L["ny_chunk"] == nyp
+        assert L["chunk"] == (nz // P) * nyp * nx
+        assert L["local_size"] == nx * ny * nz // P and L["local_offset"] == r * L["local_size"]
+        assert L["work_size"] == max(L["local_size"], P * L["chunk"])
+    assert sum(rows) == ny
+
+
 def test_slab_layout_errors():
     import circulantpreconditioner_amd as cp
     from circulantpreconditioner_amd.distributed import slab_layout

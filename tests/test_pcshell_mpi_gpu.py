@@ -105,7 +105,8 @@ def _rank(rank, world, port, dims, lam, pieces, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dims,world,pieces", [((32, 16, 24), 2, 0), ((64, 64, 64), 2, 4), ((32, 32, 16), 4, 2)])
+@pytest.mark.parametrize("dims,world,pieces", [((32, 16, 24), 2, 0), ((64, 64, 64), 2, 4), ((32, 32, 16), 4, 2),
+                                               ((32, 30, 16), 4, 0), ((64, 40, 32), 4, 0)])  # P | n_y or not
 def test_pcshell_and_direct_solver_on_several_ranks(dims, world, pieces, oracle):
     import torch.multiprocessing as mp
     lam = (0.6, 0.15 - 0.1j, 0.02)

@@ -143,6 +143,21 @@ def test_ksp_b_equals_x_and_maxits():
     xo, its_o, reason_o, _, _ = OT.gmres(A, b, rtol=1e-12, maxits=7)
     assert its_o == 7 and reason_o == -3
     np.testing.assert_allclose(v.array(), xo, rtol=0, atol=1e-10 * np.abs(xo).max())
+    # in place across restarts: b lives in x until the first update, then in the KSP's copy
+    for side in ("left", "right"):
+        ksp.set_tolerances(1e-10, 1e-50, P.PETSC_DEFAULT, 500).set_restart(3)
+        ksp.set_pc_side(P.PC_LEFT if side == "left" else P.PC_RIGHT)
+        v = P.Vec.seq(n).set_array(b)
+        assert ksp.solve(v, v) == 2
+        xo, its_o, reason_o, _, _ = OT.gmres(A, b, rtol=1e-10, maxits=500, restart=3, side=side)
+        assert ksp.its == its_o and reason_o == 2
+        np.testing.assert_allclose(v.array(), xo, rtol=0, atol=1e-9 * np.abs(xo).max())
+    # b = 0: converged before any update, x = 0 whatever it held
+    v = P.Vec.seq(n).set_array(np.zeros(n, dtype=complex))
+    ksp.set_tolerances(1e-10, 1e-50, P.PETSC_DEFAULT, 500)
+    xz = P.Vec.seq(n).set_array(np.ones(n, dtype=complex))
+    ksp.solve(v, xz)
+    assert ksp.its == 0 and np.array_equal(xz.array(), np.zeros(n))
 
 
 def test_ksp_errors():

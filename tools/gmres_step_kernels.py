@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Device time per implicit step of a GMRES run, by kernel, from a rocprofv3 kernel trace.
+
+The solve region starts after the setup (vector fills, the Diag build) with the first step's
+leading copies; the number of implicit steps comes from --steps (the run's own count).  Prints
+per-kernel calls, median and total microseconds, and the device busy time per step.
+
+    python tools/gmres_step_kernels.py gpurun_out/r04a_gmres256_trace [--steps 6]
+"""
+import argparse
+import collections
+import csv
+import glob
+import os
+import statistics
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace_dir")
+    ap.add_argument("--steps", type=int, default=6)
+    a = ap.parse_args()
+    paths = glob.glob(os.path.join(a.trace_dir, "**", "*kernel_trace.csv"), recursive=True)
+    rows = []
+    for p in paths:
+        with open(p) as f:
+            for r in csv.DictReader(f):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    first = next(i for i, r in enumerate(rows) if "k_csr_spmv" in r[2])
+    # the step's leading copies / sets queued before the first SpMV belong to the solve region
+    while first > 0 and "fillBufferAligned" not in rows[first - 1][2] and "k_build_diag" not in rows[first - 1][2]:
+        first -= 1
+    sol = rows[first:]
+    by = collections.defaultdict(list)
+    for s, e, n in sol:
+        key = n.split("(")[0][:60]
+        by[key].append((e - s) / 1e3)
+    tot = sum(sum(v) for v in by.values())
+    print(f"solve region: {len(sol)} kernels, device busy {tot:.1f} us, {tot / a.steps:.1f} us per step "
+          f"({a.steps} steps), span {(sol[-1][1] - sol[0][0]) / 1e3 / a.steps:.1f} us per step")
+    for k, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
+        print(f"{k:60s} calls {len(v):4d}  median {statistics.median(v):7.1f} us  total {sum(v):8.1f} us  "
+              f"per step {sum(v) / a.steps:7.1f} us")
+
+
+if __name__ == "__main__":
+    main()
