@@ -1,11 +1,18 @@
-// cfp_blas.h -- device vector kernels of the PETSc-compatible layer (cfp_blas.hip).
+// cfp_blas.h -- device vector kernels of the PETSc-compatible layer (cfp_blas.hip), for complex
+// double (the default stand-in PETSc) and double (the real-scalar build, PetscScalar = double).
 #pragma once
+#include <type_traits>
+#include <vector>
+
 #include "cfp_internal.h"
 
 namespace cfp {
 #define MV_MAX 32
-struct MVPtrs { const cd* p[MV_MAX]; };
-struct MVCoef { cd a[MV_MAX]; };
+template <class T> struct MVPtrsT { const T* p[MV_MAX]; };
+template <class T> struct MVCoefT { T a[MV_MAX]; };
+using MVPtrs = MVPtrsT<cd>;
+using MVCoef = MVCoefT<cd>;
+
 hipError_t blas_set(cd* x, cd a, i64 n, hipStream_t s);
 hipError_t blas_shift(cd* x, cd a, i64 n, hipStream_t s);
 hipError_t blas_copy(cd* y, const cd* x, i64 n, hipStream_t s);
@@ -28,4 +35,24 @@ hipError_t blas_dot(const cd* x, const cd* y, i64 n, cd* val, hipStream_t s);
 hipError_t blas_norm(const cd* x, i64 n, int type, double* val, hipStream_t s);
 // vals[j] = ys[j]^H x  (ys: host array of k device pointers)
 hipError_t blas_mdot(const cd* x, int k, const cd* const* ys, i64 n, cd* vals, hipStream_t s);
+
+// the same on real vectors (PetscScalar = double), plus the scale and the divide that the
+// complex build takes from cfp_kernels.hip (launch_scale, launch_pointwise_divide)
+hipError_t blas_set(double* x, double a, i64 n, hipStream_t s);
+hipError_t blas_shift(double* x, double a, i64 n, hipStream_t s);
+hipError_t blas_copy(double* y, const double* x, i64 n, hipStream_t s);
+hipError_t blas_axpy(double* y, double a, const double* x, i64 n, hipStream_t s);
+hipError_t blas_aypx(double* y, double b, const double* x, i64 n, hipStream_t s);
+hipError_t blas_waxpy(double* w, double a, const double* x, const double* y, i64 n, hipStream_t s);
+hipError_t blas_pmult(double* w, const double* x, const double* y, i64 n, hipStream_t s);
+hipError_t blas_scale(double* x, double a, i64 n, hipStream_t s);
+hipError_t blas_pdivide(double* w, const double* x, const double* y, i64 n, hipStream_t s);  // 0 where y = 0
+hipError_t blas_maxpy(double* y, int k, const double* a, const double* const* xs, i64 n, hipStream_t s);
+hipError_t blas_maxpy_norm(double* y, int k, const double* a, const double* const* xs, i64 n, bool overwrite,
+                           double* norm2, hipStream_t s);
+hipError_t blas_csr_spmv(i64 m, i64 nnz, const i64* rowptr, const i64* col, const double* val, const double* x,
+                         double* y, hipStream_t s);
+hipError_t blas_dot(const double* x, const double* y, i64 n, double* val, hipStream_t s);
+hipError_t blas_norm(const double* x, i64 n, int type, double* val, hipStream_t s);
+hipError_t blas_mdot(const double* x, int k, const double* const* ys, i64 n, double* vals, hipStream_t s);
 }  // namespace cfp

@@ -1,6 +1,7 @@
-// cfp_blas.hip -- device vector kernels (complex double) behind the PETSc-compatible Vec/Mat
-// layer: axpy-family updates, PETSc-convention dot / norms, CSR SpMV.  These carry the
-// GMRES harness, not the FFT hot path.
+// cfp_blas.hip -- device vector kernels behind the PETSc-compatible Vec/Mat layer: axpy-family
+// updates, PETSc-convention dot / norms, CSR SpMV.  These carry the GMRES harness (SURVEY.md §8f
+// row f1), not the FFT hot path.  Every kernel is templated on the scalar: complex double (cd,
+// the default stand-in PETSc) and double (the real-scalar build, PetscScalar = double).
 #include "cfp_blas.h"
 
 namespace cfp {
@@ -8,8 +9,25 @@ namespace cfp {
 #define BLAS_THREADS 256
 #define RED_BLOCKS 1024
 
-__device__ __forceinline__ cd bcadd(cd a, cd b) { return make_cd(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ cd bcmul(cd a, cd b) { return make_cd(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+__device__ __forceinline__ cd badd(cd a, cd b) { return make_cd(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ cd bmul(cd a, cd b) { return make_cd(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+__device__ __forceinline__ double badd(double a, double b) { return a + b; }
+__device__ __forceinline__ double bmul(double a, double b) { return a * b; }
+template <class T> __device__ __forceinline__ T bzero();
+template <> __device__ __forceinline__ cd bzero<cd>() { return make_cd(0.0, 0.0); }
+template <> __device__ __forceinline__ double bzero<double>() { return 0.0; }
+// |v|^2, and the dot contribution u conj(v) as (re, im)
+__device__ __forceinline__ double babs2(cd v) { return v.x * v.x + v.y * v.y; }
+__device__ __forceinline__ double babs2(double v) { return v * v; }
+__device__ __forceinline__ double babs1(cd v) { return fabs(v.x) + fabs(v.y); }
+__device__ __forceinline__ double babs1(double v) { return fabs(v); }
+__device__ __forceinline__ double bmod(cd v) { return hypot(v.x, v.y); }
+__device__ __forceinline__ double bmod(double v) { return fabs(v); }
+__device__ __forceinline__ void bdot(cd u, cd v, double& a, double& b) {
+  a += u.x * v.x + u.y * v.y;
+  b += u.y * v.x - u.x * v.y;
+}
+__device__ __forceinline__ void bdot(double u, double v, double& a, double&) { a += u * v; }
 
 static unsigned nblocks(i64 n) {
   i64 b = (n + BLAS_THREADS - 1) / BLAS_THREADS;
@@ -19,25 +37,23 @@ static unsigned nblocks(i64 n) {
 
 #define GRID_LOOP(i, n) for (i64 i = (i64)blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += (i64)gridDim.x * blockDim.x)
 
-__global__ void k_set(cd* x, cd a, i64 n) { GRID_LOOP(i, n) x[i] = a; }
-__global__ void k_shift(cd* x, cd a, i64 n) { GRID_LOOP(i, n) x[i] = bcadd(x[i], a); }
-__global__ void k_copy(cd* y, const cd* x, i64 n) { GRID_LOOP(i, n) y[i] = x[i]; }
+template <class T> __global__ void k_set(T* x, T a, i64 n) { GRID_LOOP(i, n) x[i] = a; }
+template <class T> __global__ void k_shift(T* x, T a, i64 n) { GRID_LOOP(i, n) x[i] = badd(x[i], a); }
+template <class T> __global__ void k_copy(T* y, const T* x, i64 n) { GRID_LOOP(i, n) y[i] = x[i]; }
+template <class T> __global__ void k_scal(T* x, T a, i64 n) { GRID_LOOP(i, n) x[i] = bmul(a, x[i]); }
 // y = y + a x
-__global__ void k_axpy(cd* y, cd a, const cd* x, i64 n) { GRID_LOOP(i, n) y[i] = bcadd(y[i], bcmul(a, x[i])); }
+template <class T> __global__ void k_axpy(T* y, T a, const T* x, i64 n) { GRID_LOOP(i, n) y[i] = badd(y[i], bmul(a, x[i])); }
 // y = x + b y
-__global__ void k_aypx(cd* y, cd b, const cd* x, i64 n) { GRID_LOOP(i, n) y[i] = bcadd(x[i], bcmul(b, y[i])); }
+template <class T> __global__ void k_aypx(T* y, T b, const T* x, i64 n) { GRID_LOOP(i, n) y[i] = badd(x[i], bmul(b, y[i])); }
 // w = a x + y
-__global__ void k_waxpy(cd* w, cd a, const cd* x, const cd* y, i64 n) {
-  GRID_LOOP(i, n) w[i] = bcadd(bcmul(a, x[i]), y[i]);
+template <class T> __global__ void k_waxpy(T* w, T a, const T* x, const T* y, i64 n) {
+  GRID_LOOP(i, n) w[i] = badd(bmul(a, x[i]), y[i]);
 }
-__global__ void k_pmult(cd* w, const cd* x, const cd* y, i64 n) { GRID_LOOP(i, n) w[i] = bcmul(x[i], y[i]); }
-// y += sum_j a_j x_j  (the GMRES basis update, up to MV_MAX vectors per launch)
-__global__ void k_maxpy(cd* y, int k, MVCoef a, MVPtrs xs, i64 n) {
-  GRID_LOOP(i, n) {
-    cd acc = y[i];
-    for (int j = 0; j < k; ++j) acc = bcadd(acc, bcmul(a.a[j], xs.p[j][i]));
-    y[i] = acc;
-  }
+template <class T> __global__ void k_pmult(T* w, const T* x, const T* y, i64 n) { GRID_LOOP(i, n) w[i] = bmul(x[i], y[i]); }
+// real w = x / y with PETSc's rule: a zero divisor gives 0 (VecPointwiseDivide, bvec2.c); the
+// complex divide is launch_pointwise_divide (cfp_kernels.hip)
+__global__ void k_pdiv_real(double* w, const double* x, const double* y, i64 n) {
+  GRID_LOOP(i, n) w[i] = y[i] != 0.0 ? x[i] / y[i] : 0.0;
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -49,23 +65,42 @@ __device__ __forceinline__ double wave_max(double v) {
   return v;
 }
 
+// y = (OW ? 0 : y) + sum_j a_j x_j (the GMRES basis update, up to MV_MAX vectors per launch),
+// with NRM: per-block sums of |y|^2 of the result (one sweep)
+template <class T, bool OW, bool NRM>
+__global__ void __launch_bounds__(BLAS_THREADS) k_maxpy(T* y, int k, MVCoefT<T> a, MVPtrsT<T> xs, i64 n,
+                                                         double* partial) {
+  double s2 = 0.0;
+  GRID_LOOP(i, n) {
+    T acc = OW ? bzero<T>() : y[i];
+    for (int j = 0; j < k; ++j) acc = badd(acc, bmul(a.a[j], xs.p[j][i]));
+    y[i] = acc;
+    if (NRM) s2 += babs2(acc);
+  }
+  if constexpr (NRM) {
+    __shared__ double sm[BLAS_THREADS / 64];
+    s2 = wave_sum(s2);
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s2;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int q = 0; q < BLAS_THREADS / 64; ++q) t += sm[q];
+      partial[blockIdx.x] = t;
+    }
+  }
+}
+
 // kind: 0 = dot y^H x (re, im), 1 = sum |x|^2, 2 = sum |re|+|im|, 3 = max |x|
-__global__ void k_reduce(const cd* x, const cd* y, i64 n, int kind, double* partial) {
+template <class T>
+__global__ void k_reduce(const T* x, const T* y, i64 n, int kind, double* partial) {
   __shared__ double s0[BLAS_THREADS / 64], s1[BLAS_THREADS / 64];
   double a = 0.0, b = 0.0;
   GRID_LOOP(i, n) {
-    const cd u = x[i];
-    if (kind == 0) {
-      const cd v = y[i];  // u * conj(v)
-      a += u.x * v.x + u.y * v.y;
-      b += u.y * v.x - u.x * v.y;
-    } else if (kind == 1) {
-      a += u.x * u.x + u.y * u.y;
-    } else if (kind == 2) {
-      a += fabs(u.x) + fabs(u.y);
-    } else {
-      a = fmax(a, hypot(u.x, u.y));
-    }
+    const T u = x[i];
+    if (kind == 0) bdot(u, y[i], a, b);
+    else if (kind == 1) a += babs2(u);
+    else if (kind == 2) a += babs1(u);
+    else a = fmax(a, bmod(u));
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (kind == 3) a = wave_max(a);
@@ -86,21 +121,17 @@ __global__ void k_reduce(const cd* x, const cd* y, i64 n, int kind, double* part
 // several dots against one vector, PETSc VecMDot(x, k, y[], val): val_j = y_j^H x.
 // One sweep of x per launch; up to MDOT_K accumulators per thread.
 #define MDOT_K 8
-__global__ void k_mdot(const cd* x, int k, MVPtrs ys, i64 n, double* partial) {
+template <class T>
+__global__ void k_mdot(const T* x, int k, MVPtrsT<T> ys, i64 n, double* partial) {
   __shared__ double sm[2 * MDOT_K][BLAS_THREADS / 64];
   double a[MDOT_K], b[MDOT_K];
 #pragma unroll
   for (int j = 0; j < MDOT_K; ++j) { a[j] = 0.0; b[j] = 0.0; }
   GRID_LOOP(i, n) {
-    const cd u = x[i];
+    const T u = x[i];
 #pragma unroll
-    for (int j = 0; j < MDOT_K; ++j) {
-      if (j < k) {
-        const cd v = ys.p[j][i];
-        a[j] += u.x * v.x + u.y * v.y;
-        b[j] += u.y * v.x - u.x * v.y;
-      }
-    }
+    for (int j = 0; j < MDOT_K; ++j)
+      if (j < k) bdot(u, ys.p[j][i], a[j], b[j]);
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -116,34 +147,12 @@ __global__ void k_mdot(const cd* x, int k, MVPtrs ys, i64 n, double* partial) {
   }
 }
 
-// y = (OW ? 0 : y) + sum_j a_j x_j, with NRM: per-block sums of |y|^2 of the result (one sweep)
-template <bool OW, bool NRM>
-__global__ void __launch_bounds__(BLAS_THREADS) k_maxpy_nrm(cd* y, int k, MVCoef a, MVPtrs xs, i64 n, double* partial) {
-  double s2 = 0.0;
-  GRID_LOOP(i, n) {
-    cd acc = OW ? make_cd(0.0, 0.0) : y[i];
-    for (int j = 0; j < k; ++j) acc = bcadd(acc, bcmul(a.a[j], xs.p[j][i]));
-    y[i] = acc;
-    if (NRM) s2 += acc.x * acc.x + acc.y * acc.y;
-  }
-  if constexpr (NRM) {
-    __shared__ double sm[BLAS_THREADS / 64];
-    s2 = wave_sum(s2);
-    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s2;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double t = 0.0;
-      for (int q = 0; q < BLAS_THREADS / 64; ++q) t += sm[q];
-      partial[blockIdx.x] = t;
-    }
-  }
-}
-
 // CSR y = A x, one thread per row (rows of about one nonzero)
-__global__ void k_csr_spmv(i64 m, const i64* rowptr, const i64* col, const cd* val, const cd* x, cd* y) {
+template <class T>
+__global__ void k_csr_spmv(i64 m, const i64* rowptr, const i64* col, const T* val, const T* x, T* y) {
   GRID_LOOP(r, m) {
-    cd acc = make_cd(0.0, 0.0);
-    for (i64 p = rowptr[r]; p < rowptr[r + 1]; ++p) acc = bcadd(acc, bcmul(val[p], x[col[p]]));
+    T acc = bzero<T>();
+    for (i64 p = rowptr[r]; p < rowptr[r + 1]; ++p) acc = badd(acc, bmul(val[p], x[col[p]]));
     y[r] = acc;
   }
 }
@@ -152,67 +161,70 @@ __global__ void k_csr_spmv(i64 m, const i64* rowptr, const i64* col, const cd* v
 // loads of val / col are contiguous runs over 64 / L consecutive rows (one thread per row reads
 // them at a stride of the row length: 4.5x below bandwidth on the 7-nonzero wave-system rows).
 // The L partial sums meet through lane shuffles; lane 0 of the group stores.
-template <int L>
+__device__ __forceinline__ void spmv_acc(cd a, cd b, double& ax, double& ay) {
+  ax = fma(a.x, b.x, fma(-a.y, b.y, ax));
+  ay = fma(a.x, b.y, fma(a.y, b.x, ay));
+}
+__device__ __forceinline__ void spmv_acc(double a, double b, double& ax, double&) { ax = fma(a, b, ax); }
+__device__ __forceinline__ void spmv_store(cd* y, double ax, double ay) { *y = make_cd(ax, ay); }
+__device__ __forceinline__ void spmv_store(double* y, double ax, double) { *y = ax; }
+
+template <class T, int L>
 __global__ void __launch_bounds__(BLAS_THREADS) k_csr_spmv_vec(i64 m, const i64* rowptr, const i64* col,
-                                                               const cd* val, const cd* x, cd* y) {
+                                                               const T* val, const T* x, T* y) {
   const int lane = threadIdx.x & (L - 1);
   const i64 groups = (i64)gridDim.x * (blockDim.x / L);
   for (i64 r = (i64)blockIdx.x * (blockDim.x / L) + threadIdx.x / L; r < m; r += groups) {
     const i64 p0 = rowptr[r], p1 = rowptr[r + 1];
     double ax = 0.0, ay = 0.0;
-    for (i64 p = p0 + lane; p < p1; p += L) {
-      const cd a = val[p], b = x[col[p]];
-      ax = fma(a.x, b.x, fma(-a.y, b.y, ax));
-      ay = fma(a.x, b.y, fma(a.y, b.x, ay));
-    }
+    for (i64 p = p0 + lane; p < p1; p += L) spmv_acc(val[p], x[col[p]], ax, ay);
 #pragma unroll
     for (int o = L / 2; o > 0; o >>= 1) {
       ax += __shfl_xor(ax, o, L);
-      ay += __shfl_xor(ay, o, L);
+      if constexpr (std::is_same<T, cd>::value) ay += __shfl_xor(ay, o, L);
     }
-    if (lane == 0) y[r] = make_cd(ax, ay);
+    if (lane == 0) spmv_store(y + r, ax, ay);
   }
 }
 
-hipError_t blas_set(cd* x, cd a, i64 n, hipStream_t s) {
-  if (n > 0) hipLaunchKernelGGL(k_set, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, x, a, n);
-  return hipGetLastError();
+// ------------------------------------------------------------------ host launchers
+#define L1(K, ...) \
+  do { if (n > 0) hipLaunchKernelGGL(K, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, __VA_ARGS__); return hipGetLastError(); } while (0)
+
+template <class T> static hipError_t set_t(T* x, T a, i64 n, hipStream_t s) { L1(k_set<T>, x, a, n); }
+template <class T> static hipError_t shift_t(T* x, T a, i64 n, hipStream_t s) { L1(k_shift<T>, x, a, n); }
+template <class T> static hipError_t copy_t(T* y, const T* x, i64 n, hipStream_t s) { L1(k_copy<T>, y, x, n); }
+template <class T> static hipError_t axpy_t(T* y, T a, const T* x, i64 n, hipStream_t s) { L1(k_axpy<T>, y, a, x, n); }
+template <class T> static hipError_t aypx_t(T* y, T b, const T* x, i64 n, hipStream_t s) { L1(k_aypx<T>, y, b, x, n); }
+template <class T> static hipError_t waxpy_t(T* w, T a, const T* x, const T* y, i64 n, hipStream_t s) {
+  L1(k_waxpy<T>, w, a, x, y, n);
 }
-hipError_t blas_shift(cd* x, cd a, i64 n, hipStream_t s) {
-  if (n > 0) hipLaunchKernelGGL(k_shift, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, x, a, n);
-  return hipGetLastError();
+template <class T> static hipError_t pmult_t(T* w, const T* x, const T* y, i64 n, hipStream_t s) {
+  L1(k_pmult<T>, w, x, y, n);
 }
-hipError_t blas_copy(cd* y, const cd* x, i64 n, hipStream_t s) {
-  if (n > 0) hipLaunchKernelGGL(k_copy, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, y, x, n);
-  return hipGetLastError();
+
+hipError_t blas_set(cd* x, cd a, i64 n, hipStream_t s) { return set_t(x, a, n, s); }
+hipError_t blas_shift(cd* x, cd a, i64 n, hipStream_t s) { return shift_t(x, a, n, s); }
+hipError_t blas_copy(cd* y, const cd* x, i64 n, hipStream_t s) { return copy_t(y, x, n, s); }
+hipError_t blas_axpy(cd* y, cd a, const cd* x, i64 n, hipStream_t s) { return axpy_t(y, a, x, n, s); }
+hipError_t blas_aypx(cd* y, cd b, const cd* x, i64 n, hipStream_t s) { return aypx_t(y, b, x, n, s); }
+hipError_t blas_waxpy(cd* w, cd a, const cd* x, const cd* y, i64 n, hipStream_t s) { return waxpy_t(w, a, x, y, n, s); }
+hipError_t blas_pmult(cd* w, const cd* x, const cd* y, i64 n, hipStream_t s) { return pmult_t(w, x, y, n, s); }
+hipError_t blas_set(double* x, double a, i64 n, hipStream_t s) { return set_t(x, a, n, s); }
+hipError_t blas_shift(double* x, double a, i64 n, hipStream_t s) { return shift_t(x, a, n, s); }
+hipError_t blas_copy(double* y, const double* x, i64 n, hipStream_t s) { return copy_t(y, x, n, s); }
+hipError_t blas_axpy(double* y, double a, const double* x, i64 n, hipStream_t s) { return axpy_t(y, a, x, n, s); }
+hipError_t blas_aypx(double* y, double b, const double* x, i64 n, hipStream_t s) { return aypx_t(y, b, x, n, s); }
+hipError_t blas_waxpy(double* w, double a, const double* x, const double* y, i64 n, hipStream_t s) {
+  return waxpy_t(w, a, x, y, n, s);
 }
-hipError_t blas_axpy(cd* y, cd a, const cd* x, i64 n, hipStream_t s) {
-  if (n > 0) hipLaunchKernelGGL(k_axpy, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, y, a, x, n);
-  return hipGetLastError();
-}
-hipError_t blas_aypx(cd* y, cd b, const cd* x, i64 n, hipStream_t s) {
-  if (n > 0) hipLaunchKernelGGL(k_aypx, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, y, b, x, n);
-  return hipGetLastError();
-}
-hipError_t blas_waxpy(cd* w, cd a, const cd* x, const cd* y, i64 n, hipStream_t s) {
-  if (n > 0) hipLaunchKernelGGL(k_waxpy, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, w, a, x, y, n);
-  return hipGetLastError();
-}
-hipError_t blas_pmult(cd* w, const cd* x, const cd* y, i64 n, hipStream_t s) {
-  if (n > 0) hipLaunchKernelGGL(k_pmult, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, w, x, y, n);
-  return hipGetLastError();
-}
-hipError_t blas_maxpy(cd* y, int k, const cd* a, const cd* const* xs, i64 n, hipStream_t s) {
-  for (int j0 = 0; j0 < k; j0 += MV_MAX) {
-    const int kk = k - j0 < MV_MAX ? k - j0 : MV_MAX;
-    MVCoef c;
-    MVPtrs p;
-    for (int j = 0; j < kk; ++j) { c.a[j] = a[j0 + j]; p.p[j] = xs[j0 + j]; }
-    if (n > 0) hipLaunchKernelGGL(k_maxpy, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, y, kk, c, p, n);
-  }
-  return hipGetLastError();
-}
-hipError_t blas_csr_spmv(i64 m, i64 nnz, const i64* rowptr, const i64* col, const cd* val, const cd* x, cd* y,
+hipError_t blas_pmult(double* w, const double* x, const double* y, i64 n, hipStream_t s) { return pmult_t(w, x, y, n, s); }
+hipError_t blas_scale(double* x, double a, i64 n, hipStream_t s) { L1(k_scal<double>, x, a, n); }
+hipError_t blas_pdivide(double* w, const double* x, const double* y, i64 n, hipStream_t s) { L1(k_pdiv_real, w, x, y, n); }
+#undef L1
+
+template <class T>
+static hipError_t spmv_t(i64 m, i64 nnz, const i64* rowptr, const i64* col, const T* val, const T* x, T* y,
                          hipStream_t s) {
   if (m <= 0) return hipSuccess;
   // lanes per row: the power of two at or above the mean row length, 1 .. 16
@@ -220,73 +232,58 @@ hipError_t blas_csr_spmv(i64 m, i64 nnz, const i64* rowptr, const i64* col, cons
   const int L = mean <= 1.5 ? 1 : mean <= 2.5 ? 2 : mean <= 4.5 ? 4 : mean <= 8.5 ? 8 : 16;
   const dim3 blk(BLAS_THREADS);
   switch (L) {
-    case 1: hipLaunchKernelGGL(k_csr_spmv, dim3(nblocks(m)), blk, 0, s, m, rowptr, col, val, x, y); break;
-    case 2: hipLaunchKernelGGL((k_csr_spmv_vec<2>), dim3(nblocks(m * 2)), blk, 0, s, m, rowptr, col, val, x, y); break;
-    case 4: hipLaunchKernelGGL((k_csr_spmv_vec<4>), dim3(nblocks(m * 4)), blk, 0, s, m, rowptr, col, val, x, y); break;
-    case 8: hipLaunchKernelGGL((k_csr_spmv_vec<8>), dim3(nblocks(m * 8)), blk, 0, s, m, rowptr, col, val, x, y); break;
-    default: hipLaunchKernelGGL((k_csr_spmv_vec<16>), dim3(nblocks(m * 16)), blk, 0, s, m, rowptr, col, val, x, y);
+    case 1: hipLaunchKernelGGL(k_csr_spmv<T>, dim3(nblocks(m)), blk, 0, s, m, rowptr, col, val, x, y); break;
+    case 2: hipLaunchKernelGGL((k_csr_spmv_vec<T, 2>), dim3(nblocks(m * 2)), blk, 0, s, m, rowptr, col, val, x, y); break;
+    case 4: hipLaunchKernelGGL((k_csr_spmv_vec<T, 4>), dim3(nblocks(m * 4)), blk, 0, s, m, rowptr, col, val, x, y); break;
+    case 8: hipLaunchKernelGGL((k_csr_spmv_vec<T, 8>), dim3(nblocks(m * 8)), blk, 0, s, m, rowptr, col, val, x, y); break;
+    default: hipLaunchKernelGGL((k_csr_spmv_vec<T, 16>), dim3(nblocks(m * 16)), blk, 0, s, m, rowptr, col, val, x, y);
   }
   return hipGetLastError();
 }
-
-// Synchronous reductions (the result is needed on the host, as in PETSc).
-static hipError_t reduce(const cd* x, const cd* y, i64 n, int kind, double out[2], hipStream_t s) {
-  static thread_local double* partial = nullptr;
-  static thread_local double* hpart = nullptr;
-  if (!partial) {
-    hipError_t e = hipMalloc(&partial, sizeof(double) * 2 * RED_BLOCKS);
-    if (e != hipSuccess) return e;
-    e = hipHostMalloc(&hpart, sizeof(double) * 2 * RED_BLOCKS);
-    if (e != hipSuccess) return e;
-  }
-  unsigned nb = nblocks(n);
-  if (nb > RED_BLOCKS) nb = RED_BLOCKS;
-  hipLaunchKernelGGL(k_reduce, dim3(nb), dim3(BLAS_THREADS), 0, s, x, y, n, kind, partial);
-  hipError_t e = hipMemcpyAsync(hpart, partial, sizeof(double) * 2 * nb, hipMemcpyDeviceToHost, s);
-  if (e != hipSuccess) return e;
-  e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return e;
-  double a = 0.0, b = 0.0;
-  for (unsigned k = 0; k < nb; ++k) {
-    if (kind == 3) a = fmax(a, hpart[2 * k]);
-    else { a += hpart[2 * k]; b += hpart[2 * k + 1]; }
-  }
-  out[0] = a;
-  out[1] = b;
-  return hipSuccess;
+hipError_t blas_csr_spmv(i64 m, i64 nnz, const i64* rowptr, const i64* col, const cd* val, const cd* x, cd* y,
+                         hipStream_t s) {
+  return spmv_t(m, nnz, rowptr, col, val, x, y, s);
+}
+hipError_t blas_csr_spmv(i64 m, i64 nnz, const i64* rowptr, const i64* col, const double* val, const double* x,
+                         double* y, hipStream_t s) {
+  return spmv_t(m, nnz, rowptr, col, val, x, y, s);
 }
 
-hipError_t blas_maxpy_norm(cd* y, int k, const cd* a, const cd* const* xs, i64 n, bool overwrite, double* norm2,
-                           hipStream_t s) {
-  static thread_local double* partial = nullptr;
-  static thread_local double* hpart = nullptr;
-  if (norm2 && !partial) {
-    hipError_t e = hipMalloc(&partial, sizeof(double) * RED_BLOCKS);
+// per-thread device + pinned staging of block partial sums (synchronous reductions)
+struct Partials {
+  double* d = nullptr;
+  double* h = nullptr;
+  hipError_t get(size_t count) {
+    if (d) return hipSuccess;
+    hipError_t e = hipMalloc(&d, sizeof(double) * count);
     if (e != hipSuccess) return e;
-    e = hipHostMalloc(&hpart, sizeof(double) * RED_BLOCKS);
+    return hipHostMalloc(&h, sizeof(double) * count);
+  }
+};
+
+template <class T>
+static hipError_t maxpy_t(T* y, int k, const T* a, const T* const* xs, i64 n, bool overwrite, double* norm2,
+                          hipStream_t s) {
+  static thread_local Partials part;
+  if (norm2) {
+    hipError_t e = part.get(RED_BLOCKS);
     if (e != hipSuccess) return e;
   }
   unsigned nb = nblocks(n);
   if (nb > RED_BLOCKS) nb = RED_BLOCKS;
-  if (k <= 0 && !overwrite) {
-    if (!norm2) return hipSuccess;
-    double v = 0.0;
-    const hipError_t e = blas_norm(y, n, 1, &v, s);
-    *norm2 = v * v;
-    return e;
-  }
-  for (int j0 = 0; j0 < (k > 0 ? k : 1); j0 += MV_MAX) {
-    const int kk = k - j0 < MV_MAX ? (k - j0 > 0 ? k - j0 : 0) : MV_MAX;
-    MVCoef c;
-    MVPtrs p;
-    for (int j = 0; j < kk; ++j) { c.a[j] = a[j0 + j]; p.p[j] = xs[j0 + j]; }
-    const bool ow = overwrite && j0 == 0, last = j0 + MV_MAX >= k, nrm = norm2 && last;
-    if (n <= 0) break;
-    const dim3 g(nb), blk(BLAS_THREADS);
-    if (ow && nrm) hipLaunchKernelGGL((k_maxpy_nrm<true, true>), g, blk, 0, s, y, kk, c, p, n, partial);
-    else if (ow) hipLaunchKernelGGL((k_maxpy_nrm<true, false>), g, blk, 0, s, y, kk, c, p, n, partial);
-    else if (nrm) hipLaunchKernelGGL((k_maxpy_nrm<false, true>), g, blk, 0, s, y, kk, c, p, n, partial);
-    else hipLaunchKernelGGL((k_maxpy_nrm<false, false>), g, blk, 0, s, y, kk, c, p, n, partial);
+  if (n > 0) {
+    for (int j0 = 0; j0 < (k > 0 ? k : 1); j0 += MV_MAX) {
+      const int kk = k - j0 < MV_MAX ? (k - j0 > 0 ? k - j0 : 0) : MV_MAX;
+      MVCoefT<T> c;
+      MVPtrsT<T> p;
+      for (int j = 0; j < kk; ++j) { c.a[j] = a[j0 + j]; p.p[j] = xs[j0 + j]; }
+      const bool ow = overwrite && j0 == 0, nrm = norm2 && j0 + MV_MAX >= k;
+      const dim3 g(nb), blk(BLAS_THREADS);
+      if (ow && nrm) hipLaunchKernelGGL((k_maxpy<T, true, true>), g, blk, 0, s, y, kk, c, p, n, part.d);
+      else if (ow) hipLaunchKernelGGL((k_maxpy<T, true, false>), g, blk, 0, s, y, kk, c, p, n, part.d);
+      else if (nrm) hipLaunchKernelGGL((k_maxpy<T, false, true>), g, blk, 0, s, y, kk, c, p, n, part.d);
+      else hipLaunchKernelGGL((k_maxpy<T, false, false>), g, blk, 0, s, y, kk, c, p, n, part.d);
+    }
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !norm2) return e;
@@ -294,13 +291,50 @@ hipError_t blas_maxpy_norm(cd* y, int k, const cd* a, const cd* const* xs, i64 n
     *norm2 = 0.0;
     return hipSuccess;
   }
-  e = hipMemcpyAsync(hpart, partial, sizeof(double) * nb, hipMemcpyDeviceToHost, s);
+  e = hipMemcpyAsync(part.h, part.d, sizeof(double) * nb, hipMemcpyDeviceToHost, s);
   if (e != hipSuccess) return e;
   e = hipStreamSynchronize(s);
   if (e != hipSuccess) return e;
   double t = 0.0;
-  for (unsigned q = 0; q < nb; ++q) t += hpart[q];
+  for (unsigned q = 0; q < nb; ++q) t += part.h[q];
   *norm2 = t;
+  return hipSuccess;
+}
+hipError_t blas_maxpy(cd* y, int k, const cd* a, const cd* const* xs, i64 n, hipStream_t s) {
+  return maxpy_t(y, k, a, xs, n, false, nullptr, s);
+}
+hipError_t blas_maxpy(double* y, int k, const double* a, const double* const* xs, i64 n, hipStream_t s) {
+  return maxpy_t(y, k, a, xs, n, false, nullptr, s);
+}
+hipError_t blas_maxpy_norm(cd* y, int k, const cd* a, const cd* const* xs, i64 n, bool overwrite, double* norm2,
+                           hipStream_t s) {
+  return maxpy_t(y, k, a, xs, n, overwrite, norm2, s);
+}
+hipError_t blas_maxpy_norm(double* y, int k, const double* a, const double* const* xs, i64 n, bool overwrite,
+                           double* norm2, hipStream_t s) {
+  return maxpy_t(y, k, a, xs, n, overwrite, norm2, s);
+}
+
+// Synchronous reductions (the result is needed on the host, as in PETSc).
+template <class T>
+static hipError_t reduce(const T* x, const T* y, i64 n, int kind, double out[2], hipStream_t s) {
+  static thread_local Partials part;
+  hipError_t e = part.get(2 * RED_BLOCKS);
+  if (e != hipSuccess) return e;
+  unsigned nb = nblocks(n);
+  if (nb > RED_BLOCKS) nb = RED_BLOCKS;
+  hipLaunchKernelGGL(k_reduce<T>, dim3(nb), dim3(BLAS_THREADS), 0, s, x, y, n, kind, part.d);
+  e = hipMemcpyAsync(part.h, part.d, sizeof(double) * 2 * nb, hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) return e;
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return e;
+  double a = 0.0, b = 0.0;
+  for (unsigned k = 0; k < nb; ++k) {
+    if (kind == 3) a = fmax(a, part.h[2 * k]);
+    else { a += part.h[2 * k]; b += part.h[2 * k + 1]; }
+  }
+  out[0] = a;
+  out[1] = b;
   return hipSuccess;
 }
 
@@ -310,45 +344,61 @@ hipError_t blas_dot(const cd* x, const cd* y, i64 n, cd* val, hipStream_t s) {
   *val = make_cd(o[0], o[1]);
   return e;
 }
-hipError_t blas_norm(const cd* x, i64 n, int type, double* val, hipStream_t s) {
+hipError_t blas_dot(const double* x, const double* y, i64 n, double* val, hipStream_t s) {
+  double o[2];
+  hipError_t e = reduce(x, y, n, 0, o, s);
+  *val = o[0];
+  return e;
+}
+template <class T>
+static hipError_t norm_t(const T* x, i64 n, int type, double* val, hipStream_t s) {
   double o[2];
   const int kind = type == 1 ? 1 : (type == 0 ? 2 : (type == 3 ? 3 : 1));
-  hipError_t e = reduce(x, nullptr, n, kind, o, s);
+  hipError_t e = reduce(x, (const T*)nullptr, n, kind, o, s);
   *val = kind == 1 ? sqrt(o[0]) : o[0];
   return e;
 }
+hipError_t blas_norm(const cd* x, i64 n, int type, double* val, hipStream_t s) { return norm_t(x, n, type, val, s); }
+hipError_t blas_norm(const double* x, i64 n, int type, double* val, hipStream_t s) { return norm_t(x, n, type, val, s); }
 
-hipError_t blas_mdot(const cd* x, int k, const cd* const* ys, i64 n, cd* vals, hipStream_t s) {
-  static thread_local double* partial = nullptr;
-  static thread_local double* hpart = nullptr;
+// vals[j] = (re, im) of ys[j]^H x
+template <class T>
+static hipError_t mdot_t(const T* x, int k, const T* const* ys, i64 n, double* vals, hipStream_t s) {
+  static thread_local Partials part;
   const int NB = 512;
-  if (!partial) {
-    hipError_t e = hipMalloc(&partial, sizeof(double) * 2 * MDOT_K * NB);
-    if (e != hipSuccess) return e;
-    e = hipHostMalloc(&hpart, sizeof(double) * 2 * MDOT_K * NB);
-    if (e != hipSuccess) return e;
-  }
+  hipError_t e = part.get(2 * MDOT_K * NB);
+  if (e != hipSuccess) return e;
   for (int j0 = 0; j0 < k; j0 += MDOT_K) {
     const int kk = k - j0 < MDOT_K ? k - j0 : MDOT_K;
-    MVPtrs p;
+    MVPtrsT<T> p;
     for (int j = 0; j < kk; ++j) p.p[j] = ys[j0 + j];
     unsigned nb = nblocks(n);
     if (nb > (unsigned)NB) nb = NB;
-    hipLaunchKernelGGL(k_mdot, dim3(nb), dim3(BLAS_THREADS), 0, s, x, kk, p, n, partial);
-    hipError_t e = hipMemcpyAsync(hpart, partial, sizeof(double) * 2 * MDOT_K * nb, hipMemcpyDeviceToHost, s);
+    hipLaunchKernelGGL(k_mdot<T>, dim3(nb), dim3(BLAS_THREADS), 0, s, x, kk, p, n, part.d);
+    e = hipMemcpyAsync(part.h, part.d, sizeof(double) * 2 * MDOT_K * nb, hipMemcpyDeviceToHost, s);
     if (e != hipSuccess) return e;
     e = hipStreamSynchronize(s);
     if (e != hipSuccess) return e;
     for (int j = 0; j < kk; ++j) {
       double ra = 0.0, rb = 0.0;
       for (unsigned q = 0; q < nb; ++q) {
-        ra += hpart[(size_t)q * 2 * MDOT_K + 2 * j];
-        rb += hpart[(size_t)q * 2 * MDOT_K + 2 * j + 1];
+        ra += part.h[(size_t)q * 2 * MDOT_K + 2 * j];
+        rb += part.h[(size_t)q * 2 * MDOT_K + 2 * j + 1];
       }
-      vals[j0 + j] = make_cd(ra, rb);
+      vals[2 * (j0 + j)] = ra;
+      vals[2 * (j0 + j) + 1] = rb;
     }
   }
   return hipSuccess;
+}
+hipError_t blas_mdot(const cd* x, int k, const cd* const* ys, i64 n, cd* vals, hipStream_t s) {
+  return mdot_t(x, k, ys, n, (double*)vals, s);
+}
+hipError_t blas_mdot(const double* x, int k, const double* const* ys, i64 n, double* vals, hipStream_t s) {
+  std::vector<double> v(2 * (size_t)(k > 0 ? k : 1));
+  hipError_t e = mdot_t(x, k, ys, n, v.data(), s);
+  for (int j = 0; j < k; ++j) vals[j] = v[2 * (size_t)j];
+  return e;
 }
 
 }  // namespace cfp

@@ -379,3 +379,73 @@ extern "C" int cfp_rplan_time_passes(cfp_rplan_t p, const double* b, double* x, 
   for (int i = 0; i < 4; ++i) ms_out[i] = acc[i] / iters;
   return CFP_SUCCESS;
 }
+
+// ------------------------------------------------------------------ real <-> complex layouts
+// Conversions of the real-scalar PETSc boundary (pcshell_fft3d_real.cpp): a real Vec <-> the
+// complex plan's data, and FFTW's r2c half spectrum ([nz][ny][nx/2 + 1] complex, what a
+// real-scalar MATFFTW MatMult produces) <-> the full spectrum by Hermitian symmetry
+// X(-k) = conj X(k) of the transform of real data.  Elementwise, one thread per output value.
+namespace {
+#define RB_LOOP(i, n) for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += (int64_t)gridDim.x * blockDim.x)
+__global__ void k_rb_promote(const double* __restrict__ x, cd* __restrict__ z, int64_t n) {
+  RB_LOOP(i, n) z[i] = make_cd(x[i], 0.0);
+}
+__global__ void k_rb_real(const cd* __restrict__ z, double* __restrict__ x, int64_t n, double scale) {
+  RB_LOOP(i, n) x[i] = z[i].x * scale;
+}
+__global__ void k_rb_half(const cd* __restrict__ full, cd* __restrict__ half, int64_t nx, int64_t M, int64_t rows) {
+  RB_LOOP(i, rows * M) {
+    const int64_t row = i / M, kx = i - row * M;
+    half[i] = full[row * nx + kx];
+  }
+}
+__global__ void k_rb_extend(const cd* __restrict__ half, cd* __restrict__ full, int64_t nx, int64_t ny, int64_t nz) {
+  const int64_t M = nx / 2 + 1;
+  RB_LOOP(i, nx * ny * nz) {
+    const int64_t kx = i % nx, r = i / nx, ky = r % ny, kz = r / ny;
+    if (kx < M) {
+      full[i] = half[r * M + kx];
+    } else {  // X(kx, ky, kz) = conj X(nx - kx, -ky, -kz)
+      const int64_t my = ky ? ny - ky : 0, mz = kz ? nz - kz : 0;
+      const cd v = half[(mz * ny + my) * M + (nx - kx)];
+      full[i] = make_cd(v.x, -v.y);
+    }
+  }
+}
+unsigned rb_grid(int64_t n) {
+  const int64_t b = (n + 255) / 256;
+  return (unsigned)(b < 1 ? 1 : (b > 16384 ? 16384 : b));
+}
+}  // namespace
+
+extern "C" int cfp_real_to_complex(const double* x, double* z, int64_t n, void* stream) {
+  if (!x || !z) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  if (n > 0) hipLaunchKernelGGL(k_rb_promote, dim3(rb_grid(n)), dim3(256), 0, (hipStream_t)stream, x, (cd*)z, n);
+  HIPCHK(hipGetLastError());
+  return CFP_SUCCESS;
+}
+extern "C" int cfp_complex_real_part(const double* z, double* x, int64_t n, double scale, void* stream) {
+  if (!x || !z) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  if (n > 0) hipLaunchKernelGGL(k_rb_real, dim3(rb_grid(n)), dim3(256), 0, (hipStream_t)stream, (const cd*)z, x, n, scale);
+  HIPCHK(hipGetLastError());
+  return CFP_SUCCESS;
+}
+extern "C" int cfp_half_spectrum_extract(const double* full, double* half, int64_t nx, int64_t ny, int64_t nz,
+                                         void* stream) {
+  if (!full || !half) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  if (nx < 1 || ny < 1 || nz < 1) return set_error(CFP_ERR_ARG_OUTOFRANGE, "grid sizes must be >= 1");
+  const int64_t M = nx / 2 + 1, rows = ny * nz;
+  hipLaunchKernelGGL(k_rb_half, dim3(rb_grid(rows * M)), dim3(256), 0, (hipStream_t)stream, (const cd*)full, (cd*)half,
+                     nx, M, rows);
+  HIPCHK(hipGetLastError());
+  return CFP_SUCCESS;
+}
+extern "C" int cfp_half_spectrum_extend(const double* half, double* full, int64_t nx, int64_t ny, int64_t nz,
+                                        void* stream) {
+  if (!full || !half) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  if (nx < 1 || ny < 1 || nz < 1) return set_error(CFP_ERR_ARG_OUTOFRANGE, "grid sizes must be >= 1");
+  hipLaunchKernelGGL(k_rb_extend, dim3(rb_grid(nx * ny * nz)), dim3(256), 0, (hipStream_t)stream, (const cd*)half,
+                     (cd*)full, nx, ny, nz);
+  HIPCHK(hipGetLastError());
+  return CFP_SUCCESS;
+}

@@ -29,6 +29,13 @@
 namespace {
 const int kKSPMagic = 0x4b535031;
 typedef std::complex<double> C;
+// the Hessenberg algebra runs in complex arithmetic; with real scalars (-DCFP_REAL_SCALAR) its
+// results are real and go back as their real parts
+#ifdef CFP_REAL_SCALAR
+static inline PetscScalar to_ps(C v) { return v.real(); }
+#else
+static inline PetscScalar to_ps(C v) { return v; }
+#endif
 
 double now() {
   struct timeval tv;
@@ -380,7 +387,7 @@ extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
     }
     if (kk > 0) {
       std::vector<PetscScalar> yy((size_t)kk);
-      for (PetscInt i = 0; i < kk; ++i) yy[(size_t)i] = y[(size_t)i] * sg[(size_t)i];  // v_i = sg_i u_i
+      for (PetscInt i = 0; i < kk; ++i) yy[(size_t)i] = to_ps(y[(size_t)i] * sg[(size_t)i]);  // v_i = sg_i u_i
       if (k->side == PC_LEFT) {
         PetscCall(VecMiniMAXPYNorm(x, kk, yy.data(), V, x_unset ? PETSC_TRUE : PETSC_FALSE, nullptr));
       } else {

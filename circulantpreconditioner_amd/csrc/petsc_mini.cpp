@@ -289,7 +289,35 @@ extern "C" int PetscMiniCommExchange(void* user, const double* src, double* dst,
     if (e__ != hipSuccess) return ERR(PETSC_ERR_LIB, hipGetErrorString(e__)); \
   } while (0)
 
-static inline cd tocd(PetscScalar s) { return cfp::make_cd(s.real(), s.imag()); }
+// Vec / AIJ storage: complex double (cd) or, in the real-scalar build (-DCFP_REAL_SCALAR,
+// PetscScalar = double, the reference's !PETSC_USE_COMPLEX branch), double.  Host arithmetic goes
+// through std::complex (C / D); with real operands its results are real.
+#ifdef CFP_REAL_SCALAR
+typedef double VS;
+static inline VS tocd(PetscScalar s) { return s; }
+static inline std::complex<double> C(VS v) { return {v, 0.0}; }
+static inline VS D(std::complex<double> v) { return v.real(); }
+static inline PetscScalar to_scalar(double re, double) { return re; }
+static inline double re_of(PetscScalar s) { return s; }
+static inline double im_of(PetscScalar) { return 0.0; }
+static inline hipError_t dev_scale(VS* x, VS a, i64 n, hipStream_t s) { return cfp::blas_scale(x, a, n, s); }
+static inline hipError_t dev_pdivide(VS* w, const VS* x, const VS* y, i64 n, hipStream_t s) {
+  return cfp::blas_pdivide(w, x, y, n, s);
+}
+#else
+typedef cd VS;
+static inline VS tocd(PetscScalar s) { return cfp::make_cd(s.real(), s.imag()); }
+static inline std::complex<double> C(VS v) { return {v.x, v.y}; }
+static inline VS D(std::complex<double> v) { return cfp::make_cd(v.real(), v.imag()); }
+static inline PetscScalar to_scalar(double re, double im) { return PetscScalar(re, im); }
+static inline double re_of(PetscScalar s) { return s.real(); }
+static inline double im_of(PetscScalar s) { return s.imag(); }
+static inline hipError_t dev_scale(VS* x, VS a, i64 n, hipStream_t s) { return cfp::launch_scale(x, a, n, s); }
+static inline hipError_t dev_pdivide(VS* w, const VS* x, const VS* y, i64 n, hipStream_t s) {
+  return cfp::launch_pointwise_divide(w, x, y, n, s);
+}
+#endif
+static constexpr int kDPS = (int)(sizeof(VS) / sizeof(double));  // doubles per scalar
 
 // ------------------------------------------------------------------ Vec
 enum { MASK_NONE = 0, MASK_CPU = 1, MASK_GPU = 2, MASK_BOTH = 3 };
@@ -303,8 +331,8 @@ struct _p_Vec {
   MPI_Comm comm = PETSC_COMM_SELF;
   int nranks = 1;
   bool hip = false;
-  cd* d = nullptr;
-  cd* h = nullptr;
+  VS* d = nullptr;
+  VS* h = nullptr;
   bool own_d = false, own_h = false;
   int mask = MASK_NONE;
   int device = 0;
@@ -312,7 +340,7 @@ struct _p_Vec {
   PetscObjectState state = 0;  // bumped by every write access (PetscObjectStateGet)
   // VecSetValues entries of rows owned by other ranks, delivered by VecAssemblyBegin/End
   std::vector<PetscInt> st_idx;
-  std::vector<cd> st_val;
+  std::vector<VS> st_val;
   std::vector<char> st_add;
 };
 
@@ -335,7 +363,7 @@ extern "C" PetscErrorCode VecMiniSynchronize(Vec v) {
 
 static PetscErrorCode ensure_host(Vec v) {
   if (!v->h) {
-    v->h = (cd*)calloc((size_t)(v->n > 0 ? v->n : 1), sizeof(cd));
+    v->h = (VS*)calloc((size_t)(v->n > 0 ? v->n : 1), sizeof(VS));
     if (!v->h) return ERR(PETSC_ERR_MEM, "host allocation");
     v->own_h = true;
   }
@@ -345,7 +373,7 @@ static PetscErrorCode ensure_host(Vec v) {
 static PetscErrorCode sync_to_host(Vec v) {
   PetscCall(ensure_host(v));
   if (v->hip && v->mask == MASK_GPU) {
-    HCHK(hipMemcpyAsync(v->h, v->d, sizeof(cd) * (size_t)v->n, hipMemcpyDeviceToHost, g_stream));
+    HCHK(hipMemcpyAsync(v->h, v->d, sizeof(VS) * (size_t)v->n, hipMemcpyDeviceToHost, g_stream));
     HCHK(hipStreamSynchronize(g_stream));
     v->mask = MASK_BOTH;
   }
@@ -355,7 +383,7 @@ static PetscErrorCode sync_to_host(Vec v) {
 static PetscErrorCode sync_to_device(Vec v) {
   if (!v->hip) return ERR(PETSC_ERR_ARG_WRONG, "not a device vector");
   if (v->mask == MASK_CPU) {
-    HCHK(hipMemcpyAsync(v->d, v->h, sizeof(cd) * (size_t)v->n, hipMemcpyHostToDevice, g_stream));
+    HCHK(hipMemcpyAsync(v->d, v->h, sizeof(VS) * (size_t)v->n, hipMemcpyHostToDevice, g_stream));
     v->mask = MASK_BOTH;
   }
   if (v->mask == MASK_NONE) v->mask = MASK_GPU;
@@ -373,12 +401,12 @@ static PetscErrorCode vec_new(PetscInt n, bool hip, const PetscScalar* devarr, V
   if (hip) {
     hipGetDevice(&v->device);
     if (devarr) {
-      v->d = (cd*)devarr;
+      v->d = (VS*)devarr;
     } else {
-      hipError_t e = hipMalloc(&v->d, sizeof(cd) * (size_t)(n > 0 ? n : 1));
+      hipError_t e = hipMalloc(&v->d, sizeof(VS) * (size_t)(n > 0 ? n : 1));
       if (e != hipSuccess) { delete v; return ERR(PETSC_ERR_MEM, hipGetErrorString(e)); }
       v->own_d = true;
-      hipMemsetAsync(v->d, 0, sizeof(cd) * (size_t)n, g_stream);
+      hipMemsetAsync(v->d, 0, sizeof(VS) * (size_t)n, g_stream);
     }
     v->mask = MASK_GPU;
   } else {
@@ -622,24 +650,24 @@ static PetscErrorCode same_size(Vec a, Vec b) {
   if (a->n != b->n) return ERR(PETSC_ERR_ARG_SIZ, "vector sizes differ");
   return PETSC_SUCCESS;
 }
-static PetscErrorCode dev_read(Vec v, const cd** p) {
+static PetscErrorCode dev_read(Vec v, const VS** p) {
   PetscCall(sync_to_device(v));
   *p = v->d;
   return PETSC_SUCCESS;
 }
-static PetscErrorCode dev_rw(Vec v, cd** p) {
+static PetscErrorCode dev_rw(Vec v, VS** p) {
   PetscCall(sync_to_device(v));
   v->mask = MASK_GPU;
   touch(v);
   *p = v->d;
   return PETSC_SUCCESS;
 }
-static PetscErrorCode host_read(Vec v, const cd** p) {
+static PetscErrorCode host_read(Vec v, const VS** p) {
   PetscCall(sync_to_host(v));
   *p = v->h;
   return PETSC_SUCCESS;
 }
-static PetscErrorCode host_rw(Vec v, cd** p) {
+static PetscErrorCode host_rw(Vec v, VS** p) {
   PetscCall(sync_to_host(v));
   v->mask = MASK_CPU;
   touch(v);
@@ -665,7 +693,7 @@ extern "C" PetscErrorCode VecSetValue(Vec v, PetscInt i, PetscScalar val, Insert
 }
 extern "C" PetscErrorCode VecSetValues(Vec v, PetscInt n, const PetscInt* idx, const PetscScalar* y, InsertMode mode) {
   VCHK(v);
-  cd* h;
+  VS* h;
   PetscCall(host_rw(v, &h));
   for (PetscInt k = 0; k < n; ++k) {
     if (idx[k] < 0) continue;
@@ -677,20 +705,20 @@ extern "C" PetscErrorCode VecSetValues(Vec v, PetscInt n, const PetscInt* idx, c
       v->st_add.push_back(mode == ADD_VALUES);
       continue;
     }
-    cd val = tocd(y[k]);
-    if (mode == ADD_VALUES) val = cfp::make_cd(h[i].x + val.x, h[i].y + val.y);
+    VS val = tocd(y[k]);
+    if (mode == ADD_VALUES) val = D(C(h[i]) + C(val));
     h[i] = val;
   }
   return PETSC_SUCCESS;
 }
 extern "C" PetscErrorCode VecGetValues(Vec v, PetscInt n, const PetscInt* idx, PetscScalar* y) {
   VCHK(v);
-  const cd* h;
+  const VS* h;
   PetscCall(host_read(v, &h));
   for (PetscInt k = 0; k < n; ++k) {
     const PetscInt i = idx[k] - v->rstart;  // local rows only, as PETSc's VecGetValues
     if (i < 0 || i >= v->n) return ERR(PETSC_ERR_ARG_OUTOFRANGE, "index not owned by this rank");
-    y[k] = PetscScalar(h[i].x, h[i].y);
+    y[k] = to_scalar(C(h[i]).real(), C(h[i]).imag());
   }
   return PETSC_SUCCESS;
 }
@@ -727,19 +755,20 @@ extern "C" PetscErrorCode VecAssemblyBegin(Vec v) {
         const size_t k = to[(size_t)q][j];
         double* rec = &send[((size_t)q * M + j) * 4];
         rec[0] = (double)v->st_idx[k];  // exact: rows < 2^53
-        rec[1] = v->st_val[k].x;
-        rec[2] = v->st_val[k].y;
+        rec[1] = C(v->st_val[k]).real();
+        rec[2] = C(v->st_val[k]).imag();
         rec[3] = v->st_add[k] ? 1.0 : 0.0;
       }
     PetscCall(comm_alltoall_host(r, send.data(), recv.data(), M * 4 * sizeof(double)));
-    cd* h;
+    VS* h;
     PetscCall(host_rw(v, &h));
     for (size_t e = 0; e < (size_t)P * M; ++e) {
       const double* rec = &recv[e * 4];
       if (rec[0] < 0) continue;  // padding
       const PetscInt i = (PetscInt)rec[0] - v->rstart;
       if (i < 0 || i >= v->n) return ERR(PETSC_ERR_PLIB, "stashed entry delivered to the wrong rank");
-      h[i] = rec[3] != 0.0 ? cfp::make_cd(h[i].x + rec[1], h[i].y + rec[2]) : cfp::make_cd(rec[1], rec[2]);
+      const std::complex<double> val(rec[1], rec[2]);
+      h[i] = rec[3] != 0.0 ? D(C(h[i]) + val) : D(val);
     }
   }
   v->st_idx.clear(), v->st_val.clear(), v->st_add.clear();
@@ -753,22 +782,22 @@ extern "C" PetscErrorCode VecCopy(Vec x, Vec y) {
   if (x == y) return PETSC_SUCCESS;
   touch(y);
   if (y->hip) {
-    cd* yd;
+    VS* yd;
     if (x->hip) {
-      const cd* xd;
+      const VS* xd;
       PetscCall(dev_read(x, &xd));
       y->mask = MASK_GPU;
-      HIPK(hipMemcpyAsync(y->d, xd, sizeof(cd) * (size_t)x->n, hipMemcpyDeviceToDevice, g_stream));
+      HIPK(hipMemcpyAsync(y->d, xd, sizeof(VS) * (size_t)x->n, hipMemcpyDeviceToDevice, g_stream));
     } else {
       (void)yd;
-      HIPK(hipMemcpyAsync(y->d, x->h, sizeof(cd) * (size_t)x->n, hipMemcpyHostToDevice, g_stream));
+      HIPK(hipMemcpyAsync(y->d, x->h, sizeof(VS) * (size_t)x->n, hipMemcpyHostToDevice, g_stream));
       HIPK(hipStreamSynchronize(g_stream));
       y->mask = MASK_GPU;
     }
   } else {
-    const cd* xh;
+    const VS* xh;
     PetscCall(host_read(x, &xh));
-    std::memcpy(y->h, xh, sizeof(cd) * (size_t)x->n);
+    std::memcpy(y->h, xh, sizeof(VS) * (size_t)x->n);
     y->mask = MASK_CPU;
   }
   return PETSC_SUCCESS;
@@ -777,16 +806,14 @@ extern "C" PetscErrorCode VecCopy(Vec x, Vec y) {
 extern "C" PetscErrorCode VecScale(Vec x, PetscScalar a) {
   VCHK(x);
   if (x->hip) {
-    cd* xd;
+    VS* xd;
     PetscCall(dev_rw(x, &xd));
-    HIPK(cfp::launch_scale(xd, tocd(a), x->n, g_stream));
+    HIPK(dev_scale(xd, tocd(a), x->n, g_stream));
   } else {
-    cd* h;
+    VS* h;
     PetscCall(host_rw(x, &h));
     for (PetscInt i = 0; i < x->n; ++i) {
-      std::complex<double> v(h[i].x, h[i].y);
-      v *= a;
-      h[i] = cfp::make_cd(v.real(), v.imag());
+      h[i] = D(C(h[i]) * a);
     }
   }
   return PETSC_SUCCESS;
@@ -794,13 +821,13 @@ extern "C" PetscErrorCode VecScale(Vec x, PetscScalar a) {
 extern "C" PetscErrorCode VecShift(Vec x, PetscScalar a) {
   VCHK(x);
   if (x->hip) {
-    cd* xd;
+    VS* xd;
     PetscCall(dev_rw(x, &xd));
     HIPK(cfp::blas_shift(xd, tocd(a), x->n, g_stream));
   } else {
-    cd* h;
+    VS* h;
     PetscCall(host_rw(x, &h));
-    for (PetscInt i = 0; i < x->n; ++i) h[i] = cfp::make_cd(h[i].x + a.real(), h[i].y + a.imag());
+    for (PetscInt i = 0; i < x->n; ++i) h[i] = D(C(h[i]) + a);
   }
   return PETSC_SUCCESS;
 }
@@ -811,101 +838,99 @@ static PetscErrorCode binop(Vec out, Vec a, Vec b, DevOp dop, HostOp hop) {
   if (b) { VCHK(b); PetscCall(same_size(a, b)); }
   PetscCall(same_size(out, a));
   if (all_hip({out, a}) && (!b || b->hip)) {
-    const cd *ad, *bd = nullptr;
+    const VS *ad, *bd = nullptr;
     PetscCall(dev_read(a, &ad));
     if (b) PetscCall(dev_read(b, &bd));
-    cd* od;
+    VS* od;
     PetscCall(dev_rw(out, &od));
     HIPK(dop(od, ad, bd));
   } else {
-    const cd *ah, *bh = nullptr;
+    const VS *ah, *bh = nullptr;
     PetscCall(host_read(a, &ah));
     if (b) PetscCall(host_read(b, &bh));
-    cd* oh;
+    VS* oh;
     PetscCall(host_rw(out, &oh));
     hop(oh, ah, bh);
     if (out->hip) {
-      HIPK(hipMemcpyAsync(out->d, out->h, sizeof(cd) * (size_t)out->n, hipMemcpyHostToDevice, g_stream));
+      HIPK(hipMemcpyAsync(out->d, out->h, sizeof(VS) * (size_t)out->n, hipMemcpyHostToDevice, g_stream));
       out->mask = MASK_BOTH;
     }
   }
   return PETSC_SUCCESS;
 }
 
-static inline std::complex<double> C(cd v) { return {v.x, v.y}; }
-static inline cd D(std::complex<double> v) { return cfp::make_cd(v.real(), v.imag()); }
-
 extern "C" PetscErrorCode VecAXPY(Vec y, PetscScalar a, Vec x) {  // y += a x
   const i64 n = y ? y->n : 0;
   return binop(y, x, nullptr,
-               [&](cd* o, const cd* xa, const cd*) { return cfp::blas_axpy(o, tocd(a), xa, n, g_stream); },
-               [&](cd* o, const cd* xa, const cd*) { for (i64 i = 0; i < n; ++i) o[i] = D(C(o[i]) + a * C(xa[i])); });
+               [&](VS* o, const VS* xa, const VS*) { return cfp::blas_axpy(o, tocd(a), xa, n, g_stream); },
+               [&](VS* o, const VS* xa, const VS*) { for (i64 i = 0; i < n; ++i) o[i] = D(C(o[i]) + a * C(xa[i])); });
 }
 extern "C" PetscErrorCode VecAYPX(Vec y, PetscScalar b, Vec x) {  // y = x + b y
   const i64 n = y ? y->n : 0;
   return binop(y, x, nullptr,
-               [&](cd* o, const cd* xa, const cd*) { return cfp::blas_aypx(o, tocd(b), xa, n, g_stream); },
-               [&](cd* o, const cd* xa, const cd*) { for (i64 i = 0; i < n; ++i) o[i] = D(C(xa[i]) + b * C(o[i])); });
+               [&](VS* o, const VS* xa, const VS*) { return cfp::blas_aypx(o, tocd(b), xa, n, g_stream); },
+               [&](VS* o, const VS* xa, const VS*) { for (i64 i = 0; i < n; ++i) o[i] = D(C(xa[i]) + b * C(o[i])); });
 }
 extern "C" PetscErrorCode VecWAXPY(Vec w, PetscScalar a, Vec x, Vec y) {  // w = a x + y
   const i64 n = w ? w->n : 0;
   return binop(w, x, y,
-               [&](cd* o, const cd* xa, const cd* yb) { return cfp::blas_waxpy(o, tocd(a), xa, yb, n, g_stream); },
-               [&](cd* o, const cd* xa, const cd* yb) { for (i64 i = 0; i < n; ++i) o[i] = D(a * C(xa[i]) + C(yb[i])); });
+               [&](VS* o, const VS* xa, const VS* yb) { return cfp::blas_waxpy(o, tocd(a), xa, yb, n, g_stream); },
+               [&](VS* o, const VS* xa, const VS* yb) { for (i64 i = 0; i < n; ++i) o[i] = D(a * C(xa[i]) + C(yb[i])); });
 }
 extern "C" PetscErrorCode VecPointwiseDivide(Vec w, Vec x, Vec y) {
   const i64 n = w ? w->n : 0;
   return binop(w, x, y,
-               [&](cd* o, const cd* xa, const cd* yb) { return cfp::launch_pointwise_divide(o, xa, yb, n, g_stream); },
-               [&](cd* o, const cd* xa, const cd* yb) {  // PETSc: a zero divisor gives 0 (bvec2.c)
+               [&](VS* o, const VS* xa, const VS* yb) { return dev_pdivide(o, xa, yb, n, g_stream); },
+               [&](VS* o, const VS* xa, const VS* yb) {  // PETSc: a zero divisor gives 0 (bvec2.c)
                  for (i64 i = 0; i < n; ++i) o[i] = C(yb[i]) != 0.0 ? D(C(xa[i]) / C(yb[i])) : D(0.0);
                });
 }
 extern "C" PetscErrorCode VecPointwiseMult(Vec w, Vec x, Vec y) {
   const i64 n = w ? w->n : 0;
   return binop(w, x, y,
-               [&](cd* o, const cd* xa, const cd* yb) { return cfp::blas_pmult(o, xa, yb, n, g_stream); },
-               [&](cd* o, const cd* xa, const cd* yb) { for (i64 i = 0; i < n; ++i) o[i] = D(C(xa[i]) * C(yb[i])); });
+               [&](VS* o, const VS* xa, const VS* yb) { return cfp::blas_pmult(o, xa, yb, n, g_stream); },
+               [&](VS* o, const VS* xa, const VS* yb) { for (i64 i = 0; i < n; ++i) o[i] = D(C(xa[i]) * C(yb[i])); });
 }
 
 extern "C" PetscErrorCode VecDot(Vec x, Vec y, PetscScalar* val) {  // y^H x
   VCHK(x); VCHK(y);
   PetscCall(same_size(x, y));
   if (x->hip && y->hip) {
-    const cd *xd, *yd;
+    const VS *xd, *yd;
     PetscCall(dev_read(x, &xd));
     PetscCall(dev_read(y, &yd));
-    cd r;
+    VS r;
     HIPK(cfp::blas_dot(xd, yd, x->n, &r, g_stream));
-    *val = PetscScalar(r.x, r.y);
+    *val = to_scalar(C(r).real(), C(r).imag());
   } else {
-    const cd *xh, *yh;
+    const VS *xh, *yh;
     PetscCall(host_read(x, &xh));
     PetscCall(host_read(y, &yh));
     std::complex<double> s = 0;
     for (i64 i = 0; i < x->n; ++i) s += C(xh[i]) * std::conj(C(yh[i]));
-    *val = s;
+    *val = to_scalar(s.real(), s.imag());
   }
-  double buf[2] = {val->real(), val->imag()};
+  double buf[2] = {re_of(*val), im_of(*val)};
   PetscCall(vec_reduce(x, buf, 2, PETSCMINI_OP_SUM));
-  *val = PetscScalar(buf[0], buf[1]);
+  *val = to_scalar(buf[0], buf[1]);
   return PETSC_SUCCESS;
 }
 extern "C" PetscErrorCode VecNorm(Vec x, NormType t, PetscReal* val) {
   VCHK(x);
   if (t == NORM_FROBENIUS) t = NORM_2;
   if (x->hip) {
-    const cd* xd;
+    const VS* xd;
     PetscCall(dev_read(x, &xd));
     HIPK(cfp::blas_norm(xd, x->n, (int)t, val, g_stream));
   } else {
-    const cd* h;
+    const VS* h;
     PetscCall(host_read(x, &h));
     double s = 0;
     for (i64 i = 0; i < x->n; ++i) {
-      if (t == NORM_2) s += h[i].x * h[i].x + h[i].y * h[i].y;
-      else if (t == NORM_1) s += std::fabs(h[i].x) + std::fabs(h[i].y);
-      else s = std::fmax(s, std::hypot(h[i].x, h[i].y));
+      const std::complex<double> v = C(h[i]);
+      if (t == NORM_2) s += std::norm(v);
+      else if (t == NORM_1) s += std::fabs(v.real()) + std::fabs(v.imag());
+      else s = std::fmax(s, std::abs(v));
     }
     *val = t == NORM_2 ? std::sqrt(s) : s;
   }
@@ -927,14 +952,14 @@ extern "C" PetscErrorCode VecMDot(Vec x, PetscInt nv, const Vec y[], PetscScalar
     dev = dev && y[j]->hip;
   }
   if (dev) {
-    const cd* xd;
+    const VS* xd;
     PetscCall(dev_read(x, &xd));
-    std::vector<const cd*> ys((size_t)nv);
+    std::vector<const VS*> ys((size_t)nv);
     for (PetscInt j = 0; j < nv; ++j) PetscCall(dev_read(y[j], &ys[(size_t)j]));
-    std::vector<cd> r((size_t)nv);
+    std::vector<VS> r((size_t)nv);
     HIPK(cfp::blas_mdot(xd, (int)nv, ys.data(), x->n, r.data(), g_stream));
-    PetscCall(vec_reduce(x, (double*)r.data(), 2 * nv, PETSCMINI_OP_SUM));  // one all-reduce for all nv
-    for (PetscInt j = 0; j < nv; ++j) val[j] = PetscScalar(r[(size_t)j].x, r[(size_t)j].y);
+    PetscCall(vec_reduce(x, (double*)r.data(), kDPS * nv, PETSCMINI_OP_SUM));  // one all-reduce for all nv
+    for (PetscInt j = 0; j < nv; ++j) val[j] = to_scalar(C(r[(size_t)j]).real(), C(r[(size_t)j]).imag());
     return PETSC_SUCCESS;
   }
   for (PetscInt j = 0; j < nv; ++j) PetscCall(VecDot(x, y[j], &val[j]));
@@ -951,13 +976,13 @@ extern "C" PetscErrorCode VecMAXPY(Vec y, PetscInt nv, const PetscScalar alpha[]
     dev = dev && x[j]->hip;
   }
   if (dev) {
-    std::vector<const cd*> xs((size_t)nv);
-    std::vector<cd> a((size_t)nv);
+    std::vector<const VS*> xs((size_t)nv);
+    std::vector<VS> a((size_t)nv);
     for (PetscInt j = 0; j < nv; ++j) {
       PetscCall(dev_read(x[j], &xs[(size_t)j]));
       a[(size_t)j] = tocd(alpha[j]);
     }
-    cd* yd;
+    VS* yd;
     PetscCall(dev_rw(y, &yd));
     HIPK(cfp::blas_maxpy(yd, (int)nv, a.data(), xs.data(), y->n, g_stream));
     return PETSC_SUCCESS;
@@ -981,13 +1006,13 @@ extern "C" PetscErrorCode VecMiniMAXPYNorm(Vec y, PetscInt nv, const PetscScalar
     if (norm) PetscCall(VecNorm(y, NORM_2, norm));
     return PETSC_SUCCESS;
   }
-  std::vector<const cd*> xs((size_t)(nv > 0 ? nv : 1));
-  std::vector<cd> a((size_t)(nv > 0 ? nv : 1));
+  std::vector<const VS*> xs((size_t)(nv > 0 ? nv : 1));
+  std::vector<VS> a((size_t)(nv > 0 ? nv : 1));
   for (PetscInt j = 0; j < nv; ++j) {
     PetscCall(dev_read(x[j], &xs[(size_t)j]));
     a[(size_t)j] = tocd(alpha[j]);
   }
-  cd* yd;
+  VS* yd;
   if (overwrite) {  // no read of y: nothing to bring to the device first
     touch(y);
     y->mask = MASK_GPU;
@@ -1044,9 +1069,9 @@ struct _p_Mat {
   MatDestroyFn destroy = nullptr;
   // AIJ (device CSR)
   i64 *rowptr = nullptr, *col = nullptr;
-  cd* val = nullptr;
+  VS* val = nullptr;
   std::vector<i64> h_rowptr, h_col;
-  std::vector<cd> h_val;
+  std::vector<VS> h_val;
 };
 
 static PetscErrorCode mcheck(Mat A, const char* f) {
@@ -1103,10 +1128,10 @@ static PetscErrorCode aij_upload(Mat M) {
   const size_t nnz = M->h_col.size();
   hipError_t e = hipMalloc(&M->rowptr, sizeof(i64) * (size_t)(M->m + 1));
   if (e == hipSuccess) e = hipMalloc(&M->col, sizeof(i64) * (nnz > 0 ? nnz : 1));
-  if (e == hipSuccess) e = hipMalloc(&M->val, sizeof(cd) * (nnz > 0 ? nnz : 1));
+  if (e == hipSuccess) e = hipMalloc(&M->val, sizeof(VS) * (nnz > 0 ? nnz : 1));
   if (e == hipSuccess) e = hipMemcpy(M->rowptr, M->h_rowptr.data(), sizeof(i64) * (size_t)(M->m + 1), hipMemcpyHostToDevice);
   if (e == hipSuccess && nnz) e = hipMemcpy(M->col, M->h_col.data(), sizeof(i64) * nnz, hipMemcpyHostToDevice);
-  if (e == hipSuccess && nnz) e = hipMemcpy(M->val, M->h_val.data(), sizeof(cd) * nnz, hipMemcpyHostToDevice);
+  if (e == hipSuccess && nnz) e = hipMemcpy(M->val, M->h_val.data(), sizeof(VS) * nnz, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     if (M->rowptr) hipFree(M->rowptr);
     if (M->col) hipFree(M->col);
@@ -1145,15 +1170,15 @@ static PetscErrorCode aij_mult(Mat A, Vec x, Vec y) {
   if (x == y) return ERR(PETSC_ERR_ARG_IDN, "x and y must be different vectors");
   if (x->hip && y->hip) {
     PetscCall(aij_upload(A));
-    const cd* xd;
+    const VS* xd;
     PetscCall(dev_read(x, &xd));
-    cd* yd;
+    VS* yd;
     PetscCall(dev_rw(y, &yd));
     HIPK(cfp::blas_csr_spmv(A->m, (i64)A->h_col.size(), A->rowptr, A->col, A->val, xd, yd, g_stream));
   } else {
-    const cd* xh;
+    const VS* xh;
     PetscCall(host_read(x, &xh));
-    cd* yh;
+    VS* yh;
     PetscCall(host_rw(y, &yh));
     for (i64 r = 0; r < A->m; ++r) {
       std::complex<double> s = 0;
@@ -1161,7 +1186,7 @@ static PetscErrorCode aij_mult(Mat A, Vec x, Vec y) {
       yh[r] = D(s);
     }
     if (y->hip) {
-      HIPK(hipMemcpyAsync(y->d, y->h, sizeof(cd) * (size_t)y->n, hipMemcpyHostToDevice, g_stream));
+      HIPK(hipMemcpyAsync(y->d, y->h, sizeof(VS) * (size_t)y->n, hipMemcpyHostToDevice, g_stream));
       y->mask = MASK_BOTH;
     }
   }
@@ -1189,7 +1214,7 @@ extern "C" PetscErrorCode MatShift(Mat A, PetscScalar a) {
     if (!found) return ERR(PETSC_ERR_ARG_WRONGSTATE, "MatShift needs an allocated diagonal");
   }
   if (A->val && !A->h_val.empty())
-    HCHK(hipMemcpy(A->val, A->h_val.data(), sizeof(cd) * A->h_val.size(), hipMemcpyHostToDevice));
+    HCHK(hipMemcpy(A->val, A->h_val.data(), sizeof(VS) * A->h_val.size(), hipMemcpyHostToDevice));
   return PETSC_SUCCESS;
 }
 extern "C" PetscErrorCode MatDestroy(Mat* pA) {
@@ -1215,11 +1240,15 @@ extern "C" PetscErrorCode MatCreateVecsFFTW(Mat A, Vec* x, Vec* y, Vec* z) {
   MCHK(A);
   int P = 1;
   MPI_Comm_size(A->comm, &P);
+  // x, z: the input / backward-output side (A's columns); y: the spectrum (A's rows).  Complex
+  // scalars: both N; real scalars: N reals and FFTW's r2c half spectrum (pcshell_fft3d.cpp)
   Vec* outs[3] = {x, y, z};
-  for (Vec* o : outs) {
+  for (int k = 0; k < 3; ++k) {
+    Vec* o = outs[k];
     if (!o) continue;
-    if (P > 1) PetscCall(VecCreateMPIHIP(A->comm, A->ln, A->n, o));  // the matrix' slab rows
-    else PetscCall(VecCreateSeqHIP(PETSC_COMM_SELF, A->n, o));
+    const PetscInt nl = k == 1 ? A->lm : A->ln, ng = k == 1 ? A->m : A->n;
+    if (P > 1) PetscCall(VecCreateMPIHIP(A->comm, nl, ng, o));  // the matrix' slab rows
+    else PetscCall(VecCreateSeqHIP(PETSC_COMM_SELF, ng, o));
   }
   return PETSC_SUCCESS;
 }

@@ -46,6 +46,20 @@ int cfp_rplan_schedule(cfp_rplan_t plan, int *three);
 int cfp_rplan_num_passes(cfp_rplan_t plan, int *passes);
 int cfp_rplan_time_passes(cfp_rplan_t plan, const double *b, double *x, int iters, double *ms_out, void *stream);
 
+/* Layout conversions of the real-scalar PETSc boundary (include/pcshell_fft3d.h built with
+ * -DCFP_REAL_SCALAR), device arrays, stream-ordered:
+ *   cfp_real_to_complex       z[i] = (x[i], 0), n values
+ *   cfp_complex_real_part     x[i] = scale * Re z[i]
+ *   cfp_half_spectrum_extract half = the [nz][ny][nx/2 + 1] complex r2c half spectrum (FFTW's
+ *                             r2c output layout, a real-scalar MATFFTW's MatMult) of the full
+ *                             [nz][ny][nx] spectrum
+ *   cfp_half_spectrum_extend  the full spectrum from the half by Hermitian symmetry,
+ *                             X(kx, ky, kz) = conj X(nx - kx, -ky, -kz) for kx > nx/2 */
+int cfp_real_to_complex(const double *x, double *z, int64_t n, void *stream);
+int cfp_complex_real_part(const double *z, double *x, int64_t n, double scale, void *stream);
+int cfp_half_spectrum_extract(const double *full, double *half, int64_t nx, int64_t ny, int64_t nz, void *stream);
+int cfp_half_spectrum_extend(const double *half, double *full, int64_t nx, int64_t ny, int64_t nz, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -31,13 +31,25 @@
 #include <stddef.h>
 #include <stdint.h>
 
+/* PetscScalar: complex double (PETSC_USE_COMPLEX, the default), or double when built with
+ * -DCFP_REAL_SCALAR (a PETSc configured with real scalars, the reference's !PETSC_USE_COMPLEX
+ * branches: libcirculant_fft_real.so) */
+#ifdef CFP_REAL_SCALAR
+typedef double PetscScalar;
+#else
+#define PETSC_USE_COMPLEX 1
+#endif
 #ifdef __cplusplus
 #include <complex>
+#ifndef CFP_REAL_SCALAR
 typedef std::complex<double> PetscScalar;
+#endif
 extern "C" {
 #else
+#ifndef CFP_REAL_SCALAR
 #include <complex.h>
 typedef double _Complex PetscScalar;
+#endif
 #endif
 
 typedef int PetscErrorCode;
