@@ -150,6 +150,16 @@ PetscErrorCode fft_mult_impl(Mat A, Vec x, Vec y, bool backward) {
   CFPCALL(rc);
   return PETSC_SUCCESS;
 }
+#ifdef CFP_WITH_PETSC
+// MatCreateVecsFFTW(A, x, y, z) on the shell: PETSc dispatches it through this composed method
+// (a MATSHELL has no MatCreateVecsFFTW_C of its own)
+PetscErrorCode fft_create_vecs(Mat A, Vec* x, Vec* y, Vec* z) {
+  if (x) PetscCall(MatCreateVecs(A, x, NULL));
+  if (y) PetscCall(MatCreateVecs(A, NULL, y));
+  if (z) PetscCall(MatCreateVecs(A, z, NULL));
+  return PETSC_SUCCESS;
+}
+#endif
 PetscErrorCode fft_mult(Mat A, Vec x, Vec y) { return fft_mult_impl(A, x, y, false); }
 PetscErrorCode fft_mult_transpose(Mat A, Vec x, Vec y) { return fft_mult_impl(A, x, y, true); }
 PetscErrorCode fft_destroy(Mat A) {
@@ -313,6 +323,9 @@ extern "C" PetscErrorCode MatCreateFFTHIP(MPI_Comm comm, PetscInt ndim, const Pe
   PetscCall(MatShellSetOperation(*A, MATOP_MULT, (void (*)(void))fft_mult));
   PetscCall(MatShellSetOperation(*A, MATOP_MULT_TRANSPOSE, (void (*)(void))fft_mult_transpose));
   PetscCall(MatShellSetOperation(*A, MATOP_DESTROY, (void (*)(void))fft_destroy));
+#ifdef CFP_WITH_PETSC
+  PetscCall(PetscObjectComposeFunction((PetscObject)*A, "MatCreateVecsFFTW_C", fft_create_vecs));
+#endif
   return PETSC_SUCCESS;
 }
 

@@ -32,8 +32,8 @@
 #include "../../include/pcshell_fft3d.h"
 #include "pcshell_common.h"
 
-#ifndef CFP_REAL_SCALAR
-#error "pcshell_fft3d_real.cpp is the real-scalar boundary: build it with -DCFP_REAL_SCALAR"
+#if defined(PETSC_USE_COMPLEX)
+#error "pcshell_fft3d_real.cpp is the real-scalar boundary: build it with -DCFP_REAL_SCALAR (stand-in) or against a real-scalar PETSc"
 #endif
 
 namespace {
@@ -127,6 +127,15 @@ PetscErrorCode rfft_mult_transpose(Mat A, Vec y, Vec x) {
   CFPCALL(rc);
   return PETSC_SUCCESS;
 }
+#ifdef CFP_WITH_PETSC
+// MatCreateVecsFFTW(A, x, y, z) on the shell: PETSc dispatches it through this composed method
+PetscErrorCode rfft_create_vecs(Mat A, Vec* x, Vec* y, Vec* z) {
+  if (x) PetscCall(MatCreateVecs(A, x, NULL));
+  if (y) PetscCall(MatCreateVecs(A, NULL, y));
+  if (z) PetscCall(MatCreateVecs(A, z, NULL));
+  return PETSC_SUCCESS;
+}
+#endif
 PetscErrorCode rfft_destroy(Mat A) {
   RShell* s;
   PetscCall(rshell(A, &s));
@@ -271,6 +280,9 @@ extern "C" PetscErrorCode MatCreateFFTHIP(MPI_Comm comm, PetscInt ndim, const Pe
   PetscCall(MatShellSetOperation(*A, MATOP_MULT, (void (*)(void))rfft_mult));
   PetscCall(MatShellSetOperation(*A, MATOP_MULT_TRANSPOSE, (void (*)(void))rfft_mult_transpose));
   PetscCall(MatShellSetOperation(*A, MATOP_DESTROY, (void (*)(void))rfft_destroy));
+#ifdef CFP_WITH_PETSC
+  PetscCall(PetscObjectComposeFunction((PetscObject)*A, "MatCreateVecsFFTW_C", rfft_create_vecs));
+#endif
   return PETSC_SUCCESS;
 }
 
