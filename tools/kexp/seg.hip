@@ -84,33 +84,46 @@ extern "C" int seg_run(int kind, int tx, int nr, int xcd, const void* in, void* 
 }
 
 // ---------------------------------------------------------------------------------------------
-// r04: the 3-sweep chain's three patterns as pure copies, natural against the
-// blocked intermediate layout (k_tp_rows<.., BL>): within the 8 rows y2 + 8 k1 of one k1 the
-// blocked layout holds [x / 8][y2][x % 8].  P1: rows y2 + 8 y1 of a plane (32 x 4 KiB runs) ->
-// rows k1 (natural: 4 KiB runs; blocked: 128-byte runs); P2 (in place): 8 x times 8 y2 times 256 z
-// (natural: 8 runs of 128 B per z; blocked: one 1 KiB run per z); P3 (in place): P1's pattern
-// reversed.  Thread maps as in the kernels: P1/P3 512 threads = (tx 16, row 32), 16 slots x = tx +
-// 16 m; P2 1024 threads = (column 64, tz 16), slots z = tz + 16 m.
-template <bool BL, bool REV>
-__global__ void __launch_bounds__(512) k_chain_rows(const cd* __restrict__ in, cd* __restrict__ out) {
+// r04: the 3-sweep chain's three patterns as pure copies, for several
+// intermediate layouts.  Within the 8 rows y2 + 8 k1 of one k1 (contiguous in every layout):
+//   mode 0 natural   [y2][x]                 P2 unit: T/8 x times 8 y2 = 8 runs of T B per z
+//   mode 1 blocked8  [x / 8][y2][x % 8]      P2 unit of 64 columns: one 1 KiB run per z
+//   mode 2 blocked4  [x / 4][y2][x % 4]      P2 unit of 32 columns: one 512 B run per z
+// P1: rows y2 + 8 y1 of a plane (32 x 4 KiB runs) -> rows k1 in the mode's layout (natural 4 KiB
+// runs, blocked8 128 B, blocked4 64 B); P2 (in place): T columns x 256 z (T = 64: 1024 threads,
+// one workgroup per CU; T = 32: 512 threads, two per CU); P3 (in place): P1's pattern reversed.
+// Thread maps as in the kernels: P1/P3 512 threads = (tx 16, row 32), slots x = tx + 16 m; P2
+// T x 16 threads = (column T, tz 16), slots z = tz + 16 m.
+__device__ __forceinline__ long long blk_off(int mode, int k1, int y2, int x) {
+  if (mode == 0) return 256LL * (y2 + 8 * k1) + x;
+  const int XB = mode == 1 ? 8 : 4;
+  return 2048LL * k1 + (long long)(x / XB) * (8 * XB) + y2 * XB + x % XB;
+}
+template <bool REV>
+__global__ void __launch_bounds__(512) k_chain_rows(const cd* __restrict__ in, cd* __restrict__ out, int mode) {
   const int tid = threadIdx.x, tx = tid % 16, r = tid / 16;
   const int z = blockIdx.x / 8, y2 = blockIdx.x % 8;
   const long long plane = (long long)n * n * z;
-  const long long nat = plane + (long long)n * (y2 + 8 * r) + tx;                  // row y2 + 8 r, natural
-  const long long blk = plane + 2048LL * r + 8 * y2 + (tx / 8) * 64 + tx % 8;       // row block r, blocked
-  const long long src = REV && BL ? blk : nat, dst = !REV && BL ? blk : nat;
-  const int ss = REV && BL ? 128 : 16, ds = !REV && BL ? 128 : 16;
   cd v[16];
 #pragma unroll
-  for (int m = 0; m < 16; ++m) v[m] = in[src + ss * m];
+  for (int m = 0; m < 16; ++m) {
+    const int x = tx + 16 * m;
+    v[m] = in[plane + (REV ? blk_off(mode, r, y2, x) : 256LL * (y2 + 8 * r) + x)];
+  }
 #pragma unroll
-  for (int m = 0; m < 16; ++m) out[dst + ds * m] = v[m];
+  for (int m = 0; m < 16; ++m) {
+    const int x = tx + 16 * m;
+    out[plane + (REV ? 256LL * (y2 + 8 * r) + x : blk_off(mode, r, y2, x))] = v[m];
+  }
 }
-template <bool BL>
-__global__ void __launch_bounds__(1024) k_chain_mid(const cd* __restrict__ in, cd* __restrict__ out) {
-  const int tid = threadIdx.x, c = tid % 64, tz = tid / 64;
-  const int xt = blockIdx.x % 32, k1 = blockIdx.x / 32;
-  const long long col = BL ? 2048LL * k1 + 64 * xt + c : (long long)n * (c / 8 + 8 * k1) + 8 * xt + c % 8;
+template <int T>
+__global__ void __launch_bounds__(T * 16) k_chain_mid(const cd* __restrict__ in, cd* __restrict__ out, int mode) {
+  constexpr int XU = T / 8, NXT = 256 / XU;  // x per unit, x tiles
+  const int tid = threadIdx.x, c = tid % T, tz = tid / T;
+  const int xt = blockIdx.x % NXT, k1 = blockIdx.x / NXT;
+  const int x = xt * XU + c % XU, y2 = c / XU;
+  const long long col = (mode == 1 && XU == 8) || (mode == 2 && XU == 4) ? 2048LL * k1 + (long long)xt * T + c
+                                                                         : blk_off(mode, k1, y2, x);
   cd v[16];
 #pragma unroll
   for (int m = 0; m < 16; ++m) v[m] = in[col + (long long)n * n * (tz + 16 * m)];
@@ -118,51 +131,47 @@ __global__ void __launch_bounds__(1024) k_chain_mid(const cd* __restrict__ in, c
   for (int m = 0; m < 16; ++m) out[col + (long long)n * n * (tz + 16 * m)] = v[m];
 }
 
-// chain b -> x (P1), x -> x (P2), x -> x (P3), iters times; us[0..2] = mean per-kernel time
-// (events between the kernels), us[3] = mean chain time without them
-extern "C" int seg_chain(int blocked, const void* b, void* x, int iters, double* us) {
+// chain b -> x (P1), x -> x (P2), x -> x (P3), iters times, layout `mode`, P2 tile T (64 or 32);
+// us[0..2] = mean per-kernel time (events between the kernels), us[3] = mean chain time without
+extern "C" int seg_chain(int mode, int T, const void* b, void* x, int iters, double* us) {
+  if (mode < 0 || mode > 2 || (T != 64 && T != 32)) return 1;
   hipEvent_t e[4];
-  for (auto& q : e) hipEventCreate(&q);
+  for (auto& q : e) (void)hipEventCreate(&q);
   float acc[3] = {0, 0, 0};
   const cd* bb = (const cd*)b;
   cd* xx = (cd*)x;
+  auto mid = [&]() {
+    if (T == 64) hipLaunchKernelGGL((k_chain_mid<64>), dim3(1024), dim3(1024), 0, 0, xx, xx, mode);
+    else hipLaunchKernelGGL((k_chain_mid<32>), dim3(2048), dim3(512), 0, 0, xx, xx, mode);
+  };
   for (int it = -1; it < iters; ++it) {
-    hipEventRecord(e[0], 0);
-    if (blocked) hipLaunchKernelGGL((k_chain_rows<true, false>), dim3(2048), dim3(512), 0, 0, bb, xx);
-    else hipLaunchKernelGGL((k_chain_rows<false, false>), dim3(2048), dim3(512), 0, 0, bb, xx);
-    hipEventRecord(e[1], 0);
-    if (blocked) hipLaunchKernelGGL((k_chain_mid<true>), dim3(1024), dim3(1024), 0, 0, xx, xx);
-    else hipLaunchKernelGGL((k_chain_mid<false>), dim3(1024), dim3(1024), 0, 0, xx, xx);
-    hipEventRecord(e[2], 0);
-    if (blocked) hipLaunchKernelGGL((k_chain_rows<true, true>), dim3(2048), dim3(512), 0, 0, xx, xx);
-    else hipLaunchKernelGGL((k_chain_rows<false, true>), dim3(2048), dim3(512), 0, 0, xx, xx);
-    hipEventRecord(e[3], 0);
-    hipEventSynchronize(e[3]);
+    (void)hipEventRecord(e[0], 0);
+    hipLaunchKernelGGL((k_chain_rows<false>), dim3(2048), dim3(512), 0, 0, bb, xx, mode);
+    (void)hipEventRecord(e[1], 0);
+    mid();
+    (void)hipEventRecord(e[2], 0);
+    hipLaunchKernelGGL((k_chain_rows<true>), dim3(2048), dim3(512), 0, 0, xx, xx, mode);
+    (void)hipEventRecord(e[3], 0);
+    (void)hipEventSynchronize(e[3]);
     if (it < 0) continue;
     for (int k = 0; k < 3; ++k) {
       float t = 0;
-      hipEventElapsedTime(&t, e[k], e[k + 1]);
+      (void)hipEventElapsedTime(&t, e[k], e[k + 1]);
       acc[k] += t;
     }
   }
   for (int k = 0; k < 3; ++k) us[k] = 1e3 * acc[k] / iters;
-  hipEventRecord(e[0], 0);
+  (void)hipEventRecord(e[0], 0);
   for (int it = 0; it < iters; ++it) {
-    if (blocked) {
-      hipLaunchKernelGGL((k_chain_rows<true, false>), dim3(2048), dim3(512), 0, 0, bb, xx);
-      hipLaunchKernelGGL((k_chain_mid<true>), dim3(1024), dim3(1024), 0, 0, xx, xx);
-      hipLaunchKernelGGL((k_chain_rows<true, true>), dim3(2048), dim3(512), 0, 0, xx, xx);
-    } else {
-      hipLaunchKernelGGL((k_chain_rows<false, false>), dim3(2048), dim3(512), 0, 0, bb, xx);
-      hipLaunchKernelGGL((k_chain_mid<false>), dim3(1024), dim3(1024), 0, 0, xx, xx);
-      hipLaunchKernelGGL((k_chain_rows<false, true>), dim3(2048), dim3(512), 0, 0, xx, xx);
-    }
+    hipLaunchKernelGGL((k_chain_rows<false>), dim3(2048), dim3(512), 0, 0, bb, xx, mode);
+    mid();
+    hipLaunchKernelGGL((k_chain_rows<true>), dim3(2048), dim3(512), 0, 0, xx, xx, mode);
   }
-  hipEventRecord(e[1], 0);
-  hipEventSynchronize(e[1]);
+  (void)hipEventRecord(e[1], 0);
+  (void)hipEventSynchronize(e[1]);
   float t = 0;
-  hipEventElapsedTime(&t, e[0], e[1]);
+  (void)hipEventElapsedTime(&t, e[0], e[1]);
   us[3] = 1e3 * t / iters;
-  for (auto& q : e) hipEventDestroy(q);
+  for (auto& q : e) (void)hipEventDestroy(q);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
