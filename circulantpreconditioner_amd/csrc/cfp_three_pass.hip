@@ -112,17 +112,19 @@ constexpr int r0_of(int n, int pts) { return n > pts ? r0_of(n / pts, pts) : n; 
 // y1), the twiddle W_32^k on the odd lane, and a radix-2 across lane bit 5 on permlane32 swaps:
 // no LDS exchange and no barrier pair in phase A.  Slot m then holds k1 = m % 8 + 8 ty + 16 (m / 8).
 //
-// BL (blocked intermediate layout, r04): the N2 rows y2 + N2 k1 of one k1 (contiguous in every
-// layout) hold [x / BX][y2][x % BX] with BX = 64 / N2 instead of [y2][x], so a P2 unit's 64
-// columns (BX x times N2 y2) are one 1 KiB run per z; P1's stores and P3's loads become BX x 16 B
-// runs instead.  Only the intermediate between the sweeps changes; b and x stay natural.
-template <bool INV, int FLAGS, int N1, int TN, int PTS = 16, bool XS = true, bool LP = false, bool BL = false>
+// BLK (blocked intermediate layout, r04): the N2 rows y2 + N2 k1 of one k1 (contiguous in every
+// layout) hold [x / BLK][y2][x % BLK] instead of [y2][x], so a P2 unit of BLK x times N2 y2
+// columns is one run of N2 BLK 16 bytes per z (1 KiB at BLK = 8); P1's stores and P3's loads
+// become BLK x 16 B runs instead.  Only the intermediate between the sweeps changes; b and x
+// stay natural.  BLK = 0: natural.
+template <bool INV, int FLAGS, int N1, int TN, int PTS = 16, bool XS = true, bool LP = false, int BLK = 0>
 __global__ void __launch_bounds__(N1 * (TN / PTS)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
   constexpr int N2 = TN / N1, TR = TN / PTS, NT = N1 * TR, TY = N1 / PTS;
-  constexpr int BX = 64 / N2;  // x per block column of the blocked layout
+  constexpr bool BL = BLK > 0;
+  constexpr int BX = BL ? BLK : 1, BW = N2 * BX;  // x per block column, values per block column
   static_assert(!LP || (TY == 2 && TN % 32 == 0), "lane pairs: two threads per column, 32 columns per wave");
-  static_assert(!BL || (N2 == 8 && TR % BX == 0), "blocked layout: 8 x times 8 y2 per block column");
+  static_assert(!BL || (N2 == 8 && TR % BX == 0 && (BX == 4 || BX == 8)), "blocked layout: 4 or 8 x times 8 y2");
   constexpr int RS = TN + TN / 16;  // padded row stride of the row-mode LDS layout
   constexpr int F = FLAGS | (XS ? F_SPLIT_LDS : 0) | F_LDS_SYNC;
   __shared__ __attribute__((aligned(16))) double lds[N1 * RS * (XS ? 1 : 2)];  // both layouts fit
@@ -151,7 +153,7 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
   const auto load = [&](int u, cd* v) {
     const int x = idx(x0), ty = idx(ty0);
     if (INV) {  // chunked rows: per-thread part + uniform part (nyl >= N2 TY)
-      const cd* const src = BL ? in + crow(u / N2, N2 * ty) + (u % N2) * BX + (x / BX) * 64 + x % BX
+      const cd* const src = BL ? in + crow(u / N2, N2 * ty) + (u % N2) * BX + (x / BX) * BW + x % BX
                                : in + crow(u / N2, u % N2 + N2 * ty) + x;
 #pragma unroll
       for (int m = 0; m < PTS; ++m) v[m] = gload<FLAGS>(src + crow(0, N2 * TY * m));
@@ -237,7 +239,7 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
       const int r = idx(r0), tx = idx(tx0);
       const double sc = a.scale, sy = INV ? -sc : sc;
       if (BL && !INV) {  // blocked: kx = tx + TR m at (kx / BX) 64 + y2 BX + kx % BX of row block r
-        cd* dst = out + crow(u / N2, N2 * r) + (u % N2) * BX + (tx / BX) * 64 + tx % BX;
+        cd* dst = out + crow(u / N2, N2 * r) + (u % N2) * BX + (tx / BX) * BW + tx % BX;
 #pragma unroll
         for (int m = 0; m < PTS; ++m) gstore<FLAGS>(dst + TR * N2 * m, make_cd(v[m].x * sc, v[m].y * sy));
       } else {
@@ -402,15 +404,21 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 // NX: x extent (row length in points) of the grid P2 runs on: TN for the complex apply, TN / 2
 // for the real-data plan's half spectrum (cfp_real.hip); y and z are TN long.
-// BL: the blocked intermediate layout of k_tp_rows<.., BL>: a unit's 64 columns c = x + XT y2 are
-// the 1 KiB run at block column xt of row block k1, for every z.
+// BL: the blocked intermediate layout of k_tp_rows<.., BLK = XT>: a unit's T columns c = x + XT y2
+// are the run at block column xt of row block k1, for every z (T 16 bytes).
+//
+// T = 32 (r04): 512 threads, two workgroups per CU that run their barrier phases independently.
+// A wave then holds two z groups of the 32 columns: lane = x (bits 0-1) + tz parity (bit 2) +
+// y2 (bits 3-5), so y2 keeps lane bits 3-5 and every y2 stage below (permlane swaps on bits 5 and
+// 4, DPP on bit 3) is the T = 64 code; c (the column x + 4 y2) and tz index memory and LDS,
+// `lane` the lane bits.
 template <int T, int N2, int TN, int PROBE = 0, bool PF = false, int NX = TN, int ST = 0, int LD = 0, bool BL = false>
 __global__ void __launch_bounds__(T * (TN / 16)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
 #ifndef CFP_KEXP
   static_assert(PROBE == 0, "timing probes are built in tools/kexp only");
 #endif
-  static_assert(T == 64, "one wave = all 64 columns of a z group");
+  static_assert(T == 64 || (T == 32 && N2 == 8), "a wave = the 64 columns of one z group, or 32 columns of two");
   static_assert(N2 == 4 || N2 == 8, "y2 = the top 2 or 3 lane bits");
   static_assert(TN == 256, "z = 16 x 16: radix-16 stage A in registers, one exchange, radix-16 stage B");
   constexpr int N1 = TN / N2, TZ = TN / 16, NT = T * TZ, XT = T / N2, NXT = NX / XT;
@@ -422,7 +430,9 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
   const int tid = threadIdx.x;
   for (int i = tid; i < TN; i += NT) tw_l[i] = a.tw[i];
   __syncthreads();  // the y2 stages read tw_l before the first exchange barrier
-  const int c0 = tid & (T - 1), tz0 = tid / T;
+  const int lane0 = tid & 63;
+  const int c0 = T == 64 ? lane0 : (lane0 & 3) | ((lane0 >> 3) << 2);
+  const int tz0 = T == 64 ? tid / 64 : 2 * (tid >> 6) + ((lane0 >> 2) & 1);
   // rows of this rank's block [TN z][nyl][NX] (one GPU: nyl = TN); unit u = (x tile, local k1)
   const i64 zs = (i64)NX << (a.lnyl ? a.lnyl : ilog2(TN));
   const auto idx = [](int i) {
@@ -446,7 +456,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
       __builtin_amdgcn_global_load_lds((glb_void_t*)(src + zs * TZ * m), (lds_void_t*)(lds + (wv * NPF + m) * 128),
                                        16, 0, (LD & F_NT_LD) ? 2 : 0);
   };
-  static_assert(!PF || 16 * NPF * 128 <= T * TN, "the prefetch fits the exchange buffer");
+  static_assert(!PF || (NT / 64) * NPF * 128 <= T * TN, "the prefetch fits the exchange buffer");
   if constexpr (PF) {
     if ((int)blockIdx.x < nunits) prefetch(blockIdx.x);
   }
@@ -454,8 +464,8 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
   // layout: v[t] = point tz + 16 t of column c
   const auto exchange_t = [&](cd* v, bool first) {
     if constexpr (PROBE & PR_NO_XCHG) return;
-    const int c = idx(c0), tz = idx(tz0);
-    const int l3 = N2 == 8 ? ((c >> 3) & 1) : 0, l4 = (c >> 4) & 1, l5 = (c >> 5) & 1;
+    const int c = idx(c0), tz = idx(tz0), lane = idx(lane0);
+    const int l3 = N2 == 8 ? ((lane >> 3) & 1) : 0, l4 = (lane >> 4) & 1, l5 = (lane >> 5) & 1;
     const int wbase = (tz * 16 + l5 + 2 * l4) * T + (c & (XT - 1)) + XT * l3;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -483,8 +493,8 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
     dft_reg<16>(v);
   };
   const auto lane_sign = [&]() {  // +1 where lane bit 3 is clear, -1 where set
-    const int c = idx(c0);
-    return (c & 8) ? -1.0 : 1.0;
+    const int lane = idx(lane0);
+    return (lane & 8) ? -1.0 : 1.0;
   };
 
   for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
@@ -501,7 +511,10 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
       if constexpr (PF) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA (and loads) landed
 #pragma unroll
-        for (int m = 0; m < NPF; ++m) v[m] = fromv(*reinterpret_cast<const dv2*>(lds + (wv * NPF + m) * 128 + 2 * c));
+        for (int m = 0; m < NPF; ++m) {  // the DMA is lane-linear
+          const int lane = idx(lane0);
+          v[m] = fromv(*reinterpret_cast<const dv2*>(lds + (wv * NPF + m) * 128 + 2 * lane));
+        }
       }
     }
     {
@@ -515,20 +528,20 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
     if constexpr (PROBE & PR_NO_Y2) {
     } else if constexpr (N2 == 8) {
       {
-        const int c = idx(c0);
-        dif_pairs<5, 1>(v, tw_l[(TN / 8) * ((c >> 3) & 3)]);  // W_8^{y2 & 3}
+        const int lane = idx(lane0);
+        dif_pairs<5, 1>(v, tw_l[(TN / 8) * ((lane >> 3) & 3)]);  // W_8^{y2 & 3}
       }
       {
-        const int c = idx(c0);
-        dif_pairs<4, 2>(v, tw_l[(TN / 4) * ((c >> 3) & 1)]);  // W_4^{y2 & 1}
+        const int lane = idx(lane0);
+        dif_pairs<4, 2>(v, tw_l[(TN / 4) * ((lane >> 3) & 1)]);  // W_4^{y2 & 1}
       }
       const double s = lane_sign();
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = bfly_l3(v[r], s);
     } else {
       {
-        const int c = idx(c0);
-        dif_pairs<5, 1>(v, tw_l[(TN / 4) * ((c >> 4) & 1)]);  // W_4^{y2 & 1}
+        const int lane = idx(lane0);
+        dif_pairs<5, 1>(v, tw_l[(TN / 4) * ((lane >> 4) & 1)]);  // W_4^{y2 & 1}
       }
       dif_pairs<4, 2, false>(v, make_cd(1.0, 0.0));
     }
@@ -554,8 +567,8 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
         for (int r = 0; r < 16; ++r) v[r] = bfly_l3(v[r], s);
       }
       {
-        const int c = idx(c0);
-        const cd w = tw_l[(TN / 4) * ((c >> 3) & 1)];  // W_4^{p & 1}, p bit 0 = lane bit 3
+        const int lane = idx(lane0);
+        const cd w = tw_l[(TN / 4) * ((lane >> 3) & 1)];  // W_4^{p & 1}, p bit 0 = lane bit 3
 #pragma unroll
         for (int k = 0; k < 16; ++k)
           if ((k & 2) == 0) swap_c<4>(v[k], v[k + 2]);
@@ -569,8 +582,8 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
       }
       {
         // W_8^{p & 3}: p bit 0 = lane bit 3, p bit 1 = register bit 1 -> W_8^{l3} (x -i if r1)
-        const int c = idx(c0);
-        const cd w = tw_l[(TN / 8) * ((c >> 3) & 1)];
+        const int lane = idx(lane0);
+        const cd w = tw_l[(TN / 8) * ((lane >> 3) & 1)];
 #pragma unroll
         for (int k = 0; k < 16; ++k)
           if ((k & 1) == 0) swap_c<5>(v[k], v[k + 1]);
@@ -854,7 +867,7 @@ constexpr bool kRowsLP = true;
 // which nothing reads after it: chain 304.4 -> 300.7 us
 constexpr int kP2LoadFlags = F_NT_LD;
 
-template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true, bool LP = false, bool BL = false>
+template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true, bool LP = false, int BL = 0>
 static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
   constexpr int units = TN * (TN / N1);  // z-planes x y2
   const unsigned g = grid_of(units, PER_CU);
@@ -873,11 +886,11 @@ static void launch_mid(cd* data, const TPArgs& a, hipStream_t s) {
   TP_LAUNCH((k_tp_mid<0, T, N2, TN, PTS, XS>), dim3(grid_of(units, PER_CU)), dim3(T * (TN / PTS)), s, data, a, units);
 }
 
-template <int N2, int TN, bool PF = false, bool BL = false>
+template <int N2, int TN, bool PF = false, bool BL = false, int T = 64>
 static void launch_mid_sw(cd* data, const TPArgs& a, hipStream_t s) {
-  constexpr int units = (TN / (64 / N2)) * (TN / N2);
-  TP_LAUNCH((k_tp_mid_sw<64, N2, TN, 0, PF, TN, 0, kP2LoadFlags, BL>), dim3(grid_of(units, 1)), dim3(64 * (TN / 16)),
-            s, data, a, units);
+  constexpr int units = (TN / (T / N2)) * (TN / N2);
+  TP_LAUNCH((k_tp_mid_sw<T, N2, TN, 0, PF, TN, 0, kP2LoadFlags, BL>), dim3(grid_of(units, 64 / T)),
+            dim3(T * (TN / 16)), s, data, a, units);
 }
 
 bool three_pass_slab_supported(const i64 n[3], int P) {
@@ -909,8 +922,8 @@ hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs
 }
 
 bool three_pass_shape_valid(int n1, int mid) {
-  return (n1 == 0 || n1 == 32 || n1 == 64) && (mid >= 0 && mid <= TP_MID_BLOCKED) &&
-         !(mid == TP_MID_BLOCKED && n1 == 64);
+  return (n1 == 0 || n1 == 32 || n1 == 64) && (mid >= 0 && mid <= TP_MID_BLOCKED32) &&
+         !(mid >= TP_MID_BLOCKED && n1 == 64);
 }
 
 hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, TPShape shape,
@@ -941,10 +954,16 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
   // the LDS-DMA prefetch (global_load_lds_dwordx4) takes 16-byte aligned addresses: a buffer that
   // is only 8-byte aligned runs the same kernel without it
   const bool pf_ok = ((uintptr_t)out & 15) == 0;
-  if (shape.mid == TP_MID_BLOCKED) {  // N1 = 32, blocked intermediate layout (k_tp_rows<.., BL>)
-    if (stage != 1) launch_rows<32, 256, 2, 16, true, kRowsLP, true>(stage, in, out, a, s);
+  if (shape.mid == TP_MID_BLOCKED) {  // N1 = 32, blocked intermediate layout (k_tp_rows<.., 8>)
+    if (stage != 1) launch_rows<32, 256, 2, 16, true, kRowsLP, 8>(stage, in, out, a, s);
     else if (pf_ok) launch_mid_sw<8, 256, true, true>(out, a, s);
     else launch_mid_sw<8, 256, false, true>(out, a, s);
+    return hipGetLastError();
+  }
+  if (shape.mid == TP_MID_BLOCKED32) {  // blocks of 4 x; P2 = 32 columns, two workgroups per CU
+    if (stage != 1) launch_rows<32, 256, 2, 16, true, kRowsLP, 4>(stage, in, out, a, s);
+    else if (pf_ok) launch_mid_sw<8, 256, true, true, 32>(out, a, s);
+    else launch_mid_sw<8, 256, false, true, 32>(out, a, s);
     return hipGetLastError();
   }
   if (stage == 1) {

@@ -171,14 +171,15 @@ class CirculantPlan:
         check(lib().cfp_plan_set_schedule(self._h, v))
         return self
 
-    TP_MIDS = {"default": 0, "lane64": 1, "lane32": 2, "swap64": 3, "swap64pf": 4, "blocked": 5}
+    TP_MIDS = {"default": 0, "lane64": 1, "lane32": 2, "swap64": 3, "swap64pf": 4, "blocked": 5, "blocked32": 6}
 
     def set_three_pass_shape(self, n1: int = 0, mid: str | int = "default") -> "CirculantPlan":
         """Kernel shape of the 256^3 3-sweep schedule (tests / measurements): the y split n1
         (0 = default, 32 or 64) and the middle kernel ('default' = 'swap64pf', 'lane64', 'lane32',
         'swap64': the y2 DFT on permlane register transposes, 64-column tile; 'swap64pf': the
         same with an LDS-DMA prefetch of half the next unit; 'blocked': 'swap64pf' with the
-        blocked intermediate layout, 1 KiB P2 runs; n1 = 32 only)."""
+        blocked intermediate layout, 1 KiB P2 runs; 'blocked32': blocks of 4 x and the permlane
+        P2 on 32 columns, two workgroups per CU; n1 = 32 only)."""
         m = self.TP_MIDS[mid] if isinstance(mid, str) else int(mid)
         check(lib().cfp_plan_set_three_pass_shape(self._h, int(n1), m))
         return self
