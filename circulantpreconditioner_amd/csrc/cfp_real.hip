@@ -156,6 +156,7 @@ struct cfp_rplan_s {
   int schedule = CFP_RSCHEDULE_AUTO;
   cd* colsym3 = nullptr;  // [kx + M ky], kx < M
   cd* axsym3 = nullptr;   // [kz]
+  cd* colsymq = nullptr;  // [ky] of the Nyquist column kx = M
 };
 
 static bool three_ok(const cfp_rplan_s* p) {
@@ -184,6 +185,7 @@ void free_rplan(cfp_rplan_s* p) {
   if (p->Q) hipFree(p->Q);
   if (p->twn) hipFree(p->twn);
   if (p->colsym3) hipFree(p->colsym3);
+  if (p->colsymq) hipFree(p->colsymq);
   if (p->axsym3) hipFree(p->axsym3);
   if (p->fork) hipEventDestroy(p->fork);
   if (p->join) hipEventDestroy(p->join);
@@ -191,10 +193,9 @@ void free_rplan(cfp_rplan_s* p) {
   delete p;
 }
 
-// 3 sweeps at 128^3 and 256^3: P1r (r2c rows + y1, Nyquist column to Q) | P2 on the half spectrum |
-// P3r (y1 inverse + c2r rows).  The Nyquist column's own y/z plan runs in between, on the same
-// stream: at 256^3 P2's workgroups fill every CU; at 128^3 there is room beside P2, but the
-// side-stream handshake costs more than the column's launches (20,800 -> 15,400 PCApply/s, r03t).
+// 3 sweeps at 128^3 and 256^3: P1r (r2c rows + y1, also of the Nyquist column into Q) | P2 on the
+// half spectrum, then on Q's 32 k1 (one small launch) | P3r (y1 inverse + c2r rows).  (Until r04
+// the column took its own 3-launch y / z plan between P2 and P3r: 18.4 us at 256^3.)
 int run_real_three(cfp_rplan_s* p, const double* b, double* x, hipStream_t s, std::vector<hipEvent_t>* ev) {
   TPArgs a;
   a.tw = p->twn;  // W_n: nx = ny = nz = n
@@ -208,7 +209,10 @@ int run_real_three(cfp_rplan_s* p, const double* b, double* x, hipStream_t s, st
   e = launch_three_pass_real(1, (int)p->n[0], nullptr, p->H, nullptr, nullptr, a, s);
   if (e != hipSuccess) return hip_error(e, "half-spectrum y2/z pass");
   if (ev) HIPCHK(hipEventRecord((*ev)[2], s));
-  CFPCHK(cfp_plan_apply(p->nyq, (const double*)p->Q, (double*)p->Q, s));
+  TPArgs aq = a;
+  aq.colsym = p->colsymq;
+  e = launch_three_pass_real(3, (int)p->n[0], nullptr, nullptr, p->Q, nullptr, aq, s);
+  if (e != hipSuccess) return hip_error(e, "Nyquist column y2/z pass");
   if (ev) HIPCHK(hipEventRecord((*ev)[3], s));
   e = launch_three_pass_real(2, (int)p->n[0], nullptr, p->H, p->Q, x, a, s);
   if (e != hipSuccess) return hip_error(e, "y1 inverse + c2r rows pass");
@@ -314,10 +318,16 @@ extern "C" int cfp_rplan_set_symbol_transport(cfp_rplan_t p, const double lam[3]
         col[(size_t)(kx + M * ky)] = make_cd(lam[0] * hx[(size_t)kx].x + lam[1] * hy[(size_t)ky].x,
                                              lam[0] * hx[(size_t)kx].y + lam[1] * hy[(size_t)ky].y);
     for (i64 kz = 0; kz < nz; ++kz) ax[(size_t)kz] = make_cd(lam[2] * hz[(size_t)kz].x, lam[2] * hz[(size_t)kz].y);
+    std::vector<cd> colq((size_t)ny);  // the Nyquist column kx = M
+    for (i64 ky = 0; ky < ny; ++ky)
+      colq[(size_t)ky] = make_cd(lam[0] * hx[(size_t)M].x + lam[1] * hy[(size_t)ky].x,
+                                 lam[0] * hx[(size_t)M].y + lam[1] * hy[(size_t)ky].y);
     if (!p->colsym3) HIPCHK(hipMalloc(&p->colsym3, sizeof(cd) * col.size()));
     if (!p->axsym3) HIPCHK(hipMalloc(&p->axsym3, sizeof(cd) * ax.size()));
+    if (!p->colsymq) HIPCHK(hipMalloc(&p->colsymq, sizeof(cd) * colq.size()));
     HIPCHK(hipMemcpy(p->colsym3, col.data(), sizeof(cd) * col.size(), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(p->axsym3, ax.data(), sizeof(cd) * ax.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(p->colsymq, colq.data(), sizeof(cd) * colq.size(), hipMemcpyHostToDevice));
   }
   p->has_sym = true;
   return CFP_SUCCESS;

@@ -39,9 +39,10 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
 bool three_pass_slab_supported(const i64 n[3], int P);
 hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs& a, int nzl, hipStream_t s);
 // real-data plan at n^3, n = 128 or 256 (cfp_real.hip): stage 0 P1r (b -> H, Q), 1 P2 on H
-// (n/2 x n x n, in place), 2 P3r (H, Q -> x, x a.scale); a.tw = W_n, a.colsym = [kx + (n/2) ky],
-// a.axsym = [kz].  Q (n x n, the Nyquist column kx = n/2) takes its own y/z plan between P1r
-// and P3r.
+// (n/2 x n x n, in place), 3 the same on the Nyquist column Q (n x n, kx = n/2, in place;
+// a.colsym = its [ky] symbol), 2 P3r (H, Q -> x, x a.scale); a.tw = W_n, a.colsym =
+// [kx + (n/2) ky], a.axsym = [kz].  P1r leaves Q after its y1 DFT, P3r takes it before its y1
+// inverse (slot layout, as H).
 hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* Q, double* x, const TPArgs& a,
                                   hipStream_t s);
 

@@ -672,14 +672,17 @@ static unsigned grid_of(int units, int per_cu) {
 // (M = 128) takes the complex schedule's four-step split of y with the x transform replaced by
 // r2c / c2r (the even/odd split of k_rx):
 //   P1r k_tp_rows_r2c<false>: one z-plane's rows y2 + 8 y1 (32 real rows of 2 KiB): r2c along x
-//       (128-point FFT in row mode, mirror bin from the partner lane), Nyquist X[128] of each
-//       row to Q, LDS transpose, 32-point y1 DFT per kx (column mode), store H in slot layout
-//   P2  k_tp_mid_sw<.., NX = 128> on H (y2 + z + divide + inverse)
-//   P3r k_tp_rows_r2c<true>: y1 inverse, transpose, c2r merge with Q (after the Nyquist
-//       column's own y/z plan), inverse 128-point FFT, x 2/N
+//       (128-point FFT in row mode, mirror bin from the partner lane), LDS transpose, 32-point y1
+//       DFT per kx (column mode), store H in slot layout; the Nyquist bins X[128] of the unit's
+//       32 rows take the same y1 DFT (one wave, a direct 32-point DFT from LDS) into Q's slots
+//   P2  k_tp_mid_sw<.., NX = 128> on H (y2 + z + divide + inverse), then the Nyquist column's
+//       y2 + z + divide + inverse on Q (k_tp_mid on 8 columns of one k1: 32 small workgroups)
+//   P3r k_tp_rows_r2c<true>: y1 inverse (H in column mode, Q by one wave from LDS), transpose,
+//       c2r merge with Q, inverse 128-point FFT, x 2/N
 // P1r/P3r move 8 N + 8 N bytes, P2 16 N: 32 N per apply against ~80 N for r2c + 3 half-spectrum
 // passes + c2r.  (Folding the Nyquist column into P2 as a 17th x tile was measured slower: 544
-// units on 256 CUs take a third round, P2 70 -> 89 us.)
+// units on 256 CUs take a third round, P2 70 -> 89 us.  Until r04 the column took its own
+// 3-launch y / z plan between P2 and P3r: 18.4 us of the 199 us apply.)
 // 8 points per thread (512 threads): the even/odd split needs every point and its mirror live
 // at once, which at 16 points per thread spills.
 // At 128^3 (r03, AUTO there too): M = 64, y = y2 + 4 y1 (N1 = 32, N2 = 4), 256 threads; P2 is
@@ -696,6 +699,7 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
   __shared__ __attribute__((aligned(16))) double lds[N1 * RS];  // row layout; the column layout (N1 x M) fits
   __shared__ cd tw_m[M];   // W_M (row FFT)
   __shared__ cd tw_1[N1];  // W_N1 (y1 DFT)
+  __shared__ cd qy[N1];    // the unit's Nyquist bins over y1 (P1r: before its y1 DFT; P3r: after)
   const int tid = threadIdx.x;
   for (int i = tid; i < M; i += NT) tw_m[i] = a.tw[2 * i];
   for (int i = tid; i < N1; i += NT) tw_1[i] = a.tw[(2 * M / N1) * i];
@@ -736,7 +740,7 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
       const cd d = make_cd(v[m].x - zm[m].x, v[m].y + zm[m].y);  // Z[k] - conj Z[M-k]
       const cd o = make_cd(0.5 * d.y, -0.5 * d.x);                // d / 2i
       v[m] = cadd(e, cmul(w, o));
-      if (x == 0) Q[(i64)z * NY + y2 + N2 * (ty + TY * m)] = csub(e, o);  // Nyquist bin X[M]
+      if (x == 0) qy[ty + TY * m] = csub(e, o);  // Nyquist bin X[M] of row y1 = ty + TY m
     }
   };
   // column mode (column kx, rows y1 = ty + TY m, conjugated) -> row mode with the c2r merge: each
@@ -758,7 +762,7 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
       }
     }
     lds_barrier();
-    if (tpc == 0) xm[0] = Q[(i64)z * NY + y2 + N2 * r];  // k = 0: the mirror is the Nyquist bin
+    if (tpc == 0) xm[0] = qy[r];  // k = 0: the mirror is the Nyquist bin (row r's y1 inverse, from LDS)
 #pragma unroll
     for (int t = 0; t < PTS; ++t) {
       const int k = tpc + TPC * t;
@@ -788,7 +792,16 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
 #pragma unroll
         for (int m = 0; m < PTS; ++m) dst[(i64)N2 * TY * M * m] = v[m];
       }
+      if (tid < N1) {  // the Nyquist column's y1 DFT (qy is visible: fft_stages held barriers)
+        const int k = idx(tid);
+        cd acc = make_cd(0.0, 0.0);
+#pragma unroll 8
+        for (int j = 0; j < N1; ++j) acc = cadd(acc, cmul(qy[j], tw_1[(j * k) & (N1 - 1)]));
+        Q[(i64)z * NY + y2 + N2 * k] = acc;  // slot layout, k1 = k
+      }
     } else {
+      cd qk = make_cd(0.0, 0.0);  // the Nyquist column, k1 = tid (first wave), from the middle launch
+      if (tid < N1) qk = Q[(i64)z * NY + y2 + N2 * idx(tid)];
       {
         const int x = idx(x0), ty = idx(ty0);
         const cd* src = H + ((i64)z * NY + y2 + N2 * ty) * M + x;
@@ -798,6 +811,16 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
 #pragma unroll
         for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
         fft_stages<N1, PTS, r0_of(N1, PTS), false, M, F>(v, lds, tw_1, x, ty, true);  // v[m]: y1 = ty + TY m
+      }
+      if (tid < 64) {  // one wave: the Nyquist column's y1 inverse into qy (read by to_rows_c2r)
+        if (tid < N1) qy[tid] = qk;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS writes before its reads
+        cd acc = make_cd(0.0, 0.0);
+        const int y1 = idx(tid) & (N1 - 1);
+#pragma unroll 8
+        for (int k = 0; k < N1; ++k) acc = cadd(acc, cmul(qy[k], cconj(tw_1[(y1 * k) & (N1 - 1)])));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane has read qy before it is overwritten
+        if (tid < N1) qy[tid] = acc;
       }
       to_rows_c2r(v, z, y2);
       {
@@ -815,6 +838,13 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
 
 hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* Q, double* x, const TPArgs& a,
                                   hipStream_t s) {
+  if (stage == 3) {  // the Nyquist column Q [n z][n y]: P2 on its N2 columns of each k1 (NX = 1)
+    if (n == 128)
+      hipLaunchKernelGGL((k_tp_mid<0, 4, 4, 128, 8, false, 1>), dim3(32), dim3(4 * 16), 0, s, Q, a, 32);
+    else
+      hipLaunchKernelGGL((k_tp_mid<0, 8, 8, 256, 16, false, 1>), dim3(32), dim3(8 * 16), 0, s, Q, a, 32);
+    return hipGetLastError();
+  }
   if (n == 128) {
     if (stage == 1) {  // x tiles of the 64-wide half spectrum (8 x times 4 y2) x k1
       constexpr int units = (64 / 8) * 32;
