@@ -7,7 +7,7 @@ TAG=${1:-r04a}
 OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out
 ROOT=${GRAFT_REPO_ROOT:-$PWD}
 B="bench.py --steps 200 --warmup 10 --no-real --scaling-grid 0 --no-cpu-baseline --no-configs"
-for rep in 1 2 3; do
+for rep in 1 2; do
   for shape in default blocked blocked32; do
     timeout -k 10 120 python $B --tp-shape 0,$shape > $OUT/${TAG}_${shape}_$rep.json 2> $OUT/${TAG}_${shape}_$rep.err
   done
