@@ -514,6 +514,11 @@ extern "C" PetscErrorCode getFFTPrec3DContext(PetscInt ndim, PetscScalar dt, Pet
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
+extern "C" FFTPrecTransportContext* FFTPrecTransportContextLast(void) {
+  static FFTPrecTransportContext last{};
+  return &last;
+}
+
 extern "C" PetscErrorCode FFTPrecTransportContextCreate(FFTPrecTransportContext** ctx) {
   PetscCheck(ctx, PETSC_COMM_SELF, PETSC_ERR_ARG_NULL, "NULL output");
   *ctx = new FFTPrecTransportContext;

@@ -15,7 +15,8 @@
  *
  * Documented differences (each fixes a reference defect):
  *   - getFFTPrec3DContext's last argument is the context to fill (the reference takes a
- *     SOLVERLAB `Mesh` by value and writes through an uninitialised pointer, item 2);
+ *     SOLVERLAB `Mesh` by value and writes through an uninitialised pointer, item 2); the
+ *     reference's 13-argument Mesh form is kept for C++ callers and fills a library slot;
  *   - the callbacks fetch the context with PCShellGetContext(pc, &ctx) (item 2);
  *   - a NULL intersectionMatrix means the identity (Cartesian mesh; the reference never
  *     creates it, item 2);
@@ -116,8 +117,26 @@ PetscErrorCode FFTPrecTransportContextSetRemapBack(FFTPrecTransportContext *ctx,
 PetscErrorCode FFTPrecTransportContextGetRemapBack(const FFTPrecTransportContext *ctx, Mat *remapBack);
 PetscErrorCode FFTPrecTransportContextCreate(FFTPrecTransportContext **ctx);
 PetscErrorCode FFTPrecTransportContextDestroy(FFTPrecTransportContext **ctx);
+/* the library's context slot that the 13-argument C++ form below fills */
+FFTPrecTransportContext *FFTPrecTransportContextLast(void);
 
 #ifdef __cplusplus
+}
+
+/* The reference's own 13-argument form, `Mesh srcMesh` by value (src/PCSHELLFft_3D.hxx:27-41),
+ * so a reference caller compiles unchanged against this header.  The mesh is not read (the
+ * reference does not read it either, src/PCSHELLFft_3D.cxx:101-151); the context lands in the
+ * library slot FFTPrecTransportContextLast(), where a caller can pick it up -- the reference
+ * writes it through an uninitialised pointer and loses it.  A call
+ * whose last argument is an FFTPrecTransportContext * resolves to the C function above. */
+template <class MeshT>
+inline PetscErrorCode getFFTPrec3DContext(PetscInt ndim, PetscScalar dt, PetscInt nbCells, PetscScalar a_x,
+                                          PetscScalar a_y, PetscScalar a_z, PetscScalar Xmin, PetscScalar Ymin,
+                                          PetscScalar Zmin, PetscScalar Xmax, PetscScalar Ymax, PetscScalar Zmax,
+                                          MeshT srcMesh) {
+  (void)srcMesh;
+  return getFFTPrec3DContext(ndim, dt, nbCells, a_x, a_y, a_z, Xmin, Ymin, Zmin, Xmax, Ymax, Zmax,
+                             FFTPrecTransportContextLast());
 }
 #endif
 #endif /* CFP_PCSHELL_FFT3D_H */

@@ -1,6 +1,7 @@
 """CPU tests of the C ABI library: it loads, exports every symbol include/*.h declares, and
 its host-only logic (slab layout, PETSc stand-in on host vectors, context factory) behaves
 as the reference's interface.  No GPU compute is issued here."""
+import os
 import ctypes
 
 import numpy as np
@@ -155,3 +156,50 @@ def test_mat_create_fft_rejects_other_types():
     d = (ctypes.c_int64 * 3)(4, 4, 4)
     rc = P.lib().MatCreateFFT(0, 3, d, b"aij", ctypes.byref(h))
     assert rc == 56  # PETSC_ERR_SUP
+
+
+REF_CALLER = r"""
+#include <cstdio>
+#include <complex>
+#include "pcshell_fft3d.h"
+static double re(double v) { return v; }
+static double re(std::complex<double> v) { return v.real(); }
+struct Mesh { long cells; double bbox[6]; };  // stands for SOLVERLAB's Mesh, passed by value
+int main() {
+  Mesh m{4096, {0, 1, 0, 2, 0, 4}};
+  // the reference's call, unchanged (src/PCSHELLFft_3D.hxx:27-41)
+  PetscErrorCode ierr = getFFTPrec3DContext(3, 0.5, m.cells, 1.0, 2.0, 3.0, 0.0, 0.0, 0.0, 1.0, 2.0, 4.0, m);
+  const FFTPrecTransportContext *c = FFTPrecTransportContextLast();
+  FFTPrecTransportContext mine;
+  PetscErrorCode ierr2 = getFFTPrec3DContext(2, 1.0, 100, 1.0, 1.0, 1.0, 0, 0, 0, 1, 1, 1, &mine);
+  std::printf("%d %d %ld %ld %ld %.17g %.17g %.17g %ld %ld\n", (int)ierr, (int)ierr2, (long)c->n_x, (long)c->n_y,
+              (long)c->n_z, re(c->lambda_x), re(c->lambda_y), re(c->lambda_z),
+              (long)mine.n_x, (long)mine.n_z);
+  return 0;
+}
+"""
+
+
+@pytest.mark.parametrize("real", [False, True])
+def test_reference_caller_compiles_unchanged(tmp_path, real):
+    """the reference's 13-argument getFFTPrec3DContext(..., Mesh srcMesh)
+    compiles and links against include/pcshell_fft3d.h; the context lands in the library slot."""
+    import shutil
+    import subprocess
+    from circulantpreconditioner_amd import LIB_PATH
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    lib = LIB_PATH if not real else LIB_PATH.replace("libcirculant_fft.so", "libcirculant_fft_real.so")
+    src = tmp_path / "caller.cpp"
+    src.write_text(REF_CALLER)
+    exe = tmp_path / "caller"
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    cmd = ["g++", "-std=c++17", "-I", inc, str(src), "-o", str(exe), lib, "-Wl,-rpath," + os.path.dirname(lib)]
+    if real:
+        cmd.insert(1, "-DCFP_REAL_SCALAR")
+    subprocess.run(cmd, check=True, capture_output=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    assert out[:5] == ["0", "0", "16", "16", "16"]
+    # lambda_d = a_d dt (max - min) / n (src/PCSHELLFft_3D.cxx:146-148)
+    np.testing.assert_allclose([float(v) for v in out[5:8]], [1 * .5 * 1 / 16, 2 * .5 * 2 / 16, 3 * .5 * 4 / 16])
+    assert out[8:] == ["10", "1"]
