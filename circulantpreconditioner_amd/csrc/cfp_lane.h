@@ -34,5 +34,35 @@ __device__ __forceinline__ double swz_xor16(double v) {
 __device__ __forceinline__ cd lane_xor16(cd v) { return make_cd(swz_xor16(v.x), swz_xor16(v.y)); }
 __device__ __forceinline__ cd mul_mi(cd v) { return make_cd(v.y, -v.x); }  // x W_4 = x (-i)
 
+// register <-> lane-bit transposes (v_permlane32_swap: lane bit 5, v_permlane16_swap: bit 4)
+// (a, b) -> lanes with bit B clear: (a[L], a[L ^ 2^B]); set: (b[L ^ 2^B], b[L])
+template <int B>
+__device__ __forceinline__ void swap32(unsigned& a, unsigned& b) {
+  if constexpr (B == 5) {
+    const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+    a = r[0];
+    b = r[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+    a = r[0];
+    b = r[1];
+  }
+}
+template <int B>
+__device__ __forceinline__ void swap_d(double& a, double& b) {
+  unsigned long long ua = (unsigned long long)__double_as_longlong(a),
+                     ub = (unsigned long long)__double_as_longlong(b);
+  unsigned al = (unsigned)ua, ah = (unsigned)(ua >> 32), bl = (unsigned)ub, bh = (unsigned)(ub >> 32);
+  swap32<B>(al, bl);
+  swap32<B>(ah, bh);
+  a = __longlong_as_double((long long)(((unsigned long long)ah << 32) | al));
+  b = __longlong_as_double((long long)(((unsigned long long)bh << 32) | bl));
+}
+template <int B>
+__device__ __forceinline__ void swap_c(cd& a, cd& b) {
+  swap_d<B>(a.x, b.x);
+  swap_d<B>(a.y, b.y);
+}
+
 }  // namespace
 }  // namespace cfp

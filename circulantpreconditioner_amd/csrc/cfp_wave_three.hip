@@ -247,6 +247,173 @@ k_wtp_mid(cd* data, WTPArgs a, int nunits) {
   }
 }
 
+// P2w with the cell's 4 comps on the top lane bits (k_wtp_mid_ct, r04, the default).  Lane =
+// y2 bit 0 (lane bit 0) + y2 bit 1 (bit 1) + xl (bit 2) + y2 bit 2 (bit 3) + comp (bits 4-5): a wave
+// still reads 8 runs of 2 cells x 4 comps (128 B) per z.  The y2 stages are one DPP move each
+// (quad_perm lane ^ 1, ^ 2; row_ror:8 for lane ^ 8) instead of ds_swizzle + two DPP moves, and the
+// arrowhead solve transposes the comps into registers with v_permlane16/32_swap (lane bits 4-5 <->
+// register bits 0-1, 8 swaps per double pair group): each lane then solves 4 whole cells in
+// registers, once, where k_wtp_mid gathers the quad with 4 DPP broadcasts per value and every lane
+// of the quad redoes the cell's reciprocal and sums.  Register r then holds comp r & 3 of slot
+// (r & 12) | L4 | 2 L5; the transpose is undone before the inverse z FFT.
+template <bool XS, int PROBE = 0>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+k_wtp_mid_ct(cd* data, WTPArgs a, int nunits) {
+#ifndef CFP_KEXP
+  static_assert(PROBE == 0, "timing probes are built in tools/kexp only");
+#endif
+  constexpr int XT = 2, T = WNC * WN2 * XT;  // 64 columns, one per lane
+  constexpr int PTS = 16, TZ = WNX / PTS;    // 8 z-groups, kz = tz + 8 m
+  constexpr int NXT = WNX / XT;
+  constexpr int F = (XS ? F_SPLIT_LDS : 0) | F_LDS_SYNC;
+  __shared__ __attribute__((aligned(16))) double lds[T * WNX * (XS ? 1 : 2)];
+  __shared__ cd tw_l[WNX];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < WNX; i += T * TZ) tw_l[i] = a.tw[i];
+  const int c0 = tid & (T - 1), tz0 = tid / T;
+  const i64 zs = WPLANE;
+  const double c0sq = a.wave.c0sq;
+  const auto y2_of = [](int l) { return (l & 3) | ((l >> 1) & 4); };
+  struct Col {
+    cd* p;
+    int y2;
+    cd w, w8;  // W_128^{y2 k1}; W_8^(y2 & 3)
+  };
+  const auto column = [&](int u) {
+    const int c = launder(c0), tz = launder(tz0);
+    Col q;
+    const int xt = u % NXT, k1 = u / NXT;
+    const int comp = c >> 4, xl = (c >> 2) & 1;
+    q.y2 = y2_of(c);
+    q.p = data + (i64)(q.y2 + WN2 * k1) * WW + (xt * XT + xl) * WNC + comp + zs * tz;
+    q.w = a.tw[(q.y2 * k1) & (WNX - 1)];
+    q.w8 = a.tw[(WNX / 8) * (q.y2 & 3)];
+    return q;
+  };
+  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+    cd v[PTS];
+    {
+      const Col q = column(u);
+      if constexpr (PROBE & WPR_NO_LOAD) {
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) v[m] = make_cd((double)m, (double)q.y2);
+      } else {
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) v[m] = q.p[zs * TZ * m];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // 8-point DIF over y2 (lane bits 3, 1, 0), branch-free as in k_wtp_mid; lane y2 ends with
+      // frequency k2 = brev3(y2)
+      const double s4 = q.y2 & 4 ? -1.0 : 1.0, s2 = q.y2 & 2 ? -1.0 : 1.0, s1 = q.y2 & 1 ? -1.0 : 1.0;
+      const bool mi = (q.y2 & 3) == 3;
+      const cd w8 = q.y2 & 4 ? q.w8 : make_cd(1.0, 0.0);
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) {
+        v[m] = cmul(v[m], q.w);
+        if constexpr (PROBE & WPR_NO_Y2) continue;
+        const cd p = lane_xor8(v[m]);
+        v[m] = cmul(make_cd(fma(s4, v[m].x, p.x), fma(s4, v[m].y, p.y)), w8);
+      }
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) {
+        if constexpr (PROBE & WPR_NO_Y2) continue;
+        const cd p = dpp_c<DPP_XOR2>(v[m]);
+        cd t = make_cd(fma(s2, v[m].x, p.x), fma(s2, v[m].y, p.y));
+        t = mi ? mul_mi(t) : t;
+        const cd r = dpp_c<DPP_XOR1>(t);
+        v[m] = make_cd(fma(s1, t.x, r.x), fma(s1, t.y, r.y));
+      }
+    }
+    {
+      const int c = launder(c0), tz = launder(tz0);
+      fft_stages<WNX, PTS, wr0_of(WNX, PTS), false, T, F>(v, lds, tw_l, c, tz, true);  // v[m]: kz = tz + TZ m
+    }
+    if constexpr (PROBE & WPR_NO_SOLVE) {
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
+    } else {
+      const int c = launder(c0), tz = launder(tz0);
+      const int xt = u % NXT, k1 = u / NXT;
+      const int y2 = y2_of(c), xl = (c >> 2) & 1;
+      const int k2 = ((y2 & 1) << 2) | (y2 & 2) | (y2 >> 2);
+      // the two non-fused axes, folded once per column (wave_col's algebra, every comp at once)
+      const double2 px = a.wave.tab[0][xt * XT + xl], py = a.wave.tab[1][k1 + WN1 * k2];
+      const double iex = 1.0 / (1.0 + px.x), iey = 1.0 / (1.0 + py.x);
+      const double wx = px.y * iex, wy = py.y * iey;
+      const double dnf = 1.0 + px.x + py.x + c0sq * (px.y * wx + py.y * wy);
+#pragma unroll
+      for (int k = 0; k < PTS; k += 2) swap_c<4>(v[k], v[k + 1]);
+#pragma unroll
+      for (int k = 0; k < PTS; ++k)
+        if ((k & 2) == 0) swap_c<5>(v[k], v[k + 2]);
+      const int sl = ((c >> 4) & 1) | (((c >> 5) & 1) << 1);  // slot bits 0-1 now on lane bits 4-5
+#pragma unroll
+      for (int g = 0; g < PTS / 4; ++g) {
+        const double2 pk = a.wave.tab[2][tz + TZ * (4 * g + sl)];
+        const double ef = 1.0 + pk.x;
+        const double D2 = fma(dnf + pk.x, ef, c0sq * pk.y * pk.y);
+        const double inv = rcp_nr(ef * D2);
+        const double id = ef * ef * inv, ief = D2 * inv;
+        const double wz = pk.y * ief;
+        cd* r = v + 4 * g;
+        const double tx = fma(wx, r[1].x, fma(wy, r[2].x, wz * r[3].x));
+        const double ty = fma(wx, r[1].y, fma(wy, r[2].y, wz * r[3].y));
+        const cd x0 = make_cd(fma(c0sq, ty, r[0].x) * id, fma(-c0sq, tx, r[0].y) * id);
+        r[1] = make_cd(fma(px.y, x0.y, r[1].x) * iex, fma(-px.y, x0.x, r[1].y) * iex);
+        r[2] = make_cd(fma(py.y, x0.y, r[2].x) * iey, fma(-py.y, x0.x, r[2].y) * iey);
+        r[3] = make_cd(fma(pk.y, x0.y, r[3].x) * ief, fma(-pk.y, x0.x, r[3].y) * ief);
+        r[0] = x0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = cconj(r[j]);
+      }
+#pragma unroll
+      for (int k = 0; k < PTS; ++k)
+        if ((k & 2) == 0) swap_c<5>(v[k], v[k + 2]);
+#pragma unroll
+      for (int k = 0; k < PTS; k += 2) swap_c<4>(v[k], v[k + 1]);
+    }
+    {
+      const int c = launder(c0), tz = launder(tz0);
+      fft_stages<WNX, PTS, wr0_of(WNX, PTS), false, T, F>(v, lds, tw_l, c, tz, false);
+    }
+    {
+      const Col q = column(u);
+      const double s4 = q.y2 & 4 ? -1.0 : 1.0, s2 = q.y2 & 2 ? -1.0 : 1.0, s1 = q.y2 & 1 ? -1.0 : 1.0;
+      const bool mi = (q.y2 & 3) == 3;
+      const cd w8 = q.y2 & 4 ? q.w8 : make_cd(1.0, 0.0);
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) {
+        if constexpr (PROBE & WPR_NO_Y2) continue;
+        const cd r = dpp_c<DPP_XOR1>(v[m]);
+        cd t = make_cd(fma(s1, v[m].x, r.x), fma(s1, v[m].y, r.y));
+        t = mi ? mul_mi(t) : t;
+        const cd p = dpp_c<DPP_XOR2>(t);
+        v[m] = make_cd(fma(s2, t.x, p.x), fma(s2, t.y, p.y));
+      }
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) {
+        if constexpr (PROBE & WPR_NO_Y2) {
+          v[m] = cmul(v[m], q.w);
+          continue;
+        }
+        const cd t = cmul(v[m], w8);
+        const cd p = lane_xor8(t);
+        v[m] = cmul(make_cd(fma(s4, t.x, p.x), fma(s4, t.y, p.y)), q.w);
+      }
+      if constexpr (PROBE & WPR_NO_STORE) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) acc += v[m].x + v[m].y;
+        if (acc == 1.2345e300) q.p[0] = make_cd(acc, 0.0);  // keeps the work live, never true
+      } else {
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) q.p[zs * TZ * m] = cconj(v[m]);
+      }
+    }
+    lds_barrier();  // the next unit's first exchange overwrites LDS
+  }
+}
+
 bool wave_three_pass_supported(const i64 n[3], int ncomp) {
   return ncomp == WNC && n[0] == WNX && n[1] == WNX && n[2] == WNX;
 }
@@ -267,7 +434,7 @@ hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArg
   const int g = 2 * wcu_count();
   if (stage == 1) {
     const int units = (WNX / 2) * WN1;  // x tiles x k1
-    hipLaunchKernelGGL((k_wtp_mid<true>), dim3(units < g ? units : g), dim3(512), 0, s, out, a, units);
+    hipLaunchKernelGGL((k_wtp_mid_ct<true>), dim3(units < g ? units : g), dim3(512), 0, s, out, a, units);
   } else {
     const int units = WNX * WN2;  // z-planes x y2
     // P1w out of place: non-temporal loads keep b out of the 256 MB Infinity Cache, which then

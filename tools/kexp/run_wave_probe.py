@@ -19,7 +19,9 @@ tab = torch.from_numpy(np.stack([0.079 * (1 - np.cos(th)), 0.079 * np.sin(th)], 
 NAMES = {0: "full", 100: "full, whole-complex LDS (1 WG/CU)", 1: "no y2 DFT", 2: "no solve", 3: "no y2, no solve",
          4: "no loads", 8: "no stores", 12: "no loads, no stores", 13: "no mem, no y2", 14: "no mem, no solve",
          15: "no mem, no y2, no solve (z FFTs + exchanges)"}
-cases = [0, 100, 1, 2, 3, 4, 8, 12, 13, 14, 15]
+for k in [0, 1, 2, 3, 4, 8, 12, 13, 14, 15]:
+    NAMES[200 + k] = "ct: " + NAMES[k]
+cases = [0, 100, 1, 2, 3, 4, 8, 12, 13, 14, 15] + [200 + k for k in [0, 1, 2, 3, 4, 8, 12, 13, 14, 15]]
 res = {c: [] for c in cases}
 for rnd in range(3):
     for c in cases:

@@ -3,6 +3,7 @@
 // instantiate k_wtp_mid with PROBE != 0 (a probe drops part of the work; its output is invalid).
 //   which < 16:  k_wtp_mid<split LDS, which>  (WPR_* bits)
 //   which = 100: k_wtp_mid<whole-complex LDS (128 KiB, one workgroup per CU), 0>
+//   which = 200 + P: k_wtp_mid_ct<split LDS, P> (comps on lane bits 4-5, permlane solve; r04)
 #define CFP_KEXP 1
 #include "cfp_wave_three.hip"
 
@@ -28,6 +29,9 @@ extern "C" int wave_probe(int which, void* data, const void* tw, const void* tab
       C(0) C(1) C(2) C(3) C(4) C(8) C(12) C(13) C(14) C(15)
 #undef C
       case 100: hipLaunchKernelGGL((k_wtp_mid<false, 0>), dim3(256), dim3(512), 0, 0, d, a, units); return 0;
+#define D(P) case 200 + P: hipLaunchKernelGGL((k_wtp_mid_ct<true, P>), dim3(512), dim3(512), 0, 0, d, a, units); return 0;
+      D(0) D(1) D(2) D(3) D(4) D(8) D(12) D(13) D(14) D(15)
+#undef D
       default: return 1;
     }
   };
