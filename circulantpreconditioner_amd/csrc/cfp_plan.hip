@@ -210,7 +210,7 @@ bool use_three_pass(const cfp_plan_s* p, bool diag_override) {
   const bool want = p->schedule == CFP_SCHEDULE_THREE_PASS ||
                     (p->schedule == CFP_SCHEDULE_AUTO && p->chunk_planes == 0 && (p->n[0] == 256 || p->n[0] == 128));
   if (!want || diag_override || p->sym_kind != 1 || p->external_x) return false;
-  return three_pass_supported(p->n);
+  return three_pass_supported(p->n) || three_pass_sq_supported(p->n);
 }
 
 // the plane schedule (n_x = n_y in {64, 100, 128}, n_z > 1): plane forward (x + y DFTs of
@@ -892,8 +892,8 @@ extern "C" int cfp_plan_set_schedule(cfp_plan_t p, int schedule) {
   if (schedule == CFP_SCHEDULE_PLANE &&
       (p->n[0] != p->n[1] || !plane_supported(p->n[0]) || p->n[2] < 2 || p->long_axes() || p->external_x))
     return set_error(CFP_ERR_SUP, "the plane schedule needs n_x = n_y in {64, 100, 128} and n_z > 1");
-  if (schedule == CFP_SCHEDULE_THREE_PASS && !three_pass_supported(p->n))
-    return set_error(CFP_ERR_SUP, "the 3-sweep schedule needs a 128^3 or 256^3 grid");
+  if (schedule == CFP_SCHEDULE_THREE_PASS && !three_pass_supported(p->n) && !three_pass_sq_supported(p->n))
+    return set_error(CFP_ERR_SUP, "the 3-sweep schedule needs a 100^3, 128^3 or 256^3 grid");
   DeviceGuard dg(p->device);
   graph_clear(p);
   const int f_old = p->fused_axis;

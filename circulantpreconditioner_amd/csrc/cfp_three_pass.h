@@ -29,6 +29,11 @@ struct TPShape {
 };
 
 bool three_pass_supported(const i64 n[3]);
+// 100^3 (n = R^2, R = 10: cfp_three_pass_sq.hip); launch_three_pass routes n = 100 there.
+// shape.mid picks its middle kernel's x tile: DEFAULT 4 x, LANE64 2 x, LANE32 5 x
+bool three_pass_sq_supported(const i64 n[3]);
+hipError_t launch_three_pass_sq(int stage, int n, const cd* in, cd* out, const TPArgs& a, TPShape shape,
+                                hipStream_t s);
 bool three_pass_shape_valid(int n1, int mid);
 // stage 0: P1 (in -> out), 1: P2 (out in place), 2: P3 (in -> out)
 hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, TPShape shape,

@@ -930,6 +930,7 @@ bool three_pass_shape_valid(int n1, int mid) {
 
 hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, TPShape shape,
                              hipStream_t s) {
+  if (n == 100) return launch_three_pass_sq(stage, n, in, out, a, shape, s);
   if (n == 128) {
     // 128^3 (N1 = 32 x N2 = 4; AUTO since r03m), 8 points per thread and whole-complex LDS
     // exchanges (one barrier pair per exchange instead of two): P1/P3 512 threads, 69 KiB (2 per

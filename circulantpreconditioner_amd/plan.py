@@ -179,7 +179,8 @@ class CirculantPlan:
         'swap64': the y2 DFT on permlane register transposes, 64-column tile; 'swap64pf': the
         same with an LDS-DMA prefetch of half the next unit; 'blocked': 'swap64pf' with the
         blocked intermediate layout, 1 KiB P2 runs; 'blocked32': blocks of 4 x and the permlane
-        P2 on 32 columns, two workgroups per CU; n1 = 32 only)."""
+        P2 on 32 columns, two workgroups per CU; n1 = 32 only).  At 100^3 (cfp_three_pass_sq.hip)
+        mid picks the middle kernel's x tile: 'default' 4 x, 'lane64' 2 x, 'lane32' 5 x."""
         m = self.TP_MIDS[mid] if isinstance(mid, str) else int(mid)
         check(lib().cfp_plan_set_three_pass_shape(self._h, int(n1), m))
         return self

@@ -448,6 +448,30 @@ def test_three_pass_128_vs_oracle(cp, oracle, lam, mid):
         assert _rel(plan.apply(_dev(b)), x) < 1e-13
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("mid", ["default", "lane64", "lane32"])
+def test_three_pass_100_vs_oracle(cp, oracle, mid):
+    """The 3-sweep schedule at the reference's default mesh 100^3 (cfp_three_pass_sq.hip: y split
+    10 x 10, radix-10 FFTs; mid = the middle kernel's x tile 4 / 2 / 5): against the oracle,
+    in place, and against the 5-pass and plane schedules."""
+    n = (100, 100, 100)
+    lam = (0.3 + 0.2j, 1.1, 0.7 - 0.4j)
+    b = oracle.c_fill_uniform(100 ** 3, 43)
+    ref = oracle.c_solve_3d(oracle.c_build_diag_transport(n, lam), b, n)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam).set_schedule("three").set_three_pass_shape(0, mid)
+        assert [p["mode"] for p in plan.passes()] == ["rows_fwd", "mid_fused", "rows_inv"]
+        x = plan.apply(_dev(b))
+        assert _rel(x, ref) < TOL
+        t = _dev(b)
+        plan.apply(t, out=t)
+        assert torch.equal(t, x)
+        plan.set_schedule("five")
+        assert _rel(plan.apply(_dev(b)), x) < 1e-13
+        plan.set_schedule("plane")
+        assert _rel(plan.apply(_dev(b)), x) < 1e-13
+
+
 # ------------------------------------------------------------------ plane schedule (n_x = n_y)
 @pytest.mark.parametrize("n", [(100, 100, 100), (64, 64, 64), (128, 128, 128), (100, 100, 7), (64, 64, 2),
                                (128, 128, 10)], ids=lambda n: "x".join(map(str, n)))

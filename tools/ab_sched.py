@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""A/B of apply schedules / 3-sweep shapes on one grid (GPU only; measurement tool, not a test).
+
+  python tools/ab_sched.py 100 plane three:0,default three:0,lane64 three:0,lane32 five
+
+Every variant applies the same b (SplitMix64 U[-1,1) complex, the bench's transport symbol) in
+place on the current stream, timed with HIP events over `--iters` back-to-back applies; the
+variants are interleaved over `--rounds` rounds.  Prints one JSON line per variant: PCApply/s of
+each round and the max relative difference of its x to the first variant's.
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import circulantpreconditioner_amd as cp  # noqa: E402
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("grid", type=int)
+    ap.add_argument("variants", nargs="+")
+    ap.add_argument("--iters", type=int, default=2000)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--lam", type=float, nargs=3, default=[0.6, 0.15, 0.02])
+    args = ap.parse_args()
+    n = (args.grid,) * 3
+    N = args.grid ** 3
+    g = torch.Generator(device="cpu").manual_seed(20251017)
+    b = (torch.rand(N, generator=g, dtype=torch.float64) * 2 - 1 +
+         1j * (torch.rand(N, generator=g, dtype=torch.float64) * 2 - 1)).to("cuda")
+    plans = []
+    for v in args.variants:
+        p = cp.CirculantPlan(n)
+        p.set_transport_symbol(tuple(args.lam))
+        sched, _, shape = v.partition(":")
+        p.set_schedule(sched)
+        if shape:
+            n1, mid = shape.split(",")
+            p.set_three_pass_shape(int(n1), mid)
+        plans.append(p)
+    ref = None
+    res = {v: {"rates": [], "rel_diff": None, "passes": [q["mode"] for q in p.passes()]}
+           for v, p in zip(args.variants, plans)}
+    for v, p in zip(args.variants, plans):
+        x = p.apply(b)
+        if ref is None:
+            ref = x
+        res[v]["rel_diff"] = float((x - ref).abs().max() / ref.abs().max())
+    x = torch.empty_like(b)
+    for _ in range(args.rounds):
+        for v, p in zip(args.variants, plans):
+            for _ in range(50):
+                p.apply(b, out=x)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.iters):
+                p.apply(b, out=x)
+            e1.record()
+            e1.synchronize()
+            res[v]["rates"].append(round(args.iters / (e0.elapsed_time(e1) * 1e-3), 1))
+    for v in args.variants:
+        print(json.dumps({"grid": args.grid, "variant": v, **res[v]}), flush=True)
+    for p in plans:
+        p.close()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
