@@ -64,7 +64,15 @@ __device__ __forceinline__ cd dft4_dit(cd v, int q) {
 // keeps the kernel out of scratch.  Lane j ends up holding frequency brev3(j).
 template <int N2>
 __device__ __forceinline__ int brev(int j) {
+  if constexpr (N2 == 16) return ((j & 1) << 3) | ((j & 2) << 1) | ((j & 4) >> 1) | (j >> 3);
   return N2 == 4 ? ((j & 1) << 1) | (j >> 1) : ((j & 1) << 2) | (j & 2) | (j >> 2);
+}
+// XCD-aware unit order of a persistent grid of G workgroups (G % 8 == 0, whole rounds): the
+// workgroups of one XCD (blockIdx % 8, round-robin dispatch) take G / 8 consecutive units of a
+// round, so units that share 128-byte lines run under one L2
+__device__ __forceinline__ int xcd_unit(int it, int G) {
+  const int b = it % G;
+  return it - b + (b & 7) * (G >> 3) + (b >> 3);
 }
 
 // first radix of an n-point FFT done as r0 x PTS x ... x PTS (n = r0 PTS^k, r0 <= PTS)
@@ -226,12 +234,14 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
 
 // Persistent over units u = (x-tile, k1); T columns per unit = T/N2 x values times N2 y2.
 // Barriers wait for LDS only, so one unit's stores drain while the next unit loads.
-template <int FLAGS, int T, int N2, int TN, int PTS = 16, bool XS = true, int NX = TN>
+// N2 = 16 (512^3, r04): one more radix-2 lane stage (lane ^ 8, twiddle W_16^(y2 & 7)) in front of
+// the 8-point one.  XCD: units in xcd_unit order (the host launches whole rounds).
+template <int FLAGS, int T, int N2, int TN, int PTS = 16, bool XS = true, int NX = TN, bool XCD = false>
 __global__ void __launch_bounds__(T * (TN / PTS)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid(cd* data, TPArgs a, int nunits) {
   constexpr int N1 = TN / N2, TZ = TN / PTS, NT = T * TZ, XT = T / N2, NXT = NX / XT;
   constexpr int F = FLAGS | (XS ? F_SPLIT_LDS : 0) | F_LDS_SYNC;
-  static_assert(N2 == 4 || N2 == 8, "the y2 DFT runs across 4 or 8 lanes");
+  static_assert(N2 == 4 || N2 == 8 || N2 == 16, "the y2 DFT runs across 4, 8 or 16 lanes");
   __shared__ __attribute__((aligned(16))) double lds[T * TN * (XS ? 1 : 2)];
   __shared__ cd tw_l[TN];
   const int tid = threadIdx.x;
@@ -244,7 +254,7 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
   struct Col {
     cd* col;  // this thread's first point; slot m adds the uniform zs * TZ m
     int y2, xk;
-    cd w, w8;  // W_256^{y2 k1}; W_8^(y2 & 3) (N2 = 8)
+    cd w, w8, w16;  // W_TN^{y2 k1}; W_8^(y2 & 3) (N2 >= 8); W_16^(y2 & 7) (N2 = 16)
   };
   const auto column = [&](int u) {
     int c = c0, tz = tz0;
@@ -256,9 +266,11 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
     q.col = data + q.xk + (i64)NX * (q.y2 + N2 * k1) + zs * tz;
     q.w = a.tw[(q.y2 * k1) & (TN - 1)];
     q.w8 = a.tw[(TN / 8) * (q.y2 & 3)];
+    if constexpr (N2 == 16) q.w16 = a.tw[(TN / 16) * (q.y2 & 7)];
     return q;
   };
-  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+  for (int it = blockIdx.x; it < nunits; it += gridDim.x) {
+    const int u = XCD ? xcd_unit(it, gridDim.x) : it;
     cd v[PTS];
     {
       const Col q = column(u);
@@ -269,7 +281,11 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
 #pragma unroll
       for (int m = 0; m < PTS; ++m) {  // the lane DFT in two sweeps over the slots: fewer live temporaries
         v[m] = cmul(v[m], q.w);
-        if constexpr (N2 == 8) {  // dft8_dif's first stage
+        if constexpr (N2 == 16) {  // dft16_dif's first stage
+          const cd p = lane_xor8(v[m]);
+          v[m] = (q.y2 & 8) ? cmul(csub(p, v[m]), q.w16) : cadd(v[m], p);
+        }
+        if constexpr (N2 >= 8) {  // dft8_dif's first stage
           const cd p = lane_xor4(v[m]);
           v[m] = (q.y2 & 4) ? cmul(csub(p, v[m]), q.w8) : cadd(v[m], p);
         }
@@ -300,10 +316,15 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
       for (int m = 0; m < PTS; ++m) v[m] = dft4_dit(v[m], q.y2 & 3);
 #pragma unroll
       for (int m = 0; m < PTS; ++m) {
-        if constexpr (N2 == 8) {  // dft8_dit's last stage
+        if constexpr (N2 >= 8) {  // dft8_dit's last stage
           const cd u = (q.y2 & 4) ? cmul(v[m], q.w8) : v[m];
           const cd p = lane_xor4(u);
           v[m] = (q.y2 & 4) ? csub(p, u) : cadd(u, p);
+        }
+        if constexpr (N2 == 16) {  // dft16_dit's last stage
+          const cd u = (q.y2 & 8) ? cmul(v[m], q.w16) : v[m];
+          const cd p = lane_xor8(u);
+          v[m] = (q.y2 & 8) ? csub(p, u) : cadd(u, p);
         }
         v[m] = cmul(v[m], q.w);
       }
@@ -619,7 +640,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
 
 
 bool three_pass_supported(const i64 n[3]) {
-  return n[0] == n[1] && n[1] == n[2] && (n[0] == 128 || n[0] == 256);
+  return n[0] == n[1] && n[1] == n[2] && (n[0] == 128 || n[0] == 256 || n[0] == 512);
 }
 
 static int cu_count() {
@@ -931,6 +952,21 @@ bool three_pass_shape_valid(int n1, int mid) {
 hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, TPShape shape,
                              hipStream_t s) {
   if (n == 100) return launch_three_pass_sq(stage, n, in, out, a, shape, s);
+  if (n == 512) {
+    // 512^3 (r04): N1 = 32 x N2 = 16.  P1 / P3: 32 rows of 512 (16 points per thread, 1024
+    // threads, split exchanges: 136 KiB, one per CU).  P2: the z FFT of 512 bounds the tile to 32
+    // columns (128 KiB split exchange) = 2 x times 16 y2, 32-byte runs; units in XCD order so
+    // the 4 tiles of a 128-byte line share an L2.  96 N bytes per apply against 160 N.
+    if (stage == 1) {
+      constexpr int units = (512 / 2) * 32;
+      const int g = (int)grid_of(units, 1) & ~7;  // whole rounds of a multiple of 8
+      if (g < 8 || units % g) return hipErrorNotSupported;
+      TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 16, true, 512, true>), dim3(g), dim3(1024), s, out, a, units);
+    } else {
+      launch_rows<32, 512, 1>(stage, in, out, a, s);
+    }
+    return hipGetLastError();
+  }
   if (n == 128) {
     // 128^3 (N1 = 32 x N2 = 4; AUTO since r03m), 8 points per thread and whole-complex LDS
     // exchanges (one barrier pair per exchange instead of two): P1/P3 512 threads, 69 KiB (2 per

@@ -278,6 +278,30 @@ def test_full_size_residual(cp, n):
         assert all(p["fast"] for p in plan.passes())
 
 
+def test_three_pass_512(cp):
+    """The 3-sweep schedule at 512^3 (r04: N1 = 32 x N2 = 16, P2 on 32 columns in XCD order):
+    residual of C x = b, in place, and against the 5-pass schedule."""
+    n = (512, 512, 512)
+    N = 512 ** 3
+    lam = (0.3 + 0.2j, 1.1, 0.7 - 0.4j)
+    b = torch.empty(N, dtype=torch.complex128, device="cuda")
+    cp.fill_uniform(b, 512)
+    with cp.CirculantPlan(n) as plan:
+        plan.set_transport_symbol(lam).set_schedule("three")
+        assert [p["mode"] for p in plan.passes()] == ["rows_fwd", "mid_fused", "rows_inv"]
+        x = plan.apply(b)
+        r = apply_C_torch(x, n, lam) - b
+        assert float(torch.linalg.vector_norm(r) / torch.linalg.vector_norm(b)) < 1e-12
+        del r
+        plan.set_schedule("five")
+        x5 = plan.apply(b)
+        assert float((x5 - x).abs().max() / x5.abs().max()) < 1e-13
+        del x5
+        plan.set_schedule("three")
+        plan.apply(b, out=b)  # in place
+        assert torch.equal(b, x)
+
+
 def test_max_size_1024_cubed(cp):
     """The largest fast-path grid, 1024^3 (2^30 points, 16 GiB per vector): residual of C x = b
     with in-place device arithmetic (peak ~4 vectors of HBM)."""

@@ -13,3 +13,4 @@ timeout -k 10 300 $T tests/test_real_gpu.py tests/test_real_scalar_gpu.py >> $OU
 timeout -k 10 400 $T tests/test_dist_gpu.py tests/test_pcshell_mpi_gpu.py tests/test_transport.py >> $OUT/r04c_tests.log 2>&1
 timeout -k 10 120 python tools/kexp/run_wave_probe.py > $OUT/r04c_wave_probe.txt 2>&1
 timeout -k 10 150 python tools/ab_sched.py 100 plane three:0,default three:0,lane64 three:0,lane32 five > $OUT/r04c_ab100.jsonl 2>&1
+timeout -k 10 150 python tools/ab_sched.py 512 auto three five --iters 20 --rounds 2 > $OUT/r04c_ab512.jsonl 2>&1
