@@ -128,6 +128,10 @@ struct cfp_plan_s {
   cd* axsym = nullptr;    //            per point of the fused axis
   cd* diag = nullptr;     // explicit
   cd* host_stage = nullptr;  // device staging buffers for cfp_plan_apply_host
+  // the 3-sweep intermediate of the blocked shapes (TP_MID_BLOCKED*): a sweep that changes the
+  // layout cannot run in place (a unit's natural rows hold other units' blocked values), so
+  // P1 writes and P3 reads this plan-owned buffer (N values, allocated on first use)
+  cd* mid_buf = nullptr;
   // HIP-graph replay (cfp_plan_set_graph): one instantiated graph of the apply's launches per
   // (b, x) pair, captured on a private stream and launched into the caller's stream.  A graph
   // holds device pointers, not values: every setter that can move a buffer or change the
@@ -416,7 +420,14 @@ int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStr
           ++g_apply_stamp.hits;
         }
       }
-      hipError_t e = launch_three_pass(q.tp, tn, q.from_b ? b : x, x, a, p->tp_shape, s);
+      const cd* tin = q.from_b ? b : x;
+      cd* tout = x;
+      if (tn == 256 && (p->tp_shape.mid == TP_MID_BLOCKED || p->tp_shape.mid == TP_MID_BLOCKED32)) {
+        if (!p->mid_buf) HIPCHK(hipMalloc(&p->mid_buf, sizeof(cd) * (size_t)p->N));
+        if (q.tp == 2) tin = p->mid_buf;
+        else tout = p->mid_buf;
+      }
+      hipError_t e = launch_three_pass(q.tp, tn, tin, tout, a, p->tp_shape, s);
       g_stamp = LaunchStamp{};
       if (e != hipSuccess) return hip_error(e, "3-sweep launch");
       continue;
@@ -652,6 +663,7 @@ extern "C" int cfp_plan_destroy(cfp_plan_t p) {
     if (p->tw4hi[a]) hipFree(p->tw4hi[a]);
   }
   if (p->host_stage) hipFree(p->host_stage);
+  if (p->mid_buf) hipFree(p->mid_buf);
   graph_clear(p);
   if (p->cap_stream) hipStreamDestroy(p->cap_stream);
   for (auto& e : p->prof_ev) hipEventDestroy(e);
@@ -914,6 +926,10 @@ extern "C" int cfp_plan_set_three_pass_shape(cfp_plan_t p, int n1, int mid) {
     return set_error(CFP_ERR_ARG_OUTOFRANGE, "3-sweep shape n1=%d mid=%d is not one of the built shapes", n1, mid);
   p->tp_shape.n1 = n1;
   p->tp_shape.mid = mid;
+  if (p->n[0] == 256 && (mid == TP_MID_BLOCKED || mid == TP_MID_BLOCKED32) && !p->mid_buf) {
+    DeviceGuard g(p->device);
+    HIPCHK(hipMalloc(&p->mid_buf, sizeof(cd) * (size_t)p->N));  // here, not inside a graph capture
+  }
   return CFP_SUCCESS;
 }
 
