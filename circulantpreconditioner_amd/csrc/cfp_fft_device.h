@@ -483,6 +483,63 @@ __device__ __forceinline__ void fft_stages(cd* v, void* lds, const cd* tws, int 
   }
 }
 
+// Two-stage column FFT (N = R0 PTS) whose exchange also permutes the columns: the thread writes
+// its stage-0 values to column cw and reads column cr for stage 1, so the lane -> column map can
+// change at the exchange (cfp_wave_three.hip: memory-friendly lanes for the global accesses,
+// register-transposable lanes for the arrowhead solve).  cw and cr must be permutations of the
+// same columns among the threads of one tpc; with cw == cr this is fft_stages.
+// `mid(v)` runs right after the exchange, before stage 1's twiddles (a column-wise step in the
+// new lane map that commutes with the FFT).
+struct NoMid {
+  __device__ void operator()(cd*) const {}
+};
+template <int N, int PTS, int R0, int T, int FLAGS, class MID = NoMid>
+__device__ __forceinline__ void fft_stages_perm(cd* v, void* ldsv, const cd* tws, int cw, int cr, int tpc, bool first,
+                                                MID mid = MID()) {
+  typedef Shape<N, PTS, R0> SH;
+  constexpr int TPC = SH::TPC, QQ = SH::QQ;
+  static_assert(SH::S == 2, "one exchange");
+#pragma unroll
+  for (int q = 0; q < QQ; ++q) {
+    cd u[R0];
+#pragma unroll
+    for (int t = 0; t < R0; ++t) u[t] = v[q + t * QQ];
+    dft_any<R0>(u);
+#pragma unroll
+    for (int t = 0; t < R0; ++t) v[q + t * QQ] = u[t];
+  }
+  const auto wpos = [&](int k) { return (tpc + (k % QQ) * TPC) * R0 + (k / QQ); };
+  const auto rpos = [&](int t) { return tpc + t * TPC; };
+  if (!first) xbarrier<FLAGS>();
+  if constexpr ((FLAGS & F_SPLIT_LDS) != 0) {
+    double* lds = (double*)ldsv;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h) xbarrier<FLAGS>();
+#pragma unroll
+      for (int k = 0; k < PTS; ++k) lds[lds_idx<N, false, T, FLAGS>(cw, wpos(k))] = h ? v[k].y : v[k].x;
+      xbarrier<FLAGS>();
+#pragma unroll
+      for (int t = 0; t < PTS; ++t) {
+        const double d = lds[lds_idx<N, false, T, FLAGS>(cr, rpos(t))];
+        if (h) v[t].y = d; else v[t].x = d;
+      }
+    }
+  } else {
+    cd* lds = (cd*)ldsv;
+#pragma unroll
+    for (int k = 0; k < PTS; ++k) lds[lds_idx<N, false, T, FLAGS>(cw, wpos(k))] = v[k];
+    xbarrier<FLAGS>();
+#pragma unroll
+    for (int t = 0; t < PTS; ++t) v[t] = lds[lds_idx<N, false, T, FLAGS>(cr, rpos(t))];
+  }
+  mid(v);
+  const int jm = tpc % R0;
+#pragma unroll
+  for (int t = 1; t < PTS; ++t) v[t] = cmul(v[t], tws[jm * t * (N / (R0 * PTS))]);
+  dft_any<PTS>(v);
+}
+
 template <int N, int PTS, int R0, bool ROW, int T, int MODE, int FLAGS>
 __global__ void __launch_bounds__(T*(N / PTS)) __attribute__((amdgpu_waves_per_eu(waves_req(FLAGS, MODE))))
 k_axis_fast(const cd* in, cd* out, KArgs a) {

@@ -962,8 +962,10 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
       const int g = (int)grid_of(units, 1) & ~7;  // whole rounds of a multiple of 8
       if (g < 8 || units % g) return hipErrorNotSupported;
       TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 16, true, 512, true>), dim3(g), dim3(1024), s, out, a, units);
-    } else {
+    } else if (shape.mid == TP_MID_LANE64) {  // A/B: phase A through LDS
       launch_rows<32, 512, 1>(stage, in, out, a, s);
+    } else {  // lane-pair phase A (no LDS exchange there)
+      launch_rows<32, 512, 1, 16, true, kRowsLP>(stage, in, out, a, s);
     }
     return hipGetLastError();
   }

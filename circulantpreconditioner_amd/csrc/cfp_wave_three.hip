@@ -414,6 +414,172 @@ k_wtp_mid_ct(cd* data, WTPArgs a, int nunits) {
   }
 }
 
+// P2w with two lane maps (k_wtp_mid_ct2, r04): the global loads and stores use k_wtp_mid's map
+// (lane = comp + 4 y2 + 32 xl: 4 lanes = one cell's 64 contiguous bytes), and the z FFT's
+// exchange switches to k_wtp_mid_ct's map (fft_stages_perm: write the old column, read the new),
+// where the y2 stages are single DPP moves and the comps sit on lane bits 4-5 for the permlane
+// solve; the inverse exchange switches back.  The y2 DFT runs between the z FFTs (it commutes
+// with them; the twiddle W_128^{y2 k1} is applied at the load and the store).  k_wtp_mid_ct
+// keeps its map for the global accesses too, and pays for it there: 49.3 against 44.5 us with
+// the y2 DFT and the solve dropped (profiles/r04_wave_probe.txt).
+template <bool XS, int PROBE = 0>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+k_wtp_mid_ct2(cd* data, WTPArgs a, int nunits) {
+#ifndef CFP_KEXP
+  static_assert(PROBE == 0, "timing probes are built in tools/kexp only");
+#endif
+  constexpr int XT = 2, T = WNC * WN2 * XT;  // 64 columns, one per lane
+  constexpr int PTS = 16, TZ = WNX / PTS;    // 8 z-groups, kz = tz + 8 m
+  constexpr int NXT = WNX / XT;
+  constexpr int F = (XS ? F_SPLIT_LDS : 0) | F_LDS_SYNC;
+  __shared__ __attribute__((aligned(16))) double lds[T * WNX * (XS ? 1 : 2)];
+  __shared__ cd tw_l[WNX];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < WNX; i += T * TZ) tw_l[i] = a.tw[i];
+  const int c0 = tid & (T - 1), tz0 = tid / T;
+  const i64 zs = WPLANE;
+  const double c0sq = a.wave.c0sq;
+  // map B (between the exchanges): y2 bits on lane bits 0, 1, 3; xl on 2; comp on 4-5
+  const auto y2_b = [](int l) { return (l & 3) | ((l >> 1) & 4); };
+  const auto col_b = [&](int l) { return (l >> 4) + WNC * y2_b(l) + WNC * WN2 * ((l >> 2) & 1); };
+  // map A (global accesses): this lane's first point and W_128^{y2 k1}
+  const auto col_ptr = [&](int u, int c, int tz) {
+    const int xt = u % NXT, k1 = u / NXT;
+    return data + (i64)(((c >> 2) & (WN2 - 1)) + WN2 * k1) * WW + (xt * XT + (c >> 5)) * WNC + (c & 3) + zs * tz;
+  };
+  const auto tw_y = [&](int u, int c) { return a.tw[(((c >> 2) & (WN2 - 1)) * (u / NXT)) & (WNX - 1)]; };
+  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+    cd v[PTS];
+    {
+      const int c = launder(c0), tz = launder(tz0);
+      const cd* src = col_ptr(u, c, tz);
+      if constexpr (PROBE & WPR_NO_LOAD) {
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) v[m] = make_cd((double)m, (double)c);
+      } else {
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) v[m] = src[zs * TZ * m];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const cd w = tw_y(u, c);
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) v[m] = cmul(v[m], w);
+    }
+    {
+      // 8-point DIF over y2 (map B lane bits 3, 1, 0), branch-free, between the z FFT's exchange and
+      // its second stage; lane y2 ends with k2 = brev3(y2)
+      const auto y2_dif = [&](cd* w_) {
+        if constexpr (!(PROBE & WPR_NO_Y2)) {
+          const int c = launder(c0);
+          const int y2 = y2_b(c);
+          const double s4 = y2 & 4 ? -1.0 : 1.0, s2 = y2 & 2 ? -1.0 : 1.0, s1 = y2 & 1 ? -1.0 : 1.0;
+          const bool mi = (y2 & 3) == 3;
+          const cd w8 = y2 & 4 ? tw_l[(WNX / 8) * (y2 & 3)] : make_cd(1.0, 0.0);
+#pragma unroll
+          for (int m = 0; m < PTS; ++m) {
+            const cd p = lane_xor8(w_[m]);
+            w_[m] = cmul(make_cd(fma(s4, w_[m].x, p.x), fma(s4, w_[m].y, p.y)), w8);
+          }
+#pragma unroll
+          for (int m = 0; m < PTS; ++m) {
+            const cd p = dpp_c<DPP_XOR2>(w_[m]);
+            cd t = make_cd(fma(s2, w_[m].x, p.x), fma(s2, w_[m].y, p.y));
+            t = mi ? mul_mi(t) : t;
+            const cd r = dpp_c<DPP_XOR1>(t);
+            w_[m] = make_cd(fma(s1, t.x, r.x), fma(s1, t.y, r.y));
+          }
+        }
+      };
+      const int c = launder(c0), tz = launder(tz0);
+      fft_stages_perm<WNX, PTS, wr0_of(WNX, PTS), T, F>(v, lds, tw_l, c, col_b(c), tz, true, y2_dif);  // map B; kz = tz + TZ m
+    }
+    if constexpr (PROBE & WPR_NO_SOLVE) {
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
+    } else {
+      const int c = launder(c0), tz = launder(tz0);
+      const int xt = u % NXT, k1 = u / NXT;
+      const int y2 = y2_b(c), xl = (c >> 2) & 1;
+      const int k2 = ((y2 & 1) << 2) | (y2 & 2) | (y2 >> 2);
+      const double2 px = a.wave.tab[0][xt * XT + xl], py = a.wave.tab[1][k1 + WN1 * k2];
+      const double iex = 1.0 / (1.0 + px.x), iey = 1.0 / (1.0 + py.x);
+      const double wx = px.y * iex, wy = py.y * iey;
+      const double dnf = 1.0 + px.x + py.x + c0sq * (px.y * wx + py.y * wy);
+#pragma unroll
+      for (int k = 0; k < PTS; k += 2) swap_c<4>(v[k], v[k + 1]);
+#pragma unroll
+      for (int k = 0; k < PTS; ++k)
+        if ((k & 2) == 0) swap_c<5>(v[k], v[k + 2]);
+      const int sl = ((c >> 4) & 1) | (((c >> 5) & 1) << 1);  // slot bits 0-1 now on lane bits 4-5
+#pragma unroll
+      for (int g = 0; g < PTS / 4; ++g) {
+        const double2 pk = a.wave.tab[2][tz + TZ * (4 * g + sl)];
+        const double ef = 1.0 + pk.x;
+        const double D2 = fma(dnf + pk.x, ef, c0sq * pk.y * pk.y);
+        const double inv = rcp_nr(ef * D2);
+        const double id = ef * ef * inv, ief = D2 * inv;
+        const double wz = pk.y * ief;
+        cd* r = v + 4 * g;
+        const double tx = fma(wx, r[1].x, fma(wy, r[2].x, wz * r[3].x));
+        const double ty = fma(wx, r[1].y, fma(wy, r[2].y, wz * r[3].y));
+        const cd x0 = make_cd(fma(c0sq, ty, r[0].x) * id, fma(-c0sq, tx, r[0].y) * id);
+        r[1] = make_cd(fma(px.y, x0.y, r[1].x) * iex, fma(-px.y, x0.x, r[1].y) * iex);
+        r[2] = make_cd(fma(py.y, x0.y, r[2].x) * iey, fma(-py.y, x0.x, r[2].y) * iey);
+        r[3] = make_cd(fma(pk.y, x0.y, r[3].x) * ief, fma(-pk.y, x0.x, r[3].y) * ief);
+        r[0] = x0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = cconj(r[j]);
+      }
+#pragma unroll
+      for (int k = 0; k < PTS; ++k)
+        if ((k & 2) == 0) swap_c<5>(v[k], v[k + 2]);
+#pragma unroll
+      for (int k = 0; k < PTS; k += 2) swap_c<4>(v[k], v[k + 1]);
+    }
+    if constexpr (!(PROBE & WPR_NO_Y2)) {
+      // inverse (forward DFT on the conjugate): DIT from the bit-reversed order back to natural
+      const int c = launder(c0);
+      const int y2 = y2_b(c);
+      const double s4 = y2 & 4 ? -1.0 : 1.0, s2 = y2 & 2 ? -1.0 : 1.0, s1 = y2 & 1 ? -1.0 : 1.0;
+      const bool mi = (y2 & 3) == 3;
+      const cd w8 = y2 & 4 ? tw_l[(WNX / 8) * (y2 & 3)] : make_cd(1.0, 0.0);
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) {
+        const cd r = dpp_c<DPP_XOR1>(v[m]);
+        cd t = make_cd(fma(s1, v[m].x, r.x), fma(s1, v[m].y, r.y));
+        t = mi ? mul_mi(t) : t;
+        const cd p = dpp_c<DPP_XOR2>(t);
+        v[m] = make_cd(fma(s2, t.x, p.x), fma(s2, t.y, p.y));
+      }
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) {
+        const cd t = cmul(v[m], w8);
+        const cd p = lane_xor8(t);
+        v[m] = make_cd(fma(s4, t.x, p.x), fma(s4, t.y, p.y));
+      }
+    }
+    {
+      const int c = launder(c0), tz = launder(tz0);
+      fft_stages_perm<WNX, PTS, wr0_of(WNX, PTS), T, F>(v, lds, tw_l, col_b(c), c, tz, false);  // map A again
+    }
+    {
+      const int c = launder(c0), tz = launder(tz0);
+      cd* dst = col_ptr(u, c, tz);
+      const cd w = tw_y(u, c);
+      if constexpr (PROBE & WPR_NO_STORE) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) acc += v[m].x * w.x + v[m].y;
+        if (acc == 1.2345e300) dst[0] = make_cd(acc, 0.0);  // keeps the work live, never true
+      } else {
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) dst[zs * TZ * m] = cconj(cmul(v[m], w));
+      }
+    }
+    lds_barrier();  // the next unit's first exchange overwrites LDS
+  }
+}
+
 bool wave_three_pass_supported(const i64 n[3], int ncomp) {
   return ncomp == WNC && n[0] == WNX && n[1] == WNX && n[2] == WNX;
 }
@@ -434,7 +600,7 @@ hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArg
   const int g = 2 * wcu_count();
   if (stage == 1) {
     const int units = (WNX / 2) * WN1;  // x tiles x k1
-    hipLaunchKernelGGL((k_wtp_mid_ct<true>), dim3(units < g ? units : g), dim3(512), 0, s, out, a, units);
+    hipLaunchKernelGGL((k_wtp_mid_ct2<true>), dim3(units < g ? units : g), dim3(512), 0, s, out, a, units);
   } else {
     const int units = WNX * WN2;  // z-planes x y2
     // P1w out of place: non-temporal loads keep b out of the 256 MB Infinity Cache, which then

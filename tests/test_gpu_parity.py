@@ -297,7 +297,9 @@ def test_three_pass_512(cp):
         x5 = plan.apply(b)
         assert float((x5 - x).abs().max() / x5.abs().max()) < 1e-13
         del x5
-        plan.set_schedule("three")
+        plan.set_schedule("three").set_three_pass_shape(0, "lane64")  # P1 / P3 with phase A through LDS
+        assert float((plan.apply(b) - x).abs().max() / x.abs().max()) < 1e-13
+        plan.set_three_pass_shape(0, "default").set_schedule("three")
         plan.apply(b, out=b)  # in place
         assert torch.equal(b, x)
 
@@ -524,7 +526,7 @@ def test_plane_vs_oracle(cp, oracle, n):
 def test_plane_schedule_rules(cp):
     with cp.CirculantPlan((100, 100, 100)) as plan:
         plan.set_transport_symbol((0.5, 0.5, 0.5))
-        assert [p["mode"] for p in plan.passes()] == ["plane_fwd", "fused_sep", "plane_inv"]  # AUTO at 100^3
+        assert [p["mode"] for p in plan.passes()] == ["rows_fwd", "mid_fused", "rows_inv"]  # AUTO at 100^3 (r04)
         plan.set_chunking(10)
         assert len(plan.passes()) == 4 * 10 + 1  # chunking asked for: the chunked 5-pass schedule
         plan.set_chunking(0).set_schedule("five")
@@ -533,6 +535,9 @@ def test_plane_schedule_rules(cp):
         with cp.CirculantPlan(n) as plan:
             with pytest.raises(cp.CirculantError):
                 plan.set_schedule("plane")
+    with cp.CirculantPlan((100, 100, 7)) as plan:  # 100^2 planes, another n_z: planes
+        plan.set_transport_symbol((0.5, 0.5, 0.5))
+        assert [p["mode"] for p in plan.passes()] == ["plane_fwd", "fused_sep", "plane_inv"]
     with cp.CirculantPlan((64, 64, 64)) as plan:  # AUTO: planes for 64^2 too
         plan.set_transport_symbol((0.5, 0.5, 0.5))
         assert len(plan.passes()) == 3

@@ -4,6 +4,7 @@
 //   which < 16:  k_wtp_mid<split LDS, which>  (WPR_* bits)
 //   which = 100: k_wtp_mid<whole-complex LDS (128 KiB, one workgroup per CU), 0>
 //   which = 200 + P: k_wtp_mid_ct<split LDS, P> (comps on lane bits 4-5, permlane solve; r04)
+//   which = 300 + P: k_wtp_mid_ct2<split LDS, P> (ct's map between the exchanges only; r04)
 #define CFP_KEXP 1
 #include "cfp_wave_three.hip"
 
@@ -32,6 +33,9 @@ extern "C" int wave_probe(int which, void* data, const void* tw, const void* tab
 #define D(P) case 200 + P: hipLaunchKernelGGL((k_wtp_mid_ct<true, P>), dim3(512), dim3(512), 0, 0, d, a, units); return 0;
       D(0) D(1) D(2) D(3) D(4) D(8) D(12) D(13) D(14) D(15)
 #undef D
+#define E(P) case 300 + P: hipLaunchKernelGGL((k_wtp_mid_ct2<true, P>), dim3(512), dim3(512), 0, 0, d, a, units); return 0;
+      E(0) E(1) E(2) E(3) E(4) E(8) E(12) E(13) E(14) E(15)
+#undef E
       default: return 1;
     }
   };
