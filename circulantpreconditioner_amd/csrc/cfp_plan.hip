@@ -424,7 +424,7 @@ int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStr
       }
       const cd* tin = q.from_b ? b : x;
       cd* tout = x;
-      if (tn == 256 && (p->tp_shape.mid == TP_MID_BLOCKED || p->tp_shape.mid == TP_MID_BLOCKED32)) {
+      if ((tn == 256 || tn == 512) && (p->tp_shape.mid == TP_MID_BLOCKED || p->tp_shape.mid == TP_MID_BLOCKED32)) {
         if (!p->mid_buf) HIPCHK(hipMalloc(&p->mid_buf, sizeof(cd) * (size_t)p->N));
         if (q.tp == 2) tin = p->mid_buf;
         else tout = p->mid_buf;
@@ -928,7 +928,7 @@ extern "C" int cfp_plan_set_three_pass_shape(cfp_plan_t p, int n1, int mid) {
     return set_error(CFP_ERR_ARG_OUTOFRANGE, "3-sweep shape n1=%d mid=%d is not one of the built shapes", n1, mid);
   p->tp_shape.n1 = n1;
   p->tp_shape.mid = mid;
-  if (p->n[0] == 256 && (mid == TP_MID_BLOCKED || mid == TP_MID_BLOCKED32) && !p->mid_buf) {
+  if ((p->n[0] == 256 || p->n[0] == 512) && (mid == TP_MID_BLOCKED || mid == TP_MID_BLOCKED32) && !p->mid_buf) {
     DeviceGuard g(p->device);
     HIPCHK(hipMalloc(&p->mid_buf, sizeof(cd) * (size_t)p->N));  // here, not inside a graph capture
   }

@@ -96,15 +96,20 @@ constexpr int r0_of(int n, int pts) { return n > pts ? r0_of(n / pts, pts) : n; 
 // layout) hold [x / BLK][y2][x % BLK] instead of [y2][x], so a P2 unit of BLK x times N2 y2
 // columns is one run of N2 BLK 16 bytes per z (1 KiB at BLK = 8); P1's stores and P3's loads
 // become BLK x 16 B runs instead.  Only the intermediate between the sweeps changes; b and x
-// stay natural.  BLK = 0: natural.
-template <bool INV, int FLAGS, int N1, int TN, int PTS = 16, bool XS = true, bool LP = false, int BLK = 0>
+// stay natural.  BLK = 0: natural.  At 512^3 (N2 = 16) blocks of BLK = 2 x: 32-byte pieces for
+// P1 / P3, 512-byte runs for P2's 2 x times 16 y2 tile.
+// XCD: units in xcd_unit order (the host launches whole rounds), so the N2 units of one z-plane,
+// whose blocked pieces share 128-byte lines, run under one L2.
+template <bool INV, int FLAGS, int N1, int TN, int PTS = 16, bool XS = true, bool LP = false, int BLK = 0,
+          bool XCD = false>
 __global__ void __launch_bounds__(N1 * (TN / PTS)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
   constexpr int N2 = TN / N1, TR = TN / PTS, NT = N1 * TR, TY = N1 / PTS;
   constexpr bool BL = BLK > 0;
   constexpr int BX = BL ? BLK : 1, BW = N2 * BX;  // x per block column, values per block column
   static_assert(!LP || (TY == 2 && TN % 32 == 0), "lane pairs: two threads per column, 32 columns per wave");
-  static_assert(!BL || (N2 == 8 && TR % BX == 0 && (BX == 4 || BX == 8)), "blocked layout: 4 or 8 x times 8 y2");
+  static_assert(!BL || (TR % BX == 0 && ((N2 == 8 && (BX == 4 || BX == 8)) || (N2 == 16 && BX == 2))),
+                "blocked layout: 4 or 8 x times 8 y2, or 2 x times 16 y2");
   constexpr int RS = TN + TN / 16;  // padded row stride of the row-mode LDS layout
   constexpr int F = FLAGS | (XS ? F_SPLIT_LDS : 0) | F_LDS_SYNC;
   __shared__ __attribute__((aligned(16))) double lds[N1 * RS * (XS ? 1 : 2)];  // both layouts fit
@@ -147,7 +152,8 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
     // (P3 100 -> 93 us at 256^3)
     __builtin_amdgcn_sched_barrier(0);
   };
-  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+  for (int it = blockIdx.x; it < nunits; it += gridDim.x) {
+    const int u = XCD ? xcd_unit(it, gridDim.x) : it;
     cd v[PTS];
     load(u, v);
     if (INV) {
@@ -236,7 +242,9 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
 // Barriers wait for LDS only, so one unit's stores drain while the next unit loads.
 // N2 = 16 (512^3, r04): one more radix-2 lane stage (lane ^ 8, twiddle W_16^(y2 & 7)) in front of
 // the 8-point one.  XCD: units in xcd_unit order (the host launches whole rounds).
-template <int FLAGS, int T, int N2, int TN, int PTS = 16, bool XS = true, int NX = TN, bool XCD = false>
+// BL: the blocked layout of k_tp_rows<.., BLK = XT> (one run of T values per z).
+template <int FLAGS, int T, int N2, int TN, int PTS = 16, bool XS = true, int NX = TN, bool XCD = false,
+          bool BL = false>
 __global__ void __launch_bounds__(T * (TN / PTS)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid(cd* data, TPArgs a, int nunits) {
   constexpr int N1 = TN / N2, TZ = TN / PTS, NT = T * TZ, XT = T / N2, NXT = NX / XT;
@@ -263,7 +271,8 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
     const int xt = u % NXT, k1 = u / NXT;
     q.y2 = c & (N2 - 1);
     q.xk = xt * XT + c / N2;
-    q.col = data + q.xk + (i64)NX * (q.y2 + N2 * k1) + zs * tz;
+    q.col = BL ? data + (i64)NX * N2 * k1 + xt * T + q.y2 * XT + c / N2 + zs * tz
+               : data + q.xk + (i64)NX * (q.y2 + N2 * k1) + zs * tz;
     q.w = a.tw[(q.y2 * k1) & (TN - 1)];
     q.w8 = a.tw[(TN / 8) * (q.y2 & 3)];
     if constexpr (N2 == 16) q.w16 = a.tw[(TN / 16) * (q.y2 & 7)];
@@ -890,17 +899,18 @@ constexpr bool kRowsLP = true;
 // which nothing reads after it: chain 304.4 -> 300.7 us
 constexpr int kP2LoadFlags = F_NT_LD;
 
-template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true, bool LP = false, int BL = 0>
+template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true, bool LP = false, int BL = 0, bool XCD = false>
 static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
   constexpr int units = TN * (TN / N1);  // z-planes x y2
-  const unsigned g = grid_of(units, PER_CU);
+  unsigned g = grid_of(units, PER_CU);
+  if (XCD) g &= ~7u;  // whole rounds of a multiple of 8 (units is a power of two)
   const dim3 blk(N1 * (TN / PTS));
   if (stage == 0 && in == out)  // in place (the direct solver's Un, Un)
-    TP_LAUNCH((k_tp_rows<false, kP1InPlaceFlags, N1, TN, PTS, XS, LP, BL>), dim3(g), blk, s, in, out, a, units);
+    TP_LAUNCH((k_tp_rows<false, kP1InPlaceFlags, N1, TN, PTS, XS, LP, BL, XCD>), dim3(g), blk, s, in, out, a, units);
   else if (stage == 0)
-    TP_LAUNCH((k_tp_rows<false, kP1Flags, N1, TN, PTS, XS, LP, BL>), dim3(g), blk, s, in, out, a, units);
+    TP_LAUNCH((k_tp_rows<false, kP1Flags, N1, TN, PTS, XS, LP, BL, XCD>), dim3(g), blk, s, in, out, a, units);
   else
-    TP_LAUNCH((k_tp_rows<true, kP3Flags, N1, TN, PTS, XS, LP, BL>), dim3(g), blk, s, in, out, a, units);
+    TP_LAUNCH((k_tp_rows<true, kP3Flags, N1, TN, PTS, XS, LP, BL, XCD>), dim3(g), blk, s, in, out, a, units);
 }
 
 template <int T, int N2, int TN, int PER_CU, int PTS = 16, bool XS = true>
@@ -957,11 +967,17 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
     // threads, split exchanges: 136 KiB, one per CU).  P2: the z FFT of 512 bounds the tile to 32
     // columns (128 KiB split exchange) = 2 x times 16 y2, 32-byte runs; units in XCD order so
     // the 4 tiles of a 128-byte line share an L2.  96 N bytes per apply against 160 N.
+    // shape.mid = blocked: blocks of 2 x (P2 reads one 512-byte run per z; P1 / P3 in XCD order,
+    // so the 16 y2 units of a plane share their lines' L2); lane64: P1 / P3 phase A through LDS.
+    const bool bl = shape.mid == TP_MID_BLOCKED;
     if (stage == 1) {
       constexpr int units = (512 / 2) * 32;
       const int g = (int)grid_of(units, 1) & ~7;  // whole rounds of a multiple of 8
       if (g < 8 || units % g) return hipErrorNotSupported;
-      TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 16, true, 512, true>), dim3(g), dim3(1024), s, out, a, units);
+      if (bl) TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 16, true, 512, true, true>), dim3(g), dim3(1024), s, out, a, units);
+      else TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 16, true, 512, true>), dim3(g), dim3(1024), s, out, a, units);
+    } else if (bl) {
+      launch_rows<32, 512, 1, 16, true, kRowsLP, 2, true>(stage, in, out, a, s);
     } else if (shape.mid == TP_MID_LANE64) {  // A/B: phase A through LDS
       launch_rows<32, 512, 1>(stage, in, out, a, s);
     } else {  // lane-pair phase A (no LDS exchange there)
@@ -1002,7 +1018,9 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
     return hipGetLastError();
   }
   if (shape.mid == TP_MID_BLOCKED32) {  // blocks of 4 x; P2 = 32 columns, two workgroups per CU
-    if (stage != 1) launch_rows<32, 256, 2, 16, true, kRowsLP, 4>(stage, in, out, a, s);
+    // P1 / P3 in XCD order: the 8 y2 units of a plane share the 128-byte lines of their 64-byte
+    // pieces (r04d without it: P3 130.6 us against 90.8 natural)
+    if (stage != 1) launch_rows<32, 256, 2, 16, true, kRowsLP, 4, true>(stage, in, out, a, s);
     else if (pf_ok) launch_mid_sw<8, 256, true, true, 32>(out, a, s);
     else launch_mid_sw<8, 256, false, true, 32>(out, a, s);
     return hipGetLastError();

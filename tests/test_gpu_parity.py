@@ -297,8 +297,9 @@ def test_three_pass_512(cp):
         x5 = plan.apply(b)
         assert float((x5 - x).abs().max() / x5.abs().max()) < 1e-13
         del x5
-        plan.set_schedule("three").set_three_pass_shape(0, "lane64")  # P1 / P3 with phase A through LDS
-        assert float((plan.apply(b) - x).abs().max() / x.abs().max()) < 1e-13
+        for mid in ("lane64", "blocked"):  # P1 / P3 with phase A through LDS; blocks of 2 x in XCD order
+            plan.set_schedule("three").set_three_pass_shape(0, mid)
+            assert float((plan.apply(b) - x).abs().max() / x.abs().max()) < 1e-13
         plan.set_three_pass_shape(0, "default").set_schedule("three")
         plan.apply(b, out=b)  # in place
         assert torch.equal(b, x)
