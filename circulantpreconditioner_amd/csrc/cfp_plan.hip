@@ -208,13 +208,13 @@ struct Step {
 };
 
 // the 3-sweep schedule serves 100^3, 128^3, 256^3 and 512^3 grids with a separable symbol: on
-// request, and by default (AUTO without chunking) at 100^3, 128^3 and 256^3, where it beats the
-// 5-pass schedule by ~18 % at 256^3 and ~6 % at 128^3, and the plane schedule by 18 % at 100^3
-// (27.6k against 23.3k PCApply/s, profiles/r04_ab100.jsonl)
+// request, and by default (AUTO without chunking), where it beats the 5-pass schedule by ~18 % at
+// 256^3, ~6 % at 128^3 and 7 % at 512^3 (262 against 246 PCApply/s), and the plane schedule by
+// 18 % at 100^3 (27.6k against 23.3k PCApply/s; profiles/r04_schedule_ab.jsonl)
 bool use_three_pass(const cfp_plan_s* p, bool diag_override) {
   const bool want = p->schedule == CFP_SCHEDULE_THREE_PASS ||
                     (p->schedule == CFP_SCHEDULE_AUTO && p->chunk_planes == 0 &&
-                     (p->n[0] == 256 || p->n[0] == 128 || p->n[0] == 100));
+                     (p->n[0] == 256 || p->n[0] == 128 || p->n[0] == 100 || p->n[0] == 512));
   if (!want || diag_override || p->sym_kind != 1 || p->external_x) return false;
   return three_pass_supported(p->n) || three_pass_sq_supported(p->n);
 }

@@ -441,7 +441,14 @@ k_wtp_mid_ct2(cd* data, WTPArgs a, int nunits) {
   const double c0sq = a.wave.c0sq;
   // map B (between the exchanges): y2 bits on lane bits 0, 1, 3; xl on 2; comp on 4-5
   const auto y2_b = [](int l) { return (l & 3) | ((l >> 1) & 4); };
-  const auto col_b = [&](int l) { return (l >> 4) + WNC * y2_b(l) + WNC * WN2 * ((l >> 2) & 1); };
+  // LDS column of (comp, y2, xl) = comp0 | (comp1 ^ xl) << 1 | y2 << 2 | xl << 5: the 32 lanes of
+  // either half-wave hit 32 different bank pairs in both maps (with comp + 4 y2 + 32 xl, map B's
+  // halves collide on xl)
+  const auto lab_a = [](int l) { return l ^ ((l >> 4) & 2); };
+  const auto lab_b = [&](int l) {
+    const int xl = (l >> 2) & 1;
+    return ((l >> 4) & 1) | ((((l >> 5) & 1) ^ xl) << 1) | (y2_b(l) << 2) | (xl << 5);
+  };
   // map A (global accesses): this lane's first point and W_128^{y2 k1}
   const auto col_ptr = [&](int u, int c, int tz) {
     const int xt = u % NXT, k1 = u / NXT;
@@ -491,7 +498,7 @@ k_wtp_mid_ct2(cd* data, WTPArgs a, int nunits) {
         }
       };
       const int c = launder(c0), tz = launder(tz0);
-      fft_stages_perm<WNX, PTS, wr0_of(WNX, PTS), T, F>(v, lds, tw_l, c, col_b(c), tz, true, y2_dif);  // map B; kz = tz + TZ m
+      fft_stages_perm<WNX, PTS, wr0_of(WNX, PTS), T, F>(v, lds, tw_l, lab_a(c), lab_b(c), tz, true, y2_dif);  // map B; kz = tz + TZ m
     }
     if constexpr (PROBE & WPR_NO_SOLVE) {
 #pragma unroll
@@ -560,7 +567,7 @@ k_wtp_mid_ct2(cd* data, WTPArgs a, int nunits) {
     }
     {
       const int c = launder(c0), tz = launder(tz0);
-      fft_stages_perm<WNX, PTS, wr0_of(WNX, PTS), T, F>(v, lds, tw_l, col_b(c), c, tz, false);  // map A again
+      fft_stages_perm<WNX, PTS, wr0_of(WNX, PTS), T, F>(v, lds, tw_l, lab_b(c), lab_a(c), tz, false);  // map A again
     }
     {
       const int c = launder(c0), tz = launder(tz0);
