@@ -234,9 +234,11 @@ bool use_plane(const cfp_plan_s* p) {
 void order_axes(cfp_plan_s* p) {
   p->axes.clear();
   const int order_z[3] = {0, 1, 2}, order_y[3] = {0, 2, 1};
-  // AUTO fuses y on large grids (512^3: 4 % faster, profiles/r01_schedule_sweep.txt), z otherwise
+  // AUTO fuses y on large grids (512^3 5 passes: 4 % faster, profiles/r01_schedule_sweep.txt), z
+  // otherwise -- and z on every grid the 3-sweep schedule serves, whose middle sweep reads the
+  // z-fused tables (decided from the geometry alone: this runs before a symbol is set)
   const bool yf = p->schedule == CFP_SCHEDULE_FIVE_PASS_YFUSED ||
-                  (p->schedule == CFP_SCHEDULE_AUTO && p->n[1] >= 512 && p->n[2] >= 512);
+                  (p->schedule == CFP_SCHEDULE_AUTO && p->n[1] >= 512 && p->n[2] >= 512 && !three_pass_supported(p->n));
   const int* o = (yf && !p->long_axes()) ? order_y : order_z;
   std::vector<int> longs;
   for (int i = 0; i < 3; ++i) {
@@ -907,7 +909,7 @@ extern "C" int cfp_plan_set_schedule(cfp_plan_t p, int schedule) {
       (p->n[0] != p->n[1] || !plane_supported(p->n[0]) || p->n[2] < 2 || p->long_axes() || p->external_x))
     return set_error(CFP_ERR_SUP, "the plane schedule needs n_x = n_y in {64, 100, 128} and n_z > 1");
   if (schedule == CFP_SCHEDULE_THREE_PASS && !three_pass_supported(p->n) && !three_pass_sq_supported(p->n))
-    return set_error(CFP_ERR_SUP, "the 3-sweep schedule needs a 100^3, 128^3 or 256^3 grid");
+    return set_error(CFP_ERR_SUP, "the 3-sweep schedule needs a 100^3, 128^3, 256^3 or 512^3 grid");
   DeviceGuard dg(p->device);
   graph_clear(p);
   const int f_old = p->fused_axis;
