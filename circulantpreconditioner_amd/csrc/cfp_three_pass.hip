@@ -689,7 +689,9 @@ static unsigned grid_of(int units, int per_cu) {
 // at once, which at 16 points per thread spills.
 // At 128^3 (r03, AUTO there too): M = 64, y = y2 + 4 y1 (N1 = 32, N2 = 4), 256 threads; P2 is
 // the lane-DFT k_tp_mid on the 64-wide half spectrum (NX = 64).
-template <bool INV, int M = 128, int N1 = 32, int N2 = 8, int NY = 256>
+// MF: policy of the accesses to b (P1r loads) and x (P3r stores), which nothing in the apply
+// reads again (the complex P1 / P3 policy, kP1Flags / kP3Flags); H and Q stay plain.
+template <bool INV, int M = 128, int N1 = 32, int N2 = 8, int NY = 256, int MF = 0>
 __global__ void __launch_bounds__(N1 * (M / 8)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nunits) {
   constexpr int PTS = 8;
@@ -782,7 +784,7 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
         const int r = idx(r0), tpc = idx(tpc0);
         const cd* src = reinterpret_cast<const cd*>(in_r) + ((i64)z * NY + y2 + N2 * r) * M + tpc;
 #pragma unroll
-        for (int t = 0; t < PTS; ++t) v[t] = src[TPC * t];
+        for (int t = 0; t < PTS; ++t) v[t] = gload<MF>(src + TPC * t);
         __builtin_amdgcn_sched_barrier(0);  // all loads out before the first butterfly
         fft_stages<M, PTS, r0_of(M, PTS), true, N1, F>(v, lds, tw_m, r, tpc, true);  // 128 = 2 x 8 x 8; v[t] = Z[tpc + TPC t]
       }
@@ -831,7 +833,7 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
         const double sc = a.scale;
         cd* dst = reinterpret_cast<cd*>(out_r) + ((i64)z * NY + y2 + N2 * r) * M + tpc;
 #pragma unroll
-        for (int t = 0; t < PTS; ++t) dst[TPC * t] = make_cd(v[t].x * sc, -v[t].y * sc);
+        for (int t = 0; t < PTS; ++t) gstore<MF>(dst + TPC * t, make_cd(v[t].x * sc, -v[t].y * sc));
       }
     }
     lds_barrier();  // the next unit's first exchange overwrites LDS
@@ -872,9 +874,11 @@ hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* 
     constexpr int units = 256 * 8;  // z-planes x y2
     const unsigned g = grid_of(units, 2);
     if (stage == 0)
-      hipLaunchKernelGGL((k_tp_rows_r2c<false>), dim3(g), dim3(512), 0, s, b, H, Q, nullptr, a, units);
+      hipLaunchKernelGGL((k_tp_rows_r2c<false, 128, 32, 8, 256, F_NT_LD>), dim3(g), dim3(512), 0, s, b, H, Q, nullptr, a,
+                         units);
     else
-      hipLaunchKernelGGL((k_tp_rows_r2c<true>), dim3(g), dim3(512), 0, s, nullptr, H, Q, x, a, units);
+      hipLaunchKernelGGL((k_tp_rows_r2c<true, 128, 32, 8, 256, F_NT_ST>), dim3(g), dim3(512), 0, s, nullptr, H, Q, x, a,
+                         units);
   }
   return hipGetLastError();
 }
