@@ -691,8 +691,9 @@ static unsigned grid_of(int units, int per_cu) {
 // the lane-DFT k_tp_mid on the 64-wide half spectrum (NX = 64).
 // MF: policy of the accesses to b (P1r loads) and x (P3r stores), which nothing in the apply
 // reads again (the complex P1 / P3 policy, kP1Flags / kP3Flags); H and Q stay plain.
-template <bool INV, int M = 128, int N1 = 32, int N2 = 8, int NY = 256, int MF = 0>
-__global__ void __launch_bounds__(N1 * (M / 8)) __attribute__((amdgpu_waves_per_eu(4)))
+// OCC: waves per SIMD asked of the compiler (4: two 512-thread workgroups per CU; 6: three)
+template <bool INV, int M = 128, int N1 = 32, int N2 = 8, int NY = 256, int MF = 0, int OCC = 4>
+__global__ void __launch_bounds__(N1 * (M / 8)) __attribute__((amdgpu_waves_per_eu(OCC)))
 k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nunits) {
   constexpr int PTS = 8;
   constexpr int TPC = M / PTS;  // threads per row (row mode)
@@ -873,9 +874,9 @@ hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* 
   } else {
     constexpr int units = 256 * 8;  // z-planes x y2
     const unsigned g = grid_of(units, 2);
-    if (stage == 0)
-      hipLaunchKernelGGL((k_tp_rows_r2c<false, 128, 32, 8, 256, F_NT_LD>), dim3(g), dim3(512), 0, s, b, H, Q, nullptr, a,
-                         units);
+    if (stage == 0)  // P1r: 80 VGPRs, three workgroups per CU
+      hipLaunchKernelGGL((k_tp_rows_r2c<false, 128, 32, 8, 256, F_NT_LD, 6>), dim3(grid_of(units, 3)), dim3(512), 0, s, b,
+                         H, Q, nullptr, a, units);
     else
       hipLaunchKernelGGL((k_tp_rows_r2c<true, 128, 32, 8, 256, F_NT_ST>), dim3(g), dim3(512), 0, s, nullptr, H, Q, x, a,
                          units);

@@ -1,0 +1,9 @@
+#!/bin/bash
+# r04j GPU session: P1r at three workgroups per CU: real parity, then two bench runs.
+set -e
+OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out
+T="python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu"
+timeout -k 10 300 $T tests/test_real_gpu.py > $OUT/r04j_tests.log 2>&1
+for rep in 1 2; do
+  timeout -k 10 200 python bench.py --steps 200 --warmup 10 --scaling-grid 0 --no-cpu-baseline --no-configs > $OUT/r04j_bench_$rep.json 2> $OUT/r04j_bench_$rep.err
+done
