@@ -82,7 +82,10 @@ __global__ void __launch_bounds__(XT * N) k_sq_mid(cd* data, TPArgs a) {
   constexpr int R = SqCfg<N>::R, TPC = N / R, T = XT * R, NXT = N / XT;
   static_assert(N % XT == 0, "whole x tiles");
   constexpr int F = 0;
-  __shared__ __attribute__((aligned(16))) cd lds[T * N];
+  // y2 mode <-> column mode transposes: rows of T + 1 (with T = 40 the 16 z of a wave's lanes
+  // otherwise fall on 2 bank groups); the z FFT's own exchange uses fft_stages' T-wide rows
+  constexpr int TP = T + 1;
+  __shared__ __attribute__((aligned(16))) cd lds[TP * N];
   __shared__ cd tws[N];
   const int tid = threadIdx.x;
   const int xt = blockIdx.x % NXT, k1 = blockIdx.x / NXT;
@@ -97,12 +100,12 @@ __global__ void __launch_bounds__(XT * N) k_sq_mid(cd* data, TPArgs a) {
 #pragma unroll
   for (int m = 1; m < R; ++m) v[m] = cmul(v[m], tws[(m * k1) % N]);  // W_n^{y2 k1}
   dft_any<R>(v);  // v[k2]
-  // y2 mode -> column mode: element (column xl + XT k2, z) at z T + column
+  // y2 mode -> column mode: element (column xl + XT k2, z) at z (T + 1) + column
 #pragma unroll
-  for (int m = 0; m < R; ++m) lds[z * T + xl + XT * m] = v[m];
+  for (int m = 0; m < R; ++m) lds[z * TP + xl + XT * m] = v[m];
   __syncthreads();
 #pragma unroll
-  for (int m = 0; m < R; ++m) v[m] = lds[(tz + TPC * m) * T + c];
+  for (int m = 0; m < R; ++m) v[m] = lds[(tz + TPC * m) * TP + c];
   fft_stages<N, R, R, false, T, F>(v, lds, tws, c, tz, false);  // v[t]: kz = tz + TPC t
   {
     const int kx = xt * XT + c % XT, ky = k1 + R * (c / XT);
@@ -116,10 +119,10 @@ __global__ void __launch_bounds__(XT * N) k_sq_mid(cd* data, TPArgs a) {
   fft_stages<N, R, R, false, T, F>(v, lds, tws, c, tz, false);  // v[t]: z = tz + TPC t (conjugate domain)
   __syncthreads();
 #pragma unroll
-  for (int t = 0; t < R; ++t) lds[(tz + TPC * t) * T + c] = v[t];
+  for (int t = 0; t < R; ++t) lds[(tz + TPC * t) * TP + c] = v[t];
   __syncthreads();
 #pragma unroll
-  for (int m = 0; m < R; ++m) v[m] = lds[z * T + xl + XT * m];
+  for (int m = 0; m < R; ++m) v[m] = lds[z * TP + xl + XT * m];
   dft_any<R>(v);  // v[y2]
 #pragma unroll
   for (int m = 0; m < R; ++m) {
