@@ -87,24 +87,16 @@ __global__ void __launch_bounds__(XT * N) k_sq_mid(cd* data, TPArgs a) {
   constexpr int TP = T + 1;
   __shared__ __attribute__((aligned(16))) cd lds[TP * N];
   __shared__ cd tws[N];
-  // the symbol pieces this unit divides by, staged with the twiddles at the start: read after
-  // the first z FFT they put two global-load latencies on the unit's critical path
-  __shared__ cd axs_l[N];
-  __shared__ cd cs_l[T];
   const int tid = threadIdx.x;
   const int xt = blockIdx.x % NXT, k1 = blockIdx.x / NXT;
-  for (int i = tid; i < N; i += XT * N) {
-    tws[i] = a.tw[i];
-    axs_l[i] = a.axsym[i];
-  }
-  if (tid < T) cs_l[tid] = a.colsym[xt * XT + tid % XT + (i64)N * (k1 + R * (tid / XT))];
+  for (int i = tid; i < N; i += XT * N) tws[i] = a.tw[i];
   const int xl = tid % XT, z = tid / XT;
   const int c = tid % T, tz = tid / T;
   cd* col = data + (i64)z * N * N + (i64)R * k1 * N + xt * XT + xl;  // row y2 + R k1 at y2 = 0
   cd v[R];
 #pragma unroll
   for (int m = 0; m < R; ++m) v[m] = col[(i64)N * m];
-  __syncthreads();  // tws, axs_l, cs_l
+  __syncthreads();  // tws
 #pragma unroll
   for (int m = 1; m < R; ++m) v[m] = cmul(v[m], tws[(m * k1) % N]);  // W_n^{y2 k1}
   dft_any<R>(v);  // v[k2]
@@ -116,10 +108,11 @@ __global__ void __launch_bounds__(XT * N) k_sq_mid(cd* data, TPArgs a) {
   for (int m = 0; m < R; ++m) v[m] = lds[(tz + TPC * m) * TP + c];
   fft_stages<N, R, R, false, T, F>(v, lds, tws, c, tz, false);  // v[t]: kz = tz + TPC t
   {
-    const cd cs = cs_l[c];  // colsym[kx + n ky], kx = xt XT + c % XT, ky = k1 + R (c / XT)
+    const int kx = xt * XT + c % XT, ky = k1 + R * (c / XT);
+    const cd cs = a.colsym[kx + (i64)N * ky];
 #pragma unroll
     for (int t = 0; t < R; ++t) {
-      const cd d = cadd(cadd(cs, axs_l[tz + TPC * t]), make_cd(1.0, 0.0));
+      const cd d = cadd(cadd(cs, a.axsym[tz + TPC * t]), make_cd(1.0, 0.0));
       v[t] = cconj(cdiv_sym(v[t], d));
     }
   }
