@@ -422,7 +422,15 @@ k_wtp_mid_ct(cd* data, WTPArgs a, int nunits) {
 // with them; the twiddle W_128^{y2 k1} is applied at the load and the store).  k_wtp_mid_ct
 // keeps its map for the global accesses too, and pays for it there: 49.3 against 44.5 us with
 // the y2 DFT and the solve dropped (profiles/r04_wave_probe.txt).
-template <bool XS, int PROBE = 0>
+//
+// PF (r04): the scalar P2's LDS-DMA prefetch.  The split exchange buffer (64 columns x 128 z x 8
+// bytes) is idle from the inverse exchange's last read to the next unit's first exchange: right
+// after that read each wave DMAs slots 0..7 of its columns of unit u + gridDim.x into it
+// (global_load_lds_dwordx4, 1 KiB per wave-instruction, lane-linear), so those loads fly during
+// the last FFT stage, the twiddle and the stores; the next unit loads only slots 8..15 from HBM.
+typedef __attribute__((address_space(3))) void wlds_void_t;
+typedef __attribute__((address_space(1))) void wglb_void_t;
+template <bool XS, int PROBE = 0, bool PF = false>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 k_wtp_mid_ct2(cd* data, WTPArgs a, int nunits) {
 #ifndef CFP_KEXP
@@ -455,6 +463,21 @@ k_wtp_mid_ct2(cd* data, WTPArgs a, int nunits) {
     return data + (i64)(((c >> 2) & (WN2 - 1)) + WN2 * k1) * WW + (xt * XT + (c >> 5)) * WNC + (c & 3) + zs * tz;
   };
   const auto tw_y = [&](int u, int c) { return a.tw[(((c >> 2) & (WN2 - 1)) * (u / NXT)) & (WNX - 1)]; };
+  constexpr int NPF = PF ? 8 : 0;  // slots 0 .. NPF-1 come from the LDS prefetch
+  static_assert(!PF || XS, "the prefetch fills the split exchange buffer");
+  static_assert(!PF || (T * TZ / 64) * NPF * 128 <= T * WNX, "the prefetch fits the exchange buffer");
+  const int wv = __builtin_amdgcn_readfirstlane(tid / 64);
+  const auto prefetch = [&](int u) {  // this wave's slots 0 .. NPF-1 of unit u -> LDS
+    const int c = launder(c0), tz = launder(tz0);
+    const cd* src = col_ptr(u, c, tz);
+#pragma unroll
+    for (int m = 0; m < NPF; ++m)
+      __builtin_amdgcn_global_load_lds((wglb_void_t*)(src + zs * TZ * m), (wlds_void_t*)(lds + (wv * NPF + m) * 128),
+                                       16, 0, 0);
+  };
+  if constexpr (PF) {
+    if ((int)blockIdx.x < nunits) prefetch(blockIdx.x);
+  }
   for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
     cd v[PTS];
     {
@@ -465,7 +488,15 @@ k_wtp_mid_ct2(cd* data, WTPArgs a, int nunits) {
         for (int m = 0; m < PTS; ++m) v[m] = make_cd((double)m, (double)c);
       } else {
 #pragma unroll
-        for (int m = 0; m < PTS; ++m) v[m] = src[zs * TZ * m];
+        for (int m = NPF; m < PTS; ++m) v[m] = src[zs * TZ * m];
+        if constexpr (PF) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA (and loads) landed
+#pragma unroll
+          for (int m = 0; m < NPF; ++m) {  // the DMA is lane-linear
+            const int lane = launder(c0);
+            v[m] = fromv(*reinterpret_cast<const dv2*>(lds + (wv * NPF + m) * 128 + 2 * lane));
+          }
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
       const cd w = tw_y(u, c);
@@ -498,7 +529,8 @@ k_wtp_mid_ct2(cd* data, WTPArgs a, int nunits) {
         }
       };
       const int c = launder(c0), tz = launder(tz0);
-      fft_stages_perm<WNX, PTS, wr0_of(WNX, PTS), T, F>(v, lds, tw_l, lab_a(c), lab_b(c), tz, true, y2_dif);  // map B; kz = tz + TZ m
+      // PF: not the first exchange of the kernel -- other waves may still read their prefetched slots
+      fft_stages_perm<WNX, PTS, wr0_of(WNX, PTS), T, F>(v, lds, tw_l, lab_a(c), lab_b(c), tz, !PF, y2_dif);  // map B; kz = tz + TZ m
     }
     if constexpr (PROBE & WPR_NO_SOLVE) {
 #pragma unroll
@@ -567,7 +599,13 @@ k_wtp_mid_ct2(cd* data, WTPArgs a, int nunits) {
     }
     {
       const int c = launder(c0), tz = launder(tz0);
-      fft_stages_perm<WNX, PTS, wr0_of(WNX, PTS), T, F>(v, lds, tw_l, lab_b(c), lab_a(c), tz, false);  // map A again
+      const auto next = [&](cd*) {  // right after the exchange's last read: the buffer is free
+        if constexpr (PF) {
+          lds_barrier();  // every wave has read the exchange buffer
+          if (u + (int)gridDim.x < nunits) prefetch(u + gridDim.x);
+        }
+      };
+      fft_stages_perm<WNX, PTS, wr0_of(WNX, PTS), T, F>(v, lds, tw_l, lab_b(c), lab_a(c), tz, false, next);  // map A again
     }
     {
       const int c = launder(c0), tz = launder(tz0);
@@ -583,7 +621,7 @@ k_wtp_mid_ct2(cd* data, WTPArgs a, int nunits) {
         for (int m = 0; m < PTS; ++m) dst[zs * TZ * m] = cconj(cmul(v[m], w));
       }
     }
-    lds_barrier();  // the next unit's first exchange overwrites LDS
+    if constexpr (!PF) lds_barrier();  // the next unit's first exchange overwrites LDS
   }
 }
 
@@ -607,7 +645,11 @@ hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArg
   const int g = 2 * wcu_count();
   if (stage == 1) {
     const int units = (WNX / 2) * WN1;  // x tiles x k1
-    hipLaunchKernelGGL((k_wtp_mid_ct2<true>), dim3(units < g ? units : g), dim3(512), 0, s, out, a, units);
+    // the LDS-DMA prefetch (global_load_lds_dwordx4) takes 16-byte aligned addresses
+    if (((uintptr_t)out & 15) == 0)
+      hipLaunchKernelGGL((k_wtp_mid_ct2<true, 0, true>), dim3(units < g ? units : g), dim3(512), 0, s, out, a, units);
+    else
+      hipLaunchKernelGGL((k_wtp_mid_ct2<true>), dim3(units < g ? units : g), dim3(512), 0, s, out, a, units);
   } else {
     const int units = WNX * WN2;  // z-planes x y2
     // P1w out of place: non-temporal loads keep b out of the 256 MB Infinity Cache, which then

@@ -22,7 +22,8 @@ NAMES = {0: "full", 100: "full, whole-complex LDS (1 WG/CU)", 1: "no y2 DFT", 2:
 for k in [0, 1, 2, 3, 4, 8, 12, 13, 14, 15]:
     NAMES[200 + k] = "ct: " + NAMES[k]
     NAMES[300 + k] = "ct2: " + NAMES[k]
-cases = [0, 100, 1, 2, 3, 4, 8, 12, 13, 14, 15] + [200 + k for k in [0, 1, 2, 3, 4, 8, 12, 13, 14, 15]] + [300 + k for k in [0, 1, 2, 3, 4, 8, 12, 13, 14, 15]]
+    NAMES[400 + k] = "ct2 pf: " + NAMES[k]
+cases = [0, 100, 1, 2, 3, 4, 8, 12, 13, 14, 15] + [200 + k for k in [0, 1, 2, 3, 4, 8, 12, 13, 14, 15]] + [300 + k for k in [0, 1, 2, 3, 4, 8, 12, 13, 14, 15]] + [400 + k for k in [0, 1, 3, 8, 15]]
 res = {c: [] for c in cases}
 for rnd in range(3):
     for c in cases:

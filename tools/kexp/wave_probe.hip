@@ -5,6 +5,7 @@
 //   which = 100: k_wtp_mid<whole-complex LDS (128 KiB, one workgroup per CU), 0>
 //   which = 200 + P: k_wtp_mid_ct<split LDS, P> (comps on lane bits 4-5, permlane solve; r04)
 //   which = 300 + P: k_wtp_mid_ct2<split LDS, P> (ct's map between the exchanges only; r04)
+//   which = 400 + P: k_wtp_mid_ct2<split LDS, P, LDS-DMA prefetch> (the r04 default)
 #define CFP_KEXP 1
 #include "cfp_wave_three.hip"
 
@@ -36,6 +37,9 @@ extern "C" int wave_probe(int which, void* data, const void* tw, const void* tab
 #define E(P) case 300 + P: hipLaunchKernelGGL((k_wtp_mid_ct2<true, P>), dim3(512), dim3(512), 0, 0, d, a, units); return 0;
       E(0) E(1) E(2) E(3) E(4) E(8) E(12) E(13) E(14) E(15)
 #undef E
+#define G(P) case 400 + P: hipLaunchKernelGGL((k_wtp_mid_ct2<true, P, true>), dim3(512), dim3(512), 0, 0, d, a, units); return 0;
+      G(0) G(1) G(3) G(8) G(15)
+#undef G
       default: return 1;
     }
   };
