@@ -904,7 +904,9 @@ constexpr bool kRowsLP = true;
 // which nothing reads after it: chain 304.4 -> 300.7 us
 constexpr int kP2LoadFlags = F_NT_LD;
 
-template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true, bool LP = false, int BL = 0, bool XCD = false>
+// P1F / P3F: P1's load and P3's store policy out of place (kP1Flags / kP3Flags; 0 = plain)
+template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true, bool LP = false, int BL = 0, bool XCD = false,
+          int P1F = kP1Flags, int P3F = kP3Flags>
 static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
   constexpr int units = TN * (TN / N1);  // z-planes x y2
   unsigned g = grid_of(units, PER_CU);
@@ -913,9 +915,9 @@ static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipSt
   if (stage == 0 && in == out)  // in place (the direct solver's Un, Un)
     TP_LAUNCH((k_tp_rows<false, kP1InPlaceFlags, N1, TN, PTS, XS, LP, BL, XCD>), dim3(g), blk, s, in, out, a, units);
   else if (stage == 0)
-    TP_LAUNCH((k_tp_rows<false, kP1Flags, N1, TN, PTS, XS, LP, BL, XCD>), dim3(g), blk, s, in, out, a, units);
+    TP_LAUNCH((k_tp_rows<false, P1F, N1, TN, PTS, XS, LP, BL, XCD>), dim3(g), blk, s, in, out, a, units);
   else
-    TP_LAUNCH((k_tp_rows<true, kP3Flags, N1, TN, PTS, XS, LP, BL, XCD>), dim3(g), blk, s, in, out, a, units);
+    TP_LAUNCH((k_tp_rows<true, P3F, N1, TN, PTS, XS, LP, BL, XCD>), dim3(g), blk, s, in, out, a, units);
 }
 
 template <int T, int N2, int TN, int PER_CU, int PTS = 16, bool XS = true>
@@ -1001,8 +1003,11 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
       if (stage == 1) launch_mid<64, 4, 128, 2>(out, a, s);
       else launch_rows<32, 128, 4>(stage, in, out, a, s);
     } else {
+      // 128^3: b and x (32 MiB each) stay in the 256 MiB Infinity Cache between applies, so P1
+      // loads and P3 stores keep the default policy (shape.mid = swap64: the 256^3 NT policy, A/B)
       if (stage == 1) launch_mid<32, 4, 128, 2, 8, false>(out, a, s);
-      else launch_rows<32, 128, 2, 8, false>(stage, in, out, a, s);
+      else if (shape.mid == TP_MID_SWAP64) launch_rows<32, 128, 2, 8, false>(stage, in, out, a, s);
+      else launch_rows<32, 128, 2, 8, false, false, 0, false, 0, 0>(stage, in, out, a, s);
     }
     return hipGetLastError();
   }

@@ -454,7 +454,7 @@ def test_three_pass_schedule_rules(cp):
         assert len(plan.passes()) == 5
 
 
-@pytest.mark.parametrize("mid", ["default", "lane64"])
+@pytest.mark.parametrize("mid", ["default", "lane64", "swap64"])
 @pytest.mark.parametrize("lam", [(0.6, 0.15, 0.02), (0.3 + 0.2j, 1.1, 0.7 - 0.4j)], ids=["bench", "complex"])
 def test_three_pass_128_vs_oracle(cp, oracle, lam, mid):
     """The 3-sweep schedule at 128^3 (N1 = 32 x N2 = 4; AUTO there): the default kernels (8
