@@ -393,7 +393,8 @@ __device__ __forceinline__ void dif_pairs(cd* v, cd w) {
 
 // PROBE != 0 only in tools/kexp (tp_probe.hip, built with CFP_KEXP): timing probes that drop a
 // part of the work (output invalid).  The product library instantiates PROBE = 0 only.
-enum { PR_NO_Y2 = 1, PR_NO_ZMATH = 2, PR_NO_XCHG = 4, PR_NO_LOAD = 8, PR_NO_STORE = 16 };
+enum { PR_NO_Y2 = 1, PR_NO_ZMATH = 2, PR_NO_XCHG = 4, PR_NO_LOAD = 8, PR_NO_STORE = 16,
+       PR_PRIO = 32 /* experiment, full work: s_setprio 1 for the second half of the waves */ };
 //
 // PF (prefetch): the exchange buffer is idle from the second exchange's last read to the next
 // unit's first exchange, which is exactly where the next unit's data is needed.  Right after
@@ -450,6 +451,9 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
   const auto tw_y = [&](int u, int c) { return tw_l[((c >> XB) * (a.k1_off + u / NXT)) & (TN - 1)]; };
   constexpr int NPF = PF ? 8 : 0;  // slots 0 .. NPF-1 come from the LDS prefetch (exchange buffer)
   const int wv = __builtin_amdgcn_readfirstlane(tid / 64);
+  if constexpr ((PROBE & PR_PRIO) != 0) {
+    if (wv >= NT / 128) __builtin_amdgcn_s_setprio(1);
+  }
   const auto prefetch = [&](int u) {  // this wave's slots 0 .. NPF-1 of unit u -> LDS
     const int c = idx(c0), tz = idx(tz0);
     const cd* src = col_ptr(u, c, tz);

@@ -16,12 +16,12 @@ data = torch.randn(N, dtype=torch.complex128, device="cuda")
 tw = torch.from_numpy(np.exp(-2j * np.pi * np.arange(n) / n)).to("cuda")
 colsym = torch.full((n * n,), 0.5 + 0.1j, dtype=torch.complex128, device="cuda")
 axsym = torch.full((n,), 0.25, dtype=torch.complex128, device="cuda")
-NAMES = {0: "full (swap64)", 100: "full (lane DFT, product default)", 1: "no y2 DFT", 2: "no z math+divide",
+NAMES = {32: "full, s_setprio 1 on the second half of the waves", 0: "full (product: swap64 + prefetch)", 100: "full (lane DFT, product default)", 1: "no y2 DFT", 2: "no z math+divide",
          3: "no y2, no z math (mem + exchanges)", 4: "no exchanges", 6: "no z math, no exchanges",
          7: "mem only (no math, no exchanges)", 8: "no loads", 16: "no stores", 24: "no loads, no stores (compute+xchg)",
          26: "no mem, no z math (y2 + xchg)", 28: "no mem, no xchg (y2 + z math)", 29: "no mem, no xchg, no y2 (z math)",
          30: "no mem, no xchg, no z math (y2 only)", 31: "nothing (loop + twiddle)"}
-cases = [0, 100, 1, 2, 3, 4, 6, 7, 8, 16, 24, 26, 28, 29, 30, 31, 1000, 1100, 1007]
+cases = [0, 32, 100, 1, 2, 3, 4, 6, 7, 8, 16, 24, 26, 28, 29, 30, 31, 1000, 1007]
 res = {c: [] for c in cases}
 for rnd in range(3):
     for c in cases:
