@@ -926,7 +926,7 @@ extern "C" int cfp_plan_set_schedule(cfp_plan_t p, int schedule) {
 extern "C" int cfp_plan_set_three_pass_shape(cfp_plan_t p, int n1, int mid) {
   if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
   graph_clear(p);
-  if (!three_pass_shape_valid(n1, mid))
+  if (!three_pass_shape_valid(n1, mid, p->n[0] == p->n[1] && p->n[1] == p->n[2] ? p->n[0] : 0))
     return set_error(CFP_ERR_ARG_OUTOFRANGE, "3-sweep shape n1=%d mid=%d is not one of the built shapes", n1, mid);
   p->tp_shape.n1 = n1;
   p->tp_shape.mid = mid;

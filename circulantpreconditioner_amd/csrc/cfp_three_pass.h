@@ -34,7 +34,8 @@ bool three_pass_supported(const i64 n[3]);
 bool three_pass_sq_supported(const i64 n[3]);
 hipError_t launch_three_pass_sq(int stage, int n, const cd* in, cd* out, const TPArgs& a, TPShape shape,
                                 hipStream_t s);
-bool three_pass_shape_valid(int n1, int mid);
+// n: the grid side (0: any); n1 = 16 (y split 16 x 8) is built for 128^3 only
+bool three_pass_shape_valid(int n1, int mid, i64 n = 0);
 // stage 0: P1 (in -> out), 1: P2 (out in place), 2: P3 (in -> out)
 hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, TPShape shape,
                              hipStream_t s);

@@ -965,7 +965,8 @@ hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs
   return hipGetLastError();
 }
 
-bool three_pass_shape_valid(int n1, int mid) {
+bool three_pass_shape_valid(int n1, int mid, i64 n) {
+  if (n1 == 16) return n == 128 && (mid == TP_MID_DEFAULT || mid == TP_MID_LANE32);
   return (n1 == 0 || n1 == 32 || n1 == 64) && (mid >= 0 && mid <= TP_MID_BLOCKED32) &&
          !(mid >= TP_MID_BLOCKED && n1 == 64);
 }
@@ -1003,6 +1004,18 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
     // shape.mid = lane64 keeps the round-2 kernels (16 points per thread, split exchanges, P2
     // 64 columns) for A/B: 15.9k against 18.4k applies/s, the 5-pass schedule 17.3k
     // (profiles/r03m_128_three_sweep.md).
+    if (shape.n1 == 16) {
+      // A/B (r04): y split 16 x 8 -- P1/P3 units of 16 rows (1,024 units, 256 threads, four
+      // workgroups per CU, lane-pair phase A); P2 64 columns = 8 x times 8 y2 (256 units, 16
+      // points per thread) or, with mid = lane32, 32 columns = 4 x times 8 y2 (512 units)
+      if (stage == 1) {
+        if (shape.mid == TP_MID_LANE32) launch_mid<32, 8, 128, 2, 8, false>(out, a, s);
+        else launch_mid<64, 8, 128, 1>(out, a, s);
+      } else {
+        launch_rows<16, 128, 4, 8, false, true, 0, false, 0, 0>(stage, in, out, a, s);
+      }
+      return hipGetLastError();
+    }
     if (shape.mid == TP_MID_LANE64) {
       if (stage == 1) launch_mid<64, 4, 128, 2>(out, a, s);
       else launch_rows<32, 128, 4>(stage, in, out, a, s);
