@@ -454,9 +454,9 @@ def test_three_pass_schedule_rules(cp):
         assert len(plan.passes()) == 5
 
 
-@pytest.mark.parametrize("mid", ["default", "lane64", "swap64"])
+@pytest.mark.parametrize("n1,mid", [(0, "default"), (0, "lane64"), (0, "swap64"), (16, "default"), (16, "lane32")])
 @pytest.mark.parametrize("lam", [(0.6, 0.15, 0.02), (0.3 + 0.2j, 1.1, 0.7 - 0.4j)], ids=["bench", "complex"])
-def test_three_pass_128_vs_oracle(cp, oracle, lam, mid):
+def test_three_pass_128_vs_oracle(cp, oracle, lam, n1, mid):
     """The 3-sweep schedule at 128^3 (N1 = 32 x N2 = 4; AUTO there): the default kernels (8
     points per thread, whole-complex exchanges) and the round-2 ones (lane64): against the
     oracle, in place, and against the 5-pass schedule."""
@@ -464,7 +464,7 @@ def test_three_pass_128_vs_oracle(cp, oracle, lam, mid):
     b = oracle.c_fill_uniform(128 ** 3, 31)
     ref = oracle.c_solve_3d(oracle.c_build_diag_transport(n, lam), b, n)
     with cp.CirculantPlan(n) as plan:
-        plan.set_transport_symbol(lam).set_schedule("three").set_three_pass_shape(0, mid)
+        plan.set_transport_symbol(lam).set_schedule("three").set_three_pass_shape(n1, mid)
         assert [p["mode"] for p in plan.passes()] == ["rows_fwd", "mid_fused", "rows_inv"]
         x = plan.apply(_dev(b))
         assert _rel(x, ref) < TOL
