@@ -696,7 +696,9 @@ static unsigned grid_of(int units, int per_cu) {
 // MF: policy of the accesses to b (P1r loads) and x (P3r stores), which nothing in the apply
 // reads again (the complex P1 / P3 policy, kP1Flags / kP3Flags); H and Q stay plain.
 // OCC: waves per SIMD asked of the compiler (4: two 512-thread workgroups per CU; 6: three)
-template <bool INV, int M = 128, int N1 = 32, int N2 = 8, int NY = 256, int MF = 0, int OCC = 4>
+// WC: whole-complex LDS exchanges (ds_*_b128, one barrier pair per exchange instead of two;
+// 70 KiB at M = 128, two workgroups per CU) instead of real / imaginary halves
+template <bool INV, int M = 128, int N1 = 32, int N2 = 8, int NY = 256, int MF = 0, int OCC = 4, bool WC = false>
 __global__ void __launch_bounds__(N1 * (M / 8)) __attribute__((amdgpu_waves_per_eu(OCC)))
 k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nunits) {
   constexpr int PTS = 8;
@@ -704,8 +706,9 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
   constexpr int TY = N1 / PTS;  // 4 threads per column (column mode)
   constexpr int NT = N1 * TPC;
   constexpr int RS = M + M / 16;
-  constexpr int F = F_SPLIT_LDS | F_LDS_SYNC;
-  __shared__ __attribute__((aligned(16))) double lds[N1 * RS];  // row layout; the column layout (N1 x M) fits
+  constexpr int F = (WC ? 0 : F_SPLIT_LDS) | F_LDS_SYNC;
+  __shared__ __attribute__((aligned(16))) double lds[N1 * RS * (WC ? 2 : 1)];  // row layout; the column layout (N1 x M) fits
+  cd* const lc = reinterpret_cast<cd*>(lds);
   __shared__ cd tw_m[M];   // W_M (row FFT)
   __shared__ cd tw_1[N1];  // W_N1 (y1 DFT)
   __shared__ cd qy[N1];    // the unit's Nyquist bins over y1 (P1r: before its y1 DFT; P3r: after)
@@ -725,20 +728,36 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
     const int r = idx(r0), tpc = idx(tpc0), x = idx(x0), ty = idx(ty0);
     const int xm = (M - x) & (M - 1);
     cd zm[PTS];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    if constexpr (WC) {
       lds_barrier();
 #pragma unroll
       for (int t = 0; t < PTS; ++t) {
         const int k = tpc + TPC * t;
-        lds[r * RS + k + (k >> 4)] = h ? v[t].y : v[t].x;
+        lc[r * RS + k + (k >> 4)] = v[t];
       }
       lds_barrier();
 #pragma unroll
       for (int m = 0; m < PTS; ++m) {
         const int row = (ty + TY * m) * RS;
-        const double d = lds[row + x + (x >> 4)], dm = lds[row + xm + (xm >> 4)];
-        if (h) { v[m].y = d; zm[m].y = dm; } else { v[m].x = d; zm[m].x = dm; }
+        v[m] = lc[row + x + (x >> 4)];
+        zm[m] = lc[row + xm + (xm >> 4)];
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        lds_barrier();
+#pragma unroll
+        for (int t = 0; t < PTS; ++t) {
+          const int k = tpc + TPC * t;
+          lds[r * RS + k + (k >> 4)] = h ? v[t].y : v[t].x;
+        }
+        lds_barrier();
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) {
+          const int row = (ty + TY * m) * RS;
+          const double d = lds[row + x + (x >> 4)], dm = lds[row + xm + (xm >> 4)];
+          if (h) { v[m].y = d; zm[m].y = dm; } else { v[m].x = d; zm[m].x = dm; }
+        }
       }
     }
     lds_barrier();
@@ -757,17 +776,30 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
   const auto to_rows_c2r = [&](cd* v, int z, int y2) {
     const int r = idx(r0), tpc = idx(tpc0), x = idx(x0), ty = idx(ty0);
     cd xm[PTS];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    if constexpr (WC) {
       lds_barrier();
 #pragma unroll
-      for (int m = 0; m < PTS; ++m) lds[(ty + TY * m) * RS + x + (x >> 4)] = h ? -v[m].y : v[m].x;
+      for (int m = 0; m < PTS; ++m) lc[(ty + TY * m) * RS + x + (x >> 4)] = cconj(v[m]);
       lds_barrier();
 #pragma unroll
       for (int t = 0; t < PTS; ++t) {
         const int k = tpc + TPC * t, km = (M - k) & (M - 1);
-        const double d = lds[r * RS + k + (k >> 4)], dm = lds[r * RS + km + (km >> 4)];
-        if (h) { v[t].y = d; xm[t].y = dm; } else { v[t].x = d; xm[t].x = dm; }
+        v[t] = lc[r * RS + k + (k >> 4)];
+        xm[t] = lc[r * RS + km + (km >> 4)];
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        lds_barrier();
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) lds[(ty + TY * m) * RS + x + (x >> 4)] = h ? -v[m].y : v[m].x;
+        lds_barrier();
+#pragma unroll
+        for (int t = 0; t < PTS; ++t) {
+          const int k = tpc + TPC * t, km = (M - k) & (M - 1);
+          const double d = lds[r * RS + k + (k >> 4)], dm = lds[r * RS + km + (km >> 4)];
+          if (h) { v[t].y = d; xm[t].y = dm; } else { v[t].x = d; xm[t].x = dm; }
+        }
       }
     }
     lds_barrier();
@@ -882,7 +914,7 @@ hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* 
       hipLaunchKernelGGL((k_tp_rows_r2c<false, 128, 32, 8, 256, F_NT_LD, 6>), dim3(grid_of(units, 3)), dim3(512), 0, s, b,
                          H, Q, nullptr, a, units);
     else
-      hipLaunchKernelGGL((k_tp_rows_r2c<true, 128, 32, 8, 256, F_NT_ST>), dim3(g), dim3(512), 0, s, nullptr, H, Q, x, a,
+      hipLaunchKernelGGL((k_tp_rows_r2c<true, 128, 32, 8, 256, F_NT_ST, 4, true>), dim3(g), dim3(512), 0, s, nullptr, H, Q, x, a,
                          units);
   }
   return hipGetLastError();

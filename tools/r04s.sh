@@ -1,5 +1,5 @@
 #!/bin/bash
-# r04s GPU session: the real plan's Nyquist middle launch at 4 points per thread (512 threads):
+# r04s GPU session: real plan variants (Nyquist launch at 4 points per thread, P3r whole-complex):
 # parity, then its stage time in two bench runs.
 set -e
 OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out
