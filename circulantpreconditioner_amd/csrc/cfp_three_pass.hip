@@ -910,8 +910,8 @@ hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* 
   } else {
     constexpr int units = 256 * 8;  // z-planes x y2
     const unsigned g = grid_of(units, 2);
-    if (stage == 0)  // P1r: whole-complex exchanges, two workgroups per CU (A/B against split at three)
-      hipLaunchKernelGGL((k_tp_rows_r2c<false, 128, 32, 8, 256, F_NT_LD, 4, true>), dim3(g), dim3(512), 0, s, b,
+    if (stage == 0)  // P1r: 80 VGPRs, three workgroups per CU
+      hipLaunchKernelGGL((k_tp_rows_r2c<false, 128, 32, 8, 256, F_NT_LD, 6>), dim3(grid_of(units, 3)), dim3(512), 0, s, b,
                          H, Q, nullptr, a, units);
     else
       hipLaunchKernelGGL((k_tp_rows_r2c<true, 128, 32, 8, 256, F_NT_ST, 4, true>), dim3(g), dim3(512), 0, s, nullptr, H, Q, x, a,
