@@ -883,7 +883,7 @@ hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* 
     if (n == 128)
       hipLaunchKernelGGL((k_tp_mid<0, 4, 4, 128, 8, false, 1>), dim3(32), dim3(4 * 16), 0, s, Q, a, 32);
     else
-      hipLaunchKernelGGL((k_tp_mid<0, 8, 8, 256, 8, false, 1>), dim3(32), dim3(8 * 32), 0, s, Q, a, 32);
+      hipLaunchKernelGGL((k_tp_mid<0, 8, 8, 256, 4, false, 1>), dim3(32), dim3(8 * 64), 0, s, Q, a, 32);
     return hipGetLastError();
   }
   if (n == 128) {
