@@ -905,9 +905,8 @@ hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* 
   }
   if (stage == 1) {
     constexpr int units = (128 / 8) * 32;  // x tiles of the half spectrum x k1
-    // the complex P2's load policy (kP2LoadFlags: non-temporal loads and LDS-DMA of its input)
-    hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true, 128, 0, F_NT_LD>), dim3(grid_of(units, 1)), dim3(1024), 0,
-                       s, H, a, units);
+    hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true, 128>), dim3(grid_of(units, 1)), dim3(1024), 0, s, H, a,
+                       units);
   } else {
     constexpr int units = 256 * 8;  // z-planes x y2
     const unsigned g = grid_of(units, 2);
