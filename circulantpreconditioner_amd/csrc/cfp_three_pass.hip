@@ -672,6 +672,13 @@ static unsigned grid_of(int units, int per_cu) {
   const int g = per_cu * cu_count();
   return (unsigned)(units < g ? units : g);
 }
+// the same for the XCD-ordered kernels (xcd_unit), whose rounds must be whole and a multiple of
+// 8 workgroups: the largest power of two <= grid_of (units is a power of two), 0 if below 8
+static unsigned grid_xcd(int units, int per_cu) {
+  unsigned g = grid_of(units, per_cu), p = 1;
+  while (2 * p <= g) p *= 2;
+  return p >= 8 && units % p == 0 ? p : 0;
+}
 
 // ---------------------------------------------------------------------------------------------
 // Real-data 3-sweep (cfp_real.hip, row f4) at 256^3: the half spectrum H = M x 256 x 256
@@ -945,8 +952,8 @@ template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true, bool LP = fa
           int P1F = kP1Flags, int P3F = kP3Flags>
 static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
   constexpr int units = TN * (TN / N1);  // z-planes x y2
-  unsigned g = grid_of(units, PER_CU);
-  if (XCD) g &= ~7u;  // whole rounds of a multiple of 8 (units is a power of two)
+  const unsigned g = XCD ? grid_xcd(units, PER_CU) : grid_of(units, PER_CU);
+  if (g == 0) return;  // not on a device with fewer than 8 CUs
   const dim3 blk(N1 * (TN / PTS));
   if (stage == 0 && in == out)  // in place (the direct solver's Un, Un)
     TP_LAUNCH((k_tp_rows<false, kP1InPlaceFlags, N1, TN, PTS, XS, LP, BL, XCD>), dim3(g), blk, s, in, out, a, units);
@@ -1016,8 +1023,8 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
     const bool bl = shape.mid == TP_MID_BLOCKED;
     if (stage == 1) {
       constexpr int units = (512 / 2) * 32;
-      const int g = (int)grid_of(units, 1) & ~7;  // whole rounds of a multiple of 8
-      if (g < 8 || units % g) return hipErrorNotSupported;
+      const unsigned g = grid_xcd(units, 1);  // whole rounds of a power of two >= 8
+      if (g == 0) return hipErrorNotSupported;
       if (bl) TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 16, true, 512, true, true>), dim3(g), dim3(1024), s, out, a, units);
       else TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 16, true, 512, true>), dim3(g), dim3(1024), s, out, a, units);
     } else if (bl) {
