@@ -953,7 +953,12 @@ template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true, bool LP = fa
 static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
   constexpr int units = TN * (TN / N1);  // z-planes x y2
   const unsigned g = XCD ? grid_xcd(units, PER_CU) : grid_of(units, PER_CU);
-  if (g == 0) return;  // not on a device with fewer than 8 CUs
+  if constexpr (XCD) {
+    if (g == 0) {  // fewer than 8 workgroups: the same kernel in plain unit order
+      launch_rows<N1, TN, PER_CU, PTS, XS, LP, BL, false, P1F, P3F>(stage, in, out, a, s);
+      return;
+    }
+  }
   const dim3 blk(N1 * (TN / PTS));
   if (stage == 0 && in == out)  // in place (the direct solver's Un, Un)
     TP_LAUNCH((k_tp_rows<false, kP1InPlaceFlags, N1, TN, PTS, XS, LP, BL, XCD>), dim3(g), blk, s, in, out, a, units);
