@@ -493,12 +493,14 @@ __device__ __forceinline__ void fft_stages(cd* v, void* lds, const cd* tws, int 
 struct NoMid {
   __device__ void operator()(cd*) const {}
 };
-template <int N, int PTS, int R0, int T, int FLAGS, class MID = NoMid>
+// With S > 2 stages the later exchanges stay in the new map (column cr); `last(v)` runs right
+// after the last exchange's reads (the exchange buffer is then free; S = 2: after mid).
+template <int N, int PTS, int R0, int T, int FLAGS, class MID = NoMid, class LAST = NoMid>
 __device__ __forceinline__ void fft_stages_perm(cd* v, void* ldsv, const cd* tws, int cw, int cr, int tpc, bool first,
-                                                MID mid = MID()) {
+                                                MID mid = MID(), LAST last = LAST()) {
   typedef Shape<N, PTS, R0> SH;
-  constexpr int TPC = SH::TPC, QQ = SH::QQ;
-  static_assert(SH::S == 2, "one exchange");
+  constexpr int TPC = SH::TPC, QQ = SH::QQ, S = SH::S;
+  static_assert(S >= 2, "at least one exchange");
 #pragma unroll
   for (int q = 0; q < QQ; ++q) {
     cd u[R0];
@@ -534,10 +536,24 @@ __device__ __forceinline__ void fft_stages_perm(cd* v, void* ldsv, const cd* tws
     for (int t = 0; t < PTS; ++t) v[t] = lds[lds_idx<N, false, T, FLAGS>(cr, rpos(t))];
   }
   mid(v);
-  const int jm = tpc % R0;
+  if constexpr (S == 2) last(v);
+  int Ns = R0;
 #pragma unroll
-  for (int t = 1; t < PTS; ++t) v[t] = cmul(v[t], tws[jm * t * (N / (R0 * PTS))]);
-  dft_any<PTS>(v);
+  for (int s = 1; s < S; ++s) {
+    const int jm = tpc % Ns;  // Ns is a constant after unrolling
+    const int step = N / (Ns * PTS);
+#pragma unroll
+    for (int t = 1; t < PTS; ++t) v[t] = cmul(v[t], tws[jm * t * step]);
+    dft_any<PTS>(v);
+    if (s < S - 1) {
+      const int o = (tpc / Ns) * Ns * PTS + jm;
+      const int NsC = Ns;
+      exchange<N, false, T, FLAGS, PTS, PTS>(
+          ldsv, v, [&](int t) { return o + t * NsC; }, v, [&](int t) { return tpc + t * TPC; }, cr, false);
+      if (s == S - 2) last(v);
+    }
+    Ns *= PTS;
+  }
 }
 
 template <int N, int PTS, int R0, bool ROW, int T, int MODE, int FLAGS>

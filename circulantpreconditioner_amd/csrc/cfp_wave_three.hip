@@ -625,6 +625,198 @@ k_wtp_mid_ct2(cd* data, WTPArgs a, int nunits) {
   }
 }
 
+// P2w at 8 points per thread (k_wtp_mid_ct3, r04): the two lane maps of k_wtp_mid_ct2 with the
+// z FFT as 2 x 8 x 8 over 16 z-groups of the 64 columns (1,024 threads, 16 waves), whole-complex
+// exchanges (128 KiB, one workgroup per CU) -- the shape that won at 128^3 for the scalar P2 --
+// and, with PF, the WHOLE next unit DMA'd into the exchange buffer after the inverse FFT's last
+// exchange (the buffer holds exactly one unit), so a unit starts with no HBM load in its path.
+template <int PROBE = 0, bool PF = false>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4)))
+k_wtp_mid_ct3(cd* data, WTPArgs a, int nunits) {
+#ifndef CFP_KEXP
+  static_assert(PROBE == 0, "timing probes are built in tools/kexp only");
+#endif
+  constexpr int XT = 2, T = WNC * WN2 * XT;  // 64 columns, one per lane
+  constexpr int PTS = 8, TZ = WNX / PTS;     // 16 z-groups, kz = tz + 16 m
+  constexpr int NXT = WNX / XT;
+  constexpr int F = F_LDS_SYNC;  // whole-complex exchanges
+  __shared__ __attribute__((aligned(16))) double lds[2 * T * WNX];
+  __shared__ cd tw_l[WNX];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < WNX; i += T * TZ) tw_l[i] = a.tw[i];
+  const int c0 = tid & (T - 1), tz0 = tid / T;
+  const i64 zs = WPLANE;
+  const double c0sq = a.wave.c0sq;
+  const auto y2_b = [](int l) { return (l & 3) | ((l >> 1) & 4); };
+  const auto lab_a = [](int l) { return l ^ ((l >> 4) & 2); };
+  const auto lab_b = [&](int l) {
+    const int xl = (l >> 2) & 1;
+    return ((l >> 4) & 1) | ((((l >> 5) & 1) ^ xl) << 1) | (y2_b(l) << 2) | (xl << 5);
+  };
+  const auto col_ptr = [&](int u, int c, int tz) {
+    const int xt = u % NXT, k1 = u / NXT;
+    return data + (i64)(((c >> 2) & (WN2 - 1)) + WN2 * k1) * WW + (xt * XT + (c >> 5)) * WNC + (c & 3) + zs * tz;
+  };
+  const auto tw_y = [&](int u, int c) { return a.tw[(((c >> 2) & (WN2 - 1)) * (u / NXT)) & (WNX - 1)]; };
+  constexpr int NPF = PF ? PTS : 0;  // every slot of the next unit comes from the LDS prefetch
+  static_assert(!PF || (T * TZ / 64) * NPF * 128 <= 2 * T * WNX, "the prefetch fits the exchange buffer");
+  const int wv = __builtin_amdgcn_readfirstlane(tid / 64);
+  const auto prefetch = [&](int u) {  // this wave's slots of unit u -> LDS (lane-linear)
+    const int c = launder(c0), tz = launder(tz0);
+    const cd* src = col_ptr(u, c, tz);
+#pragma unroll
+    for (int m = 0; m < NPF; ++m)
+      __builtin_amdgcn_global_load_lds((wglb_void_t*)(src + zs * TZ * m), (wlds_void_t*)(lds + (wv * NPF + m) * 128),
+                                       16, 0, 0);
+  };
+  if constexpr (PF) {
+    if ((int)blockIdx.x < nunits) prefetch(blockIdx.x);
+  }
+  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+    cd v[PTS];
+    {
+      const int c = launder(c0), tz = launder(tz0);
+      if constexpr (PROBE & WPR_NO_LOAD) {
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) v[m] = make_cd((double)m, (double)c);
+      } else if constexpr (PF) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA landed
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) {
+          const int lane = launder(c0);
+          v[m] = fromv(*reinterpret_cast<const dv2*>(lds + (wv * NPF + m) * 128 + 2 * lane));
+        }
+      } else {
+        const cd* src = col_ptr(u, c, tz);
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) v[m] = src[zs * TZ * m];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      const cd w = tw_y(u, c);
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) v[m] = cmul(v[m], w);
+    }
+    {
+      // 8-point DIF over y2 (map B lane bits 3, 1, 0) right after the first exchange
+      const auto y2_dif = [&](cd* w_) {
+        if constexpr (!(PROBE & WPR_NO_Y2)) {
+          const int c = launder(c0);
+          const int y2 = y2_b(c);
+          const double s4 = y2 & 4 ? -1.0 : 1.0, s2 = y2 & 2 ? -1.0 : 1.0, s1 = y2 & 1 ? -1.0 : 1.0;
+          const bool mi = (y2 & 3) == 3;
+          const cd w8 = y2 & 4 ? tw_l[(WNX / 8) * (y2 & 3)] : make_cd(1.0, 0.0);
+#pragma unroll
+          for (int m = 0; m < PTS; ++m) {
+            const cd p = lane_xor8(w_[m]);
+            w_[m] = cmul(make_cd(fma(s4, w_[m].x, p.x), fma(s4, w_[m].y, p.y)), w8);
+          }
+#pragma unroll
+          for (int m = 0; m < PTS; ++m) {
+            const cd p = dpp_c<DPP_XOR2>(w_[m]);
+            cd t = make_cd(fma(s2, w_[m].x, p.x), fma(s2, w_[m].y, p.y));
+            t = mi ? mul_mi(t) : t;
+            const cd r = dpp_c<DPP_XOR1>(t);
+            w_[m] = make_cd(fma(s1, t.x, r.x), fma(s1, t.y, r.y));
+          }
+        }
+      };
+      const int c = launder(c0), tz = launder(tz0);
+      // PF: not the first exchange of the kernel -- other waves may still read their prefetched slots
+      fft_stages_perm<WNX, PTS, wr0_of(WNX, PTS), T, F>(v, lds, tw_l, lab_a(c), lab_b(c), tz, !PF, y2_dif);  // kz = tz + TZ m
+    }
+    if constexpr (PROBE & WPR_NO_SOLVE) {
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
+    } else {
+      const int c = launder(c0), tz = launder(tz0);
+      const int xt = u % NXT, k1 = u / NXT;
+      const int y2 = y2_b(c), xl = (c >> 2) & 1;
+      const int k2 = ((y2 & 1) << 2) | (y2 & 2) | (y2 >> 2);
+      const double2 px = a.wave.tab[0][xt * XT + xl], py = a.wave.tab[1][k1 + WN1 * k2];
+      const double iex = 1.0 / (1.0 + px.x), iey = 1.0 / (1.0 + py.x);
+      const double wx = px.y * iex, wy = py.y * iey;
+      const double dnf = 1.0 + px.x + py.x + c0sq * (px.y * wx + py.y * wy);
+#pragma unroll
+      for (int k = 0; k < PTS; k += 2) swap_c<4>(v[k], v[k + 1]);
+#pragma unroll
+      for (int k = 0; k < PTS; ++k)
+        if ((k & 2) == 0) swap_c<5>(v[k], v[k + 2]);
+      const int sl = ((c >> 4) & 1) | (((c >> 5) & 1) << 1);  // slot bits 0-1 now on lane bits 4-5
+#pragma unroll
+      for (int g = 0; g < PTS / 4; ++g) {
+        const double2 pk = a.wave.tab[2][tz + TZ * (4 * g + sl)];
+        const double ef = 1.0 + pk.x;
+        const double D2 = fma(dnf + pk.x, ef, c0sq * pk.y * pk.y);
+        const double inv = rcp_nr(ef * D2);
+        const double id = ef * ef * inv, ief = D2 * inv;
+        const double wz = pk.y * ief;
+        cd* r = v + 4 * g;
+        const double tx = fma(wx, r[1].x, fma(wy, r[2].x, wz * r[3].x));
+        const double ty = fma(wx, r[1].y, fma(wy, r[2].y, wz * r[3].y));
+        const cd x0 = make_cd(fma(c0sq, ty, r[0].x) * id, fma(-c0sq, tx, r[0].y) * id);
+        r[1] = make_cd(fma(px.y, x0.y, r[1].x) * iex, fma(-px.y, x0.x, r[1].y) * iex);
+        r[2] = make_cd(fma(py.y, x0.y, r[2].x) * iey, fma(-py.y, x0.x, r[2].y) * iey);
+        r[3] = make_cd(fma(pk.y, x0.y, r[3].x) * ief, fma(-pk.y, x0.x, r[3].y) * ief);
+        r[0] = x0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = cconj(r[j]);
+      }
+#pragma unroll
+      for (int k = 0; k < PTS; ++k)
+        if ((k & 2) == 0) swap_c<5>(v[k], v[k + 2]);
+#pragma unroll
+      for (int k = 0; k < PTS; k += 2) swap_c<4>(v[k], v[k + 1]);
+    }
+    if constexpr (!(PROBE & WPR_NO_Y2)) {
+      // inverse (forward DFT on the conjugate): DIT from the bit-reversed order back to natural
+      const int c = launder(c0);
+      const int y2 = y2_b(c);
+      const double s4 = y2 & 4 ? -1.0 : 1.0, s2 = y2 & 2 ? -1.0 : 1.0, s1 = y2 & 1 ? -1.0 : 1.0;
+      const bool mi = (y2 & 3) == 3;
+      const cd w8 = y2 & 4 ? tw_l[(WNX / 8) * (y2 & 3)] : make_cd(1.0, 0.0);
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) {
+        const cd r = dpp_c<DPP_XOR1>(v[m]);
+        cd t = make_cd(fma(s1, v[m].x, r.x), fma(s1, v[m].y, r.y));
+        t = mi ? mul_mi(t) : t;
+        const cd p = dpp_c<DPP_XOR2>(t);
+        v[m] = make_cd(fma(s2, t.x, p.x), fma(s2, t.y, p.y));
+      }
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) {
+        const cd t = cmul(v[m], w8);
+        const cd p = lane_xor8(t);
+        v[m] = make_cd(fma(s4, t.x, p.x), fma(s4, t.y, p.y));
+      }
+    }
+    {
+      const int c = launder(c0), tz = launder(tz0);
+      const auto next = [&](cd*) {  // right after the last exchange's reads: the buffer is free
+        if constexpr (PF) {
+          lds_barrier();  // every wave has read the exchange buffer
+          if (u + (int)gridDim.x < nunits) prefetch(u + gridDim.x);
+        }
+      };
+      fft_stages_perm<WNX, PTS, wr0_of(WNX, PTS), T, F>(v, lds, tw_l, lab_b(c), lab_a(c), tz, false, NoMid(), next);
+    }
+    {
+      const int c = launder(c0), tz = launder(tz0);
+      cd* dst = col_ptr(u, c, tz);
+      const cd w = tw_y(u, c);
+      if constexpr (PROBE & WPR_NO_STORE) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) acc += v[m].x * w.x + v[m].y;
+        if (acc == 1.2345e300) dst[0] = make_cd(acc, 0.0);  // keeps the work live, never true
+      } else {
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) dst[zs * TZ * m] = cconj(cmul(v[m], w));
+      }
+    }
+    if constexpr (!PF) lds_barrier();  // the next unit's first exchange overwrites LDS
+  }
+}
+
 bool wave_three_pass_supported(const i64 n[3], int ncomp) {
   return ncomp == WNC && n[0] == WNX && n[1] == WNX && n[2] == WNX;
 }
@@ -646,10 +838,12 @@ hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArg
   if (stage == 1) {
     const int units = (WNX / 2) * WN1;  // x tiles x k1
     // the LDS-DMA prefetch (global_load_lds_dwordx4) takes 16-byte aligned addresses
+    // k_wtp_mid_ct3: one 1,024-thread workgroup per CU
+    const int g1 = wcu_count();
     if (((uintptr_t)out & 15) == 0)
-      hipLaunchKernelGGL((k_wtp_mid_ct2<true, 0, true>), dim3(units < g ? units : g), dim3(512), 0, s, out, a, units);
+      hipLaunchKernelGGL((k_wtp_mid_ct3<0, true>), dim3(units < g1 ? units : g1), dim3(1024), 0, s, out, a, units);
     else
-      hipLaunchKernelGGL((k_wtp_mid_ct2<true>), dim3(units < g ? units : g), dim3(512), 0, s, out, a, units);
+      hipLaunchKernelGGL((k_wtp_mid_ct3<0, false>), dim3(units < g1 ? units : g1), dim3(1024), 0, s, out, a, units);
   } else {
     const int units = WNX * WN2;  // z-planes x y2
     // P1w out of place: non-temporal loads keep b out of the 256 MB Infinity Cache, which then

@@ -23,7 +23,9 @@ for k in [0, 1, 2, 3, 4, 8, 12, 13, 14, 15]:
     NAMES[200 + k] = "ct: " + NAMES[k]
     NAMES[300 + k] = "ct2: " + NAMES[k]
     NAMES[400 + k] = "ct2 pf: " + NAMES[k]
-cases = [0, 100, 1, 2, 3, 4, 8, 12, 13, 14, 15] + [200 + k for k in [0, 1, 2, 3, 4, 8, 12, 13, 14, 15]] + [300 + k for k in [0, 1, 2, 3, 4, 8, 12, 13, 14, 15]] + [400 + k for k in [0, 1, 3, 8, 15]]
+    NAMES[500 + k] = "ct3: " + NAMES[k]
+    NAMES[600 + k] = "ct3 pf: " + NAMES[k]
+cases = [0, 100, 1, 2, 3, 4, 8, 12, 13, 14, 15] + [200 + k for k in [0, 1, 2, 3, 4, 8, 12, 13, 14, 15]] + [300 + k for k in [0, 1, 2, 3, 4, 8, 12, 13, 14, 15]] + [400 + k for k in [0, 1, 3, 8, 15]] + [500 + k for k in [0, 1, 3, 15]] + [600 + k for k in [0, 1, 3]]
 res = {c: [] for c in cases}
 for rnd in range(3):
     for c in cases:

@@ -5,7 +5,9 @@
 //   which = 100: k_wtp_mid<whole-complex LDS (128 KiB, one workgroup per CU), 0>
 //   which = 200 + P: k_wtp_mid_ct<split LDS, P> (comps on lane bits 4-5, permlane solve; r04)
 //   which = 300 + P: k_wtp_mid_ct2<split LDS, P> (ct's map between the exchanges only; r04)
-//   which = 400 + P: k_wtp_mid_ct2<split LDS, P, LDS-DMA prefetch> (the r04 default)
+//   which = 400 + P: k_wtp_mid_ct2<split LDS, P, LDS-DMA prefetch> (the r04m default)
+//   which = 500 + P / 600 + P: k_wtp_mid_ct3<P> (8 points per thread, whole-complex) without / with the
+//   whole-unit prefetch
 #define CFP_KEXP 1
 #include "cfp_wave_three.hip"
 
@@ -40,6 +42,12 @@ extern "C" int wave_probe(int which, void* data, const void* tw, const void* tab
 #define G(P) case 400 + P: hipLaunchKernelGGL((k_wtp_mid_ct2<true, P, true>), dim3(512), dim3(512), 0, 0, d, a, units); return 0;
       G(0) G(1) G(3) G(8) G(15)
 #undef G
+#define H(P) case 500 + P: hipLaunchKernelGGL((k_wtp_mid_ct3<P, false>), dim3(256), dim3(1024), 0, 0, d, a, units); return 0;
+      H(0) H(1) H(3) H(15)
+#undef H
+#define I(P) case 600 + P: hipLaunchKernelGGL((k_wtp_mid_ct3<P, true>), dim3(256), dim3(1024), 0, 0, d, a, units); return 0;
+      I(0) I(1) I(3)
+#undef I
       default: return 1;
     }
   };
