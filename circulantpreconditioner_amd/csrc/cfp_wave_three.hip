@@ -625,7 +625,8 @@ k_wtp_mid_ct2(cd* data, WTPArgs a, int nunits) {
   }
 }
 
-// P2w at 8 points per thread (k_wtp_mid_ct3, r04): the two lane maps of k_wtp_mid_ct2 with the
+// P2w at 8 points per thread (k_wtp_mid_ct3, r04, measured and not kept: 79.3 us with the prefetch
+// against 63.9 for k_wtp_mid_ct2, parity green; tools/kexp only): the two lane maps of k_wtp_mid_ct2 with the
 // z FFT as 2 x 8 x 8 over 16 z-groups of the 64 columns (1,024 threads, 16 waves), whole-complex
 // exchanges (128 KiB, one workgroup per CU) -- the shape that won at 128^3 for the scalar P2 --
 // and, with PF, the WHOLE next unit DMA'd into the exchange buffer after the inverse FFT's last
@@ -838,12 +839,11 @@ hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArg
   if (stage == 1) {
     const int units = (WNX / 2) * WN1;  // x tiles x k1
     // the LDS-DMA prefetch (global_load_lds_dwordx4) takes 16-byte aligned addresses
-    // k_wtp_mid_ct3: one 1,024-thread workgroup per CU
-    const int g1 = wcu_count();
+    // the LDS-DMA prefetch (global_load_lds_dwordx4) takes 16-byte aligned addresses
     if (((uintptr_t)out & 15) == 0)
-      hipLaunchKernelGGL((k_wtp_mid_ct3<0, true>), dim3(units < g1 ? units : g1), dim3(1024), 0, s, out, a, units);
+      hipLaunchKernelGGL((k_wtp_mid_ct2<true, 0, true>), dim3(units < g ? units : g), dim3(512), 0, s, out, a, units);
     else
-      hipLaunchKernelGGL((k_wtp_mid_ct3<0, false>), dim3(units < g1 ? units : g1), dim3(1024), 0, s, out, a, units);
+      hipLaunchKernelGGL((k_wtp_mid_ct2<true>), dim3(units < g ? units : g), dim3(512), 0, s, out, a, units);
   } else {
     const int units = WNX * WN2;  // z-planes x y2
     // P1w out of place: non-temporal loads keep b out of the 256 MB Infinity Cache, which then
