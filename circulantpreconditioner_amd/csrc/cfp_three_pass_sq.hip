@@ -88,8 +88,15 @@ __global__ void __launch_bounds__(XT * N) k_sq_mid(cd* data, TPArgs a) {
   __shared__ __attribute__((aligned(16))) cd lds[TP * N];
   __shared__ cd tws[N];
   const int tid = threadIdx.x;
-  const int xt = blockIdx.x % NXT, k1 = blockIdx.x / NXT;
-  for (int i = tid; i < N; i += XT * N) tws[i] = a.tw[i];
+  // XCD-aware unit order: the workgroups of one XCD (blockIdx % 8, round-robin dispatch) take a
+  // contiguous range of units, so the x tiles that share 128-byte lines (a 1,600-byte row holds
+  // 6.25 tiles of 64 bytes) meet in one L2; in blockIdx order the unit moved 1.50 x 32 N bytes
+  // of HBM traffic (profiles/r04_pmc_small.txt)
+  constexpr int NU = NXT * R, PER = NU / 8, EXTRA = NU % 8;
+  const int b = blockIdx.x, j = b & 7, i = b >> 3;
+  const int u = j * PER + (j < EXTRA ? j : EXTRA) + i;
+  const int xt = u % NXT, k1 = u / NXT;
+  for (int i2 = tid; i2 < N; i2 += XT * N) tws[i2] = a.tw[i2];
   const int xl = tid % XT, z = tid / XT;
   const int c = tid % T, tz = tid / T;
   cd* col = data + (i64)z * N * N + (i64)R * k1 * N + xt * XT + xl;  // row y2 + R k1 at y2 = 0
