@@ -26,7 +26,9 @@ template <> struct SqCfg<100> { static constexpr int R = 10; };
 }  // namespace
 
 // S1 / S3.  N threads: column mode thread x, row mode (row k1 = tid / TPC, tpc = tid % TPC).
-template <int N, bool INV>
+// CO (S3): load in column mode (each row read by consecutive lanes) and transpose to row mode
+// through LDS, instead of the row-mode load (ten 160-byte pieces per row and instruction)
+template <int N, bool INV, bool CO = false>
 __global__ void __launch_bounds__(N) k_sq_rows(const cd* in, cd* out, const cd* tw, double scale) {
   constexpr int R = SqCfg<N>::R, TPC = N / R;
   static_assert(R * R == N, "n = R^2");
@@ -56,10 +58,21 @@ __global__ void __launch_bounds__(N) k_sq_rows(const cd* in, cd* out, const cd* 
 #pragma unroll
     for (int t = 0; t < R; ++t) gstore<F>(dst + TPC * t, v[t]);
   } else {
-    const cd* src = in + plane + (i64)(y2 + R * row) * N + tpc;  // row k1, points kx = tpc + TPC m
+    if constexpr (CO) {
+      const cd* src = in + plane + (i64)y2 * N + tid;  // column kx = tid, rows y2 + R k1
 #pragma unroll
-    for (int m = 0; m < R; ++m) v[m] = cconj(gload<F>(src + TPC * m));
-    fft_stages<N, R, R, true, R, F>(v, lds, tws, row, tpc, true);  // v[t]: x = tpc + TPC t
+      for (int m = 0; m < R; ++m) v[m] = cconj(gload<F>(src + (i64)R * N * m));
+#pragma unroll
+      for (int m = 0; m < R; ++m) lds[lds_idx<N, true, R, F>(m, tid)] = v[m];
+      xbarrier<F>();
+#pragma unroll
+      for (int m = 0; m < R; ++m) v[m] = lds[lds_idx<N, true, R, F>(row, tpc + m * TPC)];
+    } else {
+      const cd* src = in + plane + (i64)(y2 + R * row) * N + tpc;  // row k1, points kx = tpc + TPC m
+#pragma unroll
+      for (int m = 0; m < R; ++m) v[m] = cconj(gload<F>(src + TPC * m));
+    }
+    fft_stages<N, R, R, true, R, F>(v, lds, tws, row, tpc, !CO);  // v[t]: x = tpc + TPC t
     // row mode -> column x = tid
     xbarrier<F>();
 #pragma unroll
@@ -159,7 +172,7 @@ hipError_t launch_three_pass_sq(int stage, int n, const cd* in, cd* out, const T
   } else if (stage == 0) {
     hipLaunchKernelGGL((k_sq_rows<N, false>), dim3(N * R), dim3(N), 0, s, in, out, a.tw, 1.0);
   } else {
-    hipLaunchKernelGGL((k_sq_rows<N, true>), dim3(N * R), dim3(N), 0, s, in, out, a.tw, a.scale);
+    hipLaunchKernelGGL((k_sq_rows<N, true, true>), dim3(N * R), dim3(N), 0, s, in, out, a.tw, a.scale);
   }
   return hipGetLastError();
 }
