@@ -28,7 +28,7 @@ template <> struct SqCfg<100> { static constexpr int R = 10; };
 // S1 / S3.  N threads: column mode thread x, row mode (row k1 = tid / TPC, tpc = tid % TPC).
 // CO (S3): load in column mode (each row read by consecutive lanes) and transpose to row mode
 // through LDS, instead of the row-mode load (ten 160-byte pieces per row and instruction).
-// Measured slower (r04v: 11.9 against 11.0 us), not launched.
+// Measured slower (r04v, with non-temporal stores: 11.9 against 11.0 us), not launched.
 template <int N, bool INV, bool CO = false>
 __global__ void __launch_bounds__(N) k_sq_rows(const cd* in, cd* out, const cd* tw, double scale) {
   constexpr int R = SqCfg<N>::R, TPC = N / R;
