@@ -854,7 +854,7 @@ hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArg
     else if (stage == 0)
       hipLaunchKernelGGL((k_wtp_rows<false, 0>), gg, dim3(512), 0, s, in, out, a, units);
     else
-      hipLaunchKernelGGL((k_wtp_rows<true, 0>), gg, dim3(512), 0, s, in, out, a, units);  // A/B: plain stores
+      hipLaunchKernelGGL((k_wtp_rows<true, F_NT_ST>), gg, dim3(512), 0, s, in, out, a, units);
   }
   return hipGetLastError();
 }
