@@ -1031,7 +1031,7 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
       const unsigned g = grid_xcd(units, 1);  // whole rounds of a power of two >= 8
       if (g == 0) return hipErrorNotSupported;
       if (bl) TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 16, true, 512, true, true>), dim3(g), dim3(1024), s, out, a, units);
-      else TP_LAUNCH((k_tp_mid<kP2LoadFlags, 32, 16, 512, 16, true, 512, true>), dim3(g), dim3(1024), s, out, a, units);
+      else TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 16, true, 512, true>), dim3(g), dim3(1024), s, out, a, units);  // NT loads: 204 against 262 /s (r04y)
     } else if (bl) {
       launch_rows<32, 512, 1, 16, true, kRowsLP, 2, true>(stage, in, out, a, s);
     } else if (shape.mid == TP_MID_LANE64) {  // A/B: phase A through LDS
