@@ -174,7 +174,7 @@ hipError_t launch_three_pass_sq(int stage, int n, const cd* in, cd* out, const T
   } else if (stage == 0) {
     hipLaunchKernelGGL((k_sq_rows<N, false>), dim3(N * R), dim3(N), 0, s, in, out, a.tw, 1.0);
   } else {
-    hipLaunchKernelGGL((k_sq_rows<N, true>), dim3(N * R), dim3(N), 0, s, in, out, a.tw, a.scale);
+    hipLaunchKernelGGL((k_sq_rows<N, true, true>), dim3(N * R), dim3(N), 0, s, in, out, a.tw, a.scale);
   }
   return hipGetLastError();
 }
