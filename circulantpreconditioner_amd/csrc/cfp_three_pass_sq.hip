@@ -28,7 +28,8 @@ template <> struct SqCfg<100> { static constexpr int R = 10; };
 // S1 / S3.  N threads: column mode thread x, row mode (row k1 = tid / TPC, tpc = tid % TPC).
 // CO (S3): load in column mode (each row read by consecutive lanes) and transpose to row mode
 // through LDS, instead of the row-mode load (ten 160-byte pieces per row and instruction).
-// Measured slower (r04v, with non-temporal stores: 11.9 against 11.0 us), not launched.
+// Measured slower (r04v: 11.9 against 11.0 us with non-temporal stores, 11.75 against 11.1 with
+// the default policy), not launched.
 template <int N, bool INV, bool CO = false>
 __global__ void __launch_bounds__(N) k_sq_rows(const cd* in, cd* out, const cd* tw, double scale) {
   constexpr int R = SqCfg<N>::R, TPC = N / R;
@@ -174,7 +175,7 @@ hipError_t launch_three_pass_sq(int stage, int n, const cd* in, cd* out, const T
   } else if (stage == 0) {
     hipLaunchKernelGGL((k_sq_rows<N, false>), dim3(N * R), dim3(N), 0, s, in, out, a.tw, 1.0);
   } else {
-    hipLaunchKernelGGL((k_sq_rows<N, true, true>), dim3(N * R), dim3(N), 0, s, in, out, a.tw, a.scale);
+    hipLaunchKernelGGL((k_sq_rows<N, true>), dim3(N * R), dim3(N), 0, s, in, out, a.tw, a.scale);
   }
   return hipGetLastError();
 }
