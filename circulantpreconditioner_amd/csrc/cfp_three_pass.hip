@@ -1059,8 +1059,12 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
       // 20,530 /s); swap64 = 16 points, whole-complex (20,750 /s); lane32 = 32 columns = 4 x
       // times 8 y2, 8 points, whole-complex (19,130 /s)
       if (stage == 1) {
-        if (shape.mid == TP_MID_LANE32) launch_mid<32, 8, 128, 2, 8, false>(out, a, s);
-        else if (shape.mid == TP_MID_LANE64) launch_mid<64, 8, 128, 1>(out, a, s);
+        if (shape.mid == TP_MID_LANE32) {  // 64-byte tiles in XCD order (neighbours share an L2)
+          constexpr int units = (128 / 4) * 16;
+          const unsigned g = grid_xcd(units, 2);
+          if (g) TP_LAUNCH((k_tp_mid<0, 32, 8, 128, 8, false, 128, true>), dim3(g), dim3(512), s, out, a, units);
+          else launch_mid<32, 8, 128, 2, 8, false>(out, a, s);
+        } else if (shape.mid == TP_MID_LANE64) launch_mid<64, 8, 128, 1>(out, a, s);
         else if (shape.mid == TP_MID_SWAP64) launch_mid<64, 8, 128, 1, 16, false>(out, a, s);
         else launch_mid<64, 8, 128, 1, 8, false>(out, a, s);
       } else {
