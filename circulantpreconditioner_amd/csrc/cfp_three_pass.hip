@@ -1049,24 +1049,26 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
     // 64 columns) for A/B: 15.9k against 18.4k applies/s, the 5-pass schedule 17.3k
     // (profiles/r03m_128_three_sweep.md).
     // Default since r04: y split 16 x 8 -- P1/P3 units of 16 rows (1,024 units, 256 threads, four
-    // workgroups per CU, lane-pair phase A); P2 64 columns = 8 x times 8 y2 (256 units), 8 points
-    // per thread, whole-complex exchanges (1,024 threads, 128 KiB).  21,070 against 18,520
-    // applies/s for the r03 split 32 x 4 (n1 = 32) in the same process (profiles/
-    // r04_schedule_ab.jsonl): P1/P3 13.2 against 17.0 us, P2 21.3 against 19.1 us.
+    // workgroups per CU, lane-pair phase A, 13.2 against 17.0 us); P2 below.  21,475 against
+    // 18,520 applies/s for the r03 split 32 x 4 (n1 = 32) in the same process
+    // (profiles/r04_schedule_ab.jsonl).
     const int n1 = shape.n1 ? shape.n1 : (shape.mid == TP_MID_LANE64 || shape.mid == TP_MID_SWAP64 ? 32 : 16);
     if (n1 == 16) {
-      // P2 A/B: lane64 = 64 columns, 16 points per thread, split exchanges (512 threads, 64 KiB;
-      // 20,530 /s); swap64 = 16 points, whole-complex (20,750 /s); lane32 = 32 columns = 4 x
-      // times 8 y2, 8 points, whole-complex (19,130 /s)
+      // P2 default (r04z): 32 columns = 4 x times 8 y2 (64-byte tiles, 512 units, two 512-thread
+      // workgroups per CU, 8 points, whole-complex) in XCD order, so the two tiles of a 128-byte
+      // line meet in one L2: 21,475 /s; in blockIdx order 19,130.  A/B: lane32 = 64 columns,
+      // 8 points, whole-complex (1,024 threads; 21,070-21,150 /s); lane64 = 64 columns, 16
+      // points, split (20,530 /s); swap64 = 64 columns, 16 points, whole-complex (20,750 /s)
       if (stage == 1) {
-        if (shape.mid == TP_MID_LANE32) {  // 64-byte tiles in XCD order (neighbours share an L2)
+        if (shape.mid == TP_MID_LANE32) launch_mid<64, 8, 128, 1, 8, false>(out, a, s);
+        else if (shape.mid == TP_MID_LANE64) launch_mid<64, 8, 128, 1>(out, a, s);
+        else if (shape.mid == TP_MID_SWAP64) launch_mid<64, 8, 128, 1, 16, false>(out, a, s);
+        else {
           constexpr int units = (128 / 4) * 16;
           const unsigned g = grid_xcd(units, 2);
           if (g) TP_LAUNCH((k_tp_mid<0, 32, 8, 128, 8, false, 128, true>), dim3(g), dim3(512), s, out, a, units);
           else launch_mid<32, 8, 128, 2, 8, false>(out, a, s);
-        } else if (shape.mid == TP_MID_LANE64) launch_mid<64, 8, 128, 1>(out, a, s);
-        else if (shape.mid == TP_MID_SWAP64) launch_mid<64, 8, 128, 1, 16, false>(out, a, s);
-        else launch_mid<64, 8, 128, 1, 8, false>(out, a, s);
+        }
       } else {
         launch_rows<16, 128, 4, 8, false, true, 0, false, 0, 0>(stage, in, out, a, s);
       }
