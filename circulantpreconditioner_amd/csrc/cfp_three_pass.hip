@@ -415,7 +415,10 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 // y2 (bits 3-5), so y2 keeps lane bits 3-5 and every y2 stage below (permlane swaps on bits 5 and
 // 4, DPP on bit 3) is the T = 64 code; c (the column x + 4 y2) and tz index memory and LDS,
 // `lane` the lane bits.
-template <int T, int N2, int TN, int PROBE = 0, bool PF = false, int NX = TN, int ST = 0, int LD = 0, bool BL = false>
+// XCD (r04): units in xcd_unit order (whole rounds), so x tiles that share 128-byte lines run
+// under one L2 (T = 32 natural layout: 64-byte tiles).
+template <int T, int N2, int TN, int PROBE = 0, bool PF = false, int NX = TN, int ST = 0, int LD = 0, bool BL = false,
+          bool XCD = false>
 __global__ void __launch_bounds__(T * (TN / 16)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
 #ifndef CFP_KEXP
@@ -464,7 +467,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
   };
   static_assert(!PF || (NT / 64) * NPF * 128 <= T * TN, "the prefetch fits the exchange buffer");
   if constexpr (PF) {
-    if ((int)blockIdx.x < nunits) prefetch(blockIdx.x);
+    if ((int)blockIdx.x < nunits) prefetch(XCD ? xcd_unit(blockIdx.x, gridDim.x) : (int)blockIdx.x);
   }
   // split exchange from the transposed registers (first radix-16 stage done) to the column
   // layout: v[t] = point tz + 16 t of column c
@@ -503,7 +506,8 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
     return (lane & 8) ? -1.0 : 1.0;
   };
 
-  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+  for (int it = blockIdx.x; it < nunits; it += gridDim.x) {
+    const int u = XCD ? xcd_unit(it, gridDim.x) : it;
     cd v[16];
     if constexpr (PROBE & PR_NO_LOAD) {
       const int c = idx(c0), tz = idx(tz0);
@@ -630,7 +634,7 @@ k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
     exchange_t(v, false);
     if constexpr (PF) {
       lds_barrier();  // every wave has read the exchange buffer
-      if (u + (int)gridDim.x < nunits) prefetch(u + gridDim.x);
+      if (it + (int)gridDim.x < nunits) prefetch(XCD ? xcd_unit(it + gridDim.x, gridDim.x) : it + (int)gridDim.x);
     }
     stage_b(v);  // natural layout again: column c = x + XT y2, slot m = z
     {
@@ -1011,7 +1015,7 @@ hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs
 
 bool three_pass_shape_valid(int n1, int mid, i64 n) {
   if (n1 == 16) return n == 128 && mid >= TP_MID_DEFAULT && mid <= TP_MID_SWAP64;
-  return (n1 == 0 || n1 == 32 || n1 == 64) && (mid >= 0 && mid <= TP_MID_BLOCKED32) &&
+  return (n1 == 0 || n1 == 32 || n1 == 64) && (mid >= 0 && mid <= TP_MID_SWAP32X) &&
          !(mid >= TP_MID_BLOCKED && n1 == 64);
 }
 
@@ -1100,6 +1104,22 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
     if (stage != 1) launch_rows<32, 256, 2, 16, true, kRowsLP, 8>(stage, in, out, a, s);
     else if (pf_ok) launch_mid_sw<8, 256, true, true>(out, a, s);
     else launch_mid_sw<8, 256, false, true>(out, a, s);
+    return hipGetLastError();
+  }
+  if (shape.mid == TP_MID_SWAP32X) {  // natural layout; P2 = 32 columns in XCD order, two per CU
+    if (stage != 1) {
+      launch_rows<32, 256, 2, 16, true, kRowsLP>(stage, in, out, a, s);
+    } else {
+      constexpr int units = (256 / 4) * 32;
+      const unsigned g = grid_xcd(units, 2);
+      if (g == 0) return hipErrorNotSupported;
+      if (pf_ok)
+        TP_LAUNCH((k_tp_mid_sw<32, 8, 256, 0, true, 256, 0, kP2LoadFlags, false, true>), dim3(g), dim3(512), s, out, a,
+                  units);
+      else
+        TP_LAUNCH((k_tp_mid_sw<32, 8, 256, 0, false, 256, 0, kP2LoadFlags, false, true>), dim3(g), dim3(512), s, out, a,
+                  units);
+    }
     return hipGetLastError();
   }
   if (shape.mid == TP_MID_BLOCKED32) {  // blocks of 4 x; P2 = 32 columns, two workgroups per CU
