@@ -25,6 +25,8 @@ enum : int {
   F_SYM_LDS = 256,  // fused pass: stage the per-point symbol table in LDS next to the twiddles
   F_OCC8 = 512,     // ask the compiler for 8 waves per SIMD (<= 64 VGPRs)
   F_PAD1 = 1024,    // row-mode LDS rows padded by one element (n + 1) instead of n / 16
+  F_WAVE_LDS = 2048,  // every exchange stays inside one wave (its columns' threads and LDS region
+                      // belong to one wave): the exchange barriers become wave-local LDS waits
 };
 __host__ __device__ constexpr int waves_req(int flags, int mode) {
   return mode == PASS_FUSED_WAVE ? 1 : ((flags & F_OCC8) ? 8 : ((flags & F_OCC4) ? 4 : 1));
@@ -35,7 +37,10 @@ __host__ __device__ constexpr int waves_req(int flags, int mode) {
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 template <int FLAGS>
 __device__ __forceinline__ void xbarrier() {
-  if (FLAGS & F_LDS_SYNC) lds_barrier();
+  // a wave's LDS accesses complete in order: waiting for its own is enough when no other wave
+  // touches the region (the asm's memory clobber keeps the compiler from moving LDS accesses)
+  if (FLAGS & F_WAVE_LDS) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  else if (FLAGS & F_LDS_SYNC) lds_barrier();
   else __syncthreads();
 }
 

@@ -203,7 +203,8 @@ int run_real_three(cfp_rplan_s* p, const double* b, double* x, hipStream_t s, st
   a.axsym = p->axsym3;
   a.scale = 2.0 / (double)(p->n[0] * p->n[1] * p->n[2]);
   if (ev) HIPCHK(hipEventRecord((*ev)[0], s));
-  hipError_t e = launch_three_pass_real(0, (int)p->n[0], b, p->H, p->Q, nullptr, a, s);
+  const bool alt = p->schedule == CFP_RSCHEDULE_THREE_ALT;
+  hipError_t e = launch_three_pass_real(0, (int)p->n[0], b, p->H, p->Q, nullptr, a, s, alt);
   if (e != hipSuccess) return hip_error(e, "r2c rows + y1 pass");
   if (ev) HIPCHK(hipEventRecord((*ev)[1], s));
   e = launch_three_pass_real(1, (int)p->n[0], nullptr, p->H, nullptr, nullptr, a, s);
@@ -214,7 +215,7 @@ int run_real_three(cfp_rplan_s* p, const double* b, double* x, hipStream_t s, st
   e = launch_three_pass_real(3, (int)p->n[0], nullptr, nullptr, p->Q, nullptr, aq, s);
   if (e != hipSuccess) return hip_error(e, "Nyquist column y2/z pass");
   if (ev) HIPCHK(hipEventRecord((*ev)[3], s));
-  e = launch_three_pass_real(2, (int)p->n[0], nullptr, p->H, p->Q, x, a, s);
+  e = launch_three_pass_real(2, (int)p->n[0], nullptr, p->H, p->Q, x, a, s, alt);
   if (e != hipSuccess) return hip_error(e, "y1 inverse + c2r rows pass");
   if (ev) HIPCHK(hipEventRecord((*ev)[4], s));
   return CFP_SUCCESS;
@@ -335,9 +336,10 @@ extern "C" int cfp_rplan_set_symbol_transport(cfp_rplan_t p, const double lam[3]
 
 extern "C" int cfp_rplan_set_schedule(cfp_rplan_t p, int schedule) {
   if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
-  if (schedule != CFP_RSCHEDULE_AUTO && schedule != CFP_RSCHEDULE_FIVE && schedule != CFP_RSCHEDULE_THREE)
+  if (schedule != CFP_RSCHEDULE_AUTO && schedule != CFP_RSCHEDULE_FIVE && schedule != CFP_RSCHEDULE_THREE &&
+      schedule != CFP_RSCHEDULE_THREE_ALT)
     return set_error(CFP_ERR_ARG_OUTOFRANGE, "unknown real-plan schedule %d", schedule);
-  if (schedule == CFP_RSCHEDULE_THREE && !three_ok(p))
+  if ((schedule == CFP_RSCHEDULE_THREE || schedule == CFP_RSCHEDULE_THREE_ALT) && !three_ok(p))
     return set_error(CFP_ERR_SUP, "the 3-sweep real schedule needs a 128^3 or 256^3 grid");
   p->schedule = schedule;
   return CFP_SUCCESS;

@@ -52,7 +52,7 @@ hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs
 // [kx + (n/2) ky], a.axsym = [kz].  P1r leaves Q after its y1 DFT, P3r takes it before its y1
 // inverse (slot layout, as H).
 hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* Q, double* x, const TPArgs& a,
-                                  hipStream_t s);
+                                  hipStream_t s, bool alt_rows = false);
 
 // wave-system plan (cfp_wave_three.hip): the 3-sweep apply of the interleaved 4-component field
 // (idx = 4 cell + comp) on a 128^3 grid, y split 16 x 8.  stage 0 P1w (in -> out), 1 P2w (out in

@@ -709,7 +709,14 @@ static unsigned grid_xcd(int units, int per_cu) {
 // OCC: waves per SIMD asked of the compiler (4: two 512-thread workgroups per CU; 6: three)
 // WC: whole-complex LDS exchanges (ds_*_b128, one barrier pair per exchange instead of two;
 // 70 KiB at M = 128, two workgroups per CU) instead of real / imaginary halves
-template <bool INV, int M = 128, int N1 = 32, int N2 = 8, int NY = 256, int MF = 0, int OCC = 4, bool WC = false>
+// WL: wave-local FFT exchanges.  A row's TPC threads are consecutive lanes of one wave, and in
+// column mode a wave takes 16 whole columns (lane = 16 ty + column) instead of 64 columns of one
+// ty: the row FFT's and the y1 DFT's exchanges (3 of the unit's 5; 12 of its 18 barriers with
+// split exchanges) then wait for the wave's own LDS accesses only; the two transposes keep their
+// workgroup barriers.  Column-mode LDS rows are M + 16 doubles apart (the four ty rows of a
+// wave's store then fall on different bank halves).
+template <bool INV, int M = 128, int N1 = 32, int N2 = 8, int NY = 256, int MF = 0, int OCC = 4, bool WC = false,
+          bool WL = false>
 __global__ void __launch_bounds__(N1 * (M / 8)) __attribute__((amdgpu_waves_per_eu(OCC)))
 k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nunits) {
   constexpr int PTS = 8;
@@ -717,8 +724,12 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
   constexpr int TY = N1 / PTS;  // 4 threads per column (column mode)
   constexpr int NT = N1 * TPC;
   constexpr int RS = M + M / 16;
+  constexpr int TC = WL ? M + 16 : M;  // column-mode row stride of the y1 DFT's exchange
+  static_assert(!WL || (64 % TPC == 0 && TY * 16 == 64 && M % 16 == 0), "wave-local: whole rows and 16 columns per wave");
   constexpr int F = (WC ? 0 : F_SPLIT_LDS) | F_LDS_SYNC;
-  __shared__ __attribute__((aligned(16))) double lds[N1 * RS * (WC ? 2 : 1)];  // row layout; the column layout (N1 x M) fits
+  constexpr int FW = F | (WL ? F_WAVE_LDS : 0);  // the row FFT's and the y1 DFT's exchanges
+  constexpr int LDS_D = (N1 * RS > N1 * TC ? N1 * RS : N1 * TC) * (WC ? 2 : 1);
+  __shared__ __attribute__((aligned(16))) double lds[LDS_D];  // row layout; the column layout (N1 x TC) fits
   cd* const lc = reinterpret_cast<cd*>(lds);
   __shared__ cd tw_m[M];   // W_M (row FFT)
   __shared__ cd tw_1[N1];  // W_N1 (y1 DFT)
@@ -726,8 +737,10 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
   const int tid = threadIdx.x;
   for (int i = tid; i < M; i += NT) tw_m[i] = a.tw[2 * i];
   for (int i = tid; i < N1; i += NT) tw_1[i] = a.tw[(2 * M / N1) * i];
+  if constexpr (WL) __syncthreads();  // no workgroup barrier precedes the first wave-local FFT's twiddle reads
   const int r0 = tid / TPC, tpc0 = tid % TPC;  // row mode: row r (= y1), thread tpc
-  const int x0 = tid % M, ty0 = tid / M;       // column mode: column kx, thread ty
+  // column mode: column kx, thread ty
+  const int x0 = WL ? (tid >> 6) * 16 + (tid & 15) : tid % M, ty0 = WL ? (tid >> 4) & 3 : tid / M;
   const auto idx = [](int i) {
     asm volatile("" : "+v"(i));
     return i;
@@ -834,17 +847,19 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
 #pragma unroll
         for (int t = 0; t < PTS; ++t) v[t] = gload<MF>(src + TPC * t);
         __builtin_amdgcn_sched_barrier(0);  // all loads out before the first butterfly
-        fft_stages<M, PTS, r0_of(M, PTS), true, N1, F>(v, lds, tw_m, r, tpc, true);  // 128 = 2 x 8 x 8; v[t] = Z[tpc + TPC t]
+        fft_stages<M, PTS, r0_of(M, PTS), true, N1, FW>(v, lds, tw_m, r, tpc, true);  // 128 = 2 x 8 x 8; v[t] = Z[tpc + TPC t]
       }
       to_columns_r2c(v, z, y2);
       {
         const int x = idx(x0), ty = idx(ty0);
-        fft_stages<N1, PTS, r0_of(N1, PTS), false, M, F>(v, lds, tw_1, x, ty, true);  // 32 = 4 x 8; v[m]: k1 = ty + TY m
+        fft_stages<N1, PTS, r0_of(N1, PTS), false, TC, FW>(v, lds, tw_1, x, ty, true);  // 32 = 4 x 8; v[m]: k1 = ty + TY m
         cd* dst = H + ((i64)z * NY + y2 + N2 * ty) * M + x;
 #pragma unroll
         for (int m = 0; m < PTS; ++m) dst[(i64)N2 * TY * M * m] = v[m];
       }
-      if (tid < N1) {  // the Nyquist column's y1 DFT (qy is visible: fft_stages held barriers)
+      if constexpr (WL) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // qy: written by this wave's x = 0 lanes
+      if (tid < N1) {  // the Nyquist column's y1 DFT (qy is visible: fft_stages held barriers; with WL
+                       // the x = 0 lanes that wrote it are lanes 0, 16, 32, 48 of this same wave)
         const int k = idx(tid);
         cd acc = make_cd(0.0, 0.0);
 #pragma unroll 8
@@ -862,7 +877,7 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
         __builtin_amdgcn_sched_barrier(0);  // all loads out before the first butterfly (measured neutral here)
 #pragma unroll
         for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
-        fft_stages<N1, PTS, r0_of(N1, PTS), false, M, F>(v, lds, tw_1, x, ty, true);  // v[m]: y1 = ty + TY m
+        fft_stages<N1, PTS, r0_of(N1, PTS), false, TC, FW>(v, lds, tw_1, x, ty, true);  // v[m]: y1 = ty + TY m
       }
       if (tid < 64) {  // one wave: the Nyquist column's y1 inverse into qy (read by to_rows_c2r)
         if (tid < N1) qy[tid] = qk;
@@ -877,7 +892,7 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
       to_rows_c2r(v, z, y2);
       {
         const int r = idx(r0), tpc = idx(tpc0);
-        fft_stages<M, PTS, r0_of(M, PTS), true, N1, F>(v, lds, tw_m, r, tpc, true);
+        fft_stages<M, PTS, r0_of(M, PTS), true, N1, FW>(v, lds, tw_m, r, tpc, true);
         const double sc = a.scale;
         cd* dst = reinterpret_cast<cd*>(out_r) + ((i64)z * NY + y2 + N2 * r) * M + tpc;
 #pragma unroll
@@ -889,7 +904,7 @@ k_tp_rows_r2c(const double* in_r, cd* H, cd* Q, double* out_r, TPArgs a, int nun
 }
 
 hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* Q, double* x, const TPArgs& a,
-                                  hipStream_t s) {
+                                  hipStream_t s, bool alt_rows) {
   if (stage == 3) {  // the Nyquist column Q [n z][n y]: P2 on its N2 columns of each k1 (NX = 1)
     if (n == 128)
       hipLaunchKernelGGL((k_tp_mid<0, 4, 4, 128, 8, false, 1>), dim3(32), dim3(4 * 16), 0, s, Q, a, 32);
@@ -921,9 +936,16 @@ hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* 
   } else {
     constexpr int units = 256 * 8;  // z-planes x y2
     const unsigned g = grid_of(units, 2);
-    if (stage == 0)  // P1r: 80 VGPRs, three workgroups per CU
+    // alt_rows (CFP_RSCHEDULE_THREE_ALT, A/B): the row FFT's and y1 DFT's exchanges wave-local (WL)
+    if (stage == 0 && alt_rows)
+      hipLaunchKernelGGL((k_tp_rows_r2c<false, 128, 32, 8, 256, F_NT_LD, 6, false, true>), dim3(grid_of(units, 3)),
+                         dim3(512), 0, s, b, H, Q, nullptr, a, units);
+    else if (stage == 0)  // P1r: 80 VGPRs, three workgroups per CU
       hipLaunchKernelGGL((k_tp_rows_r2c<false, 128, 32, 8, 256, F_NT_LD, 6>), dim3(grid_of(units, 3)), dim3(512), 0, s, b,
                          H, Q, nullptr, a, units);
+    else if (alt_rows)
+      hipLaunchKernelGGL((k_tp_rows_r2c<true, 128, 32, 8, 256, F_NT_ST, 4, true, true>), dim3(g), dim3(512), 0, s,
+                         nullptr, H, Q, x, a, units);
     else
       hipLaunchKernelGGL((k_tp_rows_r2c<true, 128, 32, 8, 256, F_NT_ST, 4, true>), dim3(g), dim3(512), 0, s, nullptr, H, Q, x, a,
                          units);

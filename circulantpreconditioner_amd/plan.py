@@ -297,11 +297,12 @@ class RealPlan:
         check(lib().cfp_rplan_set_symbol_transport(self._h, (ctypes.c_double * 3)(*vals)))
         return self
 
-    SCHEDULES = {"auto": 0, "five": 1, "three": 2}
+    SCHEDULES = {"auto": 0, "five": 1, "three": 2, "three_alt": 3}
 
     def set_schedule(self, schedule: str | int) -> "RealPlan":
-        """'auto' (3 sweeps at 128^3 and 256^3), 'five' (r2c + 3 half-spectrum passes + c2r) or 'three'
-        (128^3 and 256^3 only)."""
+        """'auto' (3 sweeps at 128^3 and 256^3), 'five' (r2c + 3 half-spectrum passes + c2r), 'three'
+        (128^3 and 256^3 only) or 'three_alt' (the 3 sweeps with the alternative row-sweep kernels
+        of DESIGN.md, for A/B; 256^3, else as 'three')."""
         v = self.SCHEDULES[schedule] if isinstance(schedule, str) else int(schedule)
         check(lib().cfp_rplan_set_schedule(self._h, v))
         return self

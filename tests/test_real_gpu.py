@@ -68,6 +68,13 @@ def test_real_three_sweep_256_vs_oracle(cp, oracle, lam, side):
         t = torch.from_numpy(b).cuda()
         plan.apply(t, out=t)
         assert torch.equal(t, x)
+        plan.set_schedule("three_alt")  # the alternative row-sweep kernels (wave-local exchanges)
+        assert plan.three_sweep
+        xa = plan.apply(torch.from_numpy(b).cuda())
+        assert float(torch.linalg.vector_norm(xa - x) / torch.linalg.vector_norm(x)) < 1e-13
+        t = torch.from_numpy(b).cuda()
+        plan.apply(t, out=t)
+        assert torch.equal(t, xa)
         plan.set_schedule("five")
         assert not plan.three_sweep
         x5 = plan.apply(torch.from_numpy(b).cuda())
