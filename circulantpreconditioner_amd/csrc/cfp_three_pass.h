@@ -23,8 +23,10 @@ struct TPArgs {
 // BLOCKED32: blocks of 4 x and the permlane P2 on 32 columns, two workgroups per CU
 // SWAP32X: the permlane P2 on 32 columns (4 x times 8 y2, natural layout: 64-byte tiles), two
 // workgroups per CU, units in XCD order (r04)
+// ROWSALT: the default shape (n1 = 0 only; 128^3, 256^3, 512^3) with P1 / P3's row-FFT exchanges
+// the other way (workgroup barriers instead of wave-local, or the reverse: kRowsWave), for A/B
 enum { TP_MID_DEFAULT = 0, TP_MID_LANE64 = 1, TP_MID_LANE32 = 2, TP_MID_SWAP64 = 3, TP_MID_SWAP64_PF = 4,
-       TP_MID_BLOCKED = 5, TP_MID_BLOCKED32 = 6, TP_MID_SWAP32X = 7 };
+       TP_MID_BLOCKED = 5, TP_MID_BLOCKED32 = 6, TP_MID_SWAP32X = 7, TP_MID_ROWSALT = 8 };
 struct TPShape {
   int n1 = 0;   // y split ny = n1 * n2: 0 (default 32), 32 or 64
   int mid = 0;  // TP_MID_* (DEFAULT = SWAP64_PF at 256^3)

@@ -112,6 +112,11 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
                 "blocked layout: 4 or 8 x times 8 y2, or 2 x times 16 y2");
   constexpr int RS = TN + TN / 16;  // padded row stride of the row-mode LDS layout
   constexpr int F = FLAGS | (XS ? F_SPLIT_LDS : 0) | F_LDS_SYNC;
+  // F_WAVE_LDS in FLAGS: phase C's row-FFT exchanges wave-local (a row's TR threads are
+  // consecutive lanes of one wave and its LDS row is theirs alone); phase A (columns spread over
+  // waves) and the transposes keep workgroup barriers
+  constexpr int FA = F & ~F_WAVE_LDS;
+  static_assert(!(FLAGS & F_WAVE_LDS) || 64 % TR == 0, "wave-local rows: whole rows per wave");
   __shared__ __attribute__((aligned(16))) double lds[N1 * RS * (XS ? 1 : 2)];  // both layouts fit
   __shared__ cd tw_l[N1];  // W_N1 for phase A; phase C reads W_256 from global memory (L2 hits),
                            // which keeps it out of scratch (20 B/lane with the table in LDS)
@@ -183,7 +188,7 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
     } else {
       // phase A: N1-point DFT over y1 for every x (column mode, TN columns x TY threads)
       const int x = idx(x0), ty = idx(ty0);
-      fft_stages<N1, PTS, r0_of(N1, PTS), false, TN, F>(v, lds, tw_l, x, ty, true);  // v[m]: k1 = ty + TY m
+      fft_stages<N1, PTS, r0_of(N1, PTS), false, TN, FA>(v, lds, tw_l, x, ty, true);  // v[m]: k1 = ty + TY m
       lds_barrier();  // phase A's last LDS reads are done
     }
     // phase B: transpose to rows k1, thread (row r, tx) gets x = tx + TR m
@@ -920,12 +925,19 @@ hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* 
     } else {
       constexpr int units = 128 * 4;  // z-planes x y2
       const unsigned g = grid_of(units, 4);
-      if (stage == 0)
+      // wave-local FFT exchanges (WL) by default since r04ab; alt_rows: workgroup barriers
+      if (stage == 0 && alt_rows)
         hipLaunchKernelGGL((k_tp_rows_r2c<false, 64, 32, 4, 128>), dim3(g), dim3(256), 0, s, b, H, Q, nullptr, a,
                            units);
-      else
+      else if (stage == 0)
+        hipLaunchKernelGGL((k_tp_rows_r2c<false, 64, 32, 4, 128, 0, 4, false, true>), dim3(g), dim3(256), 0, s, b, H,
+                           Q, nullptr, a, units);
+      else if (alt_rows)
         hipLaunchKernelGGL((k_tp_rows_r2c<true, 64, 32, 4, 128>), dim3(g), dim3(256), 0, s, nullptr, H, Q, x, a,
                            units);
+      else
+        hipLaunchKernelGGL((k_tp_rows_r2c<true, 64, 32, 4, 128, 0, 4, false, true>), dim3(g), dim3(256), 0, s, nullptr,
+                           H, Q, x, a, units);
     }
     return hipGetLastError();
   }
@@ -936,14 +948,15 @@ hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* 
   } else {
     constexpr int units = 256 * 8;  // z-planes x y2
     const unsigned g = grid_of(units, 2);
-    // alt_rows (CFP_RSCHEDULE_THREE_ALT, A/B): the row FFT's and y1 DFT's exchanges wave-local (WL)
-    if (stage == 0 && alt_rows)
+    // the row FFT's and y1 DFT's exchanges wave-local (WL; r04aa: 5,720 against 5,343 real
+    // PCApply/s, P1r 64 -> ~57 us); alt_rows (CFP_RSCHEDULE_THREE_ALT, A/B): workgroup barriers
+    if (stage == 0 && !alt_rows)  // P1r: 80 VGPRs, three workgroups per CU
       hipLaunchKernelGGL((k_tp_rows_r2c<false, 128, 32, 8, 256, F_NT_LD, 6, false, true>), dim3(grid_of(units, 3)),
                          dim3(512), 0, s, b, H, Q, nullptr, a, units);
-    else if (stage == 0)  // P1r: 80 VGPRs, three workgroups per CU
+    else if (stage == 0)
       hipLaunchKernelGGL((k_tp_rows_r2c<false, 128, 32, 8, 256, F_NT_LD, 6>), dim3(grid_of(units, 3)), dim3(512), 0, s, b,
                          H, Q, nullptr, a, units);
-    else if (alt_rows)
+    else if (!alt_rows)
       hipLaunchKernelGGL((k_tp_rows_r2c<true, 128, 32, 8, 256, F_NT_ST, 4, true, true>), dim3(g), dim3(512), 0, s,
                          nullptr, H, Q, x, a, units);
     else
@@ -972,26 +985,37 @@ constexpr bool kRowsLP = true;
 // P2 load policy (r03z, profiles/r03z_tp_p2nt.txt): non-temporal loads and LDS-DMA of its input,
 // which nothing reads after it: chain 304.4 -> 300.7 us
 constexpr int kP2LoadFlags = F_NT_LD;
+// P1 / P3 phase C (the row FFT) with wave-local exchanges (r04ab): shape TP_MID_ROWSALT runs the
+// other setting for A/B
+constexpr bool kRowsWave = true;
 
 // P1F / P3F: P1's load and P3's store policy out of place (kP1Flags / kP3Flags; 0 = plain)
+// WR: phase C's exchanges wave-local (F_WAVE_LDS)
 template <int N1, int TN, int PER_CU, int PTS = 16, bool XS = true, bool LP = false, int BL = 0, bool XCD = false,
-          int P1F = kP1Flags, int P3F = kP3Flags>
+          int P1F = kP1Flags, int P3F = kP3Flags, bool WR = kRowsWave>
 static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
   constexpr int units = TN * (TN / N1);  // z-planes x y2
+  constexpr int W = WR ? F_WAVE_LDS : 0;
   const unsigned g = XCD ? grid_xcd(units, PER_CU) : grid_of(units, PER_CU);
   if constexpr (XCD) {
     if (g == 0) {  // fewer than 8 workgroups: the same kernel in plain unit order
-      launch_rows<N1, TN, PER_CU, PTS, XS, LP, BL, false, P1F, P3F>(stage, in, out, a, s);
+      launch_rows<N1, TN, PER_CU, PTS, XS, LP, BL, false, P1F, P3F, WR>(stage, in, out, a, s);
       return;
     }
   }
   const dim3 blk(N1 * (TN / PTS));
   if (stage == 0 && in == out)  // in place (the direct solver's Un, Un)
-    TP_LAUNCH((k_tp_rows<false, kP1InPlaceFlags, N1, TN, PTS, XS, LP, BL, XCD>), dim3(g), blk, s, in, out, a, units);
+    TP_LAUNCH((k_tp_rows<false, kP1InPlaceFlags | W, N1, TN, PTS, XS, LP, BL, XCD>), dim3(g), blk, s, in, out, a, units);
   else if (stage == 0)
-    TP_LAUNCH((k_tp_rows<false, P1F, N1, TN, PTS, XS, LP, BL, XCD>), dim3(g), blk, s, in, out, a, units);
+    TP_LAUNCH((k_tp_rows<false, P1F | W, N1, TN, PTS, XS, LP, BL, XCD>), dim3(g), blk, s, in, out, a, units);
   else
-    TP_LAUNCH((k_tp_rows<true, P3F, N1, TN, PTS, XS, LP, BL, XCD>), dim3(g), blk, s, in, out, a, units);
+    TP_LAUNCH((k_tp_rows<true, P3F | W, N1, TN, PTS, XS, LP, BL, XCD>), dim3(g), blk, s, in, out, a, units);
+}
+// the default row sweeps, or (alt, shape TP_MID_ROWSALT) the same with the other phase-C exchanges
+template <int N1, int TN, int PER_CU, int PTS, bool XS, bool LP, int P1F = kP1Flags, int P3F = kP3Flags>
+static void launch_rows_ab(bool alt, int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
+  if (alt) launch_rows<N1, TN, PER_CU, PTS, XS, LP, 0, false, P1F, P3F, !kRowsWave>(stage, in, out, a, s);
+  else launch_rows<N1, TN, PER_CU, PTS, XS, LP, 0, false, P1F, P3F, kRowsWave>(stage, in, out, a, s);
 }
 
 template <int T, int N2, int TN, int PER_CU, int PTS = 16, bool XS = true>
@@ -1036,6 +1060,7 @@ hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs
 }
 
 bool three_pass_shape_valid(int n1, int mid, i64 n) {
+  if (mid == TP_MID_ROWSALT) return n1 == 0;
   if (n1 == 16) return n == 128 && mid >= TP_MID_DEFAULT && mid <= TP_MID_SWAP64;
   return (n1 == 0 || n1 == 32 || n1 == 64) && (mid >= 0 && mid <= TP_MID_SWAP32X) &&
          !(mid >= TP_MID_BLOCKED && n1 == 64);
@@ -1043,6 +1068,9 @@ bool three_pass_shape_valid(int n1, int mid, i64 n) {
 
 hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPArgs& a, TPShape shape,
                              hipStream_t s) {
+  // TP_MID_ROWSALT: the default shape with the other phase-C exchanges in P1 / P3 (A/B)
+  const bool ra = shape.mid == TP_MID_ROWSALT;
+  if (ra) shape.mid = TP_MID_DEFAULT;
   if (n == 100) return launch_three_pass_sq(stage, n, in, out, a, shape, s);
   if (n == 512) {
     // 512^3 (r04): N1 = 32 x N2 = 16.  P1 / P3: 32 rows of 512 (16 points per thread, 1024
@@ -1063,7 +1091,7 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
     } else if (shape.mid == TP_MID_LANE64) {  // A/B: phase A through LDS
       launch_rows<32, 512, 1>(stage, in, out, a, s);
     } else {  // lane-pair phase A (no LDS exchange there)
-      launch_rows<32, 512, 1, 16, true, kRowsLP>(stage, in, out, a, s);
+      launch_rows_ab<32, 512, 1, 16, true, kRowsLP>(ra, stage, in, out, a, s);
     }
     return hipGetLastError();
   }
@@ -1096,7 +1124,7 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
           else launch_mid<32, 8, 128, 2, 8, false>(out, a, s);
         }
       } else {
-        launch_rows<16, 128, 4, 8, false, true, 0, false, 0, 0>(stage, in, out, a, s);
+        launch_rows_ab<16, 128, 4, 8, false, true, 0, 0>(ra, stage, in, out, a, s);
       }
       return hipGetLastError();
     }
@@ -1170,7 +1198,7 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
   } else if (n1 == 64) {
     launch_rows<64, 256, 1>(stage, in, out, a, s);
   } else {
-    launch_rows<32, 256, 2, 16, true, kRowsLP>(stage, in, out, a, s);
+    launch_rows_ab<32, 256, 2, 16, true, kRowsLP>(ra, stage, in, out, a, s);
   }
   return hipGetLastError();
 }

@@ -172,7 +172,7 @@ class CirculantPlan:
         return self
 
     TP_MIDS = {"default": 0, "lane64": 1, "lane32": 2, "swap64": 3, "swap64pf": 4, "blocked": 5, "blocked32": 6,
-               "swap32x": 7}
+               "swap32x": 7, "rowsalt": 8}
 
     def set_three_pass_shape(self, n1: int = 0, mid: str | int = "default") -> "CirculantPlan":
         """Kernel shape of the 256^3 3-sweep schedule (tests / measurements): the y split n1
@@ -180,7 +180,9 @@ class CirculantPlan:
         'swap64': the y2 DFT on permlane register transposes, 64-column tile; 'swap64pf': the
         same with an LDS-DMA prefetch of half the next unit; 'blocked': 'swap64pf' with the
         blocked intermediate layout, 1 KiB P2 runs; 'blocked32': blocks of 4 x and the permlane
-        P2 on 32 columns, two workgroups per CU; n1 = 32 only).  At 100^3 (cfp_three_pass_sq.hip)
+        P2 on 32 columns, two workgroups per CU; n1 = 32 only; 'swap32x': the permlane P2 on 32
+        natural-layout columns in XCD order; 'rowsalt': the default with P1 / P3's row-FFT
+        exchanges the other way, wave-local or workgroup-wide, n1 = 0 only).  At 100^3 (cfp_three_pass_sq.hip)
         mid picks the middle kernel's x tile: 'default' 4 x, 'lane64' 2 x, 'lane32' 5 x."""
         m = self.TP_MIDS[mid] if isinstance(mid, str) else int(mid)
         check(lib().cfp_plan_set_three_pass_shape(self._h, int(n1), m))
@@ -301,8 +303,8 @@ class RealPlan:
 
     def set_schedule(self, schedule: str | int) -> "RealPlan":
         """'auto' (3 sweeps at 128^3 and 256^3), 'five' (r2c + 3 half-spectrum passes + c2r), 'three'
-        (128^3 and 256^3 only) or 'three_alt' (the 3 sweeps with the alternative row-sweep kernels
-        of DESIGN.md, for A/B; 256^3, else as 'three')."""
+        (128^3 and 256^3 only) or 'three_alt' (the 3 sweeps with the row sweeps' FFT exchanges
+        behind workgroup barriers instead of wave-local, for A/B)."""
         v = self.SCHEDULES[schedule] if isinstance(schedule, str) else int(schedule)
         check(lib().cfp_rplan_set_schedule(self._h, v))
         return self

@@ -39,8 +39,8 @@ int cfp_rplan_apply(cfp_rplan_t plan, const double *b, double *x, void *stream);
 #define CFP_RSCHEDULE_AUTO 0
 #define CFP_RSCHEDULE_FIVE 1
 #define CFP_RSCHEDULE_THREE 2
-/* the 3-sweep schedule with the alternative row-sweep kernels of DESIGN.md (A/B; 256^3 only, else the
- * 3-sweep default) */
+/* the 3-sweep schedule with the row sweeps' FFT exchanges behind workgroup barriers instead of
+ * wave-local (the r04 kernels before r04ab; A/B); 128^3 and 256^3 only */
 #define CFP_RSCHEDULE_THREE_ALT 3
 int cfp_rplan_set_schedule(cfp_rplan_t plan, int schedule);
 /* *three = 1 when the next apply runs the 3-sweep schedule */

@@ -297,7 +297,7 @@ def test_three_pass_512(cp):
         x5 = plan.apply(b)
         assert float((x5 - x).abs().max() / x5.abs().max()) < 1e-13
         del x5
-        for mid in ("lane64", "blocked"):  # P1 / P3 with phase A through LDS; blocks of 2 x in XCD order
+        for mid in ("lane64", "blocked", "rowsalt"):  # phase A through LDS; blocks of 2 x; other row-FFT sync
             plan.set_schedule("three").set_three_pass_shape(0, mid)
             assert float((plan.apply(b) - x).abs().max() / x.abs().max()) < 1e-13
         plan.set_three_pass_shape(0, "default").set_schedule("three")
@@ -444,7 +444,7 @@ def test_three_pass_schedule_rules(cp):
         b = torch.ones_like(d)
         x = plan.apply_with_diag(d, b)  # explicit Diag: the 5-pass fused-Diag path serves it
         assert torch.allclose(x, b / 2.0)
-        for n1, mid in ((16, 0), (32, 9), (32, 8), (64, 5), (-1, 0), (0, -1)):  # only built shapes; nothing from the environment
+        for n1, mid in ((16, 0), (32, 9), (32, 8), (64, 5), (-1, 0), (0, -1), (0, 9)):  # only built shapes; nothing from the environment
             with pytest.raises(cp.CirculantError):
                 plan.set_three_pass_shape(n1, mid)
     with cp.CirculantPlan((64, 64, 64)) as plan:
@@ -455,7 +455,7 @@ def test_three_pass_schedule_rules(cp):
 
 
 @pytest.mark.parametrize("n1,mid", [(0, "default"), (0, "lane64"), (0, "swap64"), (32, "default"), (16, "lane32"),
-                                    (16, "lane64"), (16, "swap64")])
+                                    (16, "lane64"), (16, "swap64"), (0, "rowsalt")])
 @pytest.mark.parametrize("lam", [(0.6, 0.15, 0.02), (0.3 + 0.2j, 1.1, 0.7 - 0.4j)], ids=["bench", "complex"])
 def test_three_pass_128_vs_oracle(cp, oracle, lam, n1, mid):
     """The 3-sweep schedule at 128^3 (N1 = 32 x N2 = 4; AUTO there): the default kernels (8
@@ -561,7 +561,7 @@ def tp_case(oracle):
 @pytest.mark.parametrize("n1,mid", [(64, "lane64"), (64, "lane32"), (32, "lane64"), (32, "lane32"), (0, "default"),
                                     (32, "swap64"), (64, "swap64"), (32, "swap64pf"), (64, "swap64pf"),
                                     (0, "blocked"), (32, "blocked"), (0, "blocked32"), (32, "blocked32"),
-                                    (0, "swap32x"), (32, "swap32x")])
+                                    (0, "swap32x"), (32, "swap32x"), (0, "rowsalt")])
 def test_three_pass_variants(cp, tp_case, n1, mid):
     """Both y splits (64 x 4 with a 4-lane y2 DFT, 32 x 8 with an 8-lane one) and both P2 tile
     widths, selected per plan through cfp_plan_set_three_pass_shape."""

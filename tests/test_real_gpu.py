@@ -68,7 +68,7 @@ def test_real_three_sweep_256_vs_oracle(cp, oracle, lam, side):
         t = torch.from_numpy(b).cuda()
         plan.apply(t, out=t)
         assert torch.equal(t, x)
-        plan.set_schedule("three_alt")  # the alternative row-sweep kernels (wave-local exchanges)
+        plan.set_schedule("three_alt")  # row sweeps with workgroup-barrier exchanges (A/B)
         assert plan.three_sweep
         xa = plan.apply(torch.from_numpy(b).cuda())
         assert float(torch.linalg.vector_norm(xa - x) / torch.linalg.vector_norm(x)) < 1e-13
