@@ -1049,11 +1049,12 @@ hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs
   } else {
     const int units = nzl * 8;  // local z-planes x y2
     const unsigned g = grid_of(units, 2);
+    constexpr int W = kRowsWave ? F_WAVE_LDS : 0;
     if (stage == 0)
-      hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD, 32, 256, 16, true, kRowsLP>), dim3(g), dim3(512), 0, s,
+      hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD | W, 32, 256, 16, true, kRowsLP>), dim3(g), dim3(512), 0, s,
                          in, out, a, units);
     else
-      hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST, 32, 256, 16, true, kRowsLP>), dim3(g), dim3(512), 0, s,
+      hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST | W, 32, 256, 16, true, kRowsLP>), dim3(g), dim3(512), 0, s,
                          in, out, a, units);
   }
   return hipGetLastError();

@@ -88,7 +88,9 @@ k_wtp_rows(const cd* in, cd* out, WTPArgs a, int nunits) {
     }
     {
       const int comp = launder(comp0), tx = launder(tx0), k = launder(k0);
-      fft_stages<WNX, PTS, wr0_of(WNX, PTS), true, NROW, F>(v, lds, a.tw, k * WNC + comp, tx, true);  // v[t]: kx = tx + TR t
+      // a row's TR threads are lanes 32 k + 4 tx + comp of one wave and its LDS row is theirs:
+      // the exchange waits for the wave's own LDS accesses only (F_WAVE_LDS, r04ab)
+      fft_stages<WNX, PTS, wr0_of(WNX, PTS), true, NROW, F | F_WAVE_LDS>(v, lds, a.tw, k * WNC + comp, tx, true);  // v[t]: kx = tx + TR t
     }
     {
       const int comp = launder(comp0), tx = launder(tx0), k = launder(k0);
