@@ -248,17 +248,14 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
 // N2 = 16 (512^3, r04): one more radix-2 lane stage (lane ^ 8, twiddle W_16^(y2 & 7)) in front of
 // the 8-point one.  XCD: units in xcd_unit order (the host launches whole rounds).
 // BL: the blocked layout of k_tp_rows<.., BLK = XT> (one run of T values per z).
-// TS: LDS stride between the exchange rows (T; T + 1 for the one-wave tiles of T = 8, whose eight
-// z-groups would otherwise write to the same banks)
 template <int FLAGS, int T, int N2, int TN, int PTS = 16, bool XS = true, int NX = TN, bool XCD = false,
-          bool BL = false, int TS = T>
+          bool BL = false>
 __global__ void __launch_bounds__(T * (TN / PTS)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid(cd* data, TPArgs a, int nunits) {
   constexpr int N1 = TN / N2, TZ = TN / PTS, NT = T * TZ, XT = T / N2, NXT = NX / XT;
   constexpr int F = FLAGS | (XS ? F_SPLIT_LDS : 0) | F_LDS_SYNC;
   static_assert(N2 == 4 || N2 == 8 || N2 == 16, "the y2 DFT runs across 4, 8 or 16 lanes");
-  static_assert(!(FLAGS & F_WAVE_LDS) || NT == 64, "wave-local exchanges: one wave per workgroup");
-  __shared__ __attribute__((aligned(16))) double lds[TS * TN * (XS ? 1 : 2)];
+  __shared__ __attribute__((aligned(16))) double lds[T * TN * (XS ? 1 : 2)];
   __shared__ cd tw_l[TN];
   const int tid = threadIdx.x;
   for (int i = tid; i < TN; i += NT) tw_l[i] = a.tw[i];
@@ -313,7 +310,7 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
     {
       int c = c0, tz = tz0;
       asm volatile("" : "+v"(c), "+v"(tz));
-      fft_stages<TN, PTS, r0_of(TN, PTS), false, TS, F>(v, lds, tw_l, c, tz, true);  // kz = tz + TZ m
+      fft_stages<TN, PTS, r0_of(TN, PTS), false, T, F>(v, lds, tw_l, c, tz, true);  // kz = tz + TZ m
     }
     {
       int c = c0, tz = tz0;
@@ -325,7 +322,7 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
         const cd d = cadd(cadd(cs, a.axsym[tz + TZ * m]), make_cd(1.0, 0.0));
         v[m] = cconj(cdiv_sym(v[m], d));
       }
-      fft_stages<TN, PTS, r0_of(TN, PTS), false, TS, F>(v, lds, tw_l, c, tz, false);
+      fft_stages<TN, PTS, r0_of(TN, PTS), false, T, F>(v, lds, tw_l, c, tz, false);
     }
     {
       const Col q = column(u);
@@ -1065,7 +1062,6 @@ hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs
 
 bool three_pass_shape_valid(int n1, int mid, i64 n) {
   if (mid == TP_MID_ROWSALT) return n1 == 0;
-  if (mid >= TP_MID_WAVE1 && mid <= TP_MID_WAVE1P) return n == 128 && (n1 == 0 || n1 == 16);
   if (n1 == 16) return n == 128 && mid >= TP_MID_DEFAULT && mid <= TP_MID_SWAP64;
   return (n1 == 0 || n1 == 32 || n1 == 64) && (mid >= 0 && mid <= TP_MID_SWAP32X) &&
          !(mid >= TP_MID_BLOCKED && n1 == 64);
@@ -1119,17 +1115,7 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
       // 8 points, whole-complex (1,024 threads; 21,070-21,150 /s); lane64 = 64 columns, 16
       // points, split (20,530 /s); swap64 = 64 columns, 16 points, whole-complex (20,750 /s)
       if (stage == 1) {
-        constexpr int wunits = 128 * 16;  // one x per unit
-        if (shape.mid == TP_MID_WAVE1)
-          TP_LAUNCH((k_tp_mid<F_WAVE_LDS, 8, 8, 128, 16, false, 128, true, false, 9>), dim3(grid_xcd(wunits, 8)), dim3(64), s, out,
-                    a, wunits);
-        else if (shape.mid == TP_MID_WAVE1S)
-          TP_LAUNCH((k_tp_mid<F_WAVE_LDS, 8, 8, 128, 16, true, 128, true, false, 9>), dim3(grid_xcd(wunits, 8)), dim3(64), s, out,
-                    a, wunits);
-        else if (shape.mid == TP_MID_WAVE1P)
-          TP_LAUNCH((k_tp_mid<F_WAVE_LDS, 8, 8, 128, 16, false, 128, true, false, 9>), dim3(grid_xcd(wunits, 4)), dim3(64), s, out,
-                    a, wunits);
-        else if (shape.mid == TP_MID_LANE32) launch_mid<64, 8, 128, 1, 8, false>(out, a, s);
+        if (shape.mid == TP_MID_LANE32) launch_mid<64, 8, 128, 1, 8, false>(out, a, s);
         else if (shape.mid == TP_MID_LANE64) launch_mid<64, 8, 128, 1>(out, a, s);
         else if (shape.mid == TP_MID_SWAP64) launch_mid<64, 8, 128, 1, 16, false>(out, a, s);
         else {
