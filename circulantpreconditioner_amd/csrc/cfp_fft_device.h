@@ -83,20 +83,6 @@ __device__ __forceinline__ cd cdiv_sym(cd a, cd b) {
 // constants after unrolling, so every branch folds and trivial factors cost nothing.
 template <int R>
 __device__ __forceinline__ cd twr(cd v, int k) {
-  if constexpr (R == 32) {  // even exponents are radix-16 factors; odd ones multiply by a constant
-    if ((k & 1) == 0) return twr<16>(v, (k >> 1) & 15);
-    constexpr double CS[8] = {0.98078528040323044913, 0.83146961230254523708, 0.55557023301960222474,
-                              0.19509032201612826785, -0.19509032201612826785, -0.55557023301960222474,
-                              -0.83146961230254523708, -0.98078528040323044913};  // cos(2 pi j / 32), j odd 1..15
-    const int j = k & 31;
-    // W^j = cos - i sin; sin(2 pi j / 32) = cos(2 pi (8 - j) / 32)
-    const int jj = j < 16 ? j : 32 - j;         // cos is even about 16
-    const double c = j < 16 ? CS[jj >> 1] : CS[jj >> 1];
-    const int sj = (8 - j) & 31, sjj = sj < 16 ? sj : 32 - sj;
-    const double sn = CS[sjj >> 1];
-    const double cc = c;
-    return make_cd(fma(v.x, cc, v.y * sn), fma(v.y, cc, -v.x * sn));
-  }
   const int e = (k * (16 / R)) & 15;  // exponent in units of 2 pi / 16
   const double x = v.x, y = v.y;
   switch (e) {

@@ -248,10 +248,9 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
 // N2 = 16 (512^3, r04): one more radix-2 lane stage (lane ^ 8, twiddle W_16^(y2 & 7)) in front of
 // the 8-point one.  XCD: units in xcd_unit order (the host launches whole rounds).
 // BL: the blocked layout of k_tp_rows<.., BLK = XT> (one run of T values per z).
-// PTS = 32 (512^3 experiment): two waves per SIMD (the 32 points take 128 VGPRs)
 template <int FLAGS, int T, int N2, int TN, int PTS = 16, bool XS = true, int NX = TN, bool XCD = false,
           bool BL = false>
-__global__ void __launch_bounds__(T * (TN / PTS)) __attribute__((amdgpu_waves_per_eu(PTS > 16 ? 2 : 4)))
+__global__ void __launch_bounds__(T * (TN / PTS)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid(cd* data, TPArgs a, int nunits) {
   constexpr int N1 = TN / N2, TZ = TN / PTS, NT = T * TZ, XT = T / N2, NXT = NX / XT;
   constexpr int F = FLAGS | (XS ? F_SPLIT_LDS : 0) | F_LDS_SYNC;
@@ -1063,7 +1062,6 @@ hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs
 
 bool three_pass_shape_valid(int n1, int mid, i64 n) {
   if (mid == TP_MID_ROWSALT) return n1 == 0;
-  if (mid == TP_MID_P32) return n == 512 && n1 == 0;
   if (n1 == 16) return n == 128 && mid >= TP_MID_DEFAULT && mid <= TP_MID_SWAP64;
   return (n1 == 0 || n1 == 32 || n1 == 64) && (mid >= 0 && mid <= TP_MID_SWAP32X) &&
          !(mid >= TP_MID_BLOCKED && n1 == 64);
@@ -1088,8 +1086,6 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
       const unsigned g = grid_xcd(units, 1);  // whole rounds of a power of two >= 8
       if (g == 0) return hipErrorNotSupported;
       if (bl) TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 16, true, 512, true, true>), dim3(g), dim3(1024), s, out, a, units);
-      else if (shape.mid == TP_MID_P32)  // 32 points per thread: one exchange per z FFT, 512 threads
-        TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 32, true, 512, true>), dim3(g), dim3(512), s, out, a, units);
       else TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 16, true, 512, true>), dim3(g), dim3(1024), s, out, a, units);  // NT loads: 204 against 262 /s (r04y)
     } else if (bl) {
       launch_rows<32, 512, 1, 16, true, kRowsLP, 2, true>(stage, in, out, a, s);
