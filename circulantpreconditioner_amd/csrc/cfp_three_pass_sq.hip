@@ -93,14 +93,10 @@ __global__ void __launch_bounds__(N) k_sq_rows(const cd* in, cd* out, const cd* 
 
 // S2.  XT N threads: y2 mode thread (xl = tid % XT, z = tid / XT); column mode (column
 // c = tid % T = xl + XT k2, tz = tid / T, points z = tz + TPC m).
-// UPW units per workgroup (r04ah): with 2 the second unit's loads are issued before the first
-// unit's transforms (register prefetch), so its memory latency hides behind them; the two units
-// are consecutive x tiles.
-template <int N, int XT, int UPW = 1>
+template <int N, int XT>
 __global__ void __launch_bounds__(XT * N) k_sq_mid(cd* data, TPArgs a) {
   constexpr int R = SqCfg<N>::R, TPC = N / R, T = XT * R, NXT = N / XT;
   static_assert(N % XT == 0, "whole x tiles");
-  static_assert(UPW == 1 || UPW == 2, "one or two units per workgroup");
   constexpr int F = 0;
   // y2 mode <-> column mode transposes: rows of T + 1 (with T = 40 the 16 z of a wave's lanes
   // otherwise fall on 2 bank groups); the z FFT's own exchange uses fft_stages' T-wide rows
@@ -112,76 +108,58 @@ __global__ void __launch_bounds__(XT * N) k_sq_mid(cd* data, TPArgs a) {
   // contiguous range of units, so the x tiles that share 128-byte lines (a 1,600-byte row holds
   // 6.25 tiles of 64 bytes) meet in one L2; in blockIdx order the unit moved 1.50 x 32 N bytes
   // of HBM traffic (profiles/r04_pmc_small.txt)
-  constexpr int NU = NXT * R / UPW, PER = NU / 8, EXTRA = NU % 8;
-  static_assert((NXT * R) % UPW == 0, "whole unit groups");
+  constexpr int NU = NXT * R, PER = NU / 8, EXTRA = NU % 8;
   const int b = blockIdx.x, j = b & 7, i = b >> 3;
-  const int g = j * PER + (j < EXTRA ? j : EXTRA) + i;  // unit group: units UPW g .. UPW g + UPW - 1
+  const int u = j * PER + (j < EXTRA ? j : EXTRA) + i;
+  const int xt = u % NXT, k1 = u / NXT;
   for (int i2 = tid; i2 < N; i2 += XT * N) tws[i2] = a.tw[i2];
   const int xl = tid % XT, z = tid / XT;
   const int c = tid % T, tz = tid / T;
-  const auto col_of = [&](int u) {  // row y2 + R k1 at y2 = 0 of this thread's column
-    const int xt = u % NXT, k1 = u / NXT;
-    return data + (i64)z * N * N + (i64)R * k1 * N + xt * XT + xl;
-  };
-  cd v[R], w[R];
+  cd* col = data + (i64)z * N * N + (i64)R * k1 * N + xt * XT + xl;  // row y2 + R k1 at y2 = 0
+  cd v[R];
 #pragma unroll
-  for (int m = 0; m < R; ++m) v[m] = col_of(UPW * g)[(i64)N * m];
-  if constexpr (UPW == 2) {
-#pragma unroll
-    for (int m = 0; m < R; ++m) w[m] = col_of(UPW * g + 1)[(i64)N * m];
-  }
+  for (int m = 0; m < R; ++m) v[m] = col[(i64)N * m];
   __syncthreads();  // tws
 #pragma unroll
-  for (int h = 0; h < UPW; ++h) {
-    const int u = UPW * g + h;
-    const int xt = u % NXT, k1 = u / NXT;
-    cd* const col = col_of(u);
-    if (h) {
+  for (int m = 1; m < R; ++m) v[m] = cmul(v[m], tws[(m * k1) % N]);  // W_n^{y2 k1}
+  dft_any<R>(v);  // v[k2]
+  // y2 mode -> column mode: element (column xl + XT k2, z) at z (T + 1) + column
 #pragma unroll
-      for (int m = 0; m < R; ++m) v[m] = w[m];
-      __syncthreads();  // the first unit's last LDS reads are done
+  for (int m = 0; m < R; ++m) lds[z * TP + xl + XT * m] = v[m];
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < R; ++m) v[m] = lds[(tz + TPC * m) * TP + c];
+  fft_stages<N, R, R, false, T, F>(v, lds, tws, c, tz, false);  // v[t]: kz = tz + TPC t
+  {
+    const int kx = xt * XT + c % XT, ky = k1 + R * (c / XT);
+    const cd cs = a.colsym[kx + (i64)N * ky];
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+      const cd d = cadd(cadd(cs, a.axsym[tz + TPC * t]), make_cd(1.0, 0.0));
+      v[t] = cconj(cdiv_sym(v[t], d));
     }
+  }
+  fft_stages<N, R, R, false, T, F>(v, lds, tws, c, tz, false);  // v[t]: z = tz + TPC t (conjugate domain)
+  __syncthreads();
 #pragma unroll
-    for (int m = 1; m < R; ++m) v[m] = cmul(v[m], tws[(m * k1) % N]);  // W_n^{y2 k1}
-    dft_any<R>(v);  // v[k2]
-    // y2 mode -> column mode: element (column xl + XT k2, z) at z (T + 1) + column
+  for (int t = 0; t < R; ++t) lds[(tz + TPC * t) * TP + c] = v[t];
+  __syncthreads();
 #pragma unroll
-    for (int m = 0; m < R; ++m) lds[z * TP + xl + XT * m] = v[m];
-    __syncthreads();
+  for (int m = 0; m < R; ++m) v[m] = lds[z * TP + xl + XT * m];
+  dft_any<R>(v);  // v[y2]
 #pragma unroll
-    for (int m = 0; m < R; ++m) v[m] = lds[(tz + TPC * m) * TP + c];
-    fft_stages<N, R, R, false, T, F>(v, lds, tws, c, tz, false);  // v[t]: kz = tz + TPC t
-    {
-      const int kx = xt * XT + c % XT, ky = k1 + R * (c / XT);
-      const cd cs = a.colsym[kx + (i64)N * ky];
-#pragma unroll
-      for (int t = 0; t < R; ++t) {
-        const cd d = cadd(cadd(cs, a.axsym[tz + TPC * t]), make_cd(1.0, 0.0));
-        v[t] = cconj(cdiv_sym(v[t], d));
-      }
-    }
-    fft_stages<N, R, R, false, T, F>(v, lds, tws, c, tz, false);  // v[t]: z = tz + TPC t (conjugate domain)
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < R; ++t) lds[(tz + TPC * t) * TP + c] = v[t];
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < R; ++m) v[m] = lds[z * TP + xl + XT * m];
-    dft_any<R>(v);  // v[y2]
-#pragma unroll
-    for (int m = 0; m < R; ++m) {
-      const cd wv = m ? cmul(v[m], tws[(m * k1) % N]) : v[m];
-      col[(i64)N * m] = cconj(wv);
-    }
+  for (int m = 0; m < R; ++m) {
+    const cd w = m ? cmul(v[m], tws[(m * k1) % N]) : v[m];
+    col[(i64)N * m] = cconj(w);
   }
 }
 
 bool three_pass_sq_supported(const i64 n[3]) { return n[0] == n[1] && n[1] == n[2] && n[0] == 100; }
 
-template <int N, int XT, int UPW = 1>
+template <int N, int XT>
 static void launch_sq_mid(cd* data, const TPArgs& a, hipStream_t s) {
   constexpr int R = SqCfg<N>::R;
-  hipLaunchKernelGGL((k_sq_mid<N, XT, UPW>), dim3((N / XT) * R / UPW), dim3(XT * N), 0, s, data, a);
+  hipLaunchKernelGGL((k_sq_mid<N, XT>), dim3((N / XT) * R), dim3(XT * N), 0, s, data, a);
 }
 
 hipError_t launch_three_pass_sq(int stage, int n, const cd* in, cd* out, const TPArgs& a, TPShape shape,
@@ -191,12 +169,8 @@ hipError_t launch_three_pass_sq(int stage, int n, const cd* in, cd* out, const T
   if (stage == 1) {
     // shape.mid picks the S2 x tile: default 4 x (250 units, 64-byte runs), LANE64 2 x (500
     // units), LANE32 5 x (200 units)
-    // A/B (r04ah): SWAP64 = 2 x tiles, two per workgroup with the second one's loads in flight
-    // during the first one's transforms; SWAP64_PF = the same with 1 x tiles
     if (shape.mid == TP_MID_LANE64) launch_sq_mid<N, 2>(out, a, s);
     else if (shape.mid == TP_MID_LANE32) launch_sq_mid<N, 5>(out, a, s);
-    else if (shape.mid == TP_MID_SWAP64) launch_sq_mid<N, 2, 2>(out, a, s);
-    else if (shape.mid == TP_MID_SWAP64_PF) launch_sq_mid<N, 1, 2>(out, a, s);
     else launch_sq_mid<N, 4>(out, a, s);
   } else if (stage == 0) {
     hipLaunchKernelGGL((k_sq_rows<N, false>), dim3(N * R), dim3(N), 0, s, in, out, a.tw, 1.0);
