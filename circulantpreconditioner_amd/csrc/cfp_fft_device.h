@@ -570,10 +570,6 @@ k_axis_fast(const cd* in, cd* out, KArgs a) {
   constexpr int LDS_N = ROW ? T * (N + N / 16) : T * N;
   constexpr bool NEED_LDS = SH::S > 1;
   constexpr bool TW_LDS = NEED_LDS && !(FLAGS & F_TW_GLOBAL);
-  // row mode with whole rows per wave (64 % TPC == 0): a row's exchange region is its own, so
-  // the FFT's exchanges wait for the wave's own LDS accesses only (F_WAVE_LDS, r04ai)
-  constexpr bool WL = ROW && NEED_LDS && (64 % TPC == 0);
-  constexpr int FX = FLAGS | (WL ? F_WAVE_LDS : 0);
   __shared__ __attribute__((aligned(16))) double lds_raw[NEED_LDS ? ((FLAGS & F_SPLIT_LDS) ? LDS_N : 2 * LDS_N) : 2];
   __shared__ cd tws_lds[TW_LDS ? N : 1];
   constexpr bool SYM_LDS = NEED_LDS && MODE == PASS_FUSED_SEP && (FLAGS & F_SYM_LDS);
@@ -633,10 +629,8 @@ k_axis_fast(const cd* in, cd* out, KArgs a) {
       for (int m = 0; m < PTS; ++m) v[m] = cmul(v[m], tw4_at(a.tw4, k1 * (tpc + m * TPC)));
     }
   }
-  // the twiddle table copy is published by the first exchange's barrier (wave-local exchanges:
-  // by a barrier of its own)
-  if constexpr (WL && (TW_LDS || SYM_LDS)) lds_barrier();
-  fft_stages<N, PTS, R0, ROW, T, FX>(v, lds_raw, tws, c, tpc, true);
+  // the twiddle table copy is published by the first exchange's barrier
+  fft_stages<N, PTS, R0, ROW, T, FLAGS>(v, lds_raw, tws, c, tpc, true);
 
   if constexpr (MODE == PASS_FUSED_WAVE) {
     // the 4 components of a cell are columns 4j..4j+3: lanes of one quad (T % 4 == 0)
@@ -658,7 +652,7 @@ k_axis_fast(const cd* in, cd* out, KArgs a) {
       r[3] = make_cd(quad_bcast<3>(v[m].x), quad_bcast<3>(v[m].y));
       v[m] = cconj(wave_point(r, comp, f, wc, pk, c0sq));
     }
-    fft_stages<N, PTS, R0, ROW, T, FX>(v, lds_raw, tws, c, tpc, false);
+    fft_stages<N, PTS, R0, ROW, T, FLAGS>(v, lds_raw, tws, c, tpc, false);
   }
   if (MODE == PASS_FUSED_SEP || MODE == PASS_FUSED_DIAG) {
     const cd cs = cs_early;
@@ -674,7 +668,7 @@ k_axis_fast(const cd* in, cd* out, KArgs a) {
         v[m] = cconj(cdiv(v[m], d));
       }
     }
-    fft_stages<N, PTS, R0, ROW, T, FX>(v, lds_raw, tws, c, tpc, false);
+    fft_stages<N, PTS, R0, ROW, T, FLAGS>(v, lds_raw, tws, c, tpc, false);
   }
   if constexpr (MODE == PASS_FWD) {
     if (a.tw4.lo) {  // uniform: a long axis' first half, post-twiddle W_n^{k1 m2}
