@@ -27,7 +27,11 @@ def main() -> int:
     ap.add_argument("--iters", type=int, default=2000)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--lam", type=float, nargs=3, default=[0.6, 0.15, 0.02])
+    ap.add_argument("--lib", default=None, help="another build of libcirculant_fft.so (A/B of two builds)")
     args = ap.parse_args()
+    if args.lib:
+        import circulantpreconditioner_amd._lib as L
+        L.LIB_PATH = os.path.abspath(args.lib)
     n = (args.grid,) * 3
     N = args.grid ** 3
     g = torch.Generator(device="cpu").manual_seed(20251017)
@@ -76,7 +80,7 @@ def main() -> int:
             e1.synchronize()
             res[v]["rates"].append(round(args.iters / (e0.elapsed_time(e1) * 1e-3), 1))
     for v in args.variants:
-        print(json.dumps({"grid": args.grid, "variant": v, **res[v]}), flush=True)
+        print(json.dumps({"grid": args.grid, "variant": v, "lib": args.lib or "in-tree", **res[v]}), flush=True)
     for p in plans:
         p.close()
     return 0
