@@ -1062,7 +1062,6 @@ hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs
 
 bool three_pass_shape_valid(int n1, int mid, i64 n) {
   if (mid == TP_MID_ROWSALT) return n1 == 0;
-  if (mid == TP_MID_T16S || mid == TP_MID_T16W) return n == 128 && (n1 == 0 || n1 == 16);
   if (n1 == 16) return n == 128 && mid >= TP_MID_DEFAULT && mid <= TP_MID_SWAP64;
   return (n1 == 0 || n1 == 32 || n1 == 64) && (mid >= 0 && mid <= TP_MID_SWAP32X) &&
          !(mid >= TP_MID_BLOCKED && n1 == 64);
@@ -1116,14 +1115,7 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
       // 8 points, whole-complex (1,024 threads; 21,070-21,150 /s); lane64 = 64 columns, 16
       // points, split (20,530 /s); swap64 = 64 columns, 16 points, whole-complex (20,750 /s)
       if (stage == 1) {
-        constexpr int units16 = (128 / 4) * 16;
-        if (shape.mid == TP_MID_T16S)
-          TP_LAUNCH((k_tp_mid<0, 32, 8, 128, 16, true, 128, true>), dim3(grid_xcd(units16, 4)), dim3(256), s, out, a,
-                    units16);
-        else if (shape.mid == TP_MID_T16W)
-          TP_LAUNCH((k_tp_mid<0, 32, 8, 128, 16, false, 128, true>), dim3(grid_xcd(units16, 2)), dim3(256), s, out, a,
-                    units16);
-        else if (shape.mid == TP_MID_LANE32) launch_mid<64, 8, 128, 1, 8, false>(out, a, s);
+        if (shape.mid == TP_MID_LANE32) launch_mid<64, 8, 128, 1, 8, false>(out, a, s);
         else if (shape.mid == TP_MID_LANE64) launch_mid<64, 8, 128, 1>(out, a, s);
         else if (shape.mid == TP_MID_SWAP64) launch_mid<64, 8, 128, 1, 16, false>(out, a, s);
         else {

@@ -455,7 +455,7 @@ def test_three_pass_schedule_rules(cp):
 
 
 @pytest.mark.parametrize("n1,mid", [(0, "default"), (0, "lane64"), (0, "swap64"), (32, "default"), (16, "lane32"),
-                                    (16, "lane64"), (16, "swap64"), (0, "rowsalt"), (0, "t16s"), (16, "t16w")])
+                                    (16, "lane64"), (16, "swap64"), (0, "rowsalt")])
 @pytest.mark.parametrize("lam", [(0.6, 0.15, 0.02), (0.3 + 0.2j, 1.1, 0.7 - 0.4j)], ids=["bench", "complex"])
 def test_three_pass_128_vs_oracle(cp, oracle, lam, n1, mid):
     """The 3-sweep schedule at 128^3 (N1 = 32 x N2 = 4; AUTO there): the default kernels (8
