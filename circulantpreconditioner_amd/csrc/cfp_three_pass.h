@@ -26,8 +26,7 @@ struct TPArgs {
 // ROWSALT: the default shape (n1 = 0 only; 128^3, 256^3, 512^3) with P1 / P3's row-FFT exchanges
 // the other way (workgroup barriers instead of wave-local, or the reverse: kRowsWave), for A/B
 enum { TP_MID_DEFAULT = 0, TP_MID_LANE64 = 1, TP_MID_LANE32 = 2, TP_MID_SWAP64 = 3, TP_MID_SWAP64_PF = 4,
-       TP_MID_BLOCKED = 5, TP_MID_BLOCKED32 = 6, TP_MID_SWAP32X = 7, TP_MID_ROWSALT = 8,
-       TP_MID_XCD = 9 /* 256^3 A/B: the default P2 with its units in XCD order */ };
+       TP_MID_BLOCKED = 5, TP_MID_BLOCKED32 = 6, TP_MID_SWAP32X = 7, TP_MID_ROWSALT = 8 };
 struct TPShape {
   int n1 = 0;   // y split ny = n1 * n2: 0 (default 32), 32 or 64
   int mid = 0;  // TP_MID_* (DEFAULT = SWAP64_PF at 256^3)

@@ -1062,7 +1062,6 @@ hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs
 
 bool three_pass_shape_valid(int n1, int mid, i64 n) {
   if (mid == TP_MID_ROWSALT) return n1 == 0;
-  if (mid == TP_MID_XCD) return n == 256 && (n1 == 0 || n1 == 32);
   if (n1 == 16) return n == 128 && mid >= TP_MID_DEFAULT && mid <= TP_MID_SWAP64;
   return (n1 == 0 || n1 == 32 || n1 == 64) && (mid >= 0 && mid <= TP_MID_SWAP32X) &&
          !(mid >= TP_MID_BLOCKED && n1 == 64);
@@ -1156,22 +1155,6 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
     if (stage != 1) launch_rows<32, 256, 2, 16, true, kRowsLP, 8>(stage, in, out, a, s);
     else if (pf_ok) launch_mid_sw<8, 256, true, true>(out, a, s);
     else launch_mid_sw<8, 256, false, true>(out, a, s);
-    return hipGetLastError();
-  }
-  if (shape.mid == TP_MID_XCD) {  // A/B: the default with P2's units in XCD order
-    if (stage != 1) {
-      launch_rows<32, 256, 2, 16, true, kRowsLP>(stage, in, out, a, s);
-    } else {
-      constexpr int units = 32 * 32;
-      const unsigned g = grid_xcd(units, 1);
-      if (g == 0) return hipErrorNotSupported;
-      if (pf_ok)
-        TP_LAUNCH((k_tp_mid_sw<64, 8, 256, 0, true, 256, 0, kP2LoadFlags, false, true>), dim3(g), dim3(1024), s, out, a,
-                  units);
-      else
-        TP_LAUNCH((k_tp_mid_sw<64, 8, 256, 0, false, 256, 0, kP2LoadFlags, false, true>), dim3(g), dim3(1024), s, out, a,
-                  units);
-    }
     return hipGetLastError();
   }
   if (shape.mid == TP_MID_SWAP32X) {  // natural layout; P2 = 32 columns in XCD order, two per CU

@@ -172,7 +172,7 @@ class CirculantPlan:
         return self
 
     TP_MIDS = {"default": 0, "lane64": 1, "lane32": 2, "swap64": 3, "swap64pf": 4, "blocked": 5, "blocked32": 6,
-               "swap32x": 7, "rowsalt": 8, "xcd": 9}
+               "swap32x": 7, "rowsalt": 8}
 
     def set_three_pass_shape(self, n1: int = 0, mid: str | int = "default") -> "CirculantPlan":
         """Kernel shape of the 256^3 3-sweep schedule (tests / measurements): the y split n1

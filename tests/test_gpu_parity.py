@@ -561,7 +561,7 @@ def tp_case(oracle):
 @pytest.mark.parametrize("n1,mid", [(64, "lane64"), (64, "lane32"), (32, "lane64"), (32, "lane32"), (0, "default"),
                                     (32, "swap64"), (64, "swap64"), (32, "swap64pf"), (64, "swap64pf"),
                                     (0, "blocked"), (32, "blocked"), (0, "blocked32"), (32, "blocked32"),
-                                    (0, "swap32x"), (32, "swap32x"), (0, "rowsalt"), (0, "xcd")])
+                                    (0, "swap32x"), (32, "swap32x"), (0, "rowsalt")])
 def test_three_pass_variants(cp, tp_case, n1, mid):
     """Both y splits (64 x 4 with a 4-lane y2 DFT, 32 x 8 with an 8-lane one) and both P2 tile
     widths, selected per plan through cfp_plan_set_three_pass_shape."""
