@@ -78,6 +78,109 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# Per-phase deadlines (seconds).  "timed" and "scaling_512" grow with the step count.
+DEADLINES = {"import": 900.0, "init": 300.0, "plan": 360.0, "first_apply": 120.0, "settle": 120.0,
+             "timed": 120.0, "check": 120.0, "real": 180.0, "configs": 300.0, "scaling_512": 420.0,
+             "cpu_baseline": 300.0, "report": 60.0, "teardown": 120.0}
+
+
+class Watchdog:
+    """Deadline on each phase of the run, so that a hang -- a rank that never joins the RCCL
+    communicator, a collective with a missing peer, a kernel that never drains -- ends the
+    process with evidence instead of being killed silently at the driver's limit.
+
+    phase(name) re-arms one timer with that phase's deadline.  On expiry the timer thread dumps
+    every thread's Python stack (faulthandler) to stderr, prints one JSON line naming the phase
+    ({"status": "timeout", ...}: rank 0 on stdout, the other ranks on stderr) and ends the
+    process with os._exit(3), skipping any teardown that could block on the hung work."""
+
+    def __init__(self, deadlines: dict, rank: int = 0, world: int = 1, metric: str = ""):
+        import threading
+        self.deadlines = dict(deadlines)
+        self.rank, self.world, self.metric = rank, world, metric
+        self.name = None
+        self.t_phase = time.monotonic()
+        self._lock = threading.Lock()
+        self._timer = None
+        self.history = []
+
+    def phase(self, name: str, seconds: float | None = None) -> None:
+        import threading
+        with self._lock:
+            if self._timer is not None:
+                self._timer.cancel()
+            now = time.monotonic()
+            if self.name is not None:
+                self.history.append((self.name, round(now - self.t_phase, 3)))
+            self.name, self.t_phase = name, now
+            limit = float(seconds if seconds is not None else self.deadlines.get(name, 300.0))
+            self._timer = threading.Timer(limit, self._expire, args=(name, limit))
+            self._timer.daemon = True
+            self._timer.start()
+
+    def stop(self) -> None:
+        with self._lock:
+            if self._timer is not None:
+                self._timer.cancel()
+                self._timer = None
+
+    def _expire(self, name: str, limit: float) -> None:
+        import faulthandler
+        try:
+            log(f"bench watchdog: rank {self.rank} phase '{name}' exceeded {limit:.0f} s; stacks follow")
+            faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+            line = json.dumps({"metric": self.metric, "value": None, "status": "timeout", "phase": name,
+                               "deadline_s": limit, "rank": self.rank, "n_gpus": self.world,
+                               "phases_done": self.history})
+            print(line, file=sys.stdout if self.rank == 0 else sys.stderr, flush=True)
+        finally:
+            os._exit(3)
+
+
+def parse_deadlines(items) -> dict:
+    """--deadline PHASE=SECONDS (repeatable) over DEADLINES."""
+    out = dict(DEADLINES)
+    for it in items or []:
+        k, _, v = it.partition("=")
+        if k not in DEADLINES or not v:
+            raise SystemExit(f"--deadline takes PHASE=SECONDS with PHASE in {sorted(DEADLINES)}")
+        out[k] = float(v)
+    return out
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(nproc: int, argv, deadlines: dict) -> int:
+    """--gpus N > 1 without a launcher: start N ranks under torch.distributed.run as a child
+    process group (this process has made no GPU call and makes none) and return their exit
+    status.  The ranks inherit stdout, so rank 0's JSON line is this run's line.  The whole group
+    is killed if it outlives the sum of the phase deadlines (its own watchdogs fire first)."""
+    import signal
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env["CFP_BENCH_SELF_LAUNCHED"] = "1"
+    log(f"bench: --gpus {nproc} without a launcher: starting {nproc} ranks under torch.distributed.run")
+    proc = subprocess.Popen(cmd, env=env, start_new_session=True)
+    limit = sum(deadlines.values()) + 60.0
+    try:
+        return proc.wait(timeout=limit)
+    except subprocess.TimeoutExpired:
+        os.killpg(proc.pid, signal.SIGKILL)
+        proc.wait()
+        print(json.dumps({"metric": "PCApply/s", "value": None, "status": "timeout", "phase": "launcher",
+                          "deadline_s": limit, "rank": -1, "n_gpus": nproc}), flush=True)
+        return 3
+
+
 def kernel_alg_bytes(mode: str, N: int, n_axis: int) -> int:
     """Algorithmic HBM bytes of one axis-pass launch (SURVEY.md §8d per-unit figure x units)."""
     b = 32 * N  # read N c128 + write N c128
@@ -332,19 +435,45 @@ def main() -> int:
                     help="record per-launch events in every n-th timed apply")
     ap.add_argument("--no-live-events", action="store_true",
                     help="time the passes in separate applies instead of inside the timed region")
+    ap.add_argument("--deadline", action="append", default=[], metavar="PHASE=SECONDS",
+                    help=f"override a phase deadline of the watchdog (phases: {', '.join(DEADLINES)})")
+    ap.add_argument("--selftest-cpu", action="store_true",
+                    help="CPU rehearsal of the launch / rendezvous / phase / report control flow with a host "
+                         "stand-in step and a gloo group: no GPU call, no measurement (value null)")
+    ap.add_argument("--selftest-stall", default=None, metavar="PHASE",
+                    help="--selftest-cpu: block forever in PHASE (exercises the watchdog)")
+    ap.add_argument("--selftest-stall-rank", type=int, default=-1, help="rank that stalls (-1 = all)")
     args = ap.parse_args()
     grid = args.grid * 3 if len(args.grid) == 1 else args.grid
     if len(grid) != 3:
         raise SystemExit("--grid takes 1 or 3 integers")
+    deadlines = parse_deadlines(args.deadline)
+
+    # N > 1 without a launcher: start the N ranks before anything touches the GPU; a run never
+    # silently measures a different GPU count than --gpus asks for
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        return self_launch(args.gpus, sys.argv[1:], deadlines)
+    world = int(world_env or "1")
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to measure a different GPU count")
+        return 2
+    launcher = ("none" if world == 1 else
+                "self (torch.distributed.run)" if os.environ.get("CFP_BENCH_SELF_LAUNCHED") else "external")
+    metric_name = ("PCApply/s on 256^3 complex grid" if grid == [256, 256, 256] else
+                   f"PCApply/s on {grid[0]}x{grid[1]}x{grid[2]} complex grid")
+    wd = Watchdog(deadlines, rank, world, metric_name)
+    wd.phase("import")
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if args.selftest_cpu:
+        return selftest_cpu(args, wd, rank, world, launcher, metric_name)
+
+    wd.phase("init")
     if os.environ.get("CFP_BENCH_SHARE_DEVICE"):  # rehearsal of N > 1 on a one-GPU box
         local_rank = local_rank % torch.cuda.device_count()
     torch.cuda.set_device(local_rank)
@@ -357,6 +486,7 @@ def main() -> int:
             dist.init_process_group(backend)
 
     import circulantpreconditioner_amd as cp
+    from circulantpreconditioner_amd.distributed import rccl_version
 
     nx, ny, nz = grid
     N = nx * ny * nz
@@ -391,8 +521,11 @@ def main() -> int:
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
             return int(t.item()) == 1
 
+        # the library's RCCL communicator gives up well inside the watchdog's "plan" deadline,
+        # so a rank that never joins becomes a labelled fallback (or a loud failure) first
         plan, exchange = choose_slab_plan(
-            lambda ex: SlabPlan(g, rank=rank, world=world, device=local_rank, exchange=ex),
+            lambda ex: SlabPlan(g, rank=rank, world=world, device=local_rank, exchange=ex,
+                                timeout_s=0.4 * deadlines["plan"]),
             os.environ.get("CFP_EXCHANGE"), agree, warn=lambda m: log(f"rank {rank}: {m}"))
         exchange_used[0] = exchange
         plan.set_transport_symbol(LAM)
@@ -450,10 +583,24 @@ def main() -> int:
             elapsed = float(t.item())
         return elapsed
 
+    wd.phase("plan")
     plan, b, x, run, parallelism = make(grid)
+    rccl = {"ranks": None, **rccl_version()}
+    if world > 1 and plan.exchange == "rccl":
+        # what RCCL saw: every rank's communicator size and creation time, agreed over the ranks
+        rccl = plan.rccl_info()
+        t = torch.tensor([rccl["ranks"], -rccl["ranks"], rccl["init_ms"]], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        rccl.update({"ranks_max_over_ranks": int(t[0].item()), "ranks_min_over_ranks": int(-t[1].item()),
+                     "init_ms_max_over_ranks": round(float(t[2].item()), 1)})
+    wd.phase("first_apply")
     for _ in range(args.warmup):
         run()
+    torch.cuda.synchronize()
+    wd.phase("settle")
     settle_n, settle_ms = settle(run, args.settle_ms)
+    wd.phase("timed", deadlines["timed"] + 0.05 * args.steps)
     timed_region_ms = None
     live_applies = 0
     every = max(1, args.event_every)
@@ -475,6 +622,7 @@ def main() -> int:
     ms_per_step = elapsed / args.steps * 1e3
     value = args.steps / elapsed  # whole-job PCApply/s (one grid per step)
     torch.cuda.synchronize()
+    wd.phase("check")
     res = residual(b, x, grid)
     check = {"residual": res, "tol": RES_TOL, "ok": res < RES_TOL,
              "what": "||C x - b|| / ||b|| of the last timed apply (transport circulant C, on the GPU)"}
@@ -565,6 +713,7 @@ def main() -> int:
     # row f4: the real-data variant on the same grid (real b, the same real lambda), reported
     # beside the headline; the headline stays the complex apply
     real_variant = None
+    wd.phase("real")
     if world == 1 and not args.no_real:
         try:
             rp = cp.RealPlan(grid, device=local_rank).set_transport_symbol([float(v) for v in LAM])
@@ -589,6 +738,7 @@ def main() -> int:
     # (128^3 complex apply), config 4's block preconditioner (wave system 128^3) and the
     # reference's default mesh (100^3); each with its own output check
     other_configs = None
+    wd.phase("configs")
     if world == 1 and not args.no_configs:
         other_configs = {}
         for key, g3 in (("config2_128", [128, 128, 128]), ("reference_mesh_100", [100, 100, 100])):
@@ -639,6 +789,7 @@ def main() -> int:
     sg = [int(v) for v in args.scaling_grid]
     sg = sg * 3 if len(sg) == 1 else sg
     if len(sg) == 3 and min(sg) > 0 and sg != grid:
+        wd.phase("scaling_512", deadlines["scaling_512"] + 0.2 * args.scaling_steps)
         if world > 1:
             plan.close()  # one library RCCL communicator at a time
             dist.barrier()
@@ -677,16 +828,17 @@ def main() -> int:
             plan = None
 
     cpu = None
+    wd.phase("cpu_baseline")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             cpu = cpu_baseline(grid, args.cpu_budget)
         except Exception as e:  # report, never fake
             log(f"cpu baseline failed: {e}")
 
+    wd.phase("report")
     if rank == 0:
         out = {
-            "metric": "PCApply/s on 256^3 complex grid" if grid == [256, 256, 256] else
-                      f"PCApply/s on {nx}x{ny}x{nz} complex grid",
+            "metric": metric_name,
             "value": round(value, 3),
             "unit": "PCApply/s",
             "n_gpus": world,
@@ -700,7 +852,10 @@ def main() -> int:
             "data": f"synthetic: SplitMix64 U[-1,1) complex b, seed {SEED}, generated in HBM",
             "config": {"workload": f"{nx}x{ny}x{nz} c128 circulant PCApply, transport symbol lambda={LAM}",
                        "grid": grid, "global_batch": 1, "parallelism": parallelism},
+            "status": "ok",
+            "launcher": launcher,
             "exchange": exchange_used[0],
+            "rccl": rccl,
             "settle": {"ms": round(settle_ms, 1), "applies": settle_n,
                        "note": "untimed applies after the W warm-up steps, before the timed region"},
             "check": check,
@@ -716,7 +871,9 @@ def main() -> int:
             out["scaling_512"] = scaling
         if passes_info is not None:
             out["passes"] = passes_info
+        out["phases_s"] = wd.history
         print(json.dumps(out), flush=True)
+    wd.phase("teardown")
     if world > 1:
         # tear down the library's RCCL communicator on every rank together, before torch's
         torch.cuda.synchronize()
@@ -725,9 +882,73 @@ def main() -> int:
             plan.close()
         dist.barrier()
         dist.destroy_process_group()
+    wd.stop()
     if not check["ok"]:
         log(f"bench: output check FAILED: {check}")
         return 3
+    return 0
+
+
+def selftest_cpu(args, wd, rank: int, world: int, launcher: str, metric: str) -> int:
+    """CPU rehearsal of bench.py's control flow: launch (self-launched or external), a gloo
+    rendezvous, the phases under the watchdog, barriers around the K steps, the max over ranks
+    and one JSON line with n_gpus = WORLD_SIZE.  The step is a host stand-in (a 16^3 numpy FFT
+    round trip plus one all_reduce); no GPU call is made and nothing is measured ("value" null,
+    "status" "selftest").  --selftest-stall PHASE blocks forever in PHASE to exercise the watchdog."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    def stall(name):
+        if args.selftest_stall == name and args.selftest_stall_rank in (-1, rank):
+            log(f"selftest: rank {rank} stalls in phase '{name}'")
+            while True:
+                time.sleep(3600)
+
+    wd.phase("init")
+    stall("init")
+    if world > 1:
+        dist.init_process_group("gloo")
+    wd.phase("plan")
+    stall("plan")
+    a = np.random.default_rng(rank).standard_normal((16, 16, 16)) + 0j
+    tok = torch.zeros(1, dtype=torch.float64)
+
+    def run():
+        np.fft.ifftn(np.fft.fftn(a))
+        if world > 1:
+            dist.all_reduce(tok)
+    wd.phase("first_apply")
+    stall("first_apply")
+    for _ in range(args.warmup):
+        run()
+    wd.phase("timed", wd.deadlines["timed"] + 0.05 * args.steps)
+    stall("timed")
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    wd.phase("report")
+    stall("report")
+    if rank == 0:
+        print(json.dumps({"metric": metric, "value": None, "unit": "PCApply/s", "status": "selftest",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(float(el.item()) / max(1, args.steps) * 1e3, 5),
+                          "launcher": launcher, "phases_s": wd.history,
+                          "note": "CPU rehearsal of bench.py's launch and control flow: host stand-in step, "
+                                  "no GPU work, no measurement"}), flush=True)
+    wd.phase("teardown")
+    stall("teardown")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    wd.stop()
     return 0
 
 

@@ -32,6 +32,7 @@
 #include "../../include/circulant_fft_dist.h"
 #include "cfp_host.h"
 #include "cfp_internal.h"
+#include "cfp_rccl.h"
 #include "cfp_three_pass.h"
 
 using namespace cfp;
@@ -126,10 +127,12 @@ struct Step {
 // exchanges; otherwise 5 axis passes.  AUTO takes 3 sweeps for P <= 4 only: measured per rank
 // (tools/slab_local_timing.py, profiles/r02i_slab_local.txt) 174 vs 219 us at P = 2 and 90 vs
 // 119 us at P = 4, a tie at P = 8 (P2 has 128 units for 256 CUs) and a loss at P = 16.
+// 512^3 (r05): 3 sweeps on every supported P (96 N / P local bytes against
+// 160 N / P; P2 keeps 1,024 units for 256 CUs at P = 8).
 bool slab_three(const SlabLayout& L, int schedule) {
   const i64 n[3] = {L.nx, L.ny, L.nz};
   if (schedule == CFP_SCHEDULE_FIVE_PASS || !three_pass_slab_supported(n, L.P)) return false;
-  return schedule == CFP_SCHEDULE_THREE_PASS || L.P <= 4;
+  return schedule == CFP_SCHEDULE_THREE_PASS || L.P <= 4 || L.nx == 512;
 }
 
 // AUTO pipeline depth: one piece on one rank and for slabs under 64 MiB (the exchanges are then
@@ -418,8 +421,8 @@ struct SlabRank {
       a.scale = s.pass.scale;
       a.lnyl = ilog2_exact(L.nyp);  // (the 3-sweep slab schedule is never padded: P | 32)
       a.chunk = L.chunk;
-      a.k1_off = (int)(L.r * (L.nyp / 8));  // N2 = 8 rows per k1
-      hipError_t e = launch_three_pass_slab(s.tp, in, out, a, s.planes, st);
+      a.k1_off = (int)(L.r * (L.nyp / three_pass_slab_n2(L.nx)));  // N2 rows per k1
+      hipError_t e = launch_three_pass_slab(s.tp, (int)L.nx, in, out, a, s.planes, st);
       return e == hipSuccess ? CFP_SUCCESS : hip_error(e, "slab 3-sweep launch");
     }
     if (s.kind == K_REPACK) {
@@ -441,6 +444,8 @@ struct cfp_dist_plan_s {
   SlabRank R;
   ncclComm_t comm = nullptr;
   bool own_comm = true;
+  double timeout_s = kRcclDefaultTimeoutS;  // RCCL init / enqueue / finalize deadline
+  double init_ms = 0.0;                     // wall time of the communicator's creation
   cfp_dist_exchange_fn xfn = nullptr;  // caller's exchange (cfp_dist_plan_set_exchange)
   void* xuser = nullptr;
   hipStream_t cstream = nullptr;  // exchange stream of the pipelined apply
@@ -524,7 +529,8 @@ static void describe(const SlabLayout& L, const Step& s, int64_t* desc, double* 
       ps ? p.out.inner_stride : 0, ps ? p.out.outer_stride : 0, ps ? p.out.pt_stride : 0, ps ? p.out.seg_len : 0,
       ps ? p.out.seg_stride : 0,
       s.src_off, s.dst_off, s.ex_off, s.ex_cnt, L.chunk, s.wait,
-      s.kind == K_TP ? ilog2_exact(L.nyp) : 0, s.kind == K_TP ? (int64_t)(L.r * (L.nyp / 8)) : 0, s.seg, s.fused};
+      s.kind == K_TP ? ilog2_exact(L.nyp) : 0, s.kind == K_TP ? (int64_t)(L.r * (L.nyp / three_pass_slab_n2(L.nx))) : 0,
+      s.seg, s.fused};
   std::memcpy(desc, v, sizeof(v));
   *scale = (ps || s.kind == K_TP) ? p.scale : 1.0;
 }
@@ -579,21 +585,61 @@ static int plan_new(int64_t nx, int64_t ny, int64_t nz, int P, int r, int device
   return CFP_SUCCESS;
 }
 
-extern "C" int cfp_dist_plan_create(cfp_dist_plan_t* plan, int64_t nx, int64_t ny, int64_t nz, int P, int r,
-                                    const char* uid, int device) {
+// The plan's own communicator is non-blocking (cfp_rccl.h): its creation is polled against
+// timeout_s, so a rank that never joins is an error (CFP_ERR_LIB, "timed out") and not a hang.
+extern "C" int cfp_dist_plan_create_timeout(cfp_dist_plan_t* plan, int64_t nx, int64_t ny, int64_t nz, int P, int r,
+                                            const char* uid, int device, double timeout_s) {
   if (!plan || !uid) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
   *plan = nullptr;
   std::unique_ptr<cfp_dist_plan_s> p;
   int rc = plan_new(nx, ny, nz, P, r, device, &p);
   if (rc) return rc;
+  if (timeout_s > 0) p->timeout_s = timeout_s;
   ncclUniqueId id;
   std::memcpy(&id, uid, sizeof(id));
-  ncclResult_t nr = ncclCommInitRank(&p->comm, P, id, r);
+  bool timed_out = false;
+  const auto t0 = std::chrono::steady_clock::now();
+  const ncclResult_t nr = rccl_init_rank(&p->comm, P, id, r, p->timeout_s, &timed_out);
+  p->init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (nr != ncclSuccess) {
     p->R.release();
-    return set_error(CFP_ERR_LIB, "ncclCommInitRank: %s", ncclGetErrorString(nr));
+    if (timed_out)
+      return set_error(CFP_ERR_LIB, "ncclCommInitRankConfig: timed out after %.1f s (rank %d of %d)", p->timeout_s, r, P);
+    return set_error(CFP_ERR_LIB, "ncclCommInitRankConfig: %s (rank %d of %d)", ncclGetErrorString(nr), r, P);
   }
   *plan = p.release();
+  return CFP_SUCCESS;
+}
+
+extern "C" int cfp_dist_plan_create(cfp_dist_plan_t* plan, int64_t nx, int64_t ny, int64_t nz, int P, int r,
+                                    const char* uid, int device) {
+  return cfp_dist_plan_create_timeout(plan, nx, ny, nz, P, r, uid, device, kRcclDefaultTimeoutS);
+}
+
+// What RCCL this plan talks through: the rank count and rank its communicator reports
+// (ncclCommCount / ncclCommUserRank; 0 / -1 without one), the library version
+// (ncclGetVersion), the creation time, and the shared object the calls bind to.
+extern "C" int cfp_dist_plan_rccl_info(cfp_dist_plan_t p, int* nranks, int* rank, int* version, double* init_ms,
+                                       char* lib_path, int path_len) {
+  if (!p) return set_error(CFP_ERR_ARG_NULL, "NULL plan");
+  int cnt = 0, rk = -1;
+  if (p->comm) {
+    NCCLCHK(ncclCommCount(p->comm, &cnt));
+    NCCLCHK(ncclCommUserRank(p->comm, &rk));
+  }
+  if (nranks) *nranks = cnt;
+  if (rank) *rank = rk;
+  if (init_ms) *init_ms = p->init_ms;
+  if (version) NCCLCHK(ncclGetVersion(version));
+  rccl_library_path(lib_path, path_len);
+  return CFP_SUCCESS;
+}
+
+// Host-only (no GPU, no communicator): the RCCL version and library this process resolved.
+extern "C" int cfp_rccl_version(int* version, char* lib_path, int path_len) {
+  if (!version) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  NCCLCHK(ncclGetVersion(version));
+  rccl_library_path(lib_path, path_len);
   return CFP_SUCCESS;
 }
 
@@ -669,7 +715,7 @@ extern "C" int cfp_dist_plan_destroy(cfp_dist_plan_t p) {
   dist_profile_free(p);
   for (auto& e : p->step_ev) hipEventDestroy(e);
   if (p->cstream) hipStreamDestroy(p->cstream);
-  if (p->comm && p->own_comm) ncclCommDestroy(p->comm);
+  if (p->comm && p->own_comm) rccl_destroy(p->comm, p->timeout_s);
   p->R.release();
   delete p;
   return CFP_SUCCESS;
@@ -682,7 +728,7 @@ static int slab_schedule_check(const SlabLayout& L, int schedule) {
     return set_error(CFP_ERR_ARG_OUTOFRANGE, "slab schedule must be AUTO, FIVE_PASS or THREE_PASS");
   const i64 n[3] = {L.nx, L.ny, L.nz};
   if (schedule == CFP_SCHEDULE_THREE_PASS && !three_pass_slab_supported(n, L.P))
-    return set_error(CFP_ERR_SUP, "the 3-sweep slab schedule needs a 256^3 grid and nranks | 32");
+    return set_error(CFP_ERR_SUP, "the 3-sweep slab schedule needs a 256^3 or 512^3 grid and nranks | 32");
   return CFP_SUCCESS;
 }
 
@@ -793,7 +839,8 @@ static int do_exchange(cfp_dist_plan_s* p, const Step& s, const cd* src, cd* dst
     NCCLCHK(ncclSend(src + q * L.chunk + s.ex_off, cnt, ncclDouble, q, p->comm, st));
     NCCLCHK(ncclRecv(dst + q * L.chunk + s.ex_off, cnt, ncclDouble, q, p->comm, st));
   }
-  NCCLCHK(ncclGroupEnd());
+  // a non-blocking communicator may still be enqueueing: settle before the next call on it
+  NCCLCHK(rccl_settle(p->comm, ncclGroupEnd(), p->timeout_s));
   return CFP_SUCCESS;
 }
 

@@ -46,8 +46,10 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
 // z-slab rank of a 256^3 grid (cfp_dist.hip): stage 0 P1 on nzl local planes (in natural ->
 // out chunked), 1 P2 on [256][nyl][256] in place, 2 P3 (in chunked -> out natural, x a.scale);
 // the default shape (N1 = 32, permlane P2 with prefetch)
+// the 3-sweep slab schedule: 256^3 and 512^3 with P | 32 ranks
 bool three_pass_slab_supported(const i64 n[3], int P);
-hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs& a, int nzl, hipStream_t s);
+int three_pass_slab_n2(i64 n);  // rows y2 per k1 of the four-step y split (8 at 256, 16 at 512)
+hipError_t launch_three_pass_slab(int stage, int n, const cd* in, cd* out, const TPArgs& a, int nzl, hipStream_t s);
 // real-data plan at n^3, n = 128 or 256 (cfp_real.hip): stage 0 P1r (b -> H, Q), 1 P2 on H
 // (n/2 x n x n, in place), 3 the same on the Nyquist column Q (n x n, kx = n/2, in place;
 // a.colsym = its [ky] symbol), 2 P3r (H, Q -> x, x a.scale); a.tw = W_n, a.colsym =

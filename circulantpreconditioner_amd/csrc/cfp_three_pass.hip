@@ -260,7 +260,9 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
   const int tid = threadIdx.x;
   for (int i = tid; i < TN; i += NT) tw_l[i] = a.tw[i];
   const int c0 = tid & (T - 1), tz0 = tid / T;
-  const i64 zs = (i64)NX * TN;  // NX: row length (TN; the real plan's half spectrum: TN / 2)
+  // NX: row length (TN; the real plan's half spectrum: TN / 2).  Slab plans (a.lnyl): this rank's
+  // z-pencil block [TN z][nyl][NX] with the global k1 range [k1_off, k1_off + nyl / N2)
+  const i64 zs = (i64)NX << (a.lnyl ? a.lnyl : ilog2(TN));
   // Everything but the 16 points is rebuilt from laundered copies of the thread indices where
   // it is used: 128 VGPRs hold the points plus one radix-16 stage's twiddles, and an address,
   // twiddle or index kept live across the FFTs (or hoisted out of the unit loop) spills.
@@ -278,7 +280,7 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
     q.xk = xt * XT + c / N2;
     q.col = BL ? data + (i64)NX * N2 * k1 + xt * T + q.y2 * XT + c / N2 + zs * tz
                : data + q.xk + (i64)NX * (q.y2 + N2 * k1) + zs * tz;
-    q.w = a.tw[(q.y2 * k1) & (TN - 1)];
+    q.w = a.tw[(q.y2 * (a.k1_off + k1)) & (TN - 1)];  // global k1
     q.w8 = a.tw[(TN / 8) * (q.y2 & 3)];
     if constexpr (N2 == 16) q.w16 = a.tw[(TN / 16) * (q.y2 & 7)];
     return q;
@@ -315,7 +317,7 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
     {
       int c = c0, tz = tz0;
       asm volatile("" : "+v"(c), "+v"(tz));
-      const int k1 = u / NXT, y2 = c & (N2 - 1);
+      const int k1 = a.k1_off + u / NXT, y2 = c & (N2 - 1);  // global k1
       const cd cs = a.colsym[(u % NXT) * XT + c / N2 + (i64)NX * (k1 + N1 * brev<N2>(y2))];
 #pragma unroll
       for (int m = 0; m < PTS; ++m) {
@@ -1032,11 +1034,37 @@ static void launch_mid_sw(cd* data, const TPArgs& a, hipStream_t s) {
 }
 
 bool three_pass_slab_supported(const i64 n[3], int P) {
-  // N1 = 32 rows per P1 unit, k1 split over the ranks; P3 reads chunk rows 16 apart (nyl >= 16)
-  return n[0] == 256 && n[1] == 256 && n[2] == 256 && P >= 1 && P <= 16 && (32 % P) == 0;
+  // N1 = 32 rows per P1 unit, k1 split over the ranks (P | 32); P3 reads chunk rows N2 apart
+  // per thread and N2 TY = 2 N2 apart per slot (nyl >= 2 N2: 256^3 N2 = 8, 512^3 N2 = 16)
+  const bool cube = n[0] == n[1] && n[1] == n[2] && (n[0] == 256 || n[0] == 512);
+  return cube && P >= 1 && P <= 16 && (32 % P) == 0;
 }
 
-hipError_t launch_three_pass_slab(int stage, const cd* in, cd* out, const TPArgs& a, int nzl, hipStream_t s) {
+int three_pass_slab_n2(i64 n) { return n == 512 ? 16 : 8; }
+
+hipError_t launch_three_pass_slab(int stage, int n, const cd* in, cd* out, const TPArgs& a, int nzl, hipStream_t s) {
+  if (n == 512) {
+    // 512^3 (r05): N1 = 32 x N2 = 16 as on one GPU; P2 on this rank's [512 z][nyl][512 x] block
+    // (2 x times 16 y2 tiles of its nyl / 16 k1, XCD order), P1 / P3 on the local planes through
+    // the per-peer chunks, one 1024-thread workgroup per CU
+    constexpr int W = kRowsWave ? F_WAVE_LDS : 0;
+    if (stage == 1) {
+      const int nk1 = (1 << a.lnyl) / 16;  // local k1 values
+      const int units = 256 * nk1;         // x tiles x local k1
+      const unsigned g = grid_xcd(units, 1);
+      if (g) TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 16, true, 512, true>), dim3(g), dim3(1024), s, out, a, units);
+      else TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 16, true, 512, false>), dim3(grid_of(units, 1)), dim3(1024), s, out, a,
+                     units);
+    } else {
+      const int units = nzl * 16;  // local z-planes x y2
+      const unsigned g = grid_of(units, 1);
+      if (stage == 0)
+        TP_LAUNCH((k_tp_rows<false, F_NT_LD | W, 32, 512, 16, true, kRowsLP>), dim3(g), dim3(1024), s, in, out, a, units);
+      else
+        TP_LAUNCH((k_tp_rows<true, F_NT_ST | W, 32, 512, 16, true, kRowsLP>), dim3(g), dim3(1024), s, in, out, a, units);
+    }
+    return hipGetLastError();
+  }
   if (stage == 1) {
     const int nk1 = a.lnyl ? (1 << a.lnyl) / 8 : 32;  // local k1 values: nyl / N2
     const int units = 32 * nk1;                        // x tiles x local k1

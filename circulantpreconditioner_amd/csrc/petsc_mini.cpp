@@ -23,6 +23,7 @@
 #include "../../include/petsc_mini.h"
 #include "cfp_blas.h"
 #include "cfp_internal.h"
+#include "cfp_rccl.h"
 
 using cfp::cd;
 using cfp::i64;
@@ -125,8 +126,9 @@ extern "C" PetscErrorCode PetscMiniCommCreateRCCL(int size, int rank, const char
   r.rank = rank;
   ncclUniqueId id;
   std::memcpy(&id, uid, sizeof(id));
-  ncclResult_t nr = ncclCommInitRank(&r.nccl, size, id, rank);
-  if (nr != ncclSuccess) return ERR(PETSC_ERR_LIB, ncclGetErrorString(nr));
+  bool timed_out = false;  // non-blocking creation against a deadline (cfp_rccl.h)
+  ncclResult_t nr = cfp::rccl_init_rank(&r.nccl, size, id, rank, cfp::kRcclDefaultTimeoutS, &timed_out);
+  if (nr != ncclSuccess) return ERR(PETSC_ERR_LIB, timed_out ? "ncclCommInitRankConfig: timed out" : ncclGetErrorString(nr));
   return comm_new(r, comm);
 }
 
@@ -137,7 +139,7 @@ extern "C" PetscErrorCode PetscMiniCommDestroy(MPI_Comm* comm) {
   CommRec& r = g_comms[(size_t)*comm];
   if (r.refs > 0)  // a slab plan still sends over it (its ncclComm_t, or the callbacks)
     return ERR(PETSC_ERR_ARG_WRONGSTATE, "communicator still used by FFT matrices: destroy them first");
-  if (r.nccl) ncclCommDestroy(r.nccl);
+  if (r.nccl) cfp::rccl_destroy(r.nccl, cfp::kRcclDefaultTimeoutS);
   if (r.dbuf) hipFree(r.dbuf);
   if (r.hsend) hipHostFree(r.hsend);
   if (r.hrecv) hipHostFree(r.hrecv);
@@ -196,8 +198,9 @@ extern "C" PetscErrorCode PetscMiniAllreduce(MPI_Comm comm, double* buf, int64_t
     }
     if (hipMemcpyAsync(r->dbuf, buf, sizeof(double) * (size_t)count, hipMemcpyHostToDevice, g_stream) != hipSuccess)
       return ERR(PETSC_ERR_LIB, "allreduce copy");
-    ncclResult_t nr = ncclAllReduce(r->dbuf, r->dbuf, (size_t)count, ncclDouble, op == PETSCMINI_OP_MAX ? ncclMax : ncclSum,
-                                    r->nccl, g_stream);
+    ncclResult_t nr = cfp::rccl_settle(
+        r->nccl, ncclAllReduce(r->dbuf, r->dbuf, (size_t)count, ncclDouble, op == PETSCMINI_OP_MAX ? ncclMax : ncclSum,
+                               r->nccl, g_stream), cfp::kRcclDefaultTimeoutS);
     if (nr != ncclSuccess) return ERR(PETSC_ERR_LIB, ncclGetErrorString(nr));
     if (hipMemcpyAsync(buf, r->dbuf, sizeof(double) * (size_t)count, hipMemcpyDeviceToHost, g_stream) != hipSuccess ||
         hipStreamSynchronize(g_stream) != hipSuccess)
@@ -230,7 +233,8 @@ static PetscErrorCode comm_alltoall_host(CommRec* r, const void* send, void* rec
       if (ncclSend(d + q * per_peer, per_peer, ncclChar, q, r->nccl, g_stream) != ncclSuccess ||
           ncclRecv(d + total + q * per_peer, per_peer, ncclChar, q, r->nccl, g_stream) != ncclSuccess)
         rc = ERR(PETSC_ERR_LIB, "ncclSend / ncclRecv");
-    if (ncclGroupEnd() != ncclSuccess && !rc) rc = ERR(PETSC_ERR_LIB, "ncclGroupEnd");
+    if (cfp::rccl_settle(r->nccl, ncclGroupEnd(), cfp::kRcclDefaultTimeoutS) != ncclSuccess && !rc)
+      rc = ERR(PETSC_ERR_LIB, "ncclGroupEnd");
   }
   if (!rc && (hipMemcpyAsync(recv, d + total, total, hipMemcpyDeviceToHost, g_stream) != hipSuccess ||
               hipStreamSynchronize(g_stream) != hipSuccess))
@@ -258,7 +262,8 @@ extern "C" int PetscMiniCommExchange(void* user, const double* src, double* dst,
           ncclRecv(d + q * chunk, 2 * (size_t)count, ncclDouble, q, r->nccl, st) != ncclSuccess)
         return PetscErrorSet(PETSC_ERR_LIB, __func__, "ncclSend / ncclRecv");
     }
-    if (ncclGroupEnd() != ncclSuccess) return PetscErrorSet(PETSC_ERR_LIB, __func__, "ncclGroupEnd");
+    if (cfp::rccl_settle(r->nccl, ncclGroupEnd(), cfp::kRcclDefaultTimeoutS) != ncclSuccess)
+      return PetscErrorSet(PETSC_ERR_LIB, __func__, "ncclGroupEnd");
     return 0;
   }
   // callback communicator: [size][count] pieces through pinned host buffers

@@ -73,6 +73,15 @@ def slab_steps(dims: Sequence[int], nranks: int, rank: int, schedule="five", pie
     return out
 
 
+def rccl_version() -> dict:
+    """Host-only: the RCCL version (ncclGetVersion) and the shared object the library's RCCL
+    calls resolve to in this process (torch bundles its own librccl.so.1)."""
+    v = ctypes.c_int()
+    path = ctypes.create_string_buffer(512)
+    check(lib().cfp_rccl_version(ctypes.byref(v), path, 512))
+    return {"version": v.value, "lib": path.value.decode(errors="replace")}
+
+
 class SlabPlan:
     """This rank's part of a slab-distributed plan.
 
@@ -85,7 +94,7 @@ class SlabPlan:
     """
 
     def __init__(self, dims: Sequence[int], rank: int, world: int, device: int | None = None, group=None,
-                 exchange: str = "rccl"):
+                 exchange: str = "rccl", timeout_s: float = 300.0):
         import torch.distributed as dist
         nx, ny, nz = (int(d) for d in dims)
         self.dims = (nx, ny, nz)
@@ -105,7 +114,10 @@ class SlabPlan:
             t = t.to(f"cuda:{self.device}") if on_dev else t.clone()
             dist.broadcast(t, src=0, group=group)
             uid = ctypes.create_string_buffer(bytes(t.cpu().numpy().tobytes()), nbytes)
-            check(lib().cfp_dist_plan_create(ctypes.byref(h), nx, ny, nz, self.world, self.rank, uid, self.device))
+            # non-blocking communicator creation polled against timeout_s (a rank that never
+            # joins raises instead of hanging, csrc/cfp_rccl.h)
+            check(lib().cfp_dist_plan_create_timeout(ctypes.byref(h), nx, ny, nz, self.world, self.rank, uid,
+                                                     self.device, float(timeout_s)))
         elif exchange == "torch":
             check(lib().cfp_dist_plan_create_external(ctypes.byref(h), nx, ny, nz, self.world, self.rank,
                                                       self.device))
@@ -115,6 +127,18 @@ class SlabPlan:
         else:
             raise ValueError("exchange must be 'rccl' or 'torch'")
         self._h = h
+
+    def rccl_info(self) -> dict:
+        """What RCCL this plan talks through: the communicator's rank count and rank
+        (ncclCommCount / ncclCommUserRank; 0 / -1 without one), ncclGetVersion, the creation
+        time and the shared object the library's RCCL calls bind to."""
+        n, r, v = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        ms = ctypes.c_double()
+        path = ctypes.create_string_buffer(512)
+        check(lib().cfp_dist_plan_rccl_info(self._h, ctypes.byref(n), ctypes.byref(r), ctypes.byref(v),
+                                            ctypes.byref(ms), path, 512))
+        return {"ranks": n.value, "rank": r.value, "version": v.value, "init_ms": round(ms.value, 1),
+                "lib": path.value.decode(errors="replace")}
 
     @property
     def local_size(self) -> int:

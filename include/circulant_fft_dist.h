@@ -90,8 +90,24 @@ int cfp_slab_step_info(int64_t nx, int64_t ny, int64_t nz, int nranks, int rank,
 int cfp_dist_unique_id_bytes(void);
 int cfp_dist_get_unique_id(char *id_out);
 
+/* The plan's own communicator is created non-blocking (ncclCommInitRankConfig, blocking = 0) and
+ * polled against a deadline: a rank that never joins returns CFP_ERR_LIB ("timed out") instead
+ * of hanging.  cfp_dist_plan_create uses 300 s; _timeout takes the deadline in seconds.  The
+ * same deadline bounds each exchange's enqueue and the finalize in cfp_dist_plan_destroy.
+ * Replaces FFTW-MPI's plan creation inside MatCreateFFT(PETSC_COMM_WORLD, ...)
+ * (src/PCSHELLFft_3D.cxx:34-35). */
 int cfp_dist_plan_create(cfp_dist_plan_t *plan, int64_t nx, int64_t ny, int64_t nz, int nranks, int rank,
                          const char *unique_id, int device);
+int cfp_dist_plan_create_timeout(cfp_dist_plan_t *plan, int64_t nx, int64_t ny, int64_t nz, int nranks, int rank,
+                                 const char *unique_id, int device, double timeout_s);
+/* What RCCL the plan talks through: ncclCommCount / ncclCommUserRank of its communicator (0 / -1
+ * for a plan without one), ncclGetVersion, the communicator's creation time (ms), and the path
+ * of the shared object that defines the RCCL entry points the library binds (any output may be
+ * NULL; lib_path gets at most path_len bytes). */
+int cfp_dist_plan_rccl_info(cfp_dist_plan_t plan, int *nranks, int *rank, int *version, double *init_ms,
+                            char *lib_path, int path_len);
+/* Host-only, no GPU: the RCCL version and library this process resolved. */
+int cfp_rccl_version(int *version, char *lib_path, int path_len);
 /* Same on the caller's RCCL communicator (an ncclComm_t of nranks ranks; it stays the caller's). */
 int cfp_dist_plan_create_with_comm(cfp_dist_plan_t *plan, int64_t nx, int64_t ny, int64_t nz, int nranks, int rank,
                                    void *nccl_comm, int device);

@@ -169,3 +169,70 @@ def test_transport_residual_two_slabs_gloo():
     one = bench.transport_residual(b, x, n, lam)
     assert res[0][1] == pytest.approx(one, rel=1e-6) and res[1][1] == pytest.approx(one, rel=1e-6)
     assert one < 1e-14
+
+
+# ---------------------------------------------------------------- launch and watchdog
+import json
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(args, extra_env=None, timeout=240):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "CFP_BENCH_SELF_LAUNCHED")}
+    env.update(extra_env or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    return p.returncode, lines, p.stderr
+
+
+def test_gpus_2_without_launcher_self_launches():
+    """bench.py --gpus 2 with no launcher starts its 2 ranks itself (torch.distributed.run child,
+    gloo here) and rank 0 prints one line with n_gpus 2 -- it never runs one GPU silently."""
+    rc, lines, err = _bench(["--gpus", "2", "--selftest-cpu", "--steps", "5", "--warmup", "2"],
+                            {"CFP_BENCH_SHARE_DEVICE": "1", "CFP_BENCH_BACKEND": "gloo"})
+    assert rc == 0, err[-3000:]
+    assert len(lines) == 1, lines
+    ln = lines[0]
+    assert ln["n_gpus"] == 2 and ln["status"] == "selftest" and ln["value"] is None
+    assert ln["launcher"] == "self (torch.distributed.run)"
+    assert [p[0] for p in ln["phases_s"]][:4] == ["import", "init", "plan", "first_apply"]
+
+
+def test_watchdog_names_the_stalled_phase():
+    """A rank that blocks in the timed region: every rank's watchdog fires, rank 0 prints the
+    timeout line naming the phase, and the run exits non-zero."""
+    rc, lines, err = _bench(["--gpus", "2", "--selftest-cpu", "--steps", "5", "--warmup", "1",
+                             "--selftest-stall", "timed", "--selftest-stall-rank", "1", "--deadline", "timed=3"])
+    assert rc != 0
+    assert len(lines) == 1, (lines, err[-2000:])
+    assert lines[0]["status"] == "timeout" and lines[0]["phase"] == "timed" and lines[0]["rank"] == 0
+    assert "phase 'timed' exceeded" in err and "Thread 0x" in err  # faulthandler stacks
+
+
+def test_watchdog_single_rank_init_stall():
+    rc, lines, err = _bench(["--gpus", "1", "--selftest-cpu", "--selftest-stall", "init", "--deadline", "init=2"])
+    assert rc == 3 and lines and lines[0]["status"] == "timeout" and lines[0]["phase"] == "init"
+
+
+def test_world_size_mismatch_is_refused():
+    rc, lines, err = _bench(["--gpus", "2", "--selftest-cpu"], {"WORLD_SIZE": "1"})
+    assert rc == 2 and not lines and "refusing" in err
+
+
+def test_deadline_override_parsing():
+    d = bench.parse_deadlines(["timed=7", "init=1.5"])
+    assert d["timed"] == 7.0 and d["init"] == 1.5 and d["plan"] == bench.DEADLINES["plan"]
+    with pytest.raises(SystemExit):
+        bench.parse_deadlines(["nosuchphase=3"])
+
+
+def test_rccl_library_is_reported_host_only():
+    """The library reports which librccl its RCCL calls bind to (torch bundles one with the same
+    soname as /opt/rocm's), without a GPU."""
+    from circulantpreconditioner_amd.distributed import rccl_version
+    v = rccl_version()
+    assert v["version"] >= 21400 and "rccl" in v["lib"]

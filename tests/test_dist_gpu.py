@@ -272,7 +272,11 @@ def test_rccl_single_rank(oracle):
         dims, lam = (64, 32, 16), (0.6, 0.15, 0.02)
         b = oracle.c_fill_uniform(int(np.prod(dims)), 21)
         ref = oracle.c_solve_3d(oracle.c_build_diag_transport(dims, lam), b, dims)
-        plan = SlabPlan(dims, rank=0, world=1, device=0)
+        plan = SlabPlan(dims, rank=0, world=1, device=0, timeout_s=60.0)
+        # the non-blocking communicator (ncclCommInitRankConfig, polled) reports what it saw
+        info = plan.rccl_info()
+        assert info["ranks"] == 1 and info["rank"] == 0 and info["version"] >= 21400
+        assert "rccl" in info["lib"] and 0.0 <= info["init_ms"] < 60e3
         plan.set_transport_symbol(lam)
         x = plan.apply(torch.from_numpy(b).cuda())
         assert oracle.rel_l2(x.cpu().numpy(), ref) < TOL

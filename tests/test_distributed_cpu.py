@@ -232,15 +232,16 @@ def test_slab_steps_pieces_layout(P):
             assert all(st[i]["dst"] == m for i in fwd) and all(st[i]["src"] == m for i in bwd)
 
 
-@pytest.mark.parametrize("P", [1, 2, 4])
+@pytest.mark.parametrize("n,P", [(256, 1), (256, 2), (256, 4), (512, 2), (512, 8), (512, 16)])
 @pytest.mark.parametrize("pieces", [1, 2, 4])
-def test_slab_three_sweep_layout(P, pieces):
-    """the 3-sweep slab schedule (AUTO at 256^3 for P <= 4) is described too: P1
-    blocks write block k of every chunk (offsets k B nyl nx), P2 runs on the rank's k1 rows
-    [r nyl / 8, ...), the chunk and row bookkeeping the kernels receive, and the exchange
-    pieces tile the chunk."""
+def test_slab_three_sweep_layout(n, P, pieces):
+    """the 3-sweep slab schedule (AUTO at 256^3 for P <= 4, at 512^3 for every P | 32
+    since r05) is described too: P1 blocks write block k of every chunk (offsets k B nyl nx), P2
+    runs on the rank's k1 rows [r nyl / N2, ...) (N2 = 8 at 256^3, 16 at 512^3), the chunk and row
+    bookkeeping the kernels receive, and the exchange pieces tile the chunk."""
     from circulantpreconditioner_amd.distributed import slab_layout, slab_steps
-    dims = (256, 256, 256)
+    dims = (n, n, n)
+    n2 = 16 if n == 512 else 8
     for r in range(P):
         L = slab_layout(dims, P, r)
         st = slab_steps(dims, P, r, schedule="auto", pieces=pieces)
@@ -252,11 +253,11 @@ def test_slab_three_sweep_layout(P, pieces):
         (p2,) = [s for s in st if s["kind"] == 2 and s["axis"] == 1]
         for k, (a, c) in enumerate(zip(p1, p3)):
             assert a["ncols"] == B and c["ncols"] == B
-            assert a["src_off"] == k * B * 256 * 256 and a["dst_off"] == k * B * L["ny_local"] * 256
-            assert c["src_off"] == k * B * L["ny_local"] * 256 and c["dst_off"] == k * B * 256 * 256
-            assert c["scale"] == pytest.approx(1.0 / 256 ** 3)
-        assert p2["k1_off"] == r * (L["ny_local"] // 8) and 1 << p2["lnyl"] == L["ny_local"]
-        assert all(s["chunk"] == L["chunk"] == L["nz_local"] * L["ny_local"] * 256 for s in st)
+            assert a["src_off"] == k * B * n * n and a["dst_off"] == k * B * L["ny_local"] * n
+            assert c["src_off"] == k * B * L["ny_local"] * n and c["dst_off"] == k * B * n * n
+            assert c["scale"] == pytest.approx(1.0 / n ** 3)
+        assert p2["k1_off"] == r * (L["ny_local"] // n2) and 1 << p2["lnyl"] == L["ny_local"]
+        assert all(s["chunk"] == L["chunk"] == L["nz_local"] * L["ny_local"] * n for s in st)
         ex = [s for s in st if s["kind"] == 1]
         assert sum(s["ex_cnt"] for s in ex[:pieces]) == L["chunk"]
     # the round-2 entry point describes the five-pass list only (its docstring says so)
