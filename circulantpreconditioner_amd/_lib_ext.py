@@ -149,6 +149,7 @@ def declare(L) -> None:
         "PetscMiniCommResolve": ([c_int, P(c_int)], c_int),
         "PetscMiniAllreduce": ([c_int, P(ctypes.c_double), i64, c_int], c_int),
         "PetscMiniCommGetNCCL": ([c_int, P(vp)], c_int),
+        "PetscMiniMatAIJGetFormat": ([vp, P(c_int)], c_int),
         "VecCreateMPI": ([c_int, i64, i64, P(vp)], c_int),
         "VecCreateMPIHIP": ([c_int, i64, i64, P(vp)], c_int),
         "VecCreateMPIHIPWithArray": ([c_int, i64, i64, i64, vp, P(vp)], c_int),

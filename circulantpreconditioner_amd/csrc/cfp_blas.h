@@ -29,6 +29,18 @@ hipError_t blas_maxpy_norm(cd* y, int k, const cd* a, const cd* const* xs, i64 n
 // y = A x for a CSR matrix of m rows and nnz nonzeros (nnz picks the lanes per row)
 hipError_t blas_csr_spmv(i64 m, i64 nnz, const i64* rowptr, const i64* col, const cd* val, const cd* x, cd* y,
                          hipStream_t s);
+// Row-class diagonal form (k_dia_spmv): nonzeros on nd <= DIA_MAX fixed diagonals (column - row =
+// off[k], ascending), each row one of ncls <= 256 classes; class c holds tab[c nd + k] on
+// diagonal k where bit k of masks[c] is set.  y[r] = sum_k tab[cls[r] nd + k] x[r + off[k]].
+#define DIA_MAX 8
+struct DiaDesc {
+  i64 off[DIA_MAX];
+  int nd = 0, ncls = 0;
+};
+hipError_t blas_dia_spmv(i64 m, const DiaDesc& d, const unsigned char* cls, const unsigned char* masks, const cd* tab,
+                         const cd* x, cd* y, hipStream_t s);
+hipError_t blas_dia_spmv(i64 m, const DiaDesc& d, const unsigned char* cls, const unsigned char* masks,
+                         const double* tab, const double* x, double* y, hipStream_t s);
 // synchronous reductions, PETSc conventions: dot = y^H x; norm type 0 = NORM_1 (sum |re|+|im|),
 // 1 = NORM_2, 3 = NORM_INFINITY (max modulus)
 hipError_t blas_dot(const cd* x, const cd* y, i64 n, cd* val, hipStream_t s);

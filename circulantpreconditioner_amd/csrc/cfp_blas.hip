@@ -187,6 +187,36 @@ __global__ void __launch_bounds__(BLAS_THREADS) k_csr_spmv_vec(i64 m, const i64*
   }
 }
 
+// Row-class diagonal SpMV (r05).  A constant-coefficient stencil on a
+// Cartesian grid -- the transport operator of configs 1 and 3 (transport_cartesian.cpp) -- has
+// its nonzeros on a few fixed diagonals and only a handful of distinct rows (interior, and the
+// borders where faces drop out).  Stored as one class byte per row and a table of the classes'
+// diagonal values (staged in LDS), y = A x reads the class bytes and x (the neighbours x[r +
+// off] come from the caches) and writes y: 33 N bytes for complex vectors, against CSR's
+// 24 B per nonzero + 8 B rowptr + the vectors (the 256^3 CSR SpMV took 271 us per call inside
+// GMRES, profiles/r04_gmres256_kernels.txt).  Absent entries are skipped (mask bit clear), so a
+// row never loads outside x.
+template <class T>
+__global__ void __launch_bounds__(BLAS_THREADS) k_dia_spmv(i64 m, DiaDesc d, const unsigned char* cls,
+                                                           const unsigned char* masks, const T* tab, const T* x, T* y) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dia_lds[];
+  T* st = reinterpret_cast<T*>(dia_lds);
+  unsigned char* sm = dia_lds + sizeof(T) * (size_t)(d.ncls * d.nd);
+  for (int i = threadIdx.x; i < d.ncls * d.nd; i += blockDim.x) st[i] = tab[i];
+  for (int i = threadIdx.x; i < d.ncls; i += blockDim.x) sm[i] = masks[i];
+  __syncthreads();
+  GRID_LOOP(r, m) {
+    const int c = cls[r];
+    const unsigned mk = sm[c];
+    const T* row = st + c * d.nd;
+    double ax = 0.0, ay = 0.0;
+#pragma unroll
+    for (int k = 0; k < DIA_MAX; ++k)
+      if (k < d.nd && ((mk >> k) & 1u)) spmv_acc(row[k], x[r + d.off[k]], ax, ay);
+    spmv_store(y + r, ax, ay);
+  }
+}
+
 // ------------------------------------------------------------------ host launchers
 #define L1(K, ...) \
   do { if (n > 0) hipLaunchKernelGGL(K, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, __VA_ARGS__); return hipGetLastError(); } while (0)
@@ -247,6 +277,24 @@ hipError_t blas_csr_spmv(i64 m, i64 nnz, const i64* rowptr, const i64* col, cons
 hipError_t blas_csr_spmv(i64 m, i64 nnz, const i64* rowptr, const i64* col, const double* val, const double* x,
                          double* y, hipStream_t s) {
   return spmv_t(m, nnz, rowptr, col, val, x, y, s);
+}
+
+template <class T>
+static hipError_t dia_t(i64 m, const DiaDesc& d, const unsigned char* cls, const unsigned char* masks, const T* tab,
+                        const T* x, T* y, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  if (d.nd < 1 || d.nd > DIA_MAX || d.ncls < 1 || d.ncls > 256) return hipErrorInvalidValue;
+  const size_t lds = sizeof(T) * (size_t)(d.ncls * d.nd) + 256;
+  hipLaunchKernelGGL(k_dia_spmv<T>, dim3(nblocks(m)), dim3(BLAS_THREADS), lds, s, m, d, cls, masks, tab, x, y);
+  return hipGetLastError();
+}
+hipError_t blas_dia_spmv(i64 m, const DiaDesc& d, const unsigned char* cls, const unsigned char* masks, const cd* tab,
+                         const cd* x, cd* y, hipStream_t s) {
+  return dia_t(m, d, cls, masks, tab, x, y, s);
+}
+hipError_t blas_dia_spmv(i64 m, const DiaDesc& d, const unsigned char* cls, const unsigned char* masks,
+                         const double* tab, const double* x, double* y, hipStream_t s) {
+  return dia_t(m, d, cls, masks, tab, x, y, s);
 }
 
 // per-thread device + pinned staging of block partial sums (synchronous reductions)

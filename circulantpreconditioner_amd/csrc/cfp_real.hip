@@ -424,6 +424,30 @@ __global__ void k_rb_extend(const cd* __restrict__ half, cd* __restrict__ full, 
     }
   }
 }
+// Z = the weighted, zero-padded half spectrum over `rows` rows of nx: Z(kx) = w(kx) S(kx) for
+// kx <= nx/2 (w = 1 on the self-mirrored columns kx = 0 and, nx even, nx/2; else 2) and 0 above,
+// with S = half (its [rows][nx/2 + 1] layout) or, half == NULL, full itself (in place); divided
+// by diag (the half-spectrum layout; 0 where diag = 0, PETSc's VecPointwiseDivide) when given.
+// For any half spectrum H, Re IDFT(Z) = Re IDFT(Hermitian extension of H) = FFTW's c2r of H, and
+// the padding needs no value from another z-plane (the extension's X(-kz) mirror does).
+__global__ void k_rb_pad(const cd* __restrict__ half, const cd* __restrict__ diag, cd* full, int64_t nx, int64_t rows) {
+  const int64_t M = nx / 2 + 1;
+  RB_LOOP(i, nx * rows) {
+    const int64_t kx = i % nx, r = i / nx;
+    cd v = make_cd(0.0, 0.0);
+    if (kx < M) {
+      v = half ? half[r * M + kx] : full[i];
+      if (diag) {
+        const cd d = diag[r * M + kx];
+        const double den = d.x * d.x + d.y * d.y;
+        v = den != 0.0 ? make_cd((v.x * d.x + v.y * d.y) / den, (v.y * d.x - v.x * d.y) / den) : make_cd(0.0, 0.0);
+      }
+      const double w = (kx == 0 || 2 * kx == nx) ? 1.0 : 2.0;
+      v = make_cd(w * v.x, w * v.y);
+    }
+    full[i] = v;
+  }
+}
 unsigned rb_grid(int64_t n) {
   const int64_t b = (n + 255) / 256;
   return (unsigned)(b < 1 ? 1 : (b > 16384 ? 16384 : b));
@@ -449,6 +473,16 @@ extern "C" int cfp_half_spectrum_extract(const double* full, double* half, int64
   const int64_t M = nx / 2 + 1, rows = ny * nz;
   hipLaunchKernelGGL(k_rb_half, dim3(rb_grid(rows * M)), dim3(256), 0, (hipStream_t)stream, (const cd*)full, (cd*)half,
                      nx, M, rows);
+  HIPCHK(hipGetLastError());
+  return CFP_SUCCESS;
+}
+extern "C" int cfp_half_spectrum_pad(const double* half, const double* diag, double* full, int64_t nx, int64_t rows,
+                                     void* stream) {
+  if (!full) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  if (nx < 1 || rows < 0) return set_error(CFP_ERR_ARG_OUTOFRANGE, "grid sizes must be >= 1");
+  if (rows > 0)
+    hipLaunchKernelGGL(k_rb_pad, dim3(rb_grid(nx * rows)), dim3(256), 0, (hipStream_t)stream, (const cd*)half,
+                       (const cd*)diag, (cd*)full, nx, rows);
   HIPCHK(hipGetLastError());
   return CFP_SUCCESS;
 }

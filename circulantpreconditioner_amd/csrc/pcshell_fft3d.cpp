@@ -42,47 +42,11 @@ extern "C" void cfp_apply_stamp_clear(void);
 
 const int kFFTMagic = 0x46465448;  // "FFTH"
 
-#ifdef CFP_WITH_PETSC
-// Exchange piece over a real MPI communicator (cfp_dist_exchange_fn): host-staged
-// MPI_Alltoall of the [size][count] pieces.
-struct MpiExchange {
-  MPI_Comm comm;
-  int size;
-  std::vector<char> hs, hr;
-};
-int mpi_exchange(void* user, const double* src, double* dst, int64_t chunk, int64_t off, int64_t count, void* stream) {
-  MpiExchange* m = (MpiExchange*)user;
-  const size_t bytes = 16 * (size_t)count, pitch = 16 * (size_t)chunk;
-  if (bytes > (size_t)INT32_MAX) return 1;
-  m->hs.resize(bytes * m->size);
-  m->hr.resize(bytes * m->size);
-  hipStream_t st = (hipStream_t)stream;
-  if (hipMemcpy2DAsync(m->hs.data(), bytes, src + 2 * off, pitch, bytes, m->size, hipMemcpyDeviceToHost, st) ||
-      hipStreamSynchronize(st))
-    return 1;
-  if (MPI_Alltoall(m->hs.data(), (int)bytes, MPI_BYTE, m->hr.data(), (int)bytes, MPI_BYTE, m->comm)) return 1;
-  if (hipMemcpy2DAsync(dst + 2 * off, pitch, m->hr.data(), bytes, bytes, m->size, hipMemcpyHostToDevice, st) ||
-      hipStreamSynchronize(st))
-    return 1;
-  return 0;
-}
-#endif
-
-// max over the ranks of the FFT matrix' communicator (one rank: itself)
-PetscErrorCode comm_max(MPI_Comm comm, int nranks, double* v, int n) {
-  if (nranks == 1) return PETSC_SUCCESS;
-#ifdef CFP_WITH_PETSC
-  PetscCallMPI(MPI_Allreduce(MPI_IN_PLACE, v, n, MPI_DOUBLE, MPI_MAX, comm));
-#else
-  PetscCall(PetscMiniAllreduce(comm, v, n, PETSCMINI_OP_MAX));
-#endif
-  return PETSC_SUCCESS;
-}
-
 struct FFTShell {
   int magic = kFFTMagic;
   cfp_plan_t plan = nullptr;        // one rank
   cfp_dist_plan_t dplan = nullptr;  // several ranks: this rank's z slab
+  SlabBacking slab;                 // several ranks: dplan's communicator (pcshell_common.h)
   MPI_Comm comm = PETSC_COMM_SELF;
   int nranks = 1, rank = 0;
   PetscInt nlocal = 0;              // this rank's rows (= N on one rank)
@@ -91,9 +55,6 @@ struct FFTShell {
   PetscObjectId dt_id = 0;
   PetscObjectState dt_state = 0;
   void* stage = nullptr;            // in-place host-Vec staging of the slab path (nlocal values)
-#ifdef CFP_WITH_PETSC
-  MpiExchange* mx = nullptr;
-#endif
   PetscInt dims[3] = {1, 1, 1};  // n_x, n_y, n_z
   bool has_lam = false;
   double lam[6] = {0, 0, 0, 0, 0, 0};
@@ -166,16 +127,9 @@ PetscErrorCode fft_destroy(Mat A) {
   FFTShell* s;
   PetscCall(fft_shell(A, &s));
   if (s->plan) cfp_plan_destroy(s->plan);
-  if (s->dplan) {
-    cfp_dist_plan_destroy(s->dplan);
-#ifndef CFP_WITH_PETSC
-    PetscMiniCommRelease(s->comm);
-#endif
-  }
+  slab_destroy(&s->slab);
+  s->dplan = nullptr;
   if (s->stage) hipFree(s->stage);
-#ifdef CFP_WITH_PETSC
-  delete s->mx;
-#endif
   s->magic = 0;
   delete s;
   return PETSC_SUCCESS;
@@ -258,31 +212,15 @@ extern "C" PetscErrorCode FFTPrecTransportContextGetRemapBack(const FFTPrecTrans
   return PETSC_SUCCESS;
 }
 
-// the z-slab plan of this rank, its exchanges over `comm`
+// the z-slab plan of this rank, its exchanges over `comm` (pcshell_common.h)
 PetscErrorCode create_dist(FFTShell* s, MPI_Comm comm, int dev) {
   int64_t lay[8];
   CFPCALL(cfp_slab_layout(s->dims[0], s->dims[1], s->dims[2], s->nranks, s->rank, lay));
   s->nlocal = lay[4];
-#ifdef CFP_WITH_PETSC
-  CFPCALL(cfp_dist_plan_create_external(&s->dplan, s->dims[0], s->dims[1], s->dims[2], s->nranks, s->rank, dev));
-  s->mx = new MpiExchange{comm, s->nranks, {}, {}};
-  CFPCALL(cfp_dist_plan_set_exchange(s->dplan, mpi_exchange, s->mx));
-#else
-  MPI_Comm c;
-  PetscCall(PetscMiniCommResolve(comm, &c));
-  void* nccl = nullptr;
-  PetscCall(PetscMiniCommGetNCCL(c, &nccl));
-  if (nccl) {  // an RCCL communicator: the plan's exchanges are grouped ncclSend / ncclRecv on it
-    CFPCALL(cfp_dist_plan_create_with_comm(&s->dplan, s->dims[0], s->dims[1], s->dims[2], s->nranks, s->rank, nccl,
-                                           dev));
-  } else {     // the caller's collectives, host-staged
-    CFPCALL(cfp_dist_plan_create_external(&s->dplan, s->dims[0], s->dims[1], s->dims[2], s->nranks, s->rank, dev));
-    CFPCALL(cfp_dist_plan_set_exchange(s->dplan, PetscMiniCommExchange, (void*)(intptr_t)c));
-  }
-  PetscCall(PetscMiniCommRetain(c));  // PetscMiniCommDestroy refuses until fft_destroy releases it
-  s->comm = c;
-#endif
-  return PETSC_SUCCESS;
+  PetscErrorCode e = slab_create(comm, s->nranks, s->rank, s->dims, dev, &s->slab);
+  s->dplan = s->slab.plan;
+  s->comm = s->slab.comm;
+  return e;
 }
 
 // ------------------------------------------------------------------ FFT matrix
@@ -308,7 +246,7 @@ extern "C" PetscErrorCode MatCreateFFTHIP(MPI_Comm comm, PetscInt ndim, const Pe
   if (nranks > 1) {
     PetscErrorCode e = create_dist(s, comm, dev);
     if (e) {
-      if (s->dplan) cfp_dist_plan_destroy(s->dplan);
+      slab_destroy(&s->slab);
       delete s;
       return e;
     }

@@ -13,11 +13,20 @@
 // the first 2 (size/4 + 1) entries (:54) and scales by 2/size (:186); neither is reproduced
 // (parity is against the correct real arithmetic, the oracle's solve of b).
 //
-// One rank (a communicator of several ranks returns PETSC_ERR_SUP).  The register-symbol path
-// runs the real plan (cfp_rplan: r2c rows, half-spectrum passes, c2r; 3 sweeps at 128^3 and
-// 256^3) where it supports the grid, else the complex plan on b promoted to complex (one extra
-// read and write of N complex values).  An explicit Diag (any change to the Diag setup made)
-// takes the complex plan with the Hermitian extension of the half-spectrum Diag.
+// One rank: the register-symbol path runs the real plan (cfp_rplan: r2c rows, half-spectrum
+// passes, c2r; 3 sweeps at 128^3 and 256^3) where it supports the grid, else the complex plan on
+// b promoted to complex (one extra read and write of N complex values).  An explicit Diag (any
+// change to the Diag setup made) takes the complex plan with the Hermitian extension of the
+// half-spectrum Diag.
+//
+// Several ranks (r05; the reference's real branch runs on PETSC_COMM_WORLD
+// like the complex one, src/FftLinearSolver_3D.c:6-78,176,186 and src/PCSHELLFft_3D.cxx:34-35):
+// the FFT matrix is backed by the complex z-slab plan (include/circulant_fft_dist.h) on b promoted
+// to complex.  Every Vec holds its rank's z-planes: the grid side nzl ny nx reals, the spectral
+// side FFTW-MPI's non-transposed r2c slab, [nzl][ny][nx/2 + 1] complex.  The half spectrum's
+// Hermitian extension would need the X(-kz) planes of another rank, so the c2r side instead
+// pads each row locally (cfp_half_spectrum_pad: weight 2 on the paired columns, 0 above nx/2),
+// whose real part after the backward transform is the same c2r.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -47,6 +56,12 @@ struct RShell {
   int magic = kRFFTMagic;
   PetscInt dims[3] = {1, 1, 1};  // n_x, n_y, n_z
   PetscInt N = 1, NS = 2;        // grid reals, half-spectrum reals
+  // several ranks: the complex slab plan (slab.plan), this rank's z-planes [z0, z0 + nzl) and its
+  // grid reals nl / half-spectrum reals nsl (one rank: nl = N, nsl = NS)
+  SlabBacking slab;
+  int nranks = 1, rank = 0;
+  PetscInt z0 = 0, nzl = 1, nl = 1, nsl = 2;
+  uint64_t dist_version = 0;  // symbol version of slab.plan (its setter is called here only)
   cfp_plan_t cplan = nullptr;    // complex plan: transforms, explicit Diag, grids cfp_rplan lacks
   cfp_rplan_t rplan = nullptr;   // real plan (NULL where it does not support the grid)
   double* zbuf = nullptr;        // N complex: promoted b / spectrum
@@ -71,7 +86,7 @@ PetscErrorCode rshell(Mat A, RShell** out) {
 }
 
 PetscErrorCode ensure_bufs(RShell* s, bool full_diag) {
-  const size_t bytes = 2 * sizeof(double) * (size_t)s->N;
+  const size_t bytes = 2 * sizeof(double) * (size_t)s->nl;
   if (!s->zbuf) PetscCheck(hipMalloc(&s->zbuf, bytes) == hipSuccess, PETSC_COMM_SELF, PETSC_ERR_MEM, "work buffer");
   if (full_diag && !s->fbuf)
     PetscCheck(hipMalloc(&s->fbuf, bytes) == hipSuccess, PETSC_COMM_SELF, PETSC_ERR_MEM, "Diag buffer");
@@ -89,17 +104,23 @@ struct Stream {
 PetscErrorCode rfft_mult(Mat A, Vec x, Vec y) {
   RShell* s;
   PetscCall(rshell(A, &s));
-  PetscCall(check_size(x, s->N, "MatMult: x has the wrong size (n_x n_y n_z reals)"));
-  PetscCall(check_size(y, s->NS, "MatMult: y has the wrong size (2 (n_x/2 + 1) n_y n_z reals)"));
-  PetscCall(ensure_bufs(s, false));
+  PetscCall(check_size(x, s->nl, "MatMult: x has the wrong size (n_x n_y n_z reals)"));
+  PetscCall(check_size(y, s->nsl, "MatMult: y has the wrong size (2 (n_x/2 + 1) n_y n_z reals)"));
+  PetscCall(ensure_bufs(s, s->slab.plan != nullptr));
   DevIn in;
   DevOut out;
-  PetscCall(in.get(x, s->N));
-  PetscCall(out.get(y, s->NS));
+  PetscCall(in.get(x, s->nl));
+  PetscCall(out.get(y, s->nsl));
   Stream q;
-  int rc = cfp_real_to_complex(in.ptr(), s->zbuf, s->N, q.st);
-  if (!rc) rc = cfp_plan_forward(s->cplan, s->zbuf, s->zbuf, q.st);
-  if (!rc) rc = cfp_half_spectrum_extract(s->zbuf, out.ptr(), s->dims[0], s->dims[1], s->dims[2], q.st);
+  int rc = cfp_real_to_complex(in.ptr(), s->zbuf, s->nl, q.st);
+  double* spec = s->zbuf;
+  if (s->slab.plan) {  // natural slab out (FFTW-MPI's non-transposed layout): the half per plane
+    if (!rc) rc = cfp_dist_plan_forward(s->slab.plan, s->zbuf, s->fbuf, q.st);
+    spec = s->fbuf;
+  } else if (!rc) {
+    rc = cfp_plan_forward(s->cplan, s->zbuf, s->zbuf, q.st);
+  }
+  if (!rc) rc = cfp_half_spectrum_extract(spec, out.ptr(), s->dims[0], s->dims[1], s->nzl, q.st);
   if (!rc) rc = cfp_stream_sync(q.st);
   PetscCall(out.put());
   PetscCall(in.put());
@@ -110,17 +131,24 @@ PetscErrorCode rfft_mult(Mat A, Vec x, Vec y) {
 PetscErrorCode rfft_mult_transpose(Mat A, Vec y, Vec x) {
   RShell* s;
   PetscCall(rshell(A, &s));
-  PetscCall(check_size(y, s->NS, "MatMultTranspose: x has the wrong size (2 (n_x/2 + 1) n_y n_z reals)"));
-  PetscCall(check_size(x, s->N, "MatMultTranspose: y has the wrong size (n_x n_y n_z reals)"));
-  PetscCall(ensure_bufs(s, false));
+  PetscCall(check_size(y, s->nsl, "MatMultTranspose: x has the wrong size (2 (n_x/2 + 1) n_y n_z reals)"));
+  PetscCall(check_size(x, s->nl, "MatMultTranspose: y has the wrong size (n_x n_y n_z reals)"));
+  PetscCall(ensure_bufs(s, s->slab.plan != nullptr));
   DevIn in;
   DevOut out;
-  PetscCall(in.get(y, s->NS));
-  PetscCall(out.get(x, s->N));
+  PetscCall(in.get(y, s->nsl));
+  PetscCall(out.get(x, s->nl));
   Stream q;
-  int rc = cfp_half_spectrum_extend(in.ptr(), s->zbuf, s->dims[0], s->dims[1], s->dims[2], q.st);
-  if (!rc) rc = cfp_plan_backward(s->cplan, s->zbuf, s->zbuf, q.st);
-  if (!rc) rc = cfp_complex_real_part(s->zbuf, out.ptr(), s->N, 1.0, q.st);
+  int rc;
+  if (s->slab.plan) {  // row-local padding instead of the extension (its -kz planes live elsewhere)
+    rc = cfp_half_spectrum_pad(in.ptr(), nullptr, s->zbuf, s->dims[0], s->dims[1] * s->nzl, q.st);
+    if (!rc) rc = cfp_dist_plan_backward(s->slab.plan, s->zbuf, s->fbuf, q.st);
+    if (!rc) rc = cfp_complex_real_part(s->fbuf, out.ptr(), s->nl, 1.0, q.st);
+  } else {
+    rc = cfp_half_spectrum_extend(in.ptr(), s->zbuf, s->dims[0], s->dims[1], s->dims[2], q.st);
+    if (!rc) rc = cfp_plan_backward(s->cplan, s->zbuf, s->zbuf, q.st);
+    if (!rc) rc = cfp_complex_real_part(s->zbuf, out.ptr(), s->N, 1.0, q.st);
+  }
   if (!rc) rc = cfp_stream_sync(q.st);
   PetscCall(out.put());
   PetscCall(in.put());
@@ -141,6 +169,7 @@ PetscErrorCode rfft_destroy(Mat A) {
   PetscCall(rshell(A, &s));
   if (s->cplan) cfp_plan_destroy(s->cplan);
   if (s->rplan) cfp_rplan_destroy(s->rplan);
+  slab_destroy(&s->slab);
   if (s->zbuf) hipFree(s->zbuf);
   if (s->fbuf) hipFree(s->fbuf);
   s->magic = 0;
@@ -149,6 +178,7 @@ PetscErrorCode rfft_destroy(Mat A) {
 }
 
 uint64_t cversion(RShell* s) {
+  if (s->slab.plan) return s->dist_version;
   uint64_t v = 0;
   cfp_plan_symbol_version(s->cplan, &v);
   return v;
@@ -158,7 +188,12 @@ PetscErrorCode ensure_transport_symbol(RShell* s, const double lam[3]) {
   if (s->has_lam && cversion(s) == s->lam_version && std::memcmp(s->lam, lam, sizeof(s->lam)) == 0)
     return PETSC_SUCCESS;
   const double l6[6] = {lam[0], 0.0, lam[1], 0.0, lam[2], 0.0};
-  CFPCALL(cfp_plan_set_symbol_transport(s->cplan, l6));
+  if (s->slab.plan) {
+    CFPCALL(cfp_dist_plan_set_symbol_transport(s->slab.plan, l6));
+    ++s->dist_version;
+  } else {
+    CFPCALL(cfp_plan_set_symbol_transport(s->cplan, l6));
+  }
   if (s->rplan) CFPCALL(cfp_rplan_set_symbol_transport(s->rplan, lam));
   std::memcpy(s->lam, lam, sizeof(s->lam));
   s->has_lam = true;
@@ -171,12 +206,25 @@ PetscErrorCode rshell_apply(RShell* s, Vec X, Vec b, bool own, Vec Diag) {
   PetscCall(ensure_bufs(s, !own));
   DevIn bin, din;
   DevOut xout;
-  PetscCall(bin.get(b, s->N));
-  if (!own) PetscCall(din.get(Diag, s->NS));
-  PetscCall(xout.get(X, s->N));
+  PetscCall(bin.get(b, s->nl));
+  if (!own) PetscCall(din.get(Diag, s->nsl));
+  PetscCall(xout.get(X, s->nl));
   Stream q;
   int rc;
-  if (own && s->rplan && cversion(s) == s->lam_version) {  // the real plan: 8-byte grid values end to end
+  if (s->slab.plan) {  // the complex slab plan on the promoted slab; its exchanges are host-driven
+    rc = cfp_real_to_complex(bin.ptr(), s->zbuf, s->nl, q.st);
+    if (own) {
+      if (!rc) rc = cfp_dist_plan_use_diag(s->slab.plan, 0);
+      if (!rc) rc = cfp_dist_plan_apply(s->slab.plan, s->zbuf, s->zbuf, q.st);
+      if (!rc) rc = cfp_complex_real_part(s->zbuf, xout.ptr(), s->nl, 1.0, q.st);
+    } else {  // (1/N) c2r(r2c(b) ./ Diag): forward, divide the half and pad per row, backward
+      if (!rc) rc = cfp_dist_plan_forward(s->slab.plan, s->zbuf, s->fbuf, q.st);
+      if (!rc) rc = cfp_half_spectrum_pad(nullptr, din.ptr(), s->fbuf, s->dims[0], s->dims[1] * s->nzl, q.st);
+      if (!rc) rc = cfp_dist_plan_backward(s->slab.plan, s->fbuf, s->zbuf, q.st);
+      if (!rc) rc = cfp_complex_real_part(s->zbuf, xout.ptr(), s->nl, 1.0 / (double)s->N, q.st);
+    }
+    if (!rc) rc = cfp_stream_sync(q.st);
+  } else if (own && s->rplan && cversion(s) == s->lam_version) {  // the real plan: 8-byte grid values end to end
     rc = cfp_rplan_apply(s->rplan, bin.ptr(), xout.ptr(), q.st);
   } else {  // the complex plan on the promoted b, real part out (x is real for a Hermitian symbol)
     rc = cfp_real_to_complex(bin.ptr(), s->zbuf, s->N, q.st);
@@ -206,19 +254,19 @@ PetscErrorCode diag_is_own_symbol(RShell* s, Vec Diag, bool* own) {
 }
 
 // the half-spectrum symbol 1 + sum_d lam_d c_d(k_d) on the host (c_d: the 1-D DFTs of the
-// transport columns, from their closed form)
-std::vector<double> half_symbol(const PetscInt d[3], const double lam[3]) {
-  const PetscInt nx = d[0], ny = d[1], nz = d[2], M = nx / 2 + 1;
+// transport columns, from their closed form), planes kz in [z0, z0 + nzl)
+std::vector<double> half_symbol(const PetscInt d[3], const double lam[3], PetscInt z0, PetscInt nzl) {
+  const PetscInt nx = d[0], ny = d[1], M = nx / 2 + 1;
   std::vector<double> c[3];
   for (int a = 0; a < 3; ++a) {
     c[a].resize(2 * (size_t)d[a]);
     cfp_transport_symbol_1d(d[a], c[a].data());
   }
-  std::vector<double> h(2 * (size_t)(M * ny * nz));
-  for (PetscInt kz = 0; kz < nz; ++kz)
+  std::vector<double> h(2 * (size_t)(M * ny * nzl));
+  for (PetscInt kz = z0; kz < z0 + nzl; ++kz)
     for (PetscInt ky = 0; ky < ny; ++ky)
       for (PetscInt kx = 0; kx < M; ++kx) {
-        const size_t i = 2 * (size_t)((kz * ny + ky) * M + kx);
+        const size_t i = 2 * (size_t)(((kz - z0) * ny + ky) * M + kx);
         h[i] = 1.0 + lam[0] * c[0][2 * kx] + lam[1] * c[1][2 * ky] + lam[2] * c[2][2 * kz];
         h[i + 1] = lam[0] * c[0][2 * kx + 1] + lam[1] * c[1][2 * ky + 1] + lam[2] * c[2][2 * kz + 1];
       }
@@ -260,23 +308,42 @@ extern "C" PetscErrorCode FFTPrecTransportContextGetRemapBack(const FFTPrecTrans
 extern "C" PetscErrorCode MatCreateFFTHIP(MPI_Comm comm, PetscInt ndim, const PetscInt dims[], Mat* A) {
   PetscCheck(ndim >= 1 && ndim <= 3, PETSC_COMM_SELF, PETSC_ERR_ARG_OUTOFRANGE, "ndim must be 1, 2 or 3");
   PetscCheck(dims && A, PETSC_COMM_SELF, PETSC_ERR_ARG_NULL, "NULL argument");
-  int nranks = 1;
+  int nranks = 1, rank = 0;
   PetscCallMPI(MPI_Comm_size(comm, &nranks));
-  PetscCheck(nranks == 1, PETSC_COMM_SELF, PETSC_ERR_SUP,
-             "the real-scalar build's FFT matrix is single-rank (the complex build distributes slabs)");
+  PetscCallMPI(MPI_Comm_rank(comm, &rank));
   RShell* s = new RShell;
   for (PetscInt d = 0; d < ndim; ++d) s->dims[d] = dims[ndim - 1 - d];  // row-major {n_z, n_y, n_x}
   s->N = s->dims[0] * s->dims[1] * s->dims[2];
   s->NS = 2 * (s->dims[0] / 2 + 1) * s->dims[1] * s->dims[2];
+  s->nranks = nranks;
+  s->rank = rank;
+  s->nzl = s->dims[2];
+  s->nl = s->N;
+  s->nsl = s->NS;
   int dev = 0;
   hipGetDevice(&dev);
-  int rc = cfp_plan_create(&s->cplan, s->dims[0], s->dims[1], s->dims[2], dev);
-  if (rc) {
-    delete s;
-    return cfp_err(rc, "MatCreateFFTHIP");
+  if (nranks > 1) {  // this rank's z-slab of the complex slab plan (needs nranks | n_z)
+    int64_t lay[8];
+    int rc = cfp_slab_layout(s->dims[0], s->dims[1], s->dims[2], nranks, rank, lay);
+    PetscErrorCode e = rc ? cfp_err(rc, "MatCreateFFTHIP") : slab_create(comm, nranks, rank, s->dims, dev, &s->slab);
+    if (e) {
+      slab_destroy(&s->slab);
+      delete s;
+      return e;
+    }
+    s->nzl = lay[0];
+    s->z0 = lay[2];
+    s->nl = lay[4];
+    s->nsl = 2 * (s->dims[0] / 2 + 1) * s->dims[1] * s->nzl;
+  } else {
+    int rc = cfp_plan_create(&s->cplan, s->dims[0], s->dims[1], s->dims[2], dev);
+    if (rc) {
+      delete s;
+      return cfp_err(rc, "MatCreateFFTHIP");
+    }
+    if (cfp_rplan_create(&s->rplan, s->dims[0], s->dims[1], s->dims[2], dev) != CFP_SUCCESS) s->rplan = nullptr;
   }
-  if (cfp_rplan_create(&s->rplan, s->dims[0], s->dims[1], s->dims[2], dev) != CFP_SUCCESS) s->rplan = nullptr;
-  PetscCall(MatCreateShell(comm, s->NS, s->N, s->NS, s->N, s, A));
+  PetscCall(MatCreateShell(comm, s->nsl, s->nl, s->NS, s->N, s, A));
   PetscCall(MatShellSetOperation(*A, MATOP_MULT, (void (*)(void))rfft_mult));
   PetscCall(MatShellSetOperation(*A, MATOP_MULT_TRANSPOSE, (void (*)(void))rfft_mult_transpose));
   PetscCall(MatShellSetOperation(*A, MATOP_DESTROY, (void (*)(void))rfft_destroy));
@@ -296,7 +363,7 @@ extern "C" PetscErrorCode MatFFTHIPGetPlan(Mat A, cfp_plan_t* plan) {
 extern "C" PetscErrorCode MatFFTHIPGetDistPlan(Mat A, struct cfp_dist_plan_s** plan) {
   RShell* s;
   PetscCall(rshell(A, &s));
-  *plan = nullptr;
+  *plan = s->slab.plan;
   return PETSC_SUCCESS;
 }
 extern "C" PetscErrorCode MatFFTHIPGetSolveCounts(Mat A, PetscInt* own_symbol, PetscInt* explicit_diag) {
@@ -334,7 +401,16 @@ extern "C" PetscErrorCode build_diag_mat_vec_3D(Vec Diag, Vec cx, Vec cy, Vec cz
                                                 PetscInt nz, PetscScalar lx, PetscScalar ly, PetscScalar lz) {
   PetscFunctionBeginUser;
   const PetscInt M = nx / 2 + 1;
-  PetscCall(check_size(Diag, 2 * M * ny * nz, "build_diag_mat_vec_3D: Diag size != 2 (n_x/2 + 1) n_y n_z"));
+  // a distributed Diag holds its rank's whole z-planes of the half spectrum
+  PetscInt Ng, nloc, lo;
+  PetscCall(VecGetSize(Diag, &Ng));
+  PetscCall(VecGetLocalSize(Diag, &nloc));
+  PetscCall(VecGetOwnershipRange(Diag, &lo, NULL));
+  PetscCheck(Ng == 2 * M * ny * nz, PETSC_COMM_SELF, PETSC_ERR_ARG_SIZ,
+             "build_diag_mat_vec_3D: Diag size != 2 (n_x/2 + 1) n_y n_z");
+  PetscCheck(lo % (2 * M * ny) == 0 && nloc % (2 * M * ny) == 0, PETSC_COMM_SELF, PETSC_ERR_ARG_SIZ,
+             "build_diag_mat_vec_3D: a distributed Diag must hold whole z-planes");
+  const PetscInt z0 = lo / (2 * M * ny), nzl = nloc / (2 * M * ny);
   PetscCall(check_size(cx, 2 * (nx / 2 + 1), "build_diag_mat_vec_3D: c_x_hat size != 2 (n_x/2 + 1)"));
   PetscCall(check_size(cy, 2 * (ny / 2 + 1), "build_diag_mat_vec_3D: c_y_hat size != 2 (n_y/2 + 1)"));
   PetscCall(check_size(cz, 2 * (nz / 2 + 1), "build_diag_mat_vec_3D: c_z_hat size != 2 (n_z/2 + 1)"));
@@ -348,11 +424,11 @@ extern "C" PetscErrorCode build_diag_mat_vec_3D(Vec Diag, Vec cx, Vec cy, Vec cz
   };
   PetscScalar* d;
   PetscCall(VecGetArrayWrite(Diag, &d));
-  for (PetscInt kz = 0; kz < nz; ++kz)
+  for (PetscInt kz = z0; kz < z0 + nzl; ++kz)
     for (PetscInt ky = 0; ky < ny; ++ky)
       for (PetscInt kx = 0; kx < M; ++kx) {
         const std::complex<double> v = 1.0 + lx * full(ax, nx, kx) + ly * full(ay, ny, ky) + lz * full(az, nz, kz);
-        const size_t i = 2 * (size_t)((kz * ny + ky) * M + kx);
+        const size_t i = 2 * (size_t)(((kz - z0) * ny + ky) * M + kx);
         d[i] = v.real();
         d[i + 1] = v.imag();
       }
@@ -371,11 +447,16 @@ extern "C" PetscErrorCode solve_3D(Mat FFT_MAT, Vec X, Vec Diag, Vec b, Vec b_ha
   RShell* s;
   PetscCall(rshell(FFT_MAT, &s));
   PetscCheck(size == s->N, PETSC_COMM_SELF, PETSC_ERR_ARG_SIZ, "solve_3D: size != number of grid cells of FFT_MAT");
-  PetscCall(check_size(X, s->N, "solve_3D: X has the wrong size"));
-  PetscCall(check_size(b, s->N, "solve_3D: b has the wrong size"));
-  PetscCall(check_size(Diag, s->NS, "solve_3D: Diag has the wrong size (2 (n_x/2 + 1) n_y n_z reals)"));
+  PetscCall(check_size(X, s->nl, "solve_3D: X has the wrong size"));
+  PetscCall(check_size(b, s->nl, "solve_3D: b has the wrong size"));
+  PetscCall(check_size(Diag, s->nsl, "solve_3D: Diag has the wrong size (2 (n_x/2 + 1) n_y n_z reals)"));
   bool own = false;
   PetscCall(diag_is_own_symbol(s, Diag, &own));
+  if (s->slab.plan) {  // every rank takes the same path (the apply holds collectives)
+    double f = own ? 0.0 : 1.0;
+    PetscCall(comm_max(s->slab.comm, s->nranks, &f, 1));
+    own = f == 0.0;
+  }
   ++(own ? s->solves_own : s->solves_diag);
   PetscCall(rshell_apply(s, X, b, own, Diag));
   PetscFunctionReturn(PETSC_SUCCESS);
@@ -391,8 +472,8 @@ extern "C" PetscErrorCode FftTransportSolver(PetscInt nx, PetscInt ny, PetscInt 
              "FftTransportSolver: grid dims do not match FFT_MAT");
   const double lam[3] = {lx, ly, lz};
   PetscCall(ensure_transport_symbol(s, lam));
-  PetscCall(check_size(X, s->N, "FftTransportSolver: X has the wrong size"));
-  PetscCall(check_size(b, s->N, "FftTransportSolver: b has the wrong size"));
+  PetscCall(check_size(X, s->nl, "FftTransportSolver: X has the wrong size"));
+  PetscCall(check_size(b, s->nl, "FftTransportSolver: b has the wrong size"));
   PetscCall(rshell_apply(s, X, b, true, nullptr));
   PetscFunctionReturn(PETSC_SUCCESS);
 }
@@ -467,7 +548,7 @@ extern "C" PetscErrorCode setupFFTPrec3D(PC pc) {
   PetscCall(rshell(ctx->FFT_MAT, &s));
   const double lam[3] = {ctx->lambda_x, ctx->lambda_y, ctx->lambda_z};
   PetscCall(ensure_transport_symbol(s, lam));
-  const std::vector<double> h = half_symbol(s->dims, lam);
+  const std::vector<double> h = half_symbol(s->dims, lam, s->z0, s->nzl);
   PetscScalar* d;
   PetscCall(VecGetArrayWrite(ctx->Diag, &d));
   std::memcpy(d, h.data(), sizeof(double) * h.size());

@@ -1077,6 +1077,11 @@ struct _p_Mat {
   VS* val = nullptr;
   std::vector<i64> h_rowptr, h_col;
   std::vector<VS> h_val;
+  // AIJ in row-class diagonal form (aij_build_dia), when the matrix has one: no device CSR then
+  int dia = -1;  // -1: not tried yet, 0: not representable, 1: built
+  cfp::DiaDesc dia_d{};
+  unsigned char *dia_cls = nullptr, *dia_mask = nullptr;
+  VS* dia_tab = nullptr;
 };
 
 static PetscErrorCode mcheck(Mat A, const char* f) {
@@ -1127,9 +1132,99 @@ extern "C" PetscErrorCode MatCreateSeqAIJWithArrays(MPI_Comm, PetscInt m, PetscI
   *A = M;  // the device copy is made by the first MatMult on HIP vectors
   return PETSC_SUCCESS;
 }
-// mirror the host CSR into device memory (once; MatShift refreshes the values)
+// Row-class diagonal form of the host CSR (cfp_blas.h, k_dia_spmv): every nonzero on one of at
+// most DIA_MAX diagonals (column - row), each row's entries on distinct diagonals, at most 256
+// distinct rows.  A constant-coefficient stencil on a Cartesian grid (the transport operator,
+// transport_cartesian.cpp: the interior row plus the border rows) qualifies; a mesh remap or the
+// interleaved wave operator does not, and keeps the CSR kernels.
+static bool aij_build_dia(Mat M, cfp::DiaDesc* d, std::vector<unsigned char>* cls, std::vector<unsigned char>* masks,
+                          std::vector<VS>* tab) {
+  const i64 m = M->m;
+  if (m <= 0 || M->h_col.empty()) return false;
+  std::vector<i64> offs;
+  for (i64 r = 0; r < m; ++r)
+    for (i64 p = M->h_rowptr[r]; p < M->h_rowptr[r + 1]; ++p) {
+      const i64 o = M->h_col[p] - r;
+      if (std::find(offs.begin(), offs.end(), o) == offs.end()) {
+        if ((int)offs.size() == DIA_MAX) return false;
+        offs.push_back(o);
+      }
+    }
+  std::sort(offs.begin(), offs.end());
+  const int nd = (int)offs.size();
+  cls->assign((size_t)m, 0);
+  masks->clear();
+  tab->clear();
+  std::vector<VS> row((size_t)nd);
+  int last = -1;
+  for (i64 r = 0; r < m; ++r) {
+    unsigned mk = 0;
+    for (int k = 0; k < nd; ++k) row[(size_t)k] = D(std::complex<double>(0.0, 0.0));
+    for (i64 p = M->h_rowptr[r]; p < M->h_rowptr[r + 1]; ++p) {
+      const int k = (int)(std::lower_bound(offs.begin(), offs.end(), M->h_col[p] - r) - offs.begin());
+      if (mk & (1u << k)) return false;  // two entries on one diagonal (duplicate column)
+      mk |= 1u << k;
+      row[(size_t)k] = M->h_val[(size_t)p];
+    }
+    const auto same = [&](int c) {
+      if ((*masks)[(size_t)c] != mk) return false;
+      return std::memcmp(&(*tab)[(size_t)c * nd], row.data(), sizeof(VS) * (size_t)nd) == 0;
+    };
+    int c = (last >= 0 && same(last)) ? last : -1;  // consecutive rows mostly share a class
+    for (int q = 0; c < 0 && q < (int)masks->size(); ++q)
+      if (same(q)) c = q;
+    if (c < 0) {
+      if (masks->size() == 256) return false;
+      c = (int)masks->size();
+      masks->push_back((unsigned char)mk);
+      tab->insert(tab->end(), row.begin(), row.end());
+    }
+    (*cls)[(size_t)r] = (unsigned char)c;
+    last = c;
+  }
+  for (int k = 0; k < nd; ++k) d->off[k] = offs[(size_t)k];
+  d->nd = nd;
+  d->ncls = (int)masks->size();
+  return true;
+}
+
+static void aij_free_device(Mat M) {
+  if (M->rowptr) hipFree(M->rowptr);
+  if (M->col) hipFree(M->col);
+  if (M->val) hipFree(M->val);
+  if (M->dia_cls) hipFree(M->dia_cls);
+  if (M->dia_mask) hipFree(M->dia_mask);
+  if (M->dia_tab) hipFree(M->dia_tab);
+  M->rowptr = M->col = nullptr;
+  M->val = M->dia_tab = nullptr;
+  M->dia_cls = M->dia_mask = nullptr;
+  M->dia = -1;
+}
+
+// the device copy: the row-class diagonal form when the matrix has one, else the CSR (once;
+// MatShift rebuilds it)
 static PetscErrorCode aij_upload(Mat M) {
-  if (M->rowptr) return PETSC_SUCCESS;
+  if (M->rowptr || M->dia == 1) return PETSC_SUCCESS;
+  if (M->dia < 0) {
+    std::vector<unsigned char> cls, masks;
+    std::vector<VS> tab;
+    cfp::DiaDesc d{};
+    M->dia = aij_build_dia(M, &d, &cls, &masks, &tab) ? 1 : 0;
+    if (M->dia == 1) {
+      hipError_t e = hipMalloc(&M->dia_cls, cls.size());
+      if (e == hipSuccess) e = hipMalloc(&M->dia_mask, masks.size());
+      if (e == hipSuccess) e = hipMalloc(&M->dia_tab, sizeof(VS) * tab.size());
+      if (e == hipSuccess) e = hipMemcpy(M->dia_cls, cls.data(), cls.size(), hipMemcpyHostToDevice);
+      if (e == hipSuccess) e = hipMemcpy(M->dia_mask, masks.data(), masks.size(), hipMemcpyHostToDevice);
+      if (e == hipSuccess) e = hipMemcpy(M->dia_tab, tab.data(), sizeof(VS) * tab.size(), hipMemcpyHostToDevice);
+      if (e != hipSuccess) {
+        aij_free_device(M);
+        return ERR(PETSC_ERR_MEM, hipGetErrorString(e));
+      }
+      M->dia_d = d;
+      return PETSC_SUCCESS;
+    }
+  }
   const size_t nnz = M->h_col.size();
   hipError_t e = hipMalloc(&M->rowptr, sizeof(i64) * (size_t)(M->m + 1));
   if (e == hipSuccess) e = hipMalloc(&M->col, sizeof(i64) * (nnz > 0 ? nnz : 1));
@@ -1145,6 +1240,13 @@ static PetscErrorCode aij_upload(Mat M) {
     M->val = nullptr;
     return ERR(PETSC_ERR_MEM, hipGetErrorString(e));
   }
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode PetscMiniMatAIJGetFormat(Mat A, int* format) {
+  MCHK(A);
+  if (!format) return ERR(PETSC_ERR_ARG_NULL, "NULL output");
+  if (A->type != MATSEQAIJ) return ERR(PETSC_ERR_ARG_WRONG, "not a MATSEQAIJ");
+  *format = A->dia == 1 ? 1 : (A->rowptr ? 0 : -1);
   return PETSC_SUCCESS;
 }
 extern "C" PetscErrorCode MatGetType(Mat A, MatType* t) {
@@ -1179,7 +1281,10 @@ static PetscErrorCode aij_mult(Mat A, Vec x, Vec y) {
     PetscCall(dev_read(x, &xd));
     VS* yd;
     PetscCall(dev_rw(y, &yd));
-    HIPK(cfp::blas_csr_spmv(A->m, (i64)A->h_col.size(), A->rowptr, A->col, A->val, xd, yd, g_stream));
+    if (A->dia == 1)
+      HIPK(cfp::blas_dia_spmv(A->m, A->dia_d, A->dia_cls, A->dia_mask, A->dia_tab, xd, yd, g_stream));
+    else
+      HIPK(cfp::blas_csr_spmv(A->m, (i64)A->h_col.size(), A->rowptr, A->col, A->val, xd, yd, g_stream));
   } else {
     const VS* xh;
     PetscCall(host_read(x, &xh));
@@ -1218,8 +1323,12 @@ extern "C" PetscErrorCode MatShift(Mat A, PetscScalar a) {
       if (A->h_col[p] == r) { A->h_val[p] = D(C(A->h_val[p]) + a); found = true; }
     if (!found) return ERR(PETSC_ERR_ARG_WRONGSTATE, "MatShift needs an allocated diagonal");
   }
-  if (A->val && !A->h_val.empty())
+  if (A->dia == 1) {  // the classes change with the diagonal: rebuild at the next device MatMult
+    HCHK(hipDeviceSynchronize());
+    aij_free_device(A);
+  } else if (A->val && !A->h_val.empty()) {
     HCHK(hipMemcpy(A->val, A->h_val.data(), sizeof(VS) * A->h_val.size(), hipMemcpyHostToDevice));
+  }
   return PETSC_SUCCESS;
 }
 extern "C" PetscErrorCode MatDestroy(Mat* pA) {
@@ -1228,9 +1337,7 @@ extern "C" PetscErrorCode MatDestroy(Mat* pA) {
   MCHK(A);
   PetscErrorCode rc = PETSC_SUCCESS;
   if (A->destroy) rc = A->destroy(A);
-  if (A->rowptr) hipFree(A->rowptr);
-  if (A->col) hipFree(A->col);
-  if (A->val) hipFree(A->val);
+  aij_free_device(A);
   A->magic = 0;
   delete A;
   *pA = nullptr;

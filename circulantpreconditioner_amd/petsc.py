@@ -354,6 +354,13 @@ class Mat:
         PetscCall(lib().MatMultTranspose(self.h, x.h, y.h))
         return y
 
+    def aij_format(self) -> str:
+        """The stand-in AIJ's device storage: 'dia' (row-class diagonal form), 'csr', or 'none'
+        before the first device MatMult."""
+        f = ctypes.c_int()
+        PetscCall(lib().PetscMiniMatAIJGetFormat(self.h, ctypes.byref(f)))
+        return {1: "dia", 0: "csr"}.get(f.value, "none")
+
     def shift(self, a) -> "Mat":
         PetscCall(lib().MatShift(self.h, _S(a)))
         return self

@@ -55,6 +55,14 @@ def _declare(L) -> None:
         "PetscErrorLastMessage": ([], ctypes.c_char_p),
         "VecCreateSeq": ([c_int, i64, P(vp)], c_int),
         "VecCreateSeqHIP": ([c_int, i64, P(vp)], c_int),
+        "VecCreateMPI": ([c_int, i64, i64, P(vp)], c_int),
+        "VecCreateMPIHIP": ([c_int, i64, i64, P(vp)], c_int),
+        "VecGetLocalSize": ([vp, P(i64)], c_int),
+        "VecGetOwnershipRange": ([vp, P(i64), P(i64)], c_int),
+        "PetscMiniCommCreate": ([c_int, c_int, vp, P(c_int)], c_int),
+        "PetscMiniCommDestroy": ([P(c_int)], c_int),
+        "PetscMiniSetCommWorld": ([c_int], c_int),
+        "MatFFTHIPGetDistPlan": ([vp, P(vp)], c_int),
         "VecDestroy": ([P(vp)], c_int),
         "VecGetSize": ([vp, P(i64)], c_int),
         "VecGetArray": ([vp, P(vp)], c_int),
@@ -151,15 +159,35 @@ class Vec:
         PetscCall((lib().VecCreateSeqHIP if hip else lib().VecCreateSeq)(PETSC_COMM_SELF, int(n), ctypes.byref(h)))
         return cls(h)
 
+    @classmethod
+    def mpi(cls, N: int, hip: bool = False, nlocal: int = -1, comm: int = PETSC_COMM_WORLD) -> "Vec":
+        """VecCreateMPI(HIP)(comm, PETSC_DECIDE or nlocal, N): this rank's block of rows."""
+        h = ctypes.c_void_p()
+        PetscCall((lib().VecCreateMPIHIP if hip else lib().VecCreateMPI)(int(comm), int(nlocal), int(N),
+                                                                          ctypes.byref(h)))
+        return cls(h)
+
     @property
     def size(self) -> int:
         n = ctypes.c_int64()
         PetscCall(lib().VecGetSize(self.h, ctypes.byref(n)))
         return n.value
 
+    @property
+    def local_size(self) -> int:
+        n = ctypes.c_int64()
+        PetscCall(lib().VecGetLocalSize(self.h, ctypes.byref(n)))
+        return n.value
+
+    def ownership_range(self) -> tuple:
+        lo, hi = ctypes.c_int64(), ctypes.c_int64()
+        PetscCall(lib().VecGetOwnershipRange(self.h, ctypes.byref(lo), ctypes.byref(hi)))
+        return lo.value, hi.value
+
     def set_array(self, a) -> "Vec":
+        """Write this rank's rows (local size)."""
         a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
-        assert a.size == self.size
+        assert a.size == self.local_size
         p = ctypes.c_void_p()
         PetscCall(lib().VecGetArray(self.h, ctypes.byref(p)))
         ctypes.memmove(p.value, a.ctypes.data, a.nbytes)
@@ -167,7 +195,8 @@ class Vec:
         return self
 
     def array(self) -> np.ndarray:
-        n = self.size
+        """This rank's rows (local size)."""
+        n = self.local_size
         p = ctypes.c_void_p()
         PetscCall(lib().VecGetArrayRead(self.h, ctypes.byref(p)))
         out = np.ctypeslib.as_array((ctypes.c_double * n).from_address(p.value)).copy()
@@ -178,6 +207,68 @@ class Vec:
         if self.h is not None and self.h.value:
             PetscCall(lib().VecDestroy(ctypes.byref(self.h)))
         self.h = None
+
+
+class Comm:
+    """A communicator of several ranks for the real-scalar stand-in (its own communicator table:
+    the library is loaded RTLD_LOCAL), with torch.distributed's collectives on `group` -- the
+    counterpart of petsc.Comm.torch.  set_world() makes it PETSC_COMM_WORLD."""
+
+    _A2A = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
+    _RED = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int64,
+                            ctypes.c_int)
+
+    class _Ops(ctypes.Structure):
+        pass
+
+    _Ops._fields_ = [("alltoall", _A2A), ("allreduce", _RED), ("user", ctypes.c_void_p)]
+    _REGISTRY: dict = {}  # callbacks of live communicators, by handle
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+        size, rank = dist.get_world_size(group), dist.get_rank(group)
+
+        def alltoall(_user, send, recv, nbytes):
+            try:
+                n = size * nbytes // 8
+                s_ = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_double * n).from_address(send)))
+                r_ = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_double * n).from_address(recv)))
+                dist.all_to_all_single(r_, s_.clone(), group=group)
+                return 0
+            except Exception:  # reported to the library as a failed collective
+                return 1
+
+        def allreduce(_user, buf, count, op):
+            try:
+                a = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_double * count).from_address(
+                    ctypes.addressof(buf.contents))))
+                t = a.clone()
+                dist.all_reduce(t, op=dist.ReduceOp.MAX if op == 1 else dist.ReduceOp.SUM, group=group)
+                a.copy_(t)
+                return 0
+            except Exception:
+                return 1
+
+        a2a, red = self._A2A(alltoall), self._RED(allreduce)
+        ops = self._Ops(a2a, red, None)
+        h = ctypes.c_int()
+        PetscCall(lib().PetscMiniCommCreate(size, rank, ctypes.byref(ops), ctypes.byref(h)))
+        self.handle = h.value
+        Comm._REGISTRY[self.handle] = (a2a, red, ops)
+
+    def set_world(self) -> "Comm":
+        PetscCall(lib().PetscMiniSetCommWorld(self.handle))
+        return self
+
+    def destroy(self) -> None:
+        h = ctypes.c_int(self.handle)
+        PetscCall(lib().PetscMiniCommDestroy(ctypes.byref(h)))
+        Comm._REGISTRY.pop(self.handle, None)
+
+
+def set_comm_world(handle: int) -> None:
+    PetscCall(lib().PetscMiniSetCommWorld(int(handle)))
 
 
 def mat_create_fft(dims) -> ctypes.c_void_p:

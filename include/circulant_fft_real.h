@@ -57,11 +57,18 @@ int cfp_rplan_time_passes(cfp_rplan_t plan, const double *b, double *x, int iter
  *                             r2c output layout, a real-scalar MATFFTW's MatMult) of the full
  *                             [nz][ny][nx] spectrum
  *   cfp_half_spectrum_extend  the full spectrum from the half by Hermitian symmetry,
- *                             X(kx, ky, kz) = conj X(nx - kx, -ky, -kz) for kx > nx/2 */
+ *                             X(kx, ky, kz) = conj X(nx - kx, -ky, -kz) for kx > nx/2
+ *   cfp_half_spectrum_pad     rows of nx: Z(kx) = w(kx) S(kx) / D(kx) for kx <= nx/2 (w = 1 at
+ *                             kx = 0 and, nx even, kx = nx/2; else 2), 0 above; S = half
+ *                             ([rows][nx/2 + 1]) or, half == NULL, full in place; D = diag (half
+ *                             layout; 0 where D = 0) or 1 when NULL.  Re IDFT(Z) is the c2r of
+ *                             the half spectrum, row-local (no -kz mirror from another z-slab). */
 int cfp_real_to_complex(const double *x, double *z, int64_t n, void *stream);
 int cfp_complex_real_part(const double *z, double *x, int64_t n, double scale, void *stream);
 int cfp_half_spectrum_extract(const double *full, double *half, int64_t nx, int64_t ny, int64_t nz, void *stream);
 int cfp_half_spectrum_extend(const double *half, double *full, int64_t nx, int64_t ny, int64_t nz, void *stream);
+int cfp_half_spectrum_pad(const double *half, const double *diag, double *full, int64_t nx, int64_t rows,
+                          void *stream);
 
 #ifdef __cplusplus
 }

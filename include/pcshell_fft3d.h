@@ -93,6 +93,12 @@ PetscErrorCode Fft1DTransportSolver(PetscInt n_x, PetscScalar a_x, PetscScalar d
 PetscErrorCode PetscFft3DTransportSolver(struct StructuredTransportContext customCtx, Vec b, Vec x);
 PetscErrorCode FftTransportSolver(PetscInt n_x, PetscInt n_y, PetscInt n_z, PetscScalar lambda_x,
                                   PetscScalar lambda_y, PetscScalar lambda_z, Vec X, Vec b, Mat FFT_MAT);
+/* X = (1/size) F^T(F(b) ./ Diag) as one fused apply.  Difference from the reference
+ * (src/FftLinearSolver_3D.c:170-176): b_hat, the reference's scratch vector, is neither read nor
+ * written -- after the call it does NOT hold F(b) ./ Diag, in the complex and the real-scalar
+ * build alike (a caller that wants the divided spectrum calls MatMult and VecPointwiseDivide).
+ * Real scalars: Diag, b_hat are half spectra; X is the correct real solve (not the reference's
+ * 2 (size/4 + 1)-entry divide and 2/size scale); several ranks work in both builds. */
 PetscErrorCode solve_3D(Mat FFT_MAT, Vec X, Vec Diag, Vec b, Vec b_hat, PetscInt size);
 PetscErrorCode build_diag_mat_vec_3D(Vec Diag, Vec c_x_hat, Vec c_y_hat, Vec c_z_hat, PetscInt n_x, PetscInt n_y,
                                      PetscInt n_z, PetscScalar lambda_x, PetscScalar lambda_y, PetscScalar lambda_z);

@@ -159,6 +159,10 @@ PetscErrorCode PetscMiniSetCommWorld(MPI_Comm comm);
 /* the communicator PETSC_COMM_WORLD currently stands for (others: themselves) */
 PetscErrorCode PetscMiniCommResolve(MPI_Comm comm, MPI_Comm *resolved);
 PetscErrorCode PetscMiniAllreduce(MPI_Comm comm, double *buf, int64_t count, int op);
+/* Device storage the stand-in AIJ picked at its first device MatMult: 1 = row-class diagonal
+ * form (k_dia_spmv: nonzeros on <= 8 fixed diagonals, <= 256 distinct rows -- Cartesian
+ * stencils), 0 = CSR, -1 = not uploaded yet (MatShift resets it). */
+PetscErrorCode PetscMiniMatAIJGetFormat(Mat A, int *format);
 /* the ncclComm_t behind an RCCL communicator (NULL for a callback communicator) */
 PetscErrorCode PetscMiniCommGetNCCL(MPI_Comm comm, void **nccl_comm);
 /* One exchange piece of a slab plan over a communicator (the cfp_dist_exchange_fn contract of

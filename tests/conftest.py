@@ -18,7 +18,8 @@ def pytest_configure(config):
 # the oracle or the golden fixtures.  (file, test name, substring of the parameter id or "")
 PRIORITY = [
     ("test_gpu_parity.py", "test_three_pass_vs_oracle", ""),          # 256^3 default: k_tp_mid_sw + LDS-DMA
-    ("test_gpu_parity.py", "test_plane_vs_oracle", "100x100x100"),    # 100^3 default mesh: plane schedule
+    ("test_gpu_parity.py", "test_three_pass_100_vs_oracle", ""),      # 100^3 default mesh: radix-10 3-sweep (AUTO)
+    ("test_gpu_parity.py", "test_plane_vs_oracle", "100x100x100"),    # 100^3 plane schedule (selectable)
     ("test_gpu_parity.py", "test_plane_vs_oracle", "64x64x64"),
     ("test_gpu_parity.py", "test_vs_oracle", "128x128x128"),          # config 2
     ("test_transport.py", "test_driver_fft_pc_matches_oracle", ""),   # config 1 (32^3 GMRES + PCSHELL)

@@ -118,6 +118,33 @@ def case512(oracle):
     return dims, lam, b, ref
 
 
+@pytest.mark.parametrize("P", [1, 8, 16])
+def test_group_three_sweep_512(P, case512):
+    """Config 5's grid on the 3-sweep slab schedule (AUTO at 512^3 for P | 32 since r05: N1 = 32 x
+    N2 = 16, P2 on the rank's nyl / 16 k1 values with the global k1 offset) against the oracle,
+    and against the 5-pass slab schedule (compared on the device)."""
+    from circulantpreconditioner_amd.distributed import SlabGroup, slab_steps
+    dims, lam, b, ref = case512
+    assert [s["kind"] for s in slab_steps(dims, P, 0, schedule="auto")].count(2) == 3
+    full = torch.from_numpy(b).cuda()
+    rd = torch.from_numpy(ref).cuda()
+    with SlabGroup(dims, P) as g:
+        g.set_transport_symbol(lam).set_pieces(1)
+        bs = g.scatter(full)
+        del full
+        x3 = torch.cat(g.apply(bs))
+        err = float(torch.linalg.vector_norm(x3 - rd) / torch.linalg.vector_norm(rd))
+        assert err < TOL, (P, err)
+        del rd
+        if P == 8:
+            g.set_schedule("five")
+            x5 = torch.cat(g.apply(bs))
+            assert float(torch.linalg.vector_norm(x5 - x3) / torch.linalg.vector_norm(x3)) < 1e-13
+            del x5
+        del bs, x3
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("P", [2, 4, 8])
 def test_group_pieces_512(P, case512):
     """Config 5's grid with the pipelined exchange: the pieced step list (K = 1, 4, 8 pieces per

@@ -27,7 +27,7 @@ def main():
             for r in csv.DictReader(f):
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    first = next(i for i, r in enumerate(rows) if "k_csr_spmv" in r[2])
+    first = next(i for i, r in enumerate(rows) if "_spmv" in r[2])
     # the step's leading copies / sets queued before the first SpMV belong to the solve region
     while first > 0 and "fillBufferAligned" not in rows[first - 1][2] and "k_build_diag" not in rows[first - 1][2]:
         first -= 1
