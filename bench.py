@@ -313,7 +313,11 @@ def cpu_baseline(grid, budget_s: float = 20.0):
         import scipy.fft as sf
         bz = b.reshape(n[2], n[1], n[0])
         dz = d.reshape(n[2], n[1], n[0])
-        for w in ([1, threads] if threads > 1 else [1]):
+        # 1 worker, the inherited thread budget (OMP_NUM_THREADS: 16 on the GPU box), and every
+        # core this process may run on (len(sched_getaffinity(0)): the box's 256), whatever
+        # OMP_NUM_THREADS says -- north_star's "same box's host cores"
+        aff = len(os.sched_getaffinity(0))
+        for w in sorted({1, threads, aff}):
             t0 = time.perf_counter()
             sf.ifftn(sf.fftn(bz, workers=w) / dz, workers=w)  # warm-up; sizes the sample
             first = time.perf_counter() - t0

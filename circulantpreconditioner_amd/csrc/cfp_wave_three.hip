@@ -841,7 +841,6 @@ hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArg
   if (stage == 1) {
     const int units = (WNX / 2) * WN1;  // x tiles x k1
     // the LDS-DMA prefetch (global_load_lds_dwordx4) takes 16-byte aligned addresses
-    // the LDS-DMA prefetch (global_load_lds_dwordx4) takes 16-byte aligned addresses
     if (((uintptr_t)out & 15) == 0)
       hipLaunchKernelGGL((k_wtp_mid_ct2<true, 0, true>), dim3(units < g ? units : g), dim3(512), 0, s, out, a, units);
     else

@@ -283,7 +283,10 @@ extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
   // KSPSolve(ksp, Un, Un): PETSc copies the right-hand side when b == x.  Here b is read from x
   // until x is first written (the end of the first cycle), and copied only if a restart follows.
   bool b_in_x = b == x;
-  // x = 0 initially: not set here; the first solution update overwrites x (VecMiniMAXPYNorm)
+  // x = 0 initially: not set here; the first solution update overwrites x (VecMiniMAXPYNorm).
+  // Consequence (unlike PETSc, which zeroes x first): if the solve returns early with an error
+  // (a failed PCApply / MatMult, PetscCall), x still holds the caller's old contents -- or b,
+  // when b == x.  x is defined only after a successful return.
   bool x_zero = !k->guess_nonzero, x_unset = x_zero;
 
   std::vector<C> H((size_t)(m + 1) * m), cc((size_t)m), ss((size_t)m), rs((size_t)m + 1), y((size_t)m);

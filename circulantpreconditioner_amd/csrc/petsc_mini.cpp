@@ -705,6 +705,8 @@ extern "C" PetscErrorCode VecSetValues(Vec v, PetscInt n, const PetscInt* idx, c
     if (idx[k] >= v->N) return ERR(PETSC_ERR_ARG_OUTOFRANGE, "index out of range");
     const PetscInt i = idx[k] - v->rstart;  // global row -> local
     if (i < 0 || i >= v->n) {  // another rank's row: stashed until VecAssemblyBegin/End
+      if (v->st_idx.size() >= ((size_t)1 << 27))
+        return ERR(PETSC_ERR_MEM, "VecSetValues: 2^27 off-rank entries stashed without VecAssemblyBegin");
       v->st_idx.push_back(idx[k]);
       v->st_val.push_back(tocd(y[k]));
       v->st_add.push_back(mode == ADD_VALUES);

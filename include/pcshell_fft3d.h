@@ -129,13 +129,21 @@ FFTPrecTransportContext *FFTPrecTransportContextLast(void);
 #ifdef __cplusplus
 }
 
+#include <cstddef>
+#include <type_traits>
+
 /* The reference's own 13-argument form, `Mesh srcMesh` by value (src/PCSHELLFft_3D.hxx:27-41),
  * so a reference caller compiles unchanged against this header.  The mesh is not read (the
  * reference does not read it either, src/PCSHELLFft_3D.cxx:101-151); the context lands in the
  * library slot FFTPrecTransportContextLast(), where a caller can pick it up -- the reference
  * writes it through an uninitialised pointer and loses it.  A call
- * whose last argument is an FFTPrecTransportContext * resolves to the C function above. */
-template <class MeshT>
+ * whose last argument is an FFTPrecTransportContext * resolves to the C function above; the
+ * template takes class types only, so NULL / 0 / nullptr there still reach the C function and its
+ * PETSC_ERR_ARG_NULL check.  The slot is one process-wide object (not thread-safe; each call
+ * overwrites it). */
+template <class MeshT, typename std::enable_if<!std::is_pointer<MeshT>::value && !std::is_integral<MeshT>::value &&
+                                                   !std::is_same<MeshT, std::nullptr_t>::value,
+                                               int>::type = 0>
 inline PetscErrorCode getFFTPrec3DContext(PetscInt ndim, PetscScalar dt, PetscInt nbCells, PetscScalar a_x,
                                           PetscScalar a_y, PetscScalar a_z, PetscScalar Xmin, PetscScalar Ymin,
                                           PetscScalar Zmin, PetscScalar Xmax, PetscScalar Ymax, PetscScalar Zmax,

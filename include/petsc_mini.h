@@ -14,8 +14,8 @@
  *     all-reduce callbacks, e.g. torch.distributed) or PetscMiniCommCreateRCCL (an RCCL
  *     communicator, one process per GPU).  Vecs made on such a communicator hold the
  *     PETSC_DECIDE block of rows of their rank; VecDot / VecNorm / VecMDot reduce over it;
- *     VecSetValues keeps the entries of the calling rank's rows only (PETSc would stash the
- *     others for their owners);
+ *     VecSetValues applies the calling rank's rows at once and stashes the others, as PETSc
+ *     does, until VecAssemblyBegin/End delivers them (see VecAssemblyBegin);
  *   - Vec is either host-only (VECSEQ) or device-resident with a host mirror (VECSEQHIP),
  *     with PETSc's offload mask semantics for the Get/Restore pairs;
  *   - Mat supports MATSHELL (user operations), MATSEQAIJ (CSR, device SpMV) and the FFT
@@ -216,6 +216,13 @@ PetscErrorCode VecSet(Vec v, PetscScalar alpha);
 PetscErrorCode VecSetValue(Vec v, PetscInt i, PetscScalar value, InsertMode mode);
 PetscErrorCode VecSetValues(Vec v, PetscInt n, const PetscInt *idx, const PetscScalar *y, InsertMode mode);
 PetscErrorCode VecGetValues(Vec v, PetscInt n, const PetscInt *idx, PetscScalar *y);
+/* VecSetValues on a Vec of several ranks: rows of other ranks go to a per-Vec stash (no size
+ * limit below PETSC_ERR_MEM at 2^27 entries) that only VecAssemblyBegin empties.
+ * VecAssemblyBegin is COLLECTIVE on the Vec's communicator, as in PETSc: every rank must call it
+ * (two all-reduces and one all-to-all), stash or no stash; a call on some ranks only blocks in
+ * the first collective (with torch.distributed callbacks: until the process group's timeout).
+ * VecAssemblyEnd completes the pair and communicates nothing.  On one rank both only clear the
+ * stash. */
 PetscErrorCode VecAssemblyBegin(Vec v);
 PetscErrorCode VecAssemblyEnd(Vec v);
 PetscErrorCode VecCopy(Vec x, Vec y);
@@ -308,6 +315,8 @@ PetscErrorCode KSPSetInitialGuessNonzero(KSP ksp, PetscBool flg);
 PetscErrorCode KSPGetPC(KSP ksp, PC *pc);
 PetscErrorCode KSPSetOperators(KSP ksp, Mat A, Mat P);
 PetscErrorCode KSPSetUp(KSP ksp);
+/* GMRES with a zero initial guess does not zero x first (the first update overwrites it): after
+ * an error return x is undefined (its old contents, or b when b == x), unlike PETSc. */
 PetscErrorCode KSPSolve(KSP ksp, Vec b, Vec x);
 PetscErrorCode KSPGetConvergedReason(KSP ksp, KSPConvergedReason *reason);
 PetscErrorCode KSPGetIterationNumber(KSP ksp, PetscInt *its);

@@ -172,9 +172,14 @@ int main() {
   const FFTPrecTransportContext *c = FFTPrecTransportContextLast();
   FFTPrecTransportContext mine;
   PetscErrorCode ierr2 = getFFTPrec3DContext(2, 1.0, 100, 1.0, 1.0, 1.0, 0, 0, 0, 1, 1, 1, &mine);
-  std::printf("%d %d %ld %ld %ld %.17g %.17g %.17g %ld %ld\n", (int)ierr, (int)ierr2, (long)c->n_x, (long)c->n_y,
-              (long)c->n_z, re(c->lambda_x), re(c->lambda_y), re(c->lambda_z),
-              (long)mine.n_x, (long)mine.n_z);
+  // ADVICE r04: NULL / 0 / nullptr as the last argument reach the C function's NULL check, not
+  // the Mesh template (which would succeed and write the library slot)
+  PetscErrorCode e0 = getFFTPrec3DContext(3, 0.5, 64, 1.0, 1.0, 1.0, 0, 0, 0, 1, 1, 1, NULL);
+  PetscErrorCode e1 = getFFTPrec3DContext(3, 0.5, 64, 1.0, 1.0, 1.0, 0, 0, 0, 1, 1, 1, 0);
+  PetscErrorCode e2 = getFFTPrec3DContext(3, 0.5, 64, 1.0, 1.0, 1.0, 0, 0, 0, 1, 1, 1, nullptr);
+  std::printf("%d %d %ld %ld %ld %.17g %.17g %.17g %ld %ld %d %d %d %ld\n", (int)ierr, (int)ierr2, (long)c->n_x,
+              (long)c->n_y, (long)c->n_z, re(c->lambda_x), re(c->lambda_y), re(c->lambda_z),
+              (long)mine.n_x, (long)mine.n_z, (int)e0, (int)e1, (int)e2, (long)FFTPrecTransportContextLast()->n_x);
   return 0;
 }
 """
@@ -202,4 +207,6 @@ def test_reference_caller_compiles_unchanged(tmp_path, real):
     assert out[:5] == ["0", "0", "16", "16", "16"]
     # lambda_d = a_d dt (max - min) / n (src/PCSHELLFft_3D.cxx:146-148)
     np.testing.assert_allclose([float(v) for v in out[5:8]], [1 * .5 * 1 / 16, 2 * .5 * 2 / 16, 3 * .5 * 4 / 16])
-    assert out[8:] == ["10", "1"]
+    assert out[8:10] == ["10", "1"]
+    assert out[10:13] == ["85", "85", "85"]  # PETSC_ERR_ARG_NULL
+    assert out[13] == "16"  # the slot still holds the Mesh call's context
