@@ -9,6 +9,29 @@ namespace cfp {
 #define BLAS_THREADS 256
 #define RED_BLOCKS 1024
 
+// Store policy of the Krylov-vector kernels (measured inside config 3's GMRES loop, DESIGN.md
+// f1): bit 0 = the SpMV's y, bit 1 = the MAXPY / AXPY results, stored non-temporally.
+#ifndef CFP_BLAS_NT
+#define CFP_BLAS_NT 0
+#endif
+typedef double bdv2 __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ void bstore(cd* p, cd v) {
+  if constexpr (NT) {
+    bdv2 w;
+    w.x = v.x;
+    w.y = v.y;
+    __builtin_nontemporal_store(w, reinterpret_cast<bdv2*>(p));
+  } else {
+    *p = v;
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void bstore(double* p, double v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 __device__ __forceinline__ cd badd(cd a, cd b) { return make_cd(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ cd bmul(cd a, cd b) { return make_cd(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
 __device__ __forceinline__ double badd(double a, double b) { return a + b; }
@@ -42,7 +65,9 @@ template <class T> __global__ void k_shift(T* x, T a, i64 n) { GRID_LOOP(i, n) x
 template <class T> __global__ void k_copy(T* y, const T* x, i64 n) { GRID_LOOP(i, n) y[i] = x[i]; }
 template <class T> __global__ void k_scal(T* x, T a, i64 n) { GRID_LOOP(i, n) x[i] = bmul(a, x[i]); }
 // y = y + a x
-template <class T> __global__ void k_axpy(T* y, T a, const T* x, i64 n) { GRID_LOOP(i, n) y[i] = badd(y[i], bmul(a, x[i])); }
+template <class T> __global__ void k_axpy(T* y, T a, const T* x, i64 n) {
+  GRID_LOOP(i, n) bstore<(CFP_BLAS_NT & 2) != 0>(y + i, badd(y[i], bmul(a, x[i])));
+}
 // y = x + b y
 template <class T> __global__ void k_aypx(T* y, T b, const T* x, i64 n) { GRID_LOOP(i, n) y[i] = badd(x[i], bmul(b, y[i])); }
 // w = a x + y
@@ -74,7 +99,7 @@ __global__ void __launch_bounds__(BLAS_THREADS) k_maxpy(T* y, int k, MVCoefT<T> 
   GRID_LOOP(i, n) {
     T acc = OW ? bzero<T>() : y[i];
     for (int j = 0; j < k; ++j) acc = badd(acc, bmul(a.a[j], xs.p[j][i]));
-    y[i] = acc;
+    bstore<(CFP_BLAS_NT & 2) != 0>(y + i, acc);
     if (NRM) s2 += babs2(acc);
   }
   if constexpr (NRM) {
@@ -166,8 +191,8 @@ __device__ __forceinline__ void spmv_acc(cd a, cd b, double& ax, double& ay) {
   ay = fma(a.x, b.y, fma(a.y, b.x, ay));
 }
 __device__ __forceinline__ void spmv_acc(double a, double b, double& ax, double&) { ax = fma(a, b, ax); }
-__device__ __forceinline__ void spmv_store(cd* y, double ax, double ay) { *y = make_cd(ax, ay); }
-__device__ __forceinline__ void spmv_store(double* y, double ax, double) { *y = ax; }
+__device__ __forceinline__ void spmv_store(cd* y, double ax, double ay) { bstore<(CFP_BLAS_NT & 1) != 0>(y, make_cd(ax, ay)); }
+__device__ __forceinline__ void spmv_store(double* y, double ax, double) { bstore<(CFP_BLAS_NT & 1) != 0>(y, ax); }
 
 template <class T, int L>
 __global__ void __launch_bounds__(BLAS_THREADS) k_csr_spmv_vec(i64 m, const i64* rowptr, const i64* col,

@@ -58,7 +58,7 @@ def main():
         check(lib().cfp_dist_plan_create_external(ctypes.byref(h), n, n, n, P, 0, 0))
         check(lib().cfp_dist_plan_set_work_buffers(h, w.data_ptr(), w2.data_ptr()))
         check(lib().cfp_dist_plan_set_symbol_transport(h, lam))
-        links = min(P - 1, 7)
+        links = max(1, min(P - 1, 7))
         x_us = 16 * loc * (P - 1) / P / (links * LINK_GBS * 1e9) * 1e6  # one all-to-all
         for name, sched in (("three", 2), ("five", 1)):
             if lib().cfp_dist_plan_set_schedule(h, sched) != 0:
