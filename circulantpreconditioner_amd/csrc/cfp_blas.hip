@@ -7,7 +7,19 @@
 namespace cfp {
 
 #define BLAS_THREADS 256
-#define RED_BLOCKS 1024
+// Workgroups of the synchronous reductions (dot / norm), the multi-dot and the MAXPY sweep
+// (whose norm rides in it).  r05 A/B inside config 3's GMRES (profiles/r05d_gmres_reduce_ab.txt):
+// the dot / norm at 2048 and the multi-dot at 1024 workgroups stream at 5.8 / 5.7 TB/s (from
+// 5.1 / 4.4 at 1024 / 512); the MAXPY loses at 2048 (171 against 155 us), so it keeps 1024.
+#ifndef RED_BLOCKS
+#define RED_BLOCKS 2048
+#endif
+#ifndef MDOT_BLOCKS
+#define MDOT_BLOCKS 1024
+#endif
+#ifndef MAXPY_BLOCKS
+#define MAXPY_BLOCKS 1024
+#endif
 
 // Store policy of the Krylov-vector kernels (measured inside config 3's GMRES loop, DESIGN.md
 // f1): bit 0 = the SpMV's y, bit 1 = the MAXPY / AXPY results, stored non-temporally.
@@ -339,11 +351,11 @@ static hipError_t maxpy_t(T* y, int k, const T* a, const T* const* xs, i64 n, bo
                           hipStream_t s) {
   static thread_local Partials part;
   if (norm2) {
-    hipError_t e = part.get(RED_BLOCKS);
+    hipError_t e = part.get(MAXPY_BLOCKS);
     if (e != hipSuccess) return e;
   }
   unsigned nb = nblocks(n);
-  if (nb > RED_BLOCKS) nb = RED_BLOCKS;
+  if (nb > MAXPY_BLOCKS) nb = MAXPY_BLOCKS;
   if (n > 0) {
     for (int j0 = 0; j0 < (k > 0 ? k : 1); j0 += MV_MAX) {
       const int kk = k - j0 < MV_MAX ? (k - j0 > 0 ? k - j0 : 0) : MV_MAX;
@@ -438,7 +450,7 @@ hipError_t blas_norm(const double* x, i64 n, int type, double* val, hipStream_t 
 template <class T>
 static hipError_t mdot_t(const T* x, int k, const T* const* ys, i64 n, double* vals, hipStream_t s) {
   static thread_local Partials part;
-  const int NB = 512;
+  const int NB = MDOT_BLOCKS;
   hipError_t e = part.get(2 * MDOT_K * NB);
   if (e != hipSuccess) return e;
   for (int j0 = 0; j0 < k; j0 += MDOT_K) {
