@@ -25,6 +25,12 @@ namespace cfp {
 namespace {
 
 constexpr int WNX = 128, WNC = 4, WW = WNX * WNC;  // cells per row, comps, values per row
+// TWR: the four-step twiddle W_128^{y2 k1} rides in P1w's stores and P3w's loads instead of P2w's
+// loads and stores (it is constant along a P1w row and uniform per P3w slot)
+#ifndef CFP_WAVE_TWR
+#define CFP_WAVE_TWR 0
+#endif
+constexpr bool kWaveTwr = CFP_WAVE_TWR != 0;
 constexpr int WN1 = 16, WN2 = 8;                   // y = y2 + WN2 y1
 constexpr i64 WPLANE = (i64)WNX * WW;              // values per z-plane
 
@@ -66,6 +72,10 @@ k_wtp_rows(const cd* in, cd* out, WTPArgs a, int nunits) {
       if (INV) {
 #pragma unroll
         for (int m = 0; m < PTS; ++m) v[m] = cconj(v[m]);
+        if constexpr (kWaveTwr) {  // slot m = k1: W_128^{y2 m}, uniform over the workgroup
+#pragma unroll
+          for (int m = 1; m < PTS; ++m) v[m] = cmul(v[m], a.tw[(y2 * m) & (WNX - 1)]);
+        }
       }
       dft_any<PTS>(v);  // v[m]: k1 = m (forward) / y1 = m (inverse)
     }
@@ -96,8 +106,14 @@ k_wtp_rows(const cd* in, cd* out, WTPArgs a, int nunits) {
       const int comp = launder(comp0), tx = launder(tx0), k = launder(k0);
       const double sc = a.scale, sy = INV ? -sc : sc;
       cd* dst = out + z * WPLANE + (i64)(y2 + WN2 * k) * WW + WNC * tx + comp;
+      if (kWaveTwr && !INV) {  // row k1 = k: W_128^{y2 k} (P1w scale is 1)
+        const cd w = a.tw[(y2 * k) & (WNX - 1)];
 #pragma unroll
-      for (int t = 0; t < PTS; ++t) gstore<FLAGS>(dst + WNC * TR * t, make_cd(v[t].x * sc, v[t].y * sy));
+        for (int t = 0; t < PTS; ++t) gstore<FLAGS>(dst + WNC * TR * t, cmul(v[t], w));
+      } else {
+#pragma unroll
+        for (int t = 0; t < PTS; ++t) gstore<FLAGS>(dst + WNC * TR * t, make_cd(v[t].x * sc, v[t].y * sy));
+      }
     }
     lds_barrier();  // the next unit's first exchange overwrites LDS
   }
@@ -501,9 +517,11 @@ k_wtp_mid_ct2(cd* data, WTPArgs a, int nunits) {
         }
       }
       __builtin_amdgcn_sched_barrier(0);
-      const cd w = tw_y(u, c);
+      if constexpr (!kWaveTwr) {
+        const cd w = tw_y(u, c);
 #pragma unroll
-      for (int m = 0; m < PTS; ++m) v[m] = cmul(v[m], w);
+        for (int m = 0; m < PTS; ++m) v[m] = cmul(v[m], w);
+      }
     }
     {
       // 8-point DIF over y2 (map B lane bits 3, 1, 0), branch-free, between the z FFT's exchange and
@@ -618,6 +636,9 @@ k_wtp_mid_ct2(cd* data, WTPArgs a, int nunits) {
 #pragma unroll
         for (int m = 0; m < PTS; ++m) acc += v[m].x * w.x + v[m].y;
         if (acc == 1.2345e300) dst[0] = make_cd(acc, 0.0);  // keeps the work live, never true
+      } else if constexpr (kWaveTwr) {
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) dst[zs * TZ * m] = cconj(v[m]);
       } else {
 #pragma unroll
         for (int m = 0; m < PTS; ++m) dst[zs * TZ * m] = cconj(cmul(v[m], w));

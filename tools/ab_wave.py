@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Block PCApply/s of the 128^3 wave plan (config 4) in this tree, with its 3-sweep output checked
+against the 5-sweep schedule -- one line of JSON, for same-box A/Bs of two library builds
+(run it from each tree's root).  GPU only; measurement tool.
+
+    python tools/ab_wave.py [--iters 1000] [--tag NAME]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.getcwd()
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=1000)
+    ap.add_argument("--tag", default=os.path.basename(ROOT))
+    a = ap.parse_args()
+    import torch
+    import circulantpreconditioner_amd as cp
+    from circulantpreconditioner_amd import wave as W
+    wp = W.WavePlan((128, 128, 128)).set_symbol((0.079, 0.079, 0.079))
+    b = torch.empty(4 * 128 ** 3, dtype=torch.complex128, device="cuda")
+    cp.fill_uniform(b, 20251017)
+    x = torch.empty_like(b)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.3:  # settle the clocks
+        for _ in range(8):
+            wp.apply(b, out=x)
+        torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.iters):
+        wp.apply(b, out=x)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / a.iters
+    stage = [round(v, 5) for v in wp.time_passes(b, x, iters=50)] if hasattr(wp, "time_passes") else None
+    wp.set_schedule("five")
+    x5 = wp.apply(b)
+    d = float(torch.linalg.vector_norm(x5 - x) / torch.linalg.vector_norm(x5))
+    print(json.dumps({"tag": a.tag, "value": round(1e3 / ms, 1), "ms": round(ms, 5), "stage_ms": stage,
+                      "rel_diff_vs_five": d, "ok": d < 1e-12}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
