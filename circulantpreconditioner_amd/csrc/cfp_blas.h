@@ -47,6 +47,10 @@ hipError_t blas_dot(const cd* x, const cd* y, i64 n, cd* val, hipStream_t s);
 hipError_t blas_norm(const cd* x, i64 n, int type, double* val, hipStream_t s);
 // vals[j] = ys[j]^H x  (ys: host array of k device pointers)
 hipError_t blas_mdot(const cd* x, int k, const cd* const* ys, i64 n, cd* vals, hipStream_t s);
+// classical Gram-Schmidt in one host round trip: dots[j] = ys[j]^H w, w += sum_j scale[j] dots[j]
+// ys[j] (coefficients formed on the device), norm2 = |w|^2; k <= MV_MAX (scale: host, real)
+hipError_t blas_mdot_maxpy_norm(cd* w, int k, const cd* const* ys, const double* scale, i64 n, cd* dots,
+                                double* norm2, hipStream_t s);
 
 // the same on real vectors (PetscScalar = double), plus the scale and the divide that the
 // complex build takes from cfp_kernels.hip (launch_scale, launch_pointwise_divide)
@@ -67,4 +71,6 @@ hipError_t blas_csr_spmv(i64 m, i64 nnz, const i64* rowptr, const i64* col, cons
 hipError_t blas_dot(const double* x, const double* y, i64 n, double* val, hipStream_t s);
 hipError_t blas_norm(const double* x, i64 n, int type, double* val, hipStream_t s);
 hipError_t blas_mdot(const double* x, int k, const double* const* ys, i64 n, double* vals, hipStream_t s);
+hipError_t blas_mdot_maxpy_norm(double* w, int k, const double* const* ys, const double* scale, i64 n, double* dots,
+                                double* norm2, hipStream_t s);
 }  // namespace cfp

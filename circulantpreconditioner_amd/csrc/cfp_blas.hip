@@ -184,6 +184,47 @@ __global__ void k_mdot(const T* x, int k, MVPtrsT<T> ys, i64 n, double* partial)
   }
 }
 
+// The dots of several k_mdot launches (chunks of MDOT_K vectors, partials of chunk c at
+// partial + c 2 MDOT_K MDOT_BLOCKS) summed on the device: one wave per output value (re or im
+// of dot j), lanes over the nb workgroups' partials, then a wave sum -- deterministic.
+__global__ void __launch_bounds__(1024) k_mdot_finish(const double* partial, int nb, int k, double* dots) {
+  const int o = blockIdx.x * 16 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (o >= 2 * k) return;  // whole waves
+  const int j = o >> 1, c = j / MDOT_K;
+  const double* p = partial + (size_t)c * 2 * MDOT_K * MDOT_BLOCKS + 2 * (j % MDOT_K) + (o & 1);
+  double s = 0.0;
+  for (int q = lane; q < nb; q += 64) s += p[(size_t)q * 2 * MDOT_K];
+  s = wave_sum(s);
+  if (lane == 0) dots[o] = s;
+}
+
+// y += sum_j scale_j dots_j xs_j with the dots on the device (k_mdot_finish), |y|^2 partials:
+// the MAXPY of classical Gram-Schmidt without the host round trip between the dots and the update
+__device__ __forceinline__ cd dcoef(const double* dots, double sc, int j, cd) {
+  return make_cd(sc * dots[2 * j], sc * dots[2 * j + 1]);
+}
+__device__ __forceinline__ double dcoef(const double* dots, double sc, int j, double) { return sc * dots[2 * j]; }
+template <class T>
+__global__ void __launch_bounds__(BLAS_THREADS) k_maxpy_dc(T* y, int k, MVCoefT<double> scale, const double* dots,
+                                                            MVPtrsT<T> xs, i64 n, double* partial) {
+  double s2 = 0.0;
+  GRID_LOOP(i, n) {
+    T acc = y[i];
+    for (int j = 0; j < k; ++j) acc = badd(acc, bmul(dcoef(dots, scale.a[j], j, acc), xs.p[j][i]));
+    bstore<(CFP_BLAS_NT & 2) != 0>(y + i, acc);
+    s2 += babs2(acc);
+  }
+  __shared__ double sm[BLAS_THREADS / 64];
+  s2 = wave_sum(s2);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s2;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int q = 0; q < BLAS_THREADS / 64; ++q) t += sm[q];
+    partial[blockIdx.x] = t;
+  }
+}
+
 // CSR y = A x, one thread per row (rows of about one nonzero)
 template <class T>
 __global__ void k_csr_spmv(i64 m, const i64* rowptr, const i64* col, const T* val, const T* x, T* y) {
@@ -478,6 +519,58 @@ static hipError_t mdot_t(const T* x, int k, const T* const* ys, i64 n, double* v
 }
 hipError_t blas_mdot(const cd* x, int k, const cd* const* ys, i64 n, cd* vals, hipStream_t s) {
   return mdot_t(x, k, ys, n, (double*)vals, s);
+}
+
+// dots_j = ys_j^H w, w += sum_j scale_j dots_j ys_j, |w|^2: multi-dot launches, the device finish,
+// the MAXPY on the device dots, one copy back and one host wait (k <= MV_MAX)
+template <class T>
+static hipError_t mdot_maxpy_norm_t(T* w, int k, const T* const* ys, const double* scale, i64 n, double* dots,
+                                    double* norm2, hipStream_t s) {
+  if (k < 1 || k > MV_MAX) return hipErrorInvalidValue;
+  static thread_local Partials part;  // [mdot chunks][2 MDOT_K][MDOT_BLOCKS] | dots [2 MV_MAX] | norm [MAXPY_BLOCKS]
+  const int chunks = (MV_MAX + MDOT_K - 1) / MDOT_K;
+  const size_t mlen = (size_t)chunks * 2 * MDOT_K * MDOT_BLOCKS, dlen = 2 * MV_MAX;
+  hipError_t e = part.get(mlen + dlen + MAXPY_BLOCKS);
+  if (e != hipSuccess) return e;
+  unsigned nb = nblocks(n);
+  if (nb > (unsigned)MDOT_BLOCKS) nb = MDOT_BLOCKS;
+  for (int j0 = 0; j0 < k; j0 += MDOT_K) {
+    const int kk = k - j0 < MDOT_K ? k - j0 : MDOT_K;
+    MVPtrsT<T> p;
+    for (int j = 0; j < kk; ++j) p.p[j] = ys[j0 + j];
+    hipLaunchKernelGGL(k_mdot<T>, dim3(nb), dim3(BLAS_THREADS), 0, s, (const T*)w, kk, p, n,
+                       part.d + (size_t)(j0 / MDOT_K) * 2 * MDOT_K * MDOT_BLOCKS);
+  }
+  double* dd = part.d + mlen;
+  hipLaunchKernelGGL(k_mdot_finish, dim3((2 * k + 15) / 16), dim3(1024), 0, s, part.d, (int)nb, k, dd);
+  MVCoefT<double> sc;
+  MVPtrsT<T> p;
+  for (int j = 0; j < k; ++j) { sc.a[j] = scale[j]; p.p[j] = ys[j]; }
+  unsigned mb = nblocks(n);
+  if (mb > MAXPY_BLOCKS) mb = MAXPY_BLOCKS;
+  hipLaunchKernelGGL(k_maxpy_dc<T>, dim3(mb), dim3(BLAS_THREADS), 0, s, w, k, sc, (const double*)dd, p, n, dd + dlen);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = hipMemcpyAsync(part.h + mlen, dd, sizeof(double) * (dlen + mb), hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) return e;
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return e;
+  for (int o = 0; o < 2 * k; ++o) dots[o] = part.h[mlen + o];
+  double t = 0.0;
+  for (unsigned q = 0; q < mb; ++q) t += part.h[mlen + dlen + q];
+  *norm2 = t;
+  return hipSuccess;
+}
+hipError_t blas_mdot_maxpy_norm(cd* w, int k, const cd* const* ys, const double* scale, i64 n, cd* dots,
+                                double* norm2, hipStream_t s) {
+  return mdot_maxpy_norm_t(w, k, ys, scale, n, (double*)dots, norm2, s);
+}
+hipError_t blas_mdot_maxpy_norm(double* w, int k, const double* const* ys, const double* scale, i64 n, double* dots,
+                                double* norm2, hipStream_t s) {
+  std::vector<double> v(2 * (size_t)(k > 0 ? k : 1));
+  hipError_t e = mdot_maxpy_norm_t(w, k, ys, scale, n, v.data(), norm2, s);
+  for (int j = 0; j < k; ++j) dots[j] = v[2 * (size_t)j];
+  return e;
 }
 hipError_t blas_mdot(const double* x, int k, const double* const* ys, i64 n, double* vals, hipStream_t s) {
   std::vector<double> v(2 * (size_t)(k > 0 ? k : 1));

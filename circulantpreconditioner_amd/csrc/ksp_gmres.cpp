@@ -331,16 +331,14 @@ extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
         PetscCall(pc_apply(k, V[j], k->t));
         PetscCall(MatMult(k->A, k->t, V[j + 1]));
       }
-      // classical Gram-Schmidt: h_ij = v_i^H w, w -= sum h_ij v_i, and |w|, in two sweeps
+      // classical Gram-Schmidt: h_ij = v_i^H w, w -= sum h_ij v_i, and |w|, in two sweeps and
+      // one host wait (the MAXPY coefficients -sg_i^2 u_i^H w' are formed on the device)
       std::vector<PetscScalar> hv((size_t)j + 1);
-      PetscCall(VecMDot(V[j + 1], j + 1, V, hv.data()));
-      std::vector<PetscScalar> neg((size_t)j + 1);
-      for (PetscInt i = 0; i <= j; ++i) {
-        h(i, j) = sg[(size_t)i] * sg[(size_t)j] * hv[(size_t)i];
-        neg[(size_t)i] = -(sg[(size_t)i] * sg[(size_t)i]) * hv[(size_t)i];
-      }
+      std::vector<PetscReal> negsq((size_t)j + 1);
+      for (PetscInt i = 0; i <= j; ++i) negsq[(size_t)i] = -(sg[(size_t)i] * sg[(size_t)i]);
       PetscReal hn;
-      PetscCall(VecMiniMAXPYNorm(V[j + 1], j + 1, neg.data(), V, PETSC_FALSE, &hn));
+      PetscCall(VecMiniMDotMAXPYNorm(V[j + 1], j + 1, negsq.data(), V, hv.data(), &hn));
+      for (PetscInt i = 0; i <= j; ++i) h(i, j) = sg[(size_t)i] * sg[(size_t)j] * hv[(size_t)i];
       hn *= sg[(size_t)j];  // |w| = sg_j |w''|
       h(j + 1, j) = hn;
       // happy breakdown test of KSPGMRESCycle: hn < min(hn / |rs_j|, haptol = 1e-30)

@@ -1036,6 +1036,38 @@ extern "C" PetscErrorCode VecMiniMAXPYNorm(Vec y, PetscInt nv, const PetscScalar
   return PETSC_SUCCESS;
 }
 
+// Classical Gram-Schmidt in one call: dots[j] = V[j]^H w, w += sum_j scale[j] dots[j] V[j],
+// *norm = |w|.  Device Vecs of one rank, nv <= 32: the coefficients are formed on the device
+// between the multi-dot and the MAXPY, so the step waits for the host once (cfp_blas.hip);
+// otherwise VecMDot (its all-reduce on several ranks) and VecMiniMAXPYNorm.
+extern "C" PetscErrorCode VecMiniMDotMAXPYNorm(Vec w, PetscInt nv, const PetscReal scale[], Vec V[],
+                                               PetscScalar dots[], PetscReal* norm) {
+  VCHK(w);
+  if (nv <= 0) return ERR(PETSC_ERR_ARG_OUTOFRANGE, "nv must be >= 1");
+  bool dev = w->hip && w->nranks == 1 && nv <= MV_MAX;
+  for (PetscInt j = 0; j < nv; ++j) {
+    VCHK(V[j]);
+    PetscCall(same_size(w, V[j]));
+    dev = dev && V[j]->hip;
+  }
+  if (!dev) {
+    PetscCall(VecMDot(w, nv, V, dots));
+    std::vector<PetscScalar> a((size_t)nv);
+    for (PetscInt j = 0; j < nv; ++j) a[(size_t)j] = scale[j] * dots[j];
+    return VecMiniMAXPYNorm(w, nv, a.data(), V, PETSC_FALSE, norm);
+  }
+  std::vector<const VS*> ys((size_t)nv);
+  for (PetscInt j = 0; j < nv; ++j) PetscCall(dev_read(V[j], &ys[(size_t)j]));
+  VS* wd;
+  PetscCall(dev_rw(w, &wd));
+  std::vector<VS> r((size_t)nv);
+  double s2 = 0.0;
+  HIPK(cfp::blas_mdot_maxpy_norm(wd, (int)nv, ys.data(), scale, w->n, r.data(), &s2, g_stream));
+  for (PetscInt j = 0; j < nv; ++j) dots[j] = to_scalar(C(r[(size_t)j]).real(), C(r[(size_t)j]).imag());
+  if (norm) *norm = std::sqrt(s2);
+  return PETSC_SUCCESS;
+}
+
 extern "C" PetscErrorCode VecDuplicateVecs(Vec v, PetscInt m, Vec* V[]) {
   VCHK(v);
   if (!V) return ERR(PETSC_ERR_ARG_NULL, "NULL output");

@@ -249,6 +249,11 @@ PetscErrorCode VecMiniSynchronize(Vec v);
 /* y = (overwrite ? 0 : y) + sum alpha_i x_i and, if norm != NULL, ||y||_2 over the Vec's ranks,
  * in one sweep of y (the stand-in GMRES's orthogonalisation + norm, and its solution update
  * into a zero x without a VecSet); not in PETSc */
+/* Classical Gram-Schmidt step of the stand-in GMRES: dots[j] = V[j]^H w (PETSc's VecMDot), then
+ * w += sum_j scale[j] dots[j] V[j] and *norm = |w| -- on one rank's device Vecs (nv <= 32) with the
+ * coefficients formed on the device, one host wait per call. */
+PetscErrorCode VecMiniMDotMAXPYNorm(Vec w, PetscInt nv, const PetscReal scale[], Vec V[], PetscScalar dots[],
+                                    PetscReal *norm);
 PetscErrorCode VecMiniMAXPYNorm(Vec y, PetscInt nv, const PetscScalar alpha[], Vec x[], PetscBool overwrite,
                                 PetscReal *norm);
 
