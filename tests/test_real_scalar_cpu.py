@@ -68,3 +68,34 @@ def test_real_host_gmres_pcnone():
     assert np.linalg.norm(vx.array() - xs) <= 1e-10 * np.linalg.norm(xs)
     R.PetscCall(L.KSPDestroy(ctypes.byref(ksp)))
     R.PetscCall(L.MatDestroy(ctypes.byref(M)))
+
+
+@pytest.mark.parametrize("dims", [(8, 6, 4), (9, 5, 7), (1, 4, 4), (2, 3, 3), (16, 1, 8)])
+def test_half_spectrum_row_padding_is_c2r(dims):
+    """The identity the real-scalar slab path rests on (pcshell_fft3d_real.cpp, cfp_half_spectrum_pad):
+    for ANY half spectrum H ([nz][ny][nx/2 + 1]), Re IDFT(pad(H)) -- pad: weight 1 on kx = 0 and,
+    nx even, nx/2, weight 2 on the other kx <= nx/2, 0 above -- equals Re IDFT of H's Hermitian
+    extension (FFTW's c2r), and it needs no value from another z-plane."""
+    nx, ny, nz = dims
+    M = nx // 2 + 1
+    rng = np.random.default_rng(3)
+    H = rng.standard_normal((nz, ny, M)) + 1j * rng.standard_normal((nz, ny, M))
+    ext = np.empty((nz, ny, nx), complex)
+    ext[..., :M] = H
+    for kx in range(M, nx):
+        ext[:, :, kx] = np.conj(H[(-np.arange(nz)) % nz][:, (-np.arange(ny)) % ny, nx - kx])
+    pad = np.zeros((nz, ny, nx), complex)
+    w = np.full(M, 2.0)
+    w[0] = 1.0
+    if nx % 2 == 0:
+        w[M - 1] = 1.0
+    pad[..., :M] = H * w
+    a = np.fft.ifftn(ext).real
+    b = np.fft.ifftn(pad).real
+    assert np.abs(a - b).max() <= 1e-13 * max(1.0, np.abs(a).max())
+    # and for a Hermitian-consistent H (the r2c of real data) both are FFTW's c2r = N * irfftn
+    x = rng.standard_normal((nz, ny, nx))
+    Hr = np.fft.rfftn(x)
+    padr = np.zeros((nz, ny, nx), complex)
+    padr[..., :M] = Hr * w
+    assert np.abs(np.fft.ifftn(padr).real - x).max() < 1e-13
