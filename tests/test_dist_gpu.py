@@ -7,9 +7,10 @@
   library's kernel segments and the two all-to-alls go through torch.distributed (gloo,
   staged through host memory), so the per-rank plan is exercised across processes.
 * The RCCL executor with world = 1; with more ranks it is exercised by bench.py --gpus N.
-* At 256^3 (AUTO for P <= 4, on request up to P = 16) every rank runs the 3-sweep schedule
-  (x + y1 into the per-peer chunks | y2 + z + symbol + inverses on its k1 rows | inverse),
-  checked against the oracle and against the 5-pass slab schedule.
+* At 256^3 (AUTO for P <= 4, on request up to P = 16) and 512^3 (AUTO for every P | 32, r05)
+  every rank runs the 3-sweep schedule (x + y1 into the per-peer chunks | y2 + z + symbol +
+  inverses on its k1 rows | inverse), checked against the oracle and against the 5-pass slab
+  schedule.
 """
 import os
 import socket
@@ -93,7 +94,7 @@ def test_slab_schedule_rules():
     from circulantpreconditioner_amd.distributed import SlabGroup
     with SlabGroup((64, 64, 64), 2) as g:
         with pytest.raises(CirculantError):
-            g.set_schedule("three")  # 256^3 only
+            g.set_schedule("three")  # 256^3 and 512^3 only
         g.set_schedule("five").set_schedule("auto")
     with SlabGroup((256, 256, 256), 32) as g:  # 8 rows per chunk: below the 16 the 3-sweep P3 reads
         with pytest.raises(CirculantError):
@@ -116,6 +117,25 @@ def case512(oracle):
     b = oracle.c_fill_uniform(512 ** 3, 512)
     ref = oracle.c_solve_3d(oracle.c_build_diag_transport(dims, lam), b, dims)
     return dims, lam, b, ref
+
+
+def test_single_gpu_512_auto_vs_oracle(case512):
+    """the single-GPU 512^3 AUTO path (3 sweeps, N1 = 32 x N2 = 16, its own
+    z-fused symbol tables) against the oracle's full-grid solve, not only by residual; in place too."""
+    import circulantpreconditioner_amd as cp
+    dims, lam, b, ref = case512
+    rd = torch.from_numpy(ref).cuda()
+    tb = torch.from_numpy(b).cuda()
+    with cp.CirculantPlan(dims) as p:
+        p.set_transport_symbol(lam)
+        assert [q["mode"] for q in p.passes()] == ["rows_fwd", "mid_fused", "rows_inv"]
+        x = p.apply(tb)
+        err = float(torch.linalg.vector_norm(x - rd) / torch.linalg.vector_norm(rd))
+        assert err < TOL, err
+        p.apply(tb, out=tb)  # in place (the direct solver's Un, Un)
+        assert torch.equal(tb, x)
+    del rd, tb, x
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("P", [1, 8, 16])
