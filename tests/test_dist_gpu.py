@@ -369,6 +369,35 @@ def test_rccl_single_rank(oracle):
             dist.destroy_process_group()
 
 
+_MISSING_PEER = r"""
+import ctypes, sys, time
+sys.path.insert(0, sys.argv[1])
+from circulantpreconditioner_amd._lib import lib
+L = lib()
+uid = ctypes.create_string_buffer(L.cfp_dist_unique_id_bytes())
+assert L.cfp_dist_get_unique_id(uid) == 0
+h = ctypes.c_void_p()
+t0 = time.perf_counter()
+rc = L.cfp_dist_plan_create_timeout(ctypes.byref(h), 32, 16, 8, 2, 0, uid, 0, 3.0)
+print(rc, bool(h.value), round(time.perf_counter() - t0, 2), L.cfp_last_error().decode(), flush=True)
+"""
+
+
+def test_rccl_missing_peer_times_out():
+    """the plan's communicator is created non-blocking and polled against a
+    deadline, so a rank whose peer never joins gets an error (CFP_ERR_LIB = 76, "timed out")
+    instead of hanging -- here rank 0 of 2 in a process whose rank 1 does not exist.  Run in a
+    child process with its own time limit, so a hang would fail the test, not the session."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", _MISSING_PEER, root], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-3000:]
+    rc, made, secs, msg = p.stdout.strip().split(" ", 3)
+    assert rc == "76" and made == "False" and "timed out" in msg, p.stdout
+    assert float(secs) < 60.0
+
+
 def test_rccl_single_rank_transforms_and_diag(oracle):
     """World 1 through the RCCL executor: the distributed MatMult / MatMultTranspose step lists
     (natural slab in and out) against torch.fft, and the explicit-Diag apply (Diag moved into the
