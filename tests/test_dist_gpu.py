@@ -393,7 +393,7 @@ def test_rccl_missing_peer_times_out():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     p = subprocess.run([sys.executable, "-c", _MISSING_PEER, root], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stderr[-3000:]
-    rc, made, secs, msg = p.stdout.strip().split(" ", 3)
+    rc, made, secs, msg = p.stdout.strip().splitlines()[-1].split(" ", 3)  # (RCCL prints a banner first)
     assert rc == "76" and made == "False" and "timed out" in msg, p.stdout
     assert float(secs) < 60.0
 
