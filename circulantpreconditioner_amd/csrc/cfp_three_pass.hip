@@ -108,8 +108,8 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
   constexpr bool BL = BLK > 0;
   constexpr int BX = BL ? BLK : 1, BW = N2 * BX;  // x per block column, values per block column
   static_assert(!LP || (TY == 2 && TN % 32 == 0), "lane pairs: two threads per column, 32 columns per wave");
-  static_assert(!BL || (TR % BX == 0 && ((N2 == 8 && (BX == 4 || BX == 8)) || (N2 == 16 && BX == 2))),
-                "blocked layout: 4 or 8 x times 8 y2, or 2 x times 16 y2");
+  static_assert(!BL || (TR % BX == 0 && ((N2 == 8 && (BX == 4 || BX == 8)) || (N2 == 16 && (BX == 2 || BX == 8)))),
+                "blocked layout: 4 or 8 x times 8 y2, or 2 or 8 x times 16 y2");
   constexpr int RS = TN + TN / 16;  // padded row stride of the row-mode LDS layout
   constexpr int F = FLAGS | (XS ? F_SPLIT_LDS : 0) | F_LDS_SYNC;
   // F_WAVE_LDS in FLAGS: phase C's row-FFT exchanges wave-local (a row's TR threads are
@@ -243,18 +243,29 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
   }
 }
 
+// PROBE != 0 only in tools/kexp (tp_probe.hip, p2_512.hip, built with CFP_KEXP): timing probes that drop a
+// part of the work (output invalid).  The product library instantiates PROBE = 0 only.
+enum { PR_NO_Y2 = 1, PR_NO_ZMATH = 2, PR_NO_XCHG = 4, PR_NO_LOAD = 8, PR_NO_STORE = 16,
+       PR_PRIO = 32 /* experiment, full work: s_setprio 1 for the second half of the waves */ };
+
 // Persistent over units u = (x-tile, k1); T columns per unit = T/N2 x values times N2 y2.
 // Barriers wait for LDS only, so one unit's stores drain while the next unit loads.
 // N2 = 16 (512^3, r04): one more radix-2 lane stage (lane ^ 8, twiddle W_16^(y2 & 7)) in front of
 // the 8-point one.  XCD: units in xcd_unit order (the host launches whole rounds).
-// BL: the blocked layout of k_tp_rows<.., BLK = XT> (one run of T values per z).
+// BLK: the blocked layout of k_tp_rows<.., BLK> (BLK = XT: one run of T values per z; 512^3 with
+// BLK = 8: the unit's 16 32-byte pieces of a z lie in one contiguous 2 KiB block, shared by the
+// four x tiles of the block, which run under one L2 in XCD order).
 template <int FLAGS, int T, int N2, int TN, int PTS = 16, bool XS = true, int NX = TN, bool XCD = false,
-          bool BL = false>
+          int BLK = 0, int PROBE = 0>
 __global__ void __launch_bounds__(T * (TN / PTS)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid(cd* data, TPArgs a, int nunits) {
+#ifndef CFP_KEXP
+  static_assert(PROBE == 0, "timing probes are built in tools/kexp only");
+#endif
   constexpr int N1 = TN / N2, TZ = TN / PTS, NT = T * TZ, XT = T / N2, NXT = NX / XT;
   constexpr int F = FLAGS | (XS ? F_SPLIT_LDS : 0) | F_LDS_SYNC;
   static_assert(N2 == 4 || N2 == 8 || N2 == 16, "the y2 DFT runs across 4, 8 or 16 lanes");
+  static_assert(BLK == 0 || (BLK % XT == 0 && NX % BLK == 0), "blocks of whole x tiles");
   __shared__ __attribute__((aligned(16))) double lds[T * TN * (XS ? 1 : 2)];
   __shared__ cd tw_l[TN];
   const int tid = threadIdx.x;
@@ -278,8 +289,8 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
     const int xt = u % NXT, k1 = u / NXT;
     q.y2 = c & (N2 - 1);
     q.xk = xt * XT + c / N2;
-    q.col = BL ? data + (i64)NX * N2 * k1 + xt * T + q.y2 * XT + c / N2 + zs * tz
-               : data + q.xk + (i64)NX * (q.y2 + N2 * k1) + zs * tz;
+    q.col = BLK ? data + (i64)NX * N2 * k1 + (q.xk / BLK) * (N2 * BLK) + q.y2 * BLK + q.xk % BLK + zs * tz
+                : data + q.xk + (i64)NX * (q.y2 + N2 * k1) + zs * tz;
     q.w = a.tw[(q.y2 * (a.k1_off + k1)) & (TN - 1)];  // global k1
     q.w8 = a.tw[(TN / 8) * (q.y2 & 3)];
     if constexpr (N2 == 16) q.w16 = a.tw[(TN / 16) * (q.y2 & 7)];
@@ -292,11 +303,13 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
       const Col q = column(u);
 #pragma unroll
       for (int m = 0; m < PTS; ++m) {
-        v[m] = gload<FLAGS>(q.col + zs * TZ * m);
+        if constexpr (PROBE & PR_NO_LOAD) v[m] = make_cd(c0 + m, tz0 + u);
+        else v[m] = gload<FLAGS>(q.col + zs * TZ * m);
       }
 #pragma unroll
       for (int m = 0; m < PTS; ++m) {  // the lane DFT in two sweeps over the slots: fewer live temporaries
         v[m] = cmul(v[m], q.w);
+        if constexpr ((PROBE & PR_NO_Y2) != 0) continue;
         if constexpr (N2 == 16) {  // dft16_dif's first stage
           const cd p = lane_xor8(v[m]);
           v[m] = (q.y2 & 8) ? cmul(csub(p, v[m]), q.w16) : cadd(v[m], p);
@@ -307,12 +320,14 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
         }
       }
 #pragma unroll
-      for (int m = 0; m < PTS; ++m) v[m] = dft4_dif(v[m], q.y2 & 3);  // the lane now holds k2
+      for (int m = 0; m < PTS; ++m)
+        if constexpr (!(PROBE & PR_NO_Y2)) v[m] = dft4_dif(v[m], q.y2 & 3);  // the lane now holds k2
     }
     {
       int c = c0, tz = tz0;
       asm volatile("" : "+v"(c), "+v"(tz));
-      fft_stages<TN, PTS, r0_of(TN, PTS), false, T, F>(v, lds, tw_l, c, tz, true);  // kz = tz + TZ m
+      if constexpr (!(PROBE & PR_NO_ZMATH))
+        fft_stages<TN, PTS, r0_of(TN, PTS), false, T, F>(v, lds, tw_l, c, tz, true);  // kz = tz + TZ m
     }
     {
       int c = c0, tz = tz0;
@@ -322,16 +337,21 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
 #pragma unroll
       for (int m = 0; m < PTS; ++m) {
         const cd d = cadd(cadd(cs, a.axsym[tz + TZ * m]), make_cd(1.0, 0.0));
-        v[m] = cconj(cdiv_sym(v[m], d));
+        v[m] = (PROBE & PR_NO_ZMATH) ? cconj(v[m]) : cconj(cdiv_sym(v[m], d));
       }
-      fft_stages<TN, PTS, r0_of(TN, PTS), false, T, F>(v, lds, tw_l, c, tz, false);
+      if constexpr (!(PROBE & PR_NO_ZMATH)) fft_stages<TN, PTS, r0_of(TN, PTS), false, T, F>(v, lds, tw_l, c, tz, false);
     }
     {
       const Col q = column(u);
 #pragma unroll
-      for (int m = 0; m < PTS; ++m) v[m] = dft4_dit(v[m], q.y2 & 3);
+      for (int m = 0; m < PTS; ++m)
+        if constexpr (!(PROBE & PR_NO_Y2)) v[m] = dft4_dit(v[m], q.y2 & 3);
 #pragma unroll
       for (int m = 0; m < PTS; ++m) {
+        if constexpr ((PROBE & PR_NO_Y2) != 0) {
+          v[m] = cmul(v[m], q.w);
+          continue;
+        }
         if constexpr (N2 >= 8) {  // dft8_dit's last stage
           const cd u = (q.y2 & 4) ? cmul(v[m], q.w8) : v[m];
           const cd p = lane_xor4(u);
@@ -344,8 +364,15 @@ k_tp_mid(cd* data, TPArgs a, int nunits) {
         }
         v[m] = cmul(v[m], q.w);
       }
+      if constexpr (PROBE & PR_NO_STORE) {
+        double acc = 0.0;
 #pragma unroll
-      for (int m = 0; m < PTS; ++m) gstore<FLAGS>(q.col + zs * TZ * m, cconj(v[m]));
+        for (int m = 0; m < PTS; ++m) acc += v[m].x + v[m].y;
+        if (acc == 1.2345e300) q.col[0] = make_cd(acc, 0.0);  // keeps the work live, never true
+      } else {
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) gstore<FLAGS>(q.col + zs * TZ * m, cconj(v[m]));
+      }
     }
     lds_barrier();  // the next unit's first exchange overwrites LDS
   }
@@ -398,10 +425,6 @@ __device__ __forceinline__ void dif_pairs(cd* v, cd w) {
     }
 }
 
-// PROBE != 0 only in tools/kexp (tp_probe.hip, built with CFP_KEXP): timing probes that drop a
-// part of the work (output invalid).  The product library instantiates PROBE = 0 only.
-enum { PR_NO_Y2 = 1, PR_NO_ZMATH = 2, PR_NO_XCHG = 4, PR_NO_LOAD = 8, PR_NO_STORE = 16,
-       PR_PRIO = 32 /* experiment, full work: s_setprio 1 for the second half of the waves */ };
 //
 // PF (prefetch): the exchange buffer is idle from the second exchange's last read to the next
 // unit's first exchange, which is exactly where the next unit's data is needed.  Right after
@@ -1107,16 +1130,21 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
     // columns (128 KiB split exchange) = 2 x times 16 y2, 32-byte runs; units in XCD order so
     // the 4 tiles of a 128-byte line share an L2.  96 N bytes per apply against 160 N.
     // shape.mid = blocked: blocks of 2 x (P2 reads one 512-byte run per z; P1 / P3 in XCD order,
-    // so the 16 y2 units of a plane share their lines' L2); lane64: P1 / P3 phase A through LDS.
-    const bool bl = shape.mid == TP_MID_BLOCKED;
+    // so the 16 y2 units of a plane share their lines' L2); blocked32: blocks of 8 x (P1 / P3
+    // move whole 128-byte lines, P2's 32-byte pieces of a z lie in one 2 KiB block); lane64: P1 /
+    // P3 phase A through LDS.
+    const bool bl = shape.mid == TP_MID_BLOCKED, bl8 = shape.mid == TP_MID_BLOCKED32;
     if (stage == 1) {
       constexpr int units = (512 / 2) * 32;
       const unsigned g = grid_xcd(units, 1);  // whole rounds of a power of two >= 8
       if (g == 0) return hipErrorNotSupported;
-      if (bl) TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 16, true, 512, true, true>), dim3(g), dim3(1024), s, out, a, units);
+      if (bl) TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 16, true, 512, true, 2>), dim3(g), dim3(1024), s, out, a, units);
+      else if (bl8) TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 16, true, 512, true, 8>), dim3(g), dim3(1024), s, out, a, units);
       else TP_LAUNCH((k_tp_mid<0, 32, 16, 512, 16, true, 512, true>), dim3(g), dim3(1024), s, out, a, units);  // NT loads: 204 against 262 /s (r04y)
     } else if (bl) {
       launch_rows<32, 512, 1, 16, true, kRowsLP, 2, true>(stage, in, out, a, s);
+    } else if (bl8) {
+      launch_rows<32, 512, 1, 16, true, kRowsLP, 8>(stage, in, out, a, s);
     } else if (shape.mid == TP_MID_LANE64) {  // A/B: phase A through LDS
       launch_rows<32, 512, 1>(stage, in, out, a, s);
     } else {  // lane-pair phase A (no LDS exchange there)

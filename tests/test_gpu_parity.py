@@ -297,7 +297,7 @@ def test_three_pass_512(cp):
         x5 = plan.apply(b)
         assert float((x5 - x).abs().max() / x5.abs().max()) < 1e-13
         del x5
-        for mid in ("lane64", "blocked", "rowsalt"):  # phase A through LDS; blocks of 2 x; other row-FFT sync
+        for mid in ("lane64", "blocked", "blocked32", "rowsalt"):  # LDS phase A; blocks of 2 / 8 x; other row sync
             plan.set_schedule("three").set_three_pass_shape(0, mid)
             assert float((plan.apply(b) - x).abs().max() / x.abs().max()) < 1e-13
         plan.set_three_pass_shape(0, "default").set_schedule("three")

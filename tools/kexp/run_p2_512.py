@@ -20,7 +20,12 @@ data = torch.randn(N, dtype=torch.complex128, device="cuda")
 tw = torch.from_numpy(np.exp(-2j * np.pi * np.arange(n) / n)).to("cuda")
 colsym = torch.full((n * n,), 0.5 + 0.1j, dtype=torch.complex128, device="cuda")
 axsym = torch.full((n,), 0.25, dtype=torch.complex128, device="cuda")
-NAMES = {0: "product (XCD order, 256 WG)", 1: "NT stores", 2: "128 WG", 3: "64 WG", 4: "blockIdx order"}
+NAMES = {0: "product (XCD order, 256 WG)", 1: "NT stores", 2: "128 WG", 3: "64 WG", 4: "blockIdx order",
+         5: "probe: no WG barriers", 6: "probe: no loads", 7: "probe: no stores", 8: "probe: math + xchg alone",
+         9: "probe: memory alone", 10: "blocks of 8 x: memory alone", 11: "blocks of 8 x",
+         12: "blocks of 2 x: memory alone", 13: "blocks of 2 x"}
+if os.environ.get("P2_WHICH"):
+    NAMES = {int(w): NAMES[int(w)] for w in os.environ["P2_WHICH"].split(",")}
 
 
 def run(w, iters):
