@@ -44,6 +44,14 @@ __device__ __forceinline__ void xbarrier() {
   else __syncthreads();
 }
 
+// blockIdx -> unit of a persistent grid of G workgroups, G a multiple of 8 (the host checks):
+// workgroups reach the XCDs round-robin (blockIdx % 8), and each XCD takes a contiguous eighth
+// of every whole round of G units; a last, partial round keeps blockIdx order
+__device__ __forceinline__ int xcd_round_unit(int it, int G, int n) {
+  const int b = it % G, base = it - b;
+  return base + G <= n ? base + (b & 7) * (G >> 3) + (b >> 3) : it;
+}
+
 // ------------------------------------------------------------------ complex helpers
 __device__ __forceinline__ cd cadd(cd a, cd b) { return make_cd(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ cd csub(cd a, cd b) { return make_cd(a.x - b.x, a.y - b.y); }

@@ -4,6 +4,13 @@
 
 namespace cfp {
 
+// Row sweeps (P1 / P3 of the scalar and wave 3-sweeps) with units in XCD order
+// (r05j-r05l, cfp_three_pass.hip kRowsXCD; the real-data rows keep blockIdx order).
+// -DCFP_ROWS_XCD=0 builds the blockIdx order for A/B.
+#ifndef CFP_ROWS_XCD
+#define CFP_ROWS_XCD 1
+#endif
+
 struct TPArgs {
   const cd* tw;      // W_n[k] = exp(-2 pi i k / n), n = the grid side (128 or 256)
   const cd* colsym;  // separable symbol, z fused: [kx + n ky] = s_x[kx] + s_y[ky] (global ky)

@@ -80,6 +80,14 @@ constexpr int r0_of(int n, int pts) { return n > pts ? r0_of(n / pts, pts) : n; 
 
 }  // namespace
 
+// PROBE != 0 only in tools/kexp (tp_probe.hip, p2_512.hip, rows_512.hip, built with
+// CFP_KEXP): timing probes that drop a
+// part of the work (output invalid).  The product library instantiates PROBE = 0 only.
+enum { PR_NO_Y2 = 1, PR_NO_ZMATH = 2, PR_NO_XCHG = 4, PR_NO_LOAD = 8, PR_NO_STORE = 16,
+       PR_PRIO = 32 /* experiment, full work: s_setprio 1 for the second half of the waves */,
+       PR_ZMAJOR = 64 /* experiment, full work (k_tp_rows): units in z-major order (the units of one
+                         round share y2 and differ in z) */ };
+
 // Persistent: a workgroup walks units blockIdx.x, + gridDim.x, ...  Prefetching the next unit
 // into VGPRs across LDS-only barriers was tried and lost: at 1024 threads the extra registers
 // spill (profiles/r01_schedule_sweep.txt); at 128^3 with 8 points per thread it fits (104
@@ -101,9 +109,12 @@ constexpr int r0_of(int n, int pts) { return n > pts ? r0_of(n / pts, pts) : n; 
 // XCD: units in xcd_unit order (the host launches whole rounds), so the N2 units of one z-plane,
 // whose blocked pieces share 128-byte lines, run under one L2.
 template <bool INV, int FLAGS, int N1, int TN, int PTS = 16, bool XS = true, bool LP = false, int BLK = 0,
-          bool XCD = false>
+          bool XCD = false, int PROBE = 0>
 __global__ void __launch_bounds__(N1 * (TN / PTS)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
+#ifndef CFP_KEXP
+  static_assert(PROBE == 0, "timing probes are built in tools/kexp only");
+#endif
   constexpr int N2 = TN / N1, TR = TN / PTS, NT = N1 * TR, TY = N1 / PTS;
   constexpr bool BL = BLK > 0;
   constexpr int BX = BL ? BLK : 1, BW = N2 * BX;  // x per block column, values per block column
@@ -142,6 +153,11 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
   // y2 + N2 (ty + TY m)
   const auto load = [&](int u, cd* v) {
     const int x = idx(x0), ty = idx(ty0);
+    if constexpr ((PROBE & PR_NO_LOAD) != 0) {
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) v[m] = make_cd(x + m, ty + u);
+      return;
+    }
     if (INV) {  // chunked rows: per-thread part + uniform part (nyl >= N2 TY)
       const cd* const src = BL ? in + crow(u / N2, N2 * ty) + (u % N2) * BX + (x / BX) * BW + x % BX
                                : in + crow(u / N2, u % N2 + N2 * ty) + x;
@@ -158,7 +174,8 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
     __builtin_amdgcn_sched_barrier(0);
   };
   for (int it = blockIdx.x; it < nunits; it += gridDim.x) {
-    const int u = XCD ? xcd_unit(it, gridDim.x) : it;
+    int u = XCD ? xcd_unit(it, gridDim.x) : it;
+    if constexpr ((PROBE & PR_ZMAJOR) != 0) u = (u % (nunits / N2)) * N2 + u / (nunits / N2);
     cd v[PTS];
     load(u, v);
     if (INV) {
@@ -168,7 +185,8 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
     const auto k1_of = [](int m, int ty) {
       return LP ? (m & (PTS / 2 - 1)) + (PTS / 2) * ty + PTS * (m / (PTS / 2)) : ty + TY * m;
     };
-    if constexpr (LP) {
+    if constexpr ((PROBE & PR_NO_ZMATH) != 0) {
+    } else if constexpr (LP) {
       // phase A on lane pairs: E / O = the 16-point DFTs of the even / odd y1 (lanes ty = 0 / 1)
       dft_reg<PTS>(v);
       {
@@ -192,7 +210,7 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
       lds_barrier();  // phase A's last LDS reads are done
     }
     // phase B: transpose to rows k1, thread (row r, tx) gets x = tx + TR m
-    {
+    if constexpr (!(PROBE & PR_NO_XCHG)) {
       const int x = idx(x0), ty = idx(ty0), r = idx(r0), tx = idx(tx0);
       if constexpr (XS) {
 #pragma unroll
@@ -224,12 +242,18 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
     {
       // phase C: TN-point DFT along row r (row mode, N1 rows x TR threads)
       const int r = idx(r0), tx = idx(tx0);
-      fft_stages<TN, PTS, r0_of(TN, PTS), true, N1, F | F_TW_GLOBAL>(v, lds, a.tw, r, tx, true);  // v[m]: kx = tx + TR m
+      if constexpr (!(PROBE & PR_NO_ZMATH))
+        fft_stages<TN, PTS, r0_of(TN, PTS), true, N1, F | F_TW_GLOBAL>(v, lds, a.tw, r, tx, true);  // v[m]: kx = tx + TR m
     }
     {
       const int r = idx(r0), tx = idx(tx0);
       const double sc = a.scale, sy = INV ? -sc : sc;
-      if (BL && !INV) {  // blocked: kx = tx + TR m at (kx / BX) 64 + y2 BX + kx % BX of row block r
+      if constexpr ((PROBE & PR_NO_STORE) != 0) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < PTS; ++m) acc += v[m].x * sc + v[m].y * sy;
+        if (acc == 1.2345e300) out[tx] = make_cd(acc, 0.0);  // keeps the work live, never true
+      } else if (BL && !INV) {  // blocked: kx = tx + TR m at (kx / BX) 64 + y2 BX + kx % BX of row block r
         cd* dst = out + crow(u / N2, N2 * r) + (u % N2) * BX + (tx / BX) * BW + tx % BX;
 #pragma unroll
         for (int m = 0; m < PTS; ++m) gstore<FLAGS>(dst + TR * N2 * m, make_cd(v[m].x * sc, v[m].y * sy));
@@ -243,10 +267,6 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
   }
 }
 
-// PROBE != 0 only in tools/kexp (tp_probe.hip, p2_512.hip, built with CFP_KEXP): timing probes that drop a
-// part of the work (output invalid).  The product library instantiates PROBE = 0 only.
-enum { PR_NO_Y2 = 1, PR_NO_ZMATH = 2, PR_NO_XCHG = 4, PR_NO_LOAD = 8, PR_NO_STORE = 16,
-       PR_PRIO = 32 /* experiment, full work: s_setprio 1 for the second half of the waves */ };
 
 // Persistent over units u = (x-tile, k1); T columns per unit = T/N2 x values times N2 y2.
 // Barriers wait for LDS only, so one unit's stores drain while the next unit loads.
@@ -975,6 +995,7 @@ hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* 
     const unsigned g = grid_of(units, 2);
     // the row FFT's and y1 DFT's exchanges wave-local (WL; r04aa: 5,720 against 5,343 real
     // PCApply/s, P1r 64 -> ~57 us); alt_rows (CFP_RSCHEDULE_THREE_ALT, A/B): workgroup barriers
+    // blockIdx order (r05l: XCD order 5,641-5,704 against 5,699-5,701 real PCApply/s)
     if (stage == 0 && !alt_rows)  // P1r: 80 VGPRs, three workgroups per CU
       hipLaunchKernelGGL((k_tp_rows_r2c<false, 128, 32, 8, 256, F_NT_LD, 6, false, true>), dim3(grid_of(units, 3)),
                          dim3(512), 0, s, b, H, Q, nullptr, a, units);
@@ -1013,6 +1034,13 @@ constexpr int kP2LoadFlags = F_NT_LD;
 // P1 / P3 phase C (the row FFT) with wave-local exchanges (r04ab): shape TP_MID_ROWSALT runs the
 // other setting for A/B
 constexpr bool kRowsWave = true;
+// P1 / P3 units in XCD order at 256^3 and 512^3 (r05j, tools/kexp/run_rows_512.py,
+// profiles/r05j_rows_probes.txt): each XCD walks whole z-planes of b / x, so an XCD's units read
+// and write one contiguous region; 256^3 P1 93.8 -> 90.8 us, P3 90.4 -> 86.6 us; 512^3 P1 911 ->
+// 884 us, P3 915 -> 866 us (the units of one plane in blockIdx order spread over all eight
+// XCDs).  Whole apply (r05k, against a -DCFP_ROWS_XCD=0 build, alternating processes): 256^3
+// 3,361-3,388 against 3,288-3,316 PCApply/s, 512^3 282.3-282.5 against 274.6-275.4.
+constexpr bool kRowsXCD = CFP_ROWS_XCD != 0;
 
 // P1F / P3F: P1's load and P3's store policy out of place (kP1Flags / kP3Flags; 0 = plain)
 // WR: phase C's exchanges wave-local (F_WAVE_LDS)
@@ -1036,11 +1064,13 @@ static void launch_rows(int stage, const cd* in, cd* out, const TPArgs& a, hipSt
   else
     TP_LAUNCH((k_tp_rows<true, P3F | W, N1, TN, PTS, XS, LP, BL, XCD>), dim3(g), blk, s, in, out, a, units);
 }
-// the default row sweeps, or (alt, shape TP_MID_ROWSALT) the same with the other phase-C exchanges
-template <int N1, int TN, int PER_CU, int PTS, bool XS, bool LP, int P1F = kP1Flags, int P3F = kP3Flags>
+// the default row sweeps, or (alt, shape TP_MID_ROWSALT) the same with the other phase-C exchanges;
+// units in XCD order (kRowsXCD)
+template <int N1, int TN, int PER_CU, int PTS, bool XS, bool LP, int P1F = kP1Flags, int P3F = kP3Flags,
+          bool XCD = kRowsXCD>
 static void launch_rows_ab(bool alt, int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s) {
-  if (alt) launch_rows<N1, TN, PER_CU, PTS, XS, LP, 0, false, P1F, P3F, !kRowsWave>(stage, in, out, a, s);
-  else launch_rows<N1, TN, PER_CU, PTS, XS, LP, 0, false, P1F, P3F, kRowsWave>(stage, in, out, a, s);
+  if (alt) launch_rows<N1, TN, PER_CU, PTS, XS, LP, 0, XCD, P1F, P3F, !kRowsWave>(stage, in, out, a, s);
+  else launch_rows<N1, TN, PER_CU, PTS, XS, LP, 0, XCD, P1F, P3F, kRowsWave>(stage, in, out, a, s);
 }
 
 template <int T, int N2, int TN, int PER_CU, int PTS = 16, bool XS = true>
@@ -1080,9 +1110,17 @@ hipError_t launch_three_pass_slab(int stage, int n, const cd* in, cd* out, const
                      units);
     } else {
       const int units = nzl * 16;  // local z-planes x y2
-      const unsigned g = grid_of(units, 1);
-      if (stage == 0)
+      // XCD order when the rounds are whole and fill the chip (r05l, profiles/r05l_rows_xcd_ab.txt:
+      // P = 8 local kernels 423-431 against 439-445 us; P = 16 in 4 pieces of 128 units: 274-276
+      // against 256-258 us, so not below a full round)
+      const unsigned gx = kRowsXCD && units >= (int)grid_of(1 << 30, 1) ? grid_xcd(units, 1) : 0;
+      const unsigned g = gx ? gx : grid_of(units, 1);
+      if (stage == 0 && gx)
+        TP_LAUNCH((k_tp_rows<false, F_NT_LD | W, 32, 512, 16, true, kRowsLP, 0, true>), dim3(g), dim3(1024), s, in, out, a, units);
+      else if (stage == 0)
         TP_LAUNCH((k_tp_rows<false, F_NT_LD | W, 32, 512, 16, true, kRowsLP>), dim3(g), dim3(1024), s, in, out, a, units);
+      else if (gx)
+        TP_LAUNCH((k_tp_rows<true, F_NT_ST | W, 32, 512, 16, true, kRowsLP, 0, true>), dim3(g), dim3(1024), s, in, out, a, units);
       else
         TP_LAUNCH((k_tp_rows<true, F_NT_ST | W, 32, 512, 16, true, kRowsLP>), dim3(g), dim3(1024), s, in, out, a, units);
     }
@@ -1099,10 +1137,18 @@ hipError_t launch_three_pass_slab(int stage, int n, const cd* in, cd* out, const
                          out, a, units);
   } else {
     const int units = nzl * 8;  // local z-planes x y2
-    const unsigned g = grid_of(units, 2);
+    // XCD order when the rounds are whole and fill the chip (as at 512^3)
+    const unsigned gx = kRowsXCD && units >= (int)grid_of(1 << 30, 2) ? grid_xcd(units, 2) : 0;
+    const unsigned g = gx ? gx : grid_of(units, 2);
     constexpr int W = kRowsWave ? F_WAVE_LDS : 0;
-    if (stage == 0)
+    if (stage == 0 && gx)
+      hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD | W, 32, 256, 16, true, kRowsLP, 0, true>), dim3(g), dim3(512), 0, s,
+                         in, out, a, units);
+    else if (stage == 0)
       hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD | W, 32, 256, 16, true, kRowsLP>), dim3(g), dim3(512), 0, s,
+                         in, out, a, units);
+    else if (gx)
+      hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST | W, 32, 256, 16, true, kRowsLP, 0, true>), dim3(g), dim3(512), 0, s,
                          in, out, a, units);
     else
       hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST | W, 32, 256, 16, true, kRowsLP>), dim3(g), dim3(512), 0, s,
@@ -1181,7 +1227,9 @@ hipError_t launch_three_pass(int stage, int n, const cd* in, cd* out, const TPAr
           else launch_mid<32, 8, 128, 2, 8, false>(out, a, s);
         }
       } else {
-        launch_rows_ab<16, 128, 4, 8, false, true, 0, 0>(ra, stage, in, out, a, s);
+        // blockIdx order (r05k: XCD order 21,370-21,420 against 21,630-21,700 PCApply/s; one
+        // round of units whose b and x stay in the Infinity Cache)
+        launch_rows_ab<16, 128, 4, 8, false, true, 0, 0, false>(ra, stage, in, out, a, s);
       }
       return hipGetLastError();
     }

@@ -45,8 +45,9 @@ constexpr int wr0_of(int n, int pts) { return n > pts ? wr0_of(n / pts, pts) : n
 }  // namespace
 
 // P1w / P3w.  512 threads, 16 points each; one unit = (z, y2); persistent over the units.
-// FLAGS: the global load / store policy (F_NT_LD, F_NT_ST).
-template <bool INV, int FLAGS>
+// FLAGS: the global load / store policy (F_NT_LD, F_NT_ST).  XCD: units in xcd_round_unit order
+// (the grid a multiple of 8 workgroups).
+template <bool INV, int FLAGS, bool XCD = false>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 k_wtp_rows(const cd* in, cd* out, WTPArgs a, int nunits) {
   constexpr int PTS = 16, TR = WNX / PTS;  // row mode: 8 threads per (row, comp)
@@ -60,7 +61,8 @@ k_wtp_rows(const cd* in, cd* out, WTPArgs a, int nunits) {
   const int tid = threadIdx.x;
   const int c0 = tid;  // column mode: column 4 x + comp
   const int comp0 = tid & 3, tx0 = (tid >> 2) & (TR - 1), k0 = tid >> 5;  // row mode
-  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+  for (int it = blockIdx.x; it < nunits; it += gridDim.x) {
+    const int u = XCD ? xcd_round_unit(it, gridDim.x, nunits) : it;
     const int z = u / WN2, y2 = u % WN2;
     cd v[PTS];
     {
@@ -871,10 +873,16 @@ hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArg
     // P1w out of place: non-temporal loads keep b out of the 256 MB Infinity Cache, which then
     // still holds much of P1w's output for P2w (the scalar 3-sweep's policy, cfp_three_pass.hip)
     const dim3 gg(units < g ? units : g);
-    if (stage == 0 && in != out)
+    // units in XCD order (CFP_ROWS_XCD) when the grid is a multiple of 8 workgroups
+    const bool xo = CFP_ROWS_XCD != 0 && gg.x % 8 == 0;
+    if (stage == 0 && in != out && xo)
+      hipLaunchKernelGGL((k_wtp_rows<false, F_NT_LD, true>), gg, dim3(512), 0, s, in, out, a, units);
+    else if (stage == 0 && in != out)
       hipLaunchKernelGGL((k_wtp_rows<false, F_NT_LD>), gg, dim3(512), 0, s, in, out, a, units);
     else if (stage == 0)
       hipLaunchKernelGGL((k_wtp_rows<false, 0>), gg, dim3(512), 0, s, in, out, a, units);
+    else if (xo)
+      hipLaunchKernelGGL((k_wtp_rows<true, F_NT_ST, true>), gg, dim3(512), 0, s, in, out, a, units);
     else
       hipLaunchKernelGGL((k_wtp_rows<true, F_NT_ST>), gg, dim3(512), 0, s, in, out, a, units);
   }

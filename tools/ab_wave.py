@@ -3,7 +3,7 @@
 against the 5-sweep schedule -- one line of JSON, for same-box A/Bs of two library builds
 (run it from each tree's root).  GPU only; measurement tool.
 
-    python tools/ab_wave.py [--iters 1000] [--tag NAME]
+    python tools/ab_wave.py [--iters 1000] [--tag NAME] [--lib SO]
 """
 import argparse
 import json
@@ -19,8 +19,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=1000)
     ap.add_argument("--tag", default=os.path.basename(ROOT))
+    ap.add_argument("--lib", default=None, help="another build of libcirculant_fft.so (A/B of two builds)")
     a = ap.parse_args()
     import torch
+    if a.lib:
+        import circulantpreconditioner_amd._lib as L
+        L.LIB_PATH = os.path.abspath(a.lib)
+        a.tag = a.lib
     import circulantpreconditioner_amd as cp
     from circulantpreconditioner_amd import wave as W
     wp = W.WavePlan((128, 128, 128)).set_symbol((0.079, 0.079, 0.079))

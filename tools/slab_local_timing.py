@@ -10,7 +10,7 @@ part, and a model of the whole apply over xGMI: one link of ~150 GB/s per peer (
   pipelined  (K > 1):   max(fwd, X) + min(fwd, X)/K + mid + max(bwd, X) + min(bwd, X)/K
                         (X: one all-to-all; the first / last piece cannot overlap)
 
-    python tools/slab_local_timing.py [--grid 512] [--ranks 2 4 8] [--pieces 1 4 8] [--iters 20]
+    python tools/slab_local_timing.py [--grid 512] [--ranks 2 4 8] [--pieces 1 4 8] [--iters 20] [--lib SO]
 """
 import argparse
 import ctypes
@@ -44,7 +44,11 @@ def main():
     ap.add_argument("--ranks", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--pieces", type=int, nargs="+", default=[1, 4, 8])
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--lib", default=None, help="another build of libcirculant_fft.so (A/B of two builds)")
     a = ap.parse_args()
+    if a.lib:
+        import circulantpreconditioner_amd._lib as Lib
+        Lib.LIB_PATH = os.path.abspath(a.lib)
     n = a.grid
     lam = (ctypes.c_double * 6)(0.6, 0.0, 0.15, 0.0, 0.02, 0.0)
     for P in a.ranks:
