@@ -124,15 +124,17 @@ struct Step {
 };
 
 // 256^3: 3 local sweeps per rank (x + y1 | y2 + z + symbol + inverses | inverse), the same two
-// exchanges; otherwise 5 axis passes.  AUTO takes 3 sweeps for P <= 4 only: measured per rank
-// (tools/slab_local_timing.py, profiles/r02i_slab_local.txt) 174 vs 219 us at P = 2 and 90 vs
-// 119 us at P = 4, a tie at P = 8 (P2 has 128 units for 256 CUs) and a loss at P = 16.
-// 512^3 (r05): 3 sweeps on every supported P (96 N / P local bytes against
-// 160 N / P; P2 keeps 1,024 units for 256 CUs at P = 8).
+// exchanges; otherwise 5 axis passes.  AUTO takes 3 sweeps on every supported P.  Per rank
+// (tools/slab_local_timing.py, exchanges skipped), 3 against 5 sweeps at 256^3: r02i
+// (profiles/r02i_slab_local.txt) 174 / 219 us at P = 2, 90 / 119 at P = 4, a tie at P = 8 and a
+// loss at P = 16, so AUTO was P <= 4 until r05; r05o (profiles/r05o_slab256_local.txt, with the
+// lane-pair and XCD-ordered rows) 86 / 119 at P = 4, 56 / 63 at P = 8, 45 / 53 at P = 16.
+// 512^3 (r05): 96 N / P local bytes against 160 N / P; P2 keeps 1,024 units
+// for 256 CUs at P = 8.
 bool slab_three(const SlabLayout& L, int schedule) {
   const i64 n[3] = {L.nx, L.ny, L.nz};
   if (schedule == CFP_SCHEDULE_FIVE_PASS || !three_pass_slab_supported(n, L.P)) return false;
-  return schedule == CFP_SCHEDULE_THREE_PASS || L.P <= 4 || L.nx == 512;
+  return true;
 }
 
 // AUTO pipeline depth: one piece on one rank and for slabs under 64 MiB (the exchanges are then

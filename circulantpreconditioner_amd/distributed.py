@@ -153,7 +153,7 @@ class SlabPlan:
         return self
 
     def set_schedule(self, schedule: str | int) -> "SlabPlan":
-        """Local passes: 'auto' (3 sweeps at 256^3 with world | 32), 'five' or 'three'."""
+        """Local passes: 'auto' (3 sweeps at 256^3 and 512^3 with world | 32, world <= 16), 'five' or 'three'."""
         check(lib().cfp_dist_plan_set_schedule(self._h, _slab_schedule(schedule)))
         return self
 
@@ -331,7 +331,7 @@ class SlabGroup:
         return self
 
     def set_schedule(self, schedule: str | int) -> "SlabGroup":
-        """Local passes per slab: 'auto' (3 sweeps at 256^3 with P | 32), 'five' or 'three'."""
+        """Local passes per slab: 'auto' (3 sweeps at 256^3 and 512^3 with P | 32, P <= 16), 'five' or 'three'."""
         check(lib().cfp_group_set_schedule(self._h, _slab_schedule(schedule)))
         return self
 

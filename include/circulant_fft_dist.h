@@ -165,8 +165,8 @@ int cfp_dist_plan_time_phases(cfp_dist_plan_t plan, const double *b_dev, double 
 int cfp_dist_plan_profile_begin(cfp_dist_plan_t plan, int max_applies, int every);
 int cfp_dist_plan_profile_end(cfp_dist_plan_t plan, double *ms_out, int *applies);
 /* local passes of each rank: CFP_SCHEDULE_AUTO (3 sweeps -- x + y1 | y2 + z + symbol + inverses |
- * inverse, cfp_three_pass.hip -- for a 256^3 grid with nranks <= 4, else 5 axis passes; 3 sweeps
- * are available up to nranks = 16, nranks | 32),
+ * inverse, cfp_three_pass.hip -- for a 256^3 or 512^3 grid with nranks | 32, nranks <= 16; else
+ * 5 axis passes),
  * CFP_SCHEDULE_FIVE_PASS, or CFP_SCHEDULE_THREE_PASS (CFP_ERR_SUP where unsupported).  The
  * exchanges and the per-peer chunk layout are the same for both. */
 int cfp_dist_plan_set_schedule(cfp_dist_plan_t plan, int schedule);

@@ -7,7 +7,7 @@
   library's kernel segments and the two all-to-alls go through torch.distributed (gloo,
   staged through host memory), so the per-rank plan is exercised across processes.
 * The RCCL executor with world = 1; with more ranks it is exercised by bench.py --gpus N.
-* At 256^3 (AUTO for P <= 4, on request up to P = 16) and 512^3 (AUTO for every P | 32, r05)
+* At 256^3 and 512^3 (AUTO for every P | 32 up to 16 since r05)
   every rank runs the 3-sweep schedule (x + y1 into the per-peer chunks | y2 + z + symbol +
   inverses on its k1 rows | inverse), checked against the oracle and against the 5-pass slab
   schedule.
@@ -75,7 +75,7 @@ def test_group_three_sweep_256(P, case256, oracle):
     dims, lam, b, ref = case256
     full = torch.from_numpy(b).cuda()
     with SlabGroup(dims, P) as g:
-        g.set_transport_symbol(lam).set_schedule("three")  # AUTO picks it for P <= 4
+        g.set_transport_symbol(lam).set_schedule("three")  # AUTO picks it too (r05)
         bs = g.scatter(full)
         x3 = torch.cat(g.apply(bs))
         assert oracle.rel_l2(x3.cpu().numpy(), ref) < TOL
@@ -192,8 +192,8 @@ def test_group_pieces_512(P, case512):
 
 @pytest.mark.parametrize("P", [2, 4, 8, 16])
 def test_group_pieces_256(P, case256):
-    """256^3 with pieces (K = 1, 4, 8 where K | 256 / P): the 3-sweep slab schedule (P <= 4, and
-    on request at 8 and 16) and the five-pass one, in place at K = 4."""
+    """256^3 with pieces (K = 1, 4, 8 where K | 256 / P): the 3-sweep slab schedule (AUTO) and
+    the five-pass one, in place at K = 4."""
     from circulantpreconditioner_amd.distributed import SlabGroup
     dims, lam, b, ref = case256
     rd = torch.from_numpy(ref).cuda()

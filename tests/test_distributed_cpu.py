@@ -235,7 +235,7 @@ def test_slab_steps_pieces_layout(P):
 @pytest.mark.parametrize("n,P", [(256, 1), (256, 2), (256, 4), (512, 2), (512, 8), (512, 16)])
 @pytest.mark.parametrize("pieces", [1, 2, 4])
 def test_slab_three_sweep_layout(n, P, pieces):
-    """the 3-sweep slab schedule (AUTO at 256^3 for P <= 4, at 512^3 for every P | 32
+    """the 3-sweep slab schedule (AUTO at 256^3 and 512^3 for every P | 32 up to 16
     since r05) is described too: P1 blocks write block k of every chunk (offsets k B nyl nx), P2
     runs on the rank's k1 rows [r nyl / N2, ...) (N2 = 8 at 256^3, 16 at 512^3), the chunk and row
     bookkeeping the kernels receive, and the exchange pieces tile the chunk."""
