@@ -26,6 +26,10 @@
 
 #include <hip/hip_ext.h>
 
+#ifndef CFP_REAL_MID_XCD
+#define CFP_REAL_MID_XCD 1
+#endif
+
 // a launch that stamps its own dispatch while per-launch profiling is on (cfp_internal.h)
 #define TP_LAUNCH(K, G, B, S, ...)                                                                    \
   do {                                                                                                \
@@ -988,8 +992,15 @@ hipError_t launch_three_pass_real(int stage, int n, const double* b, cd* H, cd* 
   }
   if (stage == 1) {
     constexpr int units = (128 / 8) * 32;  // x tiles of the half spectrum x k1
-    hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true, 128>), dim3(grid_of(units, 1)), dim3(1024), 0, s, H, a,
-                       units);
+    // units in XCD order (whole rounds: 512 units, 256 workgroups; r05q, profiles/r05q_mid_xcd_ab.txt:
+    // 5,713-5,736 against 5,639-5,681 real PCApply/s); -DCFP_REAL_MID_XCD=0: A/B
+    const unsigned gx = CFP_REAL_MID_XCD ? grid_xcd(units, 1) : 0;
+    if (gx)
+      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true, 128, 0, 0, false, true>), dim3(gx), dim3(1024), 0, s, H, a,
+                         units);
+    else
+      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true, 128>), dim3(grid_of(units, 1)), dim3(1024), 0, s, H, a,
+                         units);
   } else {
     constexpr int units = 256 * 8;  // z-planes x y2
     const unsigned g = grid_of(units, 2);

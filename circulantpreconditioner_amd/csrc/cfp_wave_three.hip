@@ -20,6 +20,10 @@
 #include "cfp_lane.h"
 #include "cfp_three_pass.h"
 
+#ifndef CFP_WAVE_MID_XCD
+#define CFP_WAVE_MID_XCD 1
+#endif
+
 namespace cfp {
 
 namespace {
@@ -450,7 +454,7 @@ k_wtp_mid_ct(cd* data, WTPArgs a, int nunits) {
 // the last FFT stage, the twiddle and the stores; the next unit loads only slots 8..15 from HBM.
 typedef __attribute__((address_space(3))) void wlds_void_t;
 typedef __attribute__((address_space(1))) void wglb_void_t;
-template <bool XS, int PROBE = 0, bool PF = false>
+template <bool XS, int PROBE = 0, bool PF = false, bool XCD = false>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 k_wtp_mid_ct2(cd* data, WTPArgs a, int nunits) {
 #ifndef CFP_KEXP
@@ -496,9 +500,10 @@ k_wtp_mid_ct2(cd* data, WTPArgs a, int nunits) {
                                        16, 0, 0);
   };
   if constexpr (PF) {
-    if ((int)blockIdx.x < nunits) prefetch(blockIdx.x);
+    if ((int)blockIdx.x < nunits) prefetch(XCD ? xcd_round_unit(blockIdx.x, gridDim.x, nunits) : (int)blockIdx.x);
   }
-  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+  for (int it = blockIdx.x; it < nunits; it += gridDim.x) {
+    const int u = XCD ? xcd_round_unit(it, gridDim.x, nunits) : it;
     cd v[PTS];
     {
       const int c = launder(c0), tz = launder(tz0);
@@ -624,7 +629,8 @@ k_wtp_mid_ct2(cd* data, WTPArgs a, int nunits) {
       const auto next = [&](cd*) {  // right after the exchange's last read: the buffer is free
         if constexpr (PF) {
           lds_barrier();  // every wave has read the exchange buffer
-          if (u + (int)gridDim.x < nunits) prefetch(u + gridDim.x);
+          if (it + (int)gridDim.x < nunits)
+            prefetch(XCD ? xcd_round_unit(it + (int)gridDim.x, gridDim.x, nunits) : it + (int)gridDim.x);
         }
       };
       fft_stages_perm<WNX, PTS, wr0_of(WNX, PTS), T, F>(v, lds, tw_l, lab_b(c), lab_a(c), tz, false, next);  // map A again
@@ -864,7 +870,12 @@ hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArg
   if (stage == 1) {
     const int units = (WNX / 2) * WN1;  // x tiles x k1
     // the LDS-DMA prefetch (global_load_lds_dwordx4) takes 16-byte aligned addresses
-    if (((uintptr_t)out & 15) == 0)
+    // units in XCD order, each XCD on whole k1 row blocks (r05q, profiles/r05q_mid_xcd_ab.txt:
+    // P2w 64.9-65.0 against 65.5-66.2 us; the whole apply within the noise); -DCFP_WAVE_MID_XCD=0: A/B
+    const unsigned gm = units < g ? units : g;
+    if (((uintptr_t)out & 15) == 0 && CFP_WAVE_MID_XCD && gm % 8 == 0)
+      hipLaunchKernelGGL((k_wtp_mid_ct2<true, 0, true, true>), dim3(gm), dim3(512), 0, s, out, a, units);
+    else if (((uintptr_t)out & 15) == 0)
       hipLaunchKernelGGL((k_wtp_mid_ct2<true, 0, true>), dim3(units < g ? units : g), dim3(512), 0, s, out, a, units);
     else
       hipLaunchKernelGGL((k_wtp_mid_ct2<true>), dim3(units < g ? units : g), dim3(512), 0, s, out, a, units);
