@@ -232,7 +232,7 @@ def test_slab_steps_pieces_layout(P):
             assert all(st[i]["dst"] == m for i in fwd) and all(st[i]["src"] == m for i in bwd)
 
 
-@pytest.mark.parametrize("n,P", [(256, 1), (256, 2), (256, 4), (512, 2), (512, 8), (512, 16)])
+@pytest.mark.parametrize("n,P", [(256, 1), (256, 2), (256, 4), (256, 8), (256, 16), (512, 2), (512, 8), (512, 16)])
 @pytest.mark.parametrize("pieces", [1, 2, 4])
 def test_slab_three_sweep_layout(n, P, pieces):
     """the 3-sweep slab schedule (AUTO at 256^3 and 512^3 for every P | 32 up to 16
