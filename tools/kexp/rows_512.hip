@@ -6,6 +6,7 @@
 //   4: memory alone (no DFTs, no transpose), 5: memory + transpose (no DFTs)
 //   6: product with units in z-major order, 7: memory alone in z-major order
 //   8: product in XCD unit order, 9: memory alone in XCD unit order
+//   10: memory alone, XCD order, 256^3 sweeps on 256 workgroups (one per CU, as at 512^3)
 #define CFP_KEXP 1
 #include "cfp_three_pass.hip"
 namespace cfp {
@@ -18,13 +19,13 @@ hipError_t launch_three_pass_sq(int, int, const cd*, cd*, const TPArgs&, TPShape
 using namespace cfp;
 
 template <int PR, bool XCD = false>
-static int launch_probe(int sweep, const cd* b, cd* x, const TPArgs& a) {
+static int launch_probe(int sweep, const cd* b, cd* x, const TPArgs& a, int g256 = 512) {
   constexpr int W = F_WAVE_LDS;
   switch (sweep) {
     case 0: hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD | W, 32, 512, 16, true, true, 0, XCD, PR>), dim3(256), dim3(1024), 0, 0, b, x, a, 512 * 16); return 0;
     case 1: hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST | W, 32, 512, 16, true, true, 0, XCD, PR>), dim3(256), dim3(1024), 0, 0, b, x, a, 512 * 16); return 0;
-    case 2: hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD | W, 32, 256, 16, true, true, 0, XCD, PR>), dim3(512), dim3(512), 0, 0, b, x, a, 256 * 8); return 0;
-    case 3: hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST | W, 32, 256, 16, true, true, 0, XCD, PR>), dim3(512), dim3(512), 0, 0, b, x, a, 256 * 8); return 0;
+    case 2: hipLaunchKernelGGL((k_tp_rows<false, F_NT_LD | W, 32, 256, 16, true, true, 0, XCD, PR>), dim3(g256), dim3(512), 0, 0, b, x, a, 256 * 8); return 0;
+    case 3: hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST | W, 32, 256, 16, true, true, 0, XCD, PR>), dim3(g256), dim3(512), 0, 0, b, x, a, 256 * 8); return 0;
     default: return 1;
   }
 }
@@ -48,6 +49,7 @@ extern "C" int rows_512(int which, const void* b, void* x, const void* tw, int i
       case 7: return launch_probe<PR_ZMAJOR | PR_NO_ZMATH | PR_NO_XCHG>(sweep, bb, xx, a);
       case 8: return launch_probe<0, true>(sweep, bb, xx, a);
       case 9: return launch_probe<PR_NO_ZMATH | PR_NO_XCHG, true>(sweep, bb, xx, a);
+      case 10: return launch_probe<PR_NO_ZMATH | PR_NO_XCHG, true>(sweep, bb, xx, a, 256);
       default: return 1;
     }
   };

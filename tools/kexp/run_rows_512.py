@@ -15,7 +15,8 @@ L.rows_512.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_int, ct
 SWEEPS = {0: ("P1", 512), 1: ("P3", 512), 2: ("P1", 256), 3: ("P3", 256)}
 PROBES = {0: "product", 1: "no loads", 2: "no stores", 3: "arithmetic + exchanges alone", 4: "memory alone",
           5: "memory + transpose", 6: "product, z-major units", 7: "memory alone, z-major units",
-          8: "product, XCD unit order", 9: "memory alone, XCD unit order"}
+          8: "product, XCD unit order", 9: "memory alone, XCD unit order",
+          10: "memory alone, XCD, 1 WG per CU"}
 if os.environ.get("ROWS_PROBES"):
     PROBES = {int(p): PROBES[int(p)] for p in os.environ["ROWS_PROBES"].split(",")}
 bufs = {}
