@@ -27,7 +27,9 @@ struct TPArgs {
 
 // kernel shape at 256^3 (cfp_plan_set_three_pass_shape); zeros = the measured default
 // BLOCKED: SWAP64_PF with the blocked intermediate layout (k_tp_rows<.., 8>; N1 = 32 only);
-// BLOCKED32: blocks of 4 x and the permlane P2 on 32 columns, two workgroups per CU
+// at 512^3 blocks of 2 x (one P2 tile)
+// BLOCKED32: blocks of 4 x and the permlane P2 on 32 columns, two workgroups per CU; at 512^3
+// blocks of 8 x (P1 / P3 move whole 128-byte lines; r05i)
 // SWAP32X: the permlane P2 on 32 columns (4 x times 8 y2, natural layout: 64-byte tiles), two
 // workgroups per CU, units in XCD order (r04)
 // ROWSALT: the default shape (n1 = 0 only; 128^3, 256^3, 512^3) with P1 / P3's row-FFT exchanges

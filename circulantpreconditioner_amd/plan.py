@@ -183,7 +183,8 @@ class CirculantPlan:
         P2 on 32 columns, two workgroups per CU; n1 = 32 only; 'swap32x': the permlane P2 on 32
         natural-layout columns in XCD order; 'rowsalt': the default with P1 / P3's row-FFT
         exchanges the other way, wave-local or workgroup-wide, n1 = 0 only).  At 100^3 (cfp_three_pass_sq.hip)
-        mid picks the middle kernel's x tile: 'default' 4 x, 'lane64' 2 x, 'lane32' 5 x."""
+        mid picks the middle kernel's x tile: 'default' 4 x, 'lane64' 2 x, 'lane32' 5 x.  At 512^3
+        'blocked' / 'blocked32' are blocks of 2 / 8 x (profiles/r05i_p2_512_layouts.md)."""
         m = self.TP_MIDS[mid] if isinstance(mid, str) else int(mid)
         check(lib().cfp_plan_set_three_pass_shape(self._h, int(n1), m))
         return self
