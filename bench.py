@@ -137,6 +137,12 @@ class Watchdog:
             os._exit(3)
 
 
+def phase_extension(steps: int, scaling_steps: int) -> float:
+    """Seconds the ranks add to the 'timed' (steps) and 'scaling_512' (scaling_steps) deadlines;
+    the self-launcher's kill limit adds the same."""
+    return 0.05 * max(0, steps) + 0.2 * max(0, scaling_steps)
+
+
 def parse_deadlines(items) -> dict:
     """--deadline PHASE=SECONDS (repeatable) over DEADLINES."""
     out = dict(DEADLINES)
@@ -157,11 +163,12 @@ def _free_port() -> int:
     return port
 
 
-def self_launch(nproc: int, argv, deadlines: dict) -> int:
+def self_launch(nproc: int, argv, deadlines: dict, extra_s: float = 0.0) -> int:
     """--gpus N > 1 without a launcher: start N ranks under torch.distributed.run as a child
     process group (this process has made no GPU call and makes none) and return their exit
     status.  The ranks inherit stdout, so rank 0's JSON line is this run's line.  The whole group
-    is killed if it outlives the sum of the phase deadlines (its own watchdogs fire first)."""
+    is killed if it outlives the sum of the phase deadlines plus the ranks' own step-count
+    extensions of them (extra_s), so their watchdogs always fire first."""
     import signal
     import subprocess
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
@@ -170,7 +177,7 @@ def self_launch(nproc: int, argv, deadlines: dict) -> int:
     env["CFP_BENCH_SELF_LAUNCHED"] = "1"
     log(f"bench: --gpus {nproc} without a launcher: starting {nproc} ranks under torch.distributed.run")
     proc = subprocess.Popen(cmd, env=env, start_new_session=True)
-    limit = sum(deadlines.values()) + 60.0
+    limit = sum(deadlines.values()) + extra_s + 60.0
     try:
         return proc.wait(timeout=limit)
     except subprocess.TimeoutExpired:
@@ -369,6 +376,44 @@ def event_ms(fn, iters: int, settle_ms: float = 150.0) -> float:
     return e0.elapsed_time(e1) / iters
 
 
+def gmres_leg(n: int, steps: int) -> dict:
+    """BASELINE config 3 (n = 256) / config 1 (n = 32): the implicit upwind transport step of the
+    reference's GMRES driver (a = (1,0,0), cfl 1e3/3, rtol = abstol = 1e-5, restart 30, fixed
+    inflow sign so the circulant matches the operator) with the FFT PCSHELL on one GPU, `steps`
+    back-to-back implicit steps after a 2-step warm-up run.  Device time per step from the
+    library's own dispatch stamps (PetscMiniProfile*: every MatMult / vector kernel and copy, plus
+    the KSP's PCApply stamps), split by kind; the same run with the fusion off (MatMult + PCApply
+    + VecMDot as separate sweeps) beside it."""
+    from circulantpreconditioner_amd import transport as T
+
+    def one(fuse: int) -> dict:
+        T.run(T.config(n, pc="fft", sign="fixed", device=True, steps=2, fuse=fuse))  # warm-up
+        r = T.run(T.config(n, pc="fft", sign="fixed", device=True, steps=steps, fuse=fuse, profile=1))
+        k = max(1, r["steps"])
+        dev = r["dev_ms"]
+        return {"steps": r["steps"], "gmres_its": r["total_its"], "its_per_step": r["total_its"] / k,
+                "converged": bool(r["all_converged"]),
+                "device_us_per_step": round(1e3 * sum(dev.values()) / k, 1),
+                "split_us_per_step": {key: round(1e3 * v / k, 1) for key, v in dev.items()},
+                "launches_per_step": {key: round(v / k, 2) for key, v in r["dev_launches"].items()},
+                "pcapply_us": round(1e6 * r["pc_seconds"] / max(1, r["pc_calls"]), 1),
+                "pc_calls_per_step": r["pc_calls"] / k,
+                "wall_ms_per_step": round(1e3 * r["loop_seconds"] / k, 4),
+                "wall_ms_per_solve": round(1e3 * r["solve_seconds"] / k, 4),
+                "fused_dots": r["fused_dots"], "fused_norms": r["fused_norms"]}
+
+    fused, unfused = one(1), one(0)
+    ok = fused["converged"] and unfused["converged"] and fused["gmres_its"] == unfused["gmres_its"]
+    return {"value": round(1e3 / fused["wall_ms_per_step"], 2), "unit": "implicit steps/s (GMRES + FFT PCSHELL)",
+            "grid": [n] * 3, **fused, "unfused": unfused,
+            "note": "device_us_per_step = the step's kernels and copies (pcapply: KSP stamps of each PCApply, "
+                    "which with the fused applyBA include the MatMult; matmult / vector / copy: the stand-in's "
+                    "stamped launches); wall_ms_per_step includes host waits and the loop's VecCopy / "
+                    "VecAXPY / VecNorm",
+            "check": {"what": "every solve converged (KSP reason 2/3); fused and unfused take the same iterations",
+                      "ok": bool(ok)}}
+
+
 def choose_slab_plan(create, requested, agree, warn=None):
     """Pick the N > 1 exchange.  create(exchange) builds this rank's SlabPlan (raises on
     failure); agree(ok) -> True when every rank's creation succeeded.  RCCL unless the
@@ -435,6 +480,8 @@ def main() -> int:
     ap.add_argument("--scaling-grid", type=int, nargs="+", default=[512],
                     help="grid of the scaling_512 line item (BASELINE config 5; 0 = skip)")
     ap.add_argument("--scaling-steps", type=int, default=20)
+    ap.add_argument("--gmres-steps", type=int, default=20,
+                    help="implicit steps of the config 1 / config 3 GMRES legs (other_configs)")
     ap.add_argument("--event-every", type=int, default=10,
                     help="record per-launch events in every n-th timed apply")
     ap.add_argument("--no-live-events", action="store_true",
@@ -457,7 +504,7 @@ def main() -> int:
     # silently measures a different GPU count than --gpus asks for
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
-        return self_launch(args.gpus, sys.argv[1:], deadlines)
+        return self_launch(args.gpus, sys.argv[1:], deadlines, phase_extension(args.steps, args.scaling_steps))
     world = int(world_env or "1")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -604,7 +651,7 @@ def main() -> int:
     torch.cuda.synchronize()
     wd.phase("settle")
     settle_n, settle_ms = settle(run, args.settle_ms)
-    wd.phase("timed", deadlines["timed"] + 0.05 * args.steps)
+    wd.phase("timed", deadlines["timed"] + phase_extension(args.steps, 0))
     timed_region_ms = None
     live_applies = 0
     every = max(1, args.event_every)
@@ -786,6 +833,16 @@ def main() -> int:
         except Exception as e:  # report, never fake
             other_configs["config4_wave128"] = {"error": str(e)}
         torch.cuda.empty_cache()
+        # BASELINE configs 1 and 3: the PCApply inside the reference caller's GMRES step
+        # (tests/TransportEquation_SphericalExplosion_impl_mpi.cxx:117-136, fixed inflow sign)
+        for key, n in (("config3_gmres256", 256), ("config1_gmres32", 32)):
+            try:
+                other_configs[key] = gmres_leg(n, args.gmres_steps)
+                if not other_configs[key]["check"]["ok"]:
+                    check["ok"] = False
+            except Exception as e:  # report, never fake
+                other_configs[key] = {"error": str(e)}
+        torch.cuda.empty_cache()
 
     # north_star's scaling curve: the same apply on the 512^3 grid (BASELINE config 5), at every
     # N the driver launches, reported beside the 256^3 headline (strong scaling, whole job)
@@ -793,7 +850,7 @@ def main() -> int:
     sg = [int(v) for v in args.scaling_grid]
     sg = sg * 3 if len(sg) == 1 else sg
     if len(sg) == 3 and min(sg) > 0 and sg != grid:
-        wd.phase("scaling_512", deadlines["scaling_512"] + 0.2 * args.scaling_steps)
+        wd.phase("scaling_512", deadlines["scaling_512"] + phase_extension(0, args.scaling_steps))
         if world > 1:
             plan.close()  # one library RCCL communicator at a time
             dist.barrier()
@@ -926,7 +983,7 @@ def selftest_cpu(args, wd, rank: int, world: int, launcher: str, metric: str) ->
     stall("first_apply")
     for _ in range(args.warmup):
         run()
-    wd.phase("timed", wd.deadlines["timed"] + 0.05 * args.steps)
+    wd.phase("timed", wd.deadlines["timed"] + phase_extension(args.steps, 0))
     stall("timed")
     if world > 1:
         dist.barrier()

@@ -42,6 +42,7 @@ def _declare(L) -> None:
         "cfp_plan_get_diag": ([vp, dp, vp], c_int),
         "cfp_plan_symbol_version": ([vp, P(u64)], c_int),
         "cfp_plan_apply": ([vp, dp, dp, vp], c_int),
+        "cfp_plan_apply_ex": ([vp, dp, dp, vp, vp], c_int),
         "cfp_plan_apply_with_diag": ([vp, dp, dp, dp, vp], c_int),
         "cfp_plan_apply_host": ([vp, dp, dp], c_int),
         "cfp_plan_apply_with_diag_host": ([vp, dp, dp, dp], c_int),

@@ -43,7 +43,8 @@ class TransportConfig(ctypes.Structure):
                 ("cfl", ctypes.c_double), ("tmax", ctypes.c_double), ("ntmax", ctypes.c_int64),
                 ("precision", ctypes.c_double), ("max_its", ctypes.c_int64), ("restart", ctypes.c_int64),
                 ("pc", ctypes.c_int), ("sign_mode", ctypes.c_int), ("lambda_mode", ctypes.c_int),
-                ("pc_side", ctypes.c_int), ("on_device", ctypes.c_int)]
+                ("pc_side", ctypes.c_int), ("on_device", ctypes.c_int), ("fuse", ctypes.c_int),
+                ("profile", ctypes.c_int)]
 
 
 class TransportResult(ctypes.Structure):
@@ -53,11 +54,14 @@ class TransportResult(ctypes.Structure):
                 ("last_reason", ctypes.c_int), ("all_converged", ctypes.c_int), ("last_residual", ctypes.c_double),
                 ("last_norm_dU", ctypes.c_double), ("solve_seconds", ctypes.c_double),
                 ("pc_seconds", ctypes.c_double), ("pc_calls", ctypes.c_int64), ("setup_seconds", ctypes.c_double),
-                ("lambda_", ctypes.c_double * 3)]
+                ("lambda_", ctypes.c_double * 3), ("loop_seconds", ctypes.c_double), ("dev_ms_", ctypes.c_double * 4),
+                ("dev_launches_", ctypes.c_int64 * 4), ("fused_dots", ctypes.c_int64), ("fused_norms", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
-        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "lambda_"}
+        d = {k: getattr(self, k) for k, _ in self._fields_ if not k.endswith("_")}
         d["lambda"] = list(self.lambda_)
+        d["dev_ms"] = dict(zip(("pcapply", "matmult", "vector", "copy"), self.dev_ms_))
+        d["dev_launches"] = dict(zip(("pcapply", "matmult", "vector", "copy"), self.dev_launches_))
         return d
 
 

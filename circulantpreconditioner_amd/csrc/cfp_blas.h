@@ -51,6 +51,15 @@ hipError_t blas_mdot(const cd* x, int k, const cd* const* ys, i64 n, cd* vals, h
 // ys[j] (coefficients formed on the device), norm2 = |w|^2; k <= MV_MAX (scale: host, real)
 hipError_t blas_mdot_maxpy_norm(cd* w, int k, const cd* const* ys, const double* scale, i64 n, cd* dots,
                                 double* norm2, hipStream_t s);
+// the two halves of it, for dots computed elsewhere (a fused PCApply, cfp_plan_apply_ex):
+// dots_dev[2 j + re/im] = ys[j]^H x (ys[j] == NULL: x itself), on the device, no host wait
+hipError_t blas_mdot_dev(const cd* x, int k, const cd* const* ys, i64 n, double* dots_dev, hipStream_t s);
+// workgroup partials in k_mdot's layout ([block][16]: 2 values per vector, k <= 8) -> dots_dev
+hipError_t blas_mdot_finish(const double* partial, int nb, int k, double* dots_dev, hipStream_t s);
+// w += sum_j scale[j] dots_j ys[j] with the dots on the device, |w|^2; copies the dots back
+// (dots, host) with the norm, one host wait
+hipError_t blas_maxpy_dc_norm(cd* w, int k, const cd* const* ys, const double* scale, const double* dots_dev, i64 n,
+                              cd* dots, double* norm2, hipStream_t s);
 
 // the same on real vectors (PetscScalar = double), plus the scale and the divide that the
 // complex build takes from cfp_kernels.hip (launch_scale, launch_pointwise_divide)
@@ -73,4 +82,12 @@ hipError_t blas_norm(const double* x, i64 n, int type, double* val, hipStream_t 
 hipError_t blas_mdot(const double* x, int k, const double* const* ys, i64 n, double* vals, hipStream_t s);
 hipError_t blas_mdot_maxpy_norm(double* w, int k, const double* const* ys, const double* scale, i64 n, double* dots,
                                 double* norm2, hipStream_t s);
+// device-time profile of the launches above (petsc_mini PetscMiniProfileBegin / End): kinds
+// 1 = MatMult kernels, 2 = vector kernels, 3 = copies (kprof_copy); kprof_take hands out the next
+// event pair for a launch of that kind (false: profile off or full)
+hipError_t kprof_begin(size_t cap);
+hipError_t kprof_end(double ms[4], long long launches[4]);
+void kprof_reset();
+bool kprof_take(int kind, hipEvent_t* e0, hipEvent_t* e1);
+hipError_t kprof_copy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s);
 }  // namespace cfp

@@ -4,7 +4,85 @@
 // the default stand-in PETSc) and double (the real-scalar build, PetscScalar = double).
 #include "cfp_blas.h"
 
+#include <hip/hip_ext.h>
+
 namespace cfp {
+
+// ------------------------------------------------------------------ kernel profile
+// (PetscMiniProfileBegin / End): each stamped launch takes two events from the pool and passes
+// them to hipExtLaunchKernelGGL, which records the kernel's own start and end (no event packets
+// between kernels); copies are bracketed by events.
+namespace {
+struct KProf {
+  bool on = false;
+  size_t used = 0;
+  std::vector<hipEvent_t> ev;  // 2 per record
+  std::vector<int> kind;
+};
+KProf g_kprof;
+}  // namespace
+
+hipError_t kprof_begin(size_t cap) {
+  kprof_reset();
+  for (size_t i = 0; i < 2 * cap; ++i) {
+    hipEvent_t e;
+    hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
+    if (r != hipSuccess) {
+      kprof_reset();
+      return r;
+    }
+    g_kprof.ev.push_back(e);
+  }
+  g_kprof.kind.assign(cap, 0);
+  g_kprof.on = true;
+  return hipSuccess;
+}
+void kprof_reset() {
+  for (auto& e : g_kprof.ev) hipEventDestroy(e);
+  g_kprof = KProf{};
+}
+bool kprof_take(int kind, hipEvent_t* e0, hipEvent_t* e1) {
+  if (!g_kprof.on || 2 * (g_kprof.used + 1) > g_kprof.ev.size()) return false;
+  g_kprof.kind[g_kprof.used] = kind;
+  *e0 = g_kprof.ev[2 * g_kprof.used];
+  *e1 = g_kprof.ev[2 * g_kprof.used + 1];
+  ++g_kprof.used;
+  return true;
+}
+hipError_t kprof_end(double ms[4], long long launches[4]) {
+  for (int k = 0; k < 4; ++k) {
+    ms[k] = 0.0;
+    launches[k] = 0;
+  }
+  hipError_t r = hipSuccess;
+  if (g_kprof.used) r = hipEventSynchronize(g_kprof.ev[2 * g_kprof.used - 1]);
+  for (size_t i = 0; r == hipSuccess && i < g_kprof.used; ++i) {
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, g_kprof.ev[2 * i], g_kprof.ev[2 * i + 1]) != hipSuccess) continue;
+    const int k = g_kprof.kind[i] & 3;
+    ms[k] += t;
+    launches[k] += 1;
+  }
+  kprof_reset();
+  return r;
+}
+
+// a kernel launch that stamps its dispatch while the profile is on
+template <typename K, typename... A>
+static void blaunch(int kind, K k, dim3 g, dim3 b, unsigned lds, hipStream_t s, A... args) {
+  hipEvent_t e0, e1;
+  if (kprof_take(kind, &e0, &e1)) hipExtLaunchKernelGGL(k, g, b, lds, s, e0, e1, 0, args...);
+  else hipLaunchKernelGGL(k, g, b, lds, s, args...);
+}
+// an async copy bracketed by events while the profile is on
+hipError_t kprof_copy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
+  hipEvent_t e0, e1;
+  const bool st = kprof_take(3, &e0, &e1);
+  if (st) hipEventRecord(e0, s);
+  hipError_t r = hipMemcpyAsync(dst, src, bytes, kind, s);
+  if (st) hipEventRecord(e1, s);
+  return r;
+}
 
 #define BLAS_THREADS 256
 // Workgroups of the synchronous reductions (dot / norm), the multi-dot and the MAXPY sweep
@@ -297,7 +375,7 @@ __global__ void __launch_bounds__(BLAS_THREADS) k_dia_spmv(i64 m, DiaDesc d, con
 
 // ------------------------------------------------------------------ host launchers
 #define L1(K, ...) \
-  do { if (n > 0) hipLaunchKernelGGL(K, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, __VA_ARGS__); return hipGetLastError(); } while (0)
+  do { if (n > 0) blaunch(2, K, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, __VA_ARGS__); return hipGetLastError(); } while (0)
 
 template <class T> static hipError_t set_t(T* x, T a, i64 n, hipStream_t s) { L1(k_set<T>, x, a, n); }
 template <class T> static hipError_t shift_t(T* x, T a, i64 n, hipStream_t s) { L1(k_shift<T>, x, a, n); }
@@ -340,11 +418,11 @@ static hipError_t spmv_t(i64 m, i64 nnz, const i64* rowptr, const i64* col, cons
   const int L = mean <= 1.5 ? 1 : mean <= 2.5 ? 2 : mean <= 4.5 ? 4 : mean <= 8.5 ? 8 : 16;
   const dim3 blk(BLAS_THREADS);
   switch (L) {
-    case 1: hipLaunchKernelGGL(k_csr_spmv<T>, dim3(nblocks(m)), blk, 0, s, m, rowptr, col, val, x, y); break;
-    case 2: hipLaunchKernelGGL((k_csr_spmv_vec<T, 2>), dim3(nblocks(m * 2)), blk, 0, s, m, rowptr, col, val, x, y); break;
-    case 4: hipLaunchKernelGGL((k_csr_spmv_vec<T, 4>), dim3(nblocks(m * 4)), blk, 0, s, m, rowptr, col, val, x, y); break;
-    case 8: hipLaunchKernelGGL((k_csr_spmv_vec<T, 8>), dim3(nblocks(m * 8)), blk, 0, s, m, rowptr, col, val, x, y); break;
-    default: hipLaunchKernelGGL((k_csr_spmv_vec<T, 16>), dim3(nblocks(m * 16)), blk, 0, s, m, rowptr, col, val, x, y);
+    case 1: blaunch(1, k_csr_spmv<T>, dim3(nblocks(m)), blk, 0, s, m, rowptr, col, val, x, y); break;
+    case 2: blaunch(1, (k_csr_spmv_vec<T, 2>), dim3(nblocks(m * 2)), blk, 0, s, m, rowptr, col, val, x, y); break;
+    case 4: blaunch(1, (k_csr_spmv_vec<T, 4>), dim3(nblocks(m * 4)), blk, 0, s, m, rowptr, col, val, x, y); break;
+    case 8: blaunch(1, (k_csr_spmv_vec<T, 8>), dim3(nblocks(m * 8)), blk, 0, s, m, rowptr, col, val, x, y); break;
+    default: blaunch(1, (k_csr_spmv_vec<T, 16>), dim3(nblocks(m * 16)), blk, 0, s, m, rowptr, col, val, x, y);
   }
   return hipGetLastError();
 }
@@ -363,7 +441,7 @@ static hipError_t dia_t(i64 m, const DiaDesc& d, const unsigned char* cls, const
   if (m <= 0) return hipSuccess;
   if (d.nd < 1 || d.nd > DIA_MAX || d.ncls < 1 || d.ncls > 256) return hipErrorInvalidValue;
   const size_t lds = sizeof(T) * (size_t)(d.ncls * d.nd) + 256;
-  hipLaunchKernelGGL(k_dia_spmv<T>, dim3(nblocks(m)), dim3(BLAS_THREADS), lds, s, m, d, cls, masks, tab, x, y);
+  blaunch(1, k_dia_spmv<T>, dim3(nblocks(m)), dim3(BLAS_THREADS), lds, s, m, d, cls, masks, tab, x, y);
   return hipGetLastError();
 }
 hipError_t blas_dia_spmv(i64 m, const DiaDesc& d, const unsigned char* cls, const unsigned char* masks, const cd* tab,
@@ -405,10 +483,10 @@ static hipError_t maxpy_t(T* y, int k, const T* a, const T* const* xs, i64 n, bo
       for (int j = 0; j < kk; ++j) { c.a[j] = a[j0 + j]; p.p[j] = xs[j0 + j]; }
       const bool ow = overwrite && j0 == 0, nrm = norm2 && j0 + MV_MAX >= k;
       const dim3 g(nb), blk(BLAS_THREADS);
-      if (ow && nrm) hipLaunchKernelGGL((k_maxpy<T, true, true>), g, blk, 0, s, y, kk, c, p, n, part.d);
-      else if (ow) hipLaunchKernelGGL((k_maxpy<T, true, false>), g, blk, 0, s, y, kk, c, p, n, part.d);
-      else if (nrm) hipLaunchKernelGGL((k_maxpy<T, false, true>), g, blk, 0, s, y, kk, c, p, n, part.d);
-      else hipLaunchKernelGGL((k_maxpy<T, false, false>), g, blk, 0, s, y, kk, c, p, n, part.d);
+      if (ow && nrm) blaunch(2, (k_maxpy<T, true, true>), g, blk, 0, s, y, kk, c, p, n, part.d);
+      else if (ow) blaunch(2, (k_maxpy<T, true, false>), g, blk, 0, s, y, kk, c, p, n, part.d);
+      else if (nrm) blaunch(2, (k_maxpy<T, false, true>), g, blk, 0, s, y, kk, c, p, n, part.d);
+      else blaunch(2, (k_maxpy<T, false, false>), g, blk, 0, s, y, kk, c, p, n, part.d);
     }
   }
   hipError_t e = hipGetLastError();
@@ -417,7 +495,7 @@ static hipError_t maxpy_t(T* y, int k, const T* a, const T* const* xs, i64 n, bo
     *norm2 = 0.0;
     return hipSuccess;
   }
-  e = hipMemcpyAsync(part.h, part.d, sizeof(double) * nb, hipMemcpyDeviceToHost, s);
+  e = kprof_copy(part.h, part.d, sizeof(double) * nb, hipMemcpyDeviceToHost, s);
   if (e != hipSuccess) return e;
   e = hipStreamSynchronize(s);
   if (e != hipSuccess) return e;
@@ -449,8 +527,8 @@ static hipError_t reduce(const T* x, const T* y, i64 n, int kind, double out[2],
   if (e != hipSuccess) return e;
   unsigned nb = nblocks(n);
   if (nb > RED_BLOCKS) nb = RED_BLOCKS;
-  hipLaunchKernelGGL(k_reduce<T>, dim3(nb), dim3(BLAS_THREADS), 0, s, x, y, n, kind, part.d);
-  e = hipMemcpyAsync(part.h, part.d, sizeof(double) * 2 * nb, hipMemcpyDeviceToHost, s);
+  blaunch(2, k_reduce<T>, dim3(nb), dim3(BLAS_THREADS), 0, s, x, y, n, kind, part.d);
+  e = kprof_copy(part.h, part.d, sizeof(double) * 2 * nb, hipMemcpyDeviceToHost, s);
   if (e != hipSuccess) return e;
   e = hipStreamSynchronize(s);
   if (e != hipSuccess) return e;
@@ -500,8 +578,8 @@ static hipError_t mdot_t(const T* x, int k, const T* const* ys, i64 n, double* v
     for (int j = 0; j < kk; ++j) p.p[j] = ys[j0 + j];
     unsigned nb = nblocks(n);
     if (nb > (unsigned)NB) nb = NB;
-    hipLaunchKernelGGL(k_mdot<T>, dim3(nb), dim3(BLAS_THREADS), 0, s, x, kk, p, n, part.d);
-    e = hipMemcpyAsync(part.h, part.d, sizeof(double) * 2 * MDOT_K * nb, hipMemcpyDeviceToHost, s);
+    blaunch(2, k_mdot<T>, dim3(nb), dim3(BLAS_THREADS), 0, s, x, kk, p, n, part.d);
+    e = kprof_copy(part.h, part.d, sizeof(double) * 2 * MDOT_K * nb, hipMemcpyDeviceToHost, s);
     if (e != hipSuccess) return e;
     e = hipStreamSynchronize(s);
     if (e != hipSuccess) return e;
@@ -521,45 +599,89 @@ hipError_t blas_mdot(const cd* x, int k, const cd* const* ys, i64 n, cd* vals, h
   return mdot_t(x, k, ys, n, (double*)vals, s);
 }
 
+// k_mdot partials [chunk][block][2 MDOT_K] -> dots (device), one k_mdot_finish
+hipError_t blas_mdot_finish(const double* partial, int nb, int k, double* dots_dev, hipStream_t s) {
+  if (k < 1 || nb < 1 || nb > MDOT_BLOCKS) return hipErrorInvalidValue;
+  blaunch(2, k_mdot_finish, dim3((2 * k + 15) / 16), dim3(1024), 0, s, partial, nb, k, dots_dev);
+  return hipGetLastError();
+}
+
+// multi-dot launches into part (chunks of MDOT_K vectors), returns the workgroup count
+template <class T>
+static unsigned mdot_launch(const T* w, int k, const T* const* ys, i64 n, double* part, hipStream_t s) {
+  unsigned nb = nblocks(n);
+  if (nb > (unsigned)MDOT_BLOCKS) nb = MDOT_BLOCKS;
+  for (int j0 = 0; j0 < k; j0 += MDOT_K) {
+    const int kk = k - j0 < MDOT_K ? k - j0 : MDOT_K;
+    MVPtrsT<T> p;
+    for (int j = 0; j < kk; ++j) p.p[j] = ys[j0 + j] ? ys[j0 + j] : w;
+    blaunch(2, k_mdot<T>, dim3(nb), dim3(BLAS_THREADS), 0, s, w, kk, p, n,
+                       part + (size_t)(j0 / MDOT_K) * 2 * MDOT_K * MDOT_BLOCKS);
+  }
+  return nb;
+}
+
+// dots_dev[2 j + re/im] = ys_j^H x (ys_j == NULL: x), on the device without a host wait
+hipError_t blas_mdot_dev(const cd* x, int k, const cd* const* ys, i64 n, double* dots_dev, hipStream_t s) {
+  if (k < 1 || k > MV_MAX || n < 1) return hipErrorInvalidValue;
+  static thread_local Partials part;
+  const size_t mlen = (size_t)((MV_MAX + MDOT_K - 1) / MDOT_K) * 2 * MDOT_K * MDOT_BLOCKS;
+  hipError_t e = part.get(mlen);
+  if (e != hipSuccess) return e;
+  const unsigned nb = mdot_launch(x, k, ys, n, part.d, s);
+  blaunch(2, k_mdot_finish, dim3((2 * k + 15) / 16), dim3(1024), 0, s, part.d, (int)nb, k, dots_dev);
+  return hipGetLastError();
+}
+
+// w += sum_j scale_j dd_j ys_j on the device dots dd (2 k doubles), |w|^2; copies dd and the norm
+// partials back with one host wait
+template <class T>
+static hipError_t maxpy_dc_norm_t(T* w, int k, const T* const* ys, const double* scale, const double* dd, i64 n,
+                                  double* dots, double* norm2, hipStream_t s) {
+  if (k < 1 || k > MV_MAX) return hipErrorInvalidValue;
+  static thread_local Partials part;  // dots [2 MV_MAX] | norm [MAXPY_BLOCKS]
+  const size_t dlen = 2 * MV_MAX;
+  hipError_t e = part.get(dlen + MAXPY_BLOCKS);
+  if (e != hipSuccess) return e;
+  MVCoefT<double> sc;
+  MVPtrsT<T> p;
+  for (int j = 0; j < k; ++j) { sc.a[j] = scale[j]; p.p[j] = ys[j]; }
+  unsigned mb = nblocks(n);
+  if (mb > MAXPY_BLOCKS) mb = MAXPY_BLOCKS;
+  blaunch(2, k_maxpy_dc<T>, dim3(mb), dim3(BLAS_THREADS), 0, s, w, k, sc, dd, p, n, part.d + dlen);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = kprof_copy(part.h, dd, sizeof(double) * 2 * (size_t)k, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = kprof_copy(part.h + dlen, part.d + dlen, sizeof(double) * mb, hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) return e;
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return e;
+  for (int o = 0; o < 2 * k; ++o) dots[o] = part.h[o];
+  double t = 0.0;
+  for (unsigned q = 0; q < mb; ++q) t += part.h[dlen + q];
+  *norm2 = t;
+  return hipSuccess;
+}
+hipError_t blas_maxpy_dc_norm(cd* w, int k, const cd* const* ys, const double* scale, const double* dots_dev, i64 n,
+                              cd* dots, double* norm2, hipStream_t s) {
+  return maxpy_dc_norm_t(w, k, ys, scale, dots_dev, n, (double*)dots, norm2, s);
+}
+
 // dots_j = ys_j^H w, w += sum_j scale_j dots_j ys_j, |w|^2: multi-dot launches, the device finish,
 // the MAXPY on the device dots, one copy back and one host wait (k <= MV_MAX)
 template <class T>
 static hipError_t mdot_maxpy_norm_t(T* w, int k, const T* const* ys, const double* scale, i64 n, double* dots,
                                     double* norm2, hipStream_t s) {
   if (k < 1 || k > MV_MAX) return hipErrorInvalidValue;
-  static thread_local Partials part;  // [mdot chunks][2 MDOT_K][MDOT_BLOCKS] | dots [2 MV_MAX] | norm [MAXPY_BLOCKS]
+  static thread_local Partials part;  // [mdot chunks][2 MDOT_K][MDOT_BLOCKS] | dots [2 MV_MAX]
   const int chunks = (MV_MAX + MDOT_K - 1) / MDOT_K;
   const size_t mlen = (size_t)chunks * 2 * MDOT_K * MDOT_BLOCKS, dlen = 2 * MV_MAX;
-  hipError_t e = part.get(mlen + dlen + MAXPY_BLOCKS);
+  hipError_t e = part.get(mlen + dlen);
   if (e != hipSuccess) return e;
-  unsigned nb = nblocks(n);
-  if (nb > (unsigned)MDOT_BLOCKS) nb = MDOT_BLOCKS;
-  for (int j0 = 0; j0 < k; j0 += MDOT_K) {
-    const int kk = k - j0 < MDOT_K ? k - j0 : MDOT_K;
-    MVPtrsT<T> p;
-    for (int j = 0; j < kk; ++j) p.p[j] = ys[j0 + j];
-    hipLaunchKernelGGL(k_mdot<T>, dim3(nb), dim3(BLAS_THREADS), 0, s, (const T*)w, kk, p, n,
-                       part.d + (size_t)(j0 / MDOT_K) * 2 * MDOT_K * MDOT_BLOCKS);
-  }
+  const unsigned nb = mdot_launch((const T*)w, k, ys, n, part.d, s);
   double* dd = part.d + mlen;
-  hipLaunchKernelGGL(k_mdot_finish, dim3((2 * k + 15) / 16), dim3(1024), 0, s, part.d, (int)nb, k, dd);
-  MVCoefT<double> sc;
-  MVPtrsT<T> p;
-  for (int j = 0; j < k; ++j) { sc.a[j] = scale[j]; p.p[j] = ys[j]; }
-  unsigned mb = nblocks(n);
-  if (mb > MAXPY_BLOCKS) mb = MAXPY_BLOCKS;
-  hipLaunchKernelGGL(k_maxpy_dc<T>, dim3(mb), dim3(BLAS_THREADS), 0, s, w, k, sc, (const double*)dd, p, n, dd + dlen);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  e = hipMemcpyAsync(part.h + mlen, dd, sizeof(double) * (dlen + mb), hipMemcpyDeviceToHost, s);
-  if (e != hipSuccess) return e;
-  e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return e;
-  for (int o = 0; o < 2 * k; ++o) dots[o] = part.h[mlen + o];
-  double t = 0.0;
-  for (unsigned q = 0; q < mb; ++q) t += part.h[mlen + dlen + q];
-  *norm2 = t;
-  return hipSuccess;
+  blaunch(2, k_mdot_finish, dim3((2 * k + 15) / 16), dim3(1024), 0, s, part.d, (int)nb, k, dd);
+  return maxpy_dc_norm_t(w, k, ys, scale, (const double*)dd, n, dots, norm2, s);
 }
 hipError_t blas_mdot_maxpy_norm(cd* w, int k, const cd* const* ys, const double* scale, i64 n, cd* dots,
                                 double* norm2, hipStream_t s) {

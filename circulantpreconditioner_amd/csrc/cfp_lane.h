@@ -10,6 +10,9 @@ namespace {
 // DPP controls: quad_perm lane ^ 1, ^ 2, ^ 3; row_half_mirror (lane ^ 7 within 8 lanes);
 // row_ror:8 (lane ^ 8 within a row of 16)
 constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_XOR3 = 0x1B, DPP_HALF_MIRROR = 0x141, DPP_ROW_ROR8 = 0x128;
+// whole-wave shifts by one lane (gfx9 DPP): wave_shr:1 gives lane L the value of lane L - 1,
+// wave_shl:1 that of lane L + 1 (lanes 0 / 63 get nothing defined)
+constexpr int DPP_WAVE_SHR1 = 0x138, DPP_WAVE_SHL1 = 0x130;
 // ds_swizzle bit mode: and 0x1f, or 0, xor 0x10 (lane ^ 16 within 32 lanes)
 constexpr int SWZ_XOR16 = (0x10 << 10) | 0x1f;
 

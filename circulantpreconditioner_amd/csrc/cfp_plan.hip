@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/circulant_fft.h"
+#include "cfp_blas.h"
 #include "cfp_internal.h"
 #include "cfp_host.h"
 #include "cfp_three_pass.h"
@@ -132,6 +133,10 @@ struct cfp_plan_s {
   // layout cannot run in place (a unit's natural rows hold other units' blocked values), so
   // P1 writes and P3 reads this plan-owned buffer (N values, allocated on first use)
   cd* mid_buf = nullptr;
+  // cfp_plan_apply_ex: the fused P3's workgroup partials (16 doubles per workgroup) and the
+  // stencil output of the unfused fallback (N values), both allocated on first use
+  double* post_partial = nullptr;
+  cd* pre_buf = nullptr;
   // HIP-graph replay (cfp_plan_set_graph): one instantiated graph of the apply's launches per
   // (b, x) pair, captured on a private stream and launched into the caller's stream.  A graph
   // holds device pointers, not values: every setter that can move a buffer or change the
@@ -388,7 +393,10 @@ int step_mode(const cfp_plan_s* p, const Step& q, bool diag_override) {
 
 // ev (profiling): 2 events per step, (*ev)[2 i] / [2 i + 1] = start / end of step i -- the 3-sweep
 // kernels' own dispatch stamps, else events recorded around the step's launches
-int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStream_t s, std::vector<hipEvent_t>* ev) {
+// fz (cfp_plan_apply_ex): the fused stencil (stage 0) and dots (stage 2) of the 3-sweep schedule;
+// *p3grid = the workgroups of the fused P3 (its partials)
+int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStream_t s, std::vector<hipEvent_t>* ev,
+              const TPArgs* fz = nullptr, unsigned* p3grid = nullptr) {
   if (!diag_override && p->sym_kind == 0)
     return set_error(CFP_ERR_ARG_WRONGSTATE, "no symbol set on plan (call cfp_plan_set_symbol_* first)");
   // no dispatch stamps into a graph being captured: a replay would record into events that
@@ -431,7 +439,24 @@ int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStr
         if (q.tp == 2) tin = p->mid_buf;
         else tout = p->mid_buf;
       }
-      hipError_t e = launch_three_pass(q.tp, tn, tin, tout, a, p->tp_shape, s);
+      hipError_t e;
+      if (fz && q.tp == 0 && fz->pre_cls) {
+        a.pre_cls = fz->pre_cls;
+        a.pre_mask = fz->pre_mask;
+        a.pre_tab = fz->pre_tab;
+        a.pre_nd = fz->pre_nd;
+        a.pre_ncls = fz->pre_ncls;
+        for (int k = 0; k < 3; ++k) a.pre_off[k] = fz->pre_off[k];
+        e = launch_three_pass_fused(0, tn, tin, tout, a, s, nullptr);
+      } else if (fz && q.tp == 2 && fz->post_nv > 0) {
+        for (int j = 0; j < TP_POST_MAX; ++j) a.post_v[j] = fz->post_v[j];
+        a.post_nv = fz->post_nv;
+        a.post_self = fz->post_self;
+        a.post_partial = fz->post_partial;
+        e = launch_three_pass_fused(2, tn, tin, tout, a, s, p3grid);
+      } else {
+        e = launch_three_pass(q.tp, tn, tin, tout, a, p->tp_shape, s);
+      }
       g_stamp = LaunchStamp{};
       if (e != hipSuccess) return hip_error(e, "3-sweep launch");
       continue;
@@ -668,6 +693,8 @@ extern "C" int cfp_plan_destroy(cfp_plan_t p) {
   }
   if (p->host_stage) hipFree(p->host_stage);
   if (p->mid_buf) hipFree(p->mid_buf);
+  if (p->post_partial) hipFree(p->post_partial);
+  if (p->pre_buf) hipFree(p->pre_buf);
   graph_clear(p);
   if (p->cap_stream) hipStreamDestroy(p->cap_stream);
   for (auto& e : p->prof_ev) hipEventDestroy(e);
@@ -791,6 +818,79 @@ extern "C" int cfp_plan_apply(cfp_plan_t p, const double* b, double* x, void* st
   }
   if (p->graph_on) return graph_apply(p, (const cd*)b, (cd*)x, (hipStream_t)stream);
   return run_apply(p, nullptr, (const cd*)b, (cd*)x, (hipStream_t)stream, nullptr);
+}
+
+// The Krylov step around one apply (circulant_fft.h cfp_apply_ex_t): y = A b in P1 and the dots
+// in P3 of the 256^3 3-sweep schedule, or the stencil and the dots as their own kernels around a
+// plain apply wherever that schedule or the stencil's shape does not allow the fusion.
+extern "C" int cfp_plan_apply_ex(cfp_plan_t p, const double* b, double* x, void* stream, cfp_apply_ex_t* ex) {
+  if (!p || !b || !x || !ex) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  const cfp_stencil_t* st = ex->pre;
+  const int nv = ex->post_nv;
+  if (nv < 0 || nv > 8) return set_error(CFP_ERR_ARG_OUTOFRANGE, "post_nv must be in 0..8");
+  if (nv > 0 && !ex->post_out) return set_error(CFP_ERR_ARG_NULL, "post_out is NULL");
+  if (st) {
+    if (!st->cls || !st->mask || !st->tab) return set_error(CFP_ERR_ARG_NULL, "stencil arrays are NULL");
+    if (st->nd < 1 || st->nd > DIA_MAX || st->ncls < 1 || st->ncls > 256)
+      return set_error(CFP_ERR_ARG_OUTOFRANGE, "stencil: 1 <= nd <= 8, 1 <= ncls <= 256");
+    if ((const void*)b == (const void*)x) return set_error(CFP_ERR_ARG_WRONG, "b and x must differ with a stencil");
+  }
+  ex->fused = 0;
+  if (!st && nv == 0) return cfp_plan_apply(p, b, x, stream);
+  DeviceGuard dg(p->device);
+  hipStream_t s = (hipStream_t)stream;
+  bool pre_ok = !st || (st->x_local && st->nd <= 3 && st->ncls <= TP_PRE_MAX_CLS);
+  for (int k = 0; st && k < st->nd; ++k) pre_ok = pre_ok && st->off[k] >= -1 && st->off[k] <= 1;
+  const bool cube = p->n[0] == p->n[1] && p->n[1] == p->n[2];
+  if (cube && use_three_pass(p, false) && three_pass_fused_supported((int)p->n[0], p->tp_shape) && pre_ok &&
+      nv <= TP_POST_MAX) {
+    TPArgs fz;
+    if (st) {
+      fz.pre_cls = st->cls;
+      fz.pre_mask = st->mask;
+      fz.pre_tab = (const cd*)st->tab;
+      fz.pre_nd = st->nd;
+      fz.pre_ncls = st->ncls;
+      for (int k = 0; k < st->nd; ++k) fz.pre_off[k] = (int)st->off[k];
+    }
+    if (nv > 0) {
+      if (!p->post_partial) HIPCHK(hipMalloc(&p->post_partial, sizeof(double) * 16 * 1024));
+      for (int j = 0; j < nv; ++j) {
+        fz.post_v[j] = (const cd*)ex->post_v[j];
+        if (!ex->post_v[j] || ex->post_v[j] == x) fz.post_self |= 1 << j;
+      }
+      fz.post_nv = nv;
+      fz.post_partial = p->post_partial;
+    }
+    unsigned g = 0;
+    int rc = run_apply(p, nullptr, (const cd*)b, (cd*)x, s, nullptr, &fz, &g);
+    if (rc) return rc;
+    if (nv > 0) {
+      if (g < 1 || g > 1024) return set_error(CFP_ERR_LIB, "fused P3 grid out of range");
+      hipError_t e = blas_mdot_finish(p->post_partial, (int)g, nv, ex->post_out, s);
+      if (e != hipSuccess) return hip_error(e, "dots finish");
+    }
+    ex->fused = 1;
+    return CFP_SUCCESS;
+  }
+  const double* src = b;
+  if (st) {
+    if (!p->pre_buf) HIPCHK(hipMalloc(&p->pre_buf, sizeof(cd) * (size_t)p->N));
+    DiaDesc d;
+    for (int k = 0; k < st->nd; ++k) d.off[k] = st->off[k];
+    d.nd = st->nd;
+    d.ncls = st->ncls;
+    hipError_t e = blas_dia_spmv(p->N, d, st->cls, st->mask, (const cd*)st->tab, (const cd*)b, p->pre_buf, s);
+    if (e != hipSuccess) return hip_error(e, "stencil");
+    src = (const double*)p->pre_buf;
+  }
+  int rc = cfp_plan_apply(p, src, x, stream);
+  if (rc || nv == 0) return rc;
+  const cd* ys[8];
+  for (int j = 0; j < nv; ++j) ys[j] = (const cd*)ex->post_v[j];
+  hipError_t e = blas_mdot_dev((const cd*)x, nv, ys, p->N, ex->post_out, s);
+  if (e != hipSuccess) return hip_error(e, "dots");
+  return CFP_SUCCESS;
 }
 
 static void profile_free(cfp_plan_s* p) {

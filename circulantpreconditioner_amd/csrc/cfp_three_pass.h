@@ -23,7 +23,22 @@ struct TPArgs {
   int lnyl = 0;     // log2 of the rows per chunk (0: nyl = n, one chunk)
   i64 chunk = 0;    // elements per peer chunk
   int k1_off = 0;   // first global k1 of this rank (P2)
+  // Fused Krylov work of the stand-in GMRES (one GPU, natural layout; r06, launch_three_pass_fused):
+  // P1 reads A b instead of b, A an x-row-local stencil in row-class diagonal form (cfp_blas.h
+  // DiaDesc: diagonals -1, 0, +1 only, no entry across an x-row end); P3 adds the workgroup partial
+  // sums of post_v[j]^H x (j < post_nv; bit j of post_self: x itself, i.e. |x|^2) to post_partial
+  // [blockIdx][2 j + re/im], the k_mdot layout (cfp_blas.hip k_mdot_finish).
+  const unsigned char* pre_cls = nullptr;   // [N] row class
+  const unsigned char* pre_mask = nullptr;  // [ncls] diagonals present per class (bit k: pre_off[k])
+  const cd* pre_tab = nullptr;              // [ncls][pre_nd] coefficients
+  int pre_nd = 0, pre_ncls = 0;
+  int pre_off[3] = {0, 0, 0};
+  const cd* post_v[4] = {nullptr, nullptr, nullptr, nullptr};
+  int post_nv = 0;
+  int post_self = 0;  // bit j: post_v[j] is x itself (NULL)
+  double* post_partial = nullptr;
 };
+
 
 // kernel shape at 256^3 (cfp_plan_set_three_pass_shape); zeros = the measured default
 // BLOCKED: SWAP64_PF with the blocked intermediate layout (k_tp_rows<.., 8>; N1 = 32 only);
@@ -40,6 +55,14 @@ struct TPShape {
   int n1 = 0;   // y split ny = n1 * n2: 0 (default 32), 32 or 64
   int mid = 0;  // TP_MID_* (DEFAULT = SWAP64_PF at 256^3)
 };
+
+// the fused stencil's limits (LDS table in P1)
+#define TP_PRE_MAX_CLS 16
+#define TP_POST_MAX 4
+// stage 0 with the stencil (a.pre_*), 2 with the dots (a.post_*): 256^3 default shape only
+bool three_pass_fused_supported(int n, TPShape shape);
+hipError_t launch_three_pass_fused(int stage, int n, const cd* in, cd* out, const TPArgs& a, hipStream_t s,
+                                   unsigned* grid_out);
 
 bool three_pass_supported(const i64 n[3]);
 // 100^3 (n = R^2, R = 10: cfp_three_pass_sq.hip); launch_three_pass routes n = 100 there.

@@ -79,6 +79,18 @@ __device__ __forceinline__ int xcd_unit(int it, int G) {
   return it - b + (b & 7) * (G >> 3) + (b >> 3);
 }
 
+// sum over the wave's 64 lanes (every lane gets it): DPP within rows, swizzle across 16, permlane32
+__device__ __forceinline__ double wave_sum_d(double v) {
+  v += dpp_d<DPP_XOR1>(v);
+  v += dpp_d<DPP_XOR2>(v);
+  v += dpp_d<DPP_XOR3>(dpp_d<DPP_HALF_MIRROR>(v));  // lane ^ 4
+  v += dpp_d<DPP_ROW_ROR8>(v);
+  v += swz_xor16(v);
+  double w = v;
+  swap_d<5>(v, w);  // lanes < 32 get (v, v[L + 32]) pairs' partner in w
+  return v + w;
+}
+
 // first radix of an n-point FFT done as r0 x PTS x ... x PTS (n = r0 PTS^k, r0 <= PTS)
 constexpr int r0_of(int n, int pts) { return n > pts ? r0_of(n / pts, pts) : n; }
 
@@ -112,14 +124,26 @@ enum { PR_NO_Y2 = 1, PR_NO_ZMATH = 2, PR_NO_XCHG = 4, PR_NO_LOAD = 8, PR_NO_STOR
 // P1 / P3, 512-byte runs for P2's 2 x times 16 y2 tile.
 // XCD: units in xcd_unit order (the host launches whole rounds), so the N2 units of one z-plane,
 // whose blocked pieces share 128-byte lines, run under one L2.
+//
+// FUSE (r06, the stand-in GMRES's Krylov step; one GPU, natural layout): P1 (!INV) with FUSE = 1
+// loads y = A b, A an x-row-local stencil (TPArgs pre_*): the neighbours b[i -+ 1] of a point are
+// the same rows' lines, so the extra loads hit the caches and the sweep still reads b once from
+// HBM.  P3 (INV) with FUSE = NP > 0 accumulates post_v[j]^H x over its stored points (j <
+// a.post_nv <= NP; a NULL vector is x itself) across all its units and writes one partial per
+// workgroup and value: the VecMDot that follows a PCApply in classical Gram-Schmidt, without the
+// separate sweep that re-reads x.
 template <bool INV, int FLAGS, int N1, int TN, int PTS = 16, bool XS = true, bool LP = false, int BLK = 0,
-          bool XCD = false, int PROBE = 0>
+          bool XCD = false, int PROBE = 0, int FUSE = 0>
 __global__ void __launch_bounds__(N1 * (TN / PTS)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
 #ifndef CFP_KEXP
   static_assert(PROBE == 0, "timing probes are built in tools/kexp only");
 #endif
   constexpr int N2 = TN / N1, TR = TN / PTS, NT = N1 * TR, TY = N1 / PTS;
+  constexpr bool PRE = !INV && FUSE == 1, POST = INV && FUSE > 0;
+  constexpr int NP = POST ? FUSE : 1;
+  static_assert(!POST || NP <= TP_POST_MAX, "post dots: at most TP_POST_MAX vectors");
+  static_assert(FUSE == 0 || (BLK == 0 && PROBE == 0), "fused work: natural layout, product kernels");
   constexpr bool BL = BLK > 0;
   constexpr int BX = BL ? BLK : 1, BW = N2 * BX;  // x per block column, values per block column
   static_assert(!LP || (TY == 2 && TN % 32 == 0), "lane pairs: two threads per column, 32 columns per wave");
@@ -135,9 +159,45 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
   __shared__ __attribute__((aligned(16))) double lds[N1 * RS * (XS ? 1 : 2)];  // both layouts fit
   __shared__ cd tw_l[N1];  // W_N1 for phase A; phase C reads W_256 from global memory (L2 hits),
                            // which keeps it out of scratch (20 B/lane with the table in LDS)
+  // PRE: the stencil's classes as dense 3-slot rows (x - 1, x, x + 1) and their slot masks
+  __shared__ cd pre_tab_l[PRE ? 3 * TP_PRE_MAX_CLS : 1];
+  __shared__ unsigned pre_mk_l[PRE ? TP_PRE_MAX_CLS + 1 : 1];  // [ncls]: slot masks, [MAX]: their union
+  __shared__ const unsigned char* pre_cls_l[1];
+  // POST: per wave and value, the running sum of its lanes' dot contributions
+  __shared__ double post_l[POST ? 2 * NP * (NT / 64) : 1];
+  __shared__ const cd* post_ptr_l[POST ? NP : 1];
+  __shared__ int post_n_l[2];  // post_nv, post_self
   const int tid = threadIdx.x;
+  if constexpr (POST) {
+    for (int i = tid; i < 2 * NP * (NT / 64); i += NT) post_l[i] = 0.0;
+    if (tid < NP) post_ptr_l[tid] = a.post_v[tid];
+    if (tid == 0) {
+      post_n_l[0] = a.post_nv;
+      post_n_l[1] = a.post_self;
+    }
+  }
   for (int i = tid; i < N1; i += NT) tw_l[i] = a.tw[N2 * i];
-  if constexpr (LP) __syncthreads();  // phase A reads tw_l before any barrier
+  if constexpr (PRE) {
+    for (int c = tid; c < a.pre_ncls; c += NT) {
+      const unsigned mk = a.pre_mask[c];
+      unsigned dense = 0;
+      pre_tab_l[3 * c] = pre_tab_l[3 * c + 1] = pre_tab_l[3 * c + 2] = make_cd(0.0, 0.0);
+      for (int k = 0; k < a.pre_nd; ++k)
+        if ((mk >> k) & 1u) {
+          const int slot = a.pre_off[k] + 1;
+          pre_tab_l[3 * c + slot] = a.pre_tab[c * a.pre_nd + k];
+          dense |= 1u << slot;
+        }
+      pre_mk_l[c] = dense;
+    }
+    if (tid == 0) {
+      unsigned all = 0;
+      for (int k = 0; k < a.pre_nd; ++k) all |= 1u << (a.pre_off[k] + 1);
+      pre_mk_l[TP_PRE_MAX_CLS] = all;
+      pre_cls_l[0] = a.pre_cls;
+    }
+  }
+  if constexpr (LP || PRE || POST) __syncthreads();  // phase A reads tw_l (and the stencil) before any barrier
   // phase A: column x, thread ty of TY
   const int x0 = LP ? (tid & 31) + 32 * (tid >> 6) : tid % TN, ty0 = LP ? (tid >> 5) & 1 : tid / TN;
   const int r0 = tid / TR, tx0 = tid % TR;  // phase C: row r, thread tx of TR
@@ -167,6 +227,55 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
                                : in + crow(u / N2, u % N2 + N2 * ty) + x;
 #pragma unroll
       for (int m = 0; m < PTS; ++m) v[m] = gload<FLAGS>(src + crow(0, N2 * TY * m));
+    } else if constexpr (PRE) {
+      // y = A b on the unit's rows.  With lane pairs (LP) lanes L and L + 1 of a wave hold x and
+      // x + 1 of one row for L % 32 < 31, so a point's x-neighbours come from its neighbour lanes
+      // (DPP wave_shr / wave_shl); only the lanes at x % 32 = 0 / 31 load theirs (exec-masked, the
+      // same lines: cache hits).  A neighbour outside the row is never used (its slot is absent
+      // from the row's class), so its address is clamped into the row.
+      static_assert(LP, "the fused stencil relies on the lane-pair layout");
+      const i64 i0 = (i64)(u / N2) * TN * TN + x + (i64)TN * (u % N2 + N2 * ty);
+      const int xm = x > 0 ? -1 : 0, xp = x < TN - 1 ? 1 : 0;
+      const int l32 = (int)(threadIdx.x & 31);
+      // the slots any class uses, and the class array, from LDS at each use (kernel-argument
+      // values would sit in SGPRs across the FFTs)
+      const unsigned slots = ((volatile unsigned*)pre_mk_l)[TP_PRE_MAX_CLS];
+      const bool hm = (slots & 1u) != 0, hp = (slots & 4u) != 0;
+      const unsigned char* const cls = ((const unsigned char* const volatile*)pre_cls_l)[0];
+      int cl[PTS];
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) {
+        const i64 i = i0 + (i64)TN * N2 * TY * m;
+        v[m] = gload<FLAGS>(in + i);
+        cl[m] = cls[i];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int m = 0; m < PTS; ++m) {
+        const i64 i = i0 + (i64)TN * N2 * TY * m;
+        cd bm = make_cd(0.0, 0.0), bp = make_cd(0.0, 0.0);
+        if (hm) {
+          bm = dpp_c<DPP_WAVE_SHR1>(v[m]);
+          if (l32 == 0) bm = gload<0>(in + i + xm);
+        }
+        if (hp) {
+          bp = dpp_c<DPP_WAVE_SHL1>(v[m]);
+          if (l32 == 31) bp = gload<0>(in + i + xp);
+        }
+        const unsigned mk = pre_mk_l[cl[m]];
+        const cd* t = pre_tab_l + 3 * cl[m];
+        // the same fma sequence, in the same diagonal order, as k_dia_spmv: bit-identical to
+        // MatMult on the row-class form
+        double ax = 0.0, ay = 0.0;
+        const auto acc = [&](cd q, cd b) {
+          ax = fma(q.x, b.x, fma(-q.y, b.y, ax));
+          ay = fma(q.x, b.y, fma(q.y, b.x, ay));
+        };
+        if (mk & 1u) acc(t[0], bm);
+        if (mk & 2u) acc(t[1], v[m]);
+        if (mk & 4u) acc(t[2], bp);
+        v[m] = make_cd(ax, ay);
+      }
     } else {
       const cd* const src = in + (i64)(u / N2) * TN * TN + x + (i64)TN * (u % N2 + N2 * ty);  // + uniform
 #pragma unroll
@@ -262,12 +371,66 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
 #pragma unroll
         for (int m = 0; m < PTS; ++m) gstore<FLAGS>(dst + TR * N2 * m, make_cd(v[m].x * sc, v[m].y * sy));
       } else {
-        cd* dst = out + (INV ? (i64)(u / N2) * TN * TN + (i64)TN * (u % N2 + N2 * r) : crow(u / N2, u % N2 + N2 * r)) + tx;
+        const i64 e0 = (INV ? (i64)(u / N2) * TN * TN + (i64)TN * (u % N2 + N2 * r) : crow(u / N2, u % N2 + N2 * r)) + tx;
+        cd* dst = out + e0;
 #pragma unroll
-        for (int m = 0; m < PTS; ++m) gstore<FLAGS>(dst + TR * m, make_cd(v[m].x * sc, v[m].y * sy));
+        for (int m = 0; m < PTS; ++m) {
+          v[m] = make_cd(v[m].x * sc, v[m].y * sy);
+          gstore<FLAGS>(dst + TR * m, v[m]);
+        }
+        if constexpr (POST) {
+          // post_v[j]^H x over the unit's stored points (the other vectors read 4 points at a
+          // time), reduced over the wave and added to the wave's slot in LDS: nothing stays live
+          // across the next unit's FFTs
+          const int lane = tid & 63, wv = tid >> 6;
+          const int pnv = ((volatile int*)post_n_l)[0], pself = ((volatile int*)post_n_l)[1];
+          constexpr int QB = 4;
+#pragma unroll
+          for (int j = 0; j < NP; ++j) {
+            if (j < pnv) {
+              double sr = 0.0, si = 0.0;
+              if ((pself >> j) & 1) {
+#pragma unroll
+                for (int m = 0; m < PTS; ++m) sr += v[m].x * v[m].x + v[m].y * v[m].y;
+              } else {
+                // the vector's address from LDS at each use (a kernel-argument pointer would be
+                // held in SGPRs across the FFTs, which already use all of them)
+                const cd* pv = ((const cd* volatile*)post_ptr_l)[j] + e0;
+#pragma unroll
+                for (int m0 = 0; m0 < PTS; m0 += QB) {
+                  cd q[QB];
+#pragma unroll
+                  for (int m = 0; m < QB; ++m) q[m] = gload<0>(pv + TR * (m0 + m));
+#pragma unroll
+                  for (int m = 0; m < QB; ++m) {
+                    const cd w = v[m0 + m];
+                    sr += q[m].x * w.x + q[m].y * w.y;
+                    si += q[m].x * w.y - q[m].y * w.x;
+                  }
+                }
+              }
+              sr = wave_sum_d(sr);
+              si = wave_sum_d(si);
+              if (lane == 0) {
+                post_l[(2 * j) * (NT / 64) + wv] += sr;
+                post_l[(2 * j + 1) * (NT / 64) + wv] += si;
+              }
+            }
+          }
+        }
       }
     }
     lds_barrier();  // the next unit's first exchange overwrites LDS
+  }
+  if constexpr (POST) {
+    // one partial per workgroup and value: the waves' sums in a fixed order
+    __syncthreads();
+    if (tid < 2 * NP) {
+      double s = 0.0;
+#pragma unroll
+      for (int q = 0; q < NT / 64; ++q) s += post_l[tid * (NT / 64) + q];
+      a.post_partial[(size_t)blockIdx.x * 16 + tid] = s;
+    }
   }
 }
 
@@ -1165,6 +1328,37 @@ hipError_t launch_three_pass_slab(int stage, int n, const cd* in, cd* out, const
       hipLaunchKernelGGL((k_tp_rows<true, F_NT_ST | W, 32, 256, 16, true, kRowsLP>), dim3(g), dim3(512), 0, s,
                          in, out, a, units);
   }
+  return hipGetLastError();
+}
+
+// The default 256^3 row sweeps with the stand-in GMRES's Krylov work fused in (TPArgs pre_* /
+// post_*): P1 on A b, P3 with the dots.  Same grids and unit order as launch_rows_ab.
+bool three_pass_fused_supported(int n, TPShape shape) { return n == 256 && shape.n1 == 0 && shape.mid == TP_MID_DEFAULT; }
+
+template <bool XCD>
+static void launch_rows_fused(int stage, const cd* in, cd* out, const TPArgs& a, hipStream_t s, unsigned g) {
+  constexpr int W = kRowsWave ? F_WAVE_LDS : 0, units = 256 * 8;
+  if (stage == 0)
+    TP_LAUNCH((k_tp_rows<false, kP1Flags | W, 32, 256, 16, true, kRowsLP, 0, XCD, 0, 1>), dim3(g), dim3(512), s, in,
+              out, a, units);
+  else
+    TP_LAUNCH((k_tp_rows<true, kP3Flags | W, 32, 256, 16, true, kRowsLP, 0, XCD, 0, TP_POST_MAX>), dim3(g), dim3(512),
+              s, in, out, a, units);
+}
+
+hipError_t launch_three_pass_fused(int stage, int n, const cd* in, cd* out, const TPArgs& a, hipStream_t s,
+                                   unsigned* grid_out) {
+  if (n != 256 || (stage != 0 && stage != 2)) return hipErrorNotSupported;
+  if (stage == 0 && (!a.pre_cls || in == out || a.pre_ncls < 1 || a.pre_ncls > TP_PRE_MAX_CLS || a.pre_nd < 1 ||
+                     a.pre_nd > 3))
+    return hipErrorInvalidValue;
+  if (stage == 2 && (a.post_nv < 1 || a.post_nv > TP_POST_MAX || !a.post_partial)) return hipErrorInvalidValue;
+  constexpr int units = 256 * 8;
+  const unsigned gx = kRowsXCD ? grid_xcd(units, 2) : 0;
+  const unsigned g = gx ? gx : grid_of(units, 2);
+  if (grid_out) *grid_out = g;
+  if (gx) launch_rows_fused<true>(stage, in, out, a, s, g);
+  else launch_rows_fused<false>(stage, in, out, a, s, g);
   return hipGetLastError();
 }
 

@@ -68,6 +68,12 @@ struct _p_KSP {
   PetscInt n = -1, nvec = 0;
   Vec* V = nullptr;  // restart + 1 basis vectors
   Vec t = nullptr, t2 = nullptr, rhs = nullptr;
+  // the dots a shell PC computes inside its apply (PCMiniApplyDots, r06): device results, and
+  // whether the basis lives on the device (requests are made only then)
+  double* dots_dev = nullptr;
+  bool dev_basis = false;
+  bool fusion = true;  // KSPMiniSetFusion
+  PetscInt fused_dots = 0, fused_norms = 0;  // how many Gram-Schmidt dots / norms came from the PC
 };
 
 static PetscErrorCode kcheck(KSP k, const char* f) {
@@ -84,6 +90,9 @@ static void free_events(KSP k) {
 }
 
 static void free_work(KSP k) {
+  if (k->dots_dev) hipFree(k->dots_dev);
+  k->dots_dev = nullptr;
+  k->dev_basis = false;
   if (k->V) VecDestroyVecs(k->nvec, &k->V);
   VecDestroy(&k->t);
   VecDestroy(&k->t2);
@@ -129,7 +138,12 @@ extern "C" PetscErrorCode KSPSetInitialGuessNonzero(KSP k, PetscBool f) {
   return PETSC_SUCCESS;
 }
 extern "C" PetscErrorCode KSPGetPC(KSP k, PC* pc) { KCHK(k); *pc = k->pc; return PETSC_SUCCESS; }
-extern "C" PetscErrorCode KSPSetOperators(KSP k, Mat A, Mat P) { KCHK(k); k->A = A; k->P = P; return PETSC_SUCCESS; }
+extern "C" PetscErrorCode KSPSetOperators(KSP k, Mat A, Mat P) {
+  KCHK(k);
+  k->A = A;
+  k->P = P;
+  return PCSetOperators(k->pc, A, P);
+}
 extern "C" PetscErrorCode KSPSetUp(KSP k) {
   KCHK(k);
   return PCSetUp(k->pc);
@@ -141,6 +155,17 @@ extern "C" PetscErrorCode KSPMiniGetPCApplyStats(KSP k, PetscInt* calls, PetscLo
   KCHK(k);
   if (calls) *calls = k->pc_calls;
   if (seconds) *seconds = k->pc_seconds;
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode KSPMiniSetFusion(KSP k, PetscBool on) {
+  KCHK(k);
+  k->fusion = on == PETSC_TRUE;
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode KSPMiniGetFusedCounts(KSP k, PetscInt* dots, PetscInt* norms) {
+  KCHK(k);
+  if (dots) *dots = k->fused_dots;
+  if (norms) *norms = k->fused_norms;
   return PETSC_SUCCESS;
 }
 extern "C" PetscErrorCode KSPDestroy(KSP* pk) {
@@ -183,12 +208,31 @@ extern "C" PetscErrorCode KSPMiniSetUpWork(KSP k, Vec v) {
     PetscCall(VecDuplicate(v, &k->t2));
     PetscCall(VecDuplicate(v, &k->rhs));
     k->n = n;
+#ifndef CFP_REAL_SCALAR
+    VecType vt;
+    PetscCall(VecGetType(v, &vt));
+    int P = 1;
+    MPI_Comm comm;
+    PetscCall(VecGetComm(v, &comm));
+    MPI_Comm_size(comm, &P);
+    k->dev_basis = P == 1 && std::strcmp(vt, VECSEQHIP) == 0 &&
+                   hipMalloc(&k->dots_dev, sizeof(double) * 16) == hipSuccess;
+    if (!k->dev_basis) hipGetLastError();
+#endif
   }
   if (k->pc_ev.empty()) grow_events(k);  // no device: the applies are timed on the host
   return PETSC_SUCCESS;
 }
 
-static PetscErrorCode pc_apply(KSP k, Vec x, Vec y) {
+// one PCApply (ba: PCApplyBAorAB on the left, y = B A x, k->t the scratch), with an optional dots
+// request to the shell (PCMiniApplyDots; req->done tells whether the apply computed them)
+static PetscErrorCode pc_apply(KSP k, Vec x, Vec y, PCMiniApplyDots* req = nullptr, bool ba = false) {
+  if (req) PetscCall(PCMiniSetApplyDots(k->pc, req));
+  const auto call = [&]() -> PetscErrorCode {
+    const PetscErrorCode rc = ba ? PCApplyBAorAB(k->pc, PC_LEFT, x, y, k->t) : PCApply(k->pc, x, y);
+    if (req) PCMiniSetApplyDots(k->pc, nullptr);
+    return rc;
+  };
   void* st = nullptr;
   PetscCall(VecMiniGetStream(&st));
   bool events = k->pc_ev_used + 4 <= k->pc_ev.size();
@@ -196,7 +240,7 @@ static PetscErrorCode pc_apply(KSP k, Vec x, Vec y) {
   if (!events) {  // no HIP device (host Vecs on a CPU-only machine): the apply is synchronous
     hipGetLastError();
     const double t0 = now();
-    PetscCall(PCApply(k->pc, x, y));
+    PetscCall(call());
     k->pc_seconds += now() - t0;
     k->pc_calls += 1;
     return PETSC_SUCCESS;
@@ -208,7 +252,7 @@ static PetscErrorCode pc_apply(KSP k, Vec x, Vec y) {
   const size_t i0 = k->pc_ev_used;
   hipEventRecord(k->pc_ev[i0], (hipStream_t)st);
   cfp::g_apply_stamp = cfp::ApplyStamp{k->pc_ev[i0 + 2], k->pc_ev[i0 + 3], 0};
-  const PetscErrorCode rc = PCApply(k->pc, x, y);
+  const PetscErrorCode rc = call();
   const bool stamped = cfp::g_apply_stamp.hits == 2;
   cfp::g_apply_stamp = cfp::ApplyStamp{};
   PetscCall(rc);
@@ -243,9 +287,23 @@ static void converged(KSP k, PetscReal rnorm0) {
   else if (k->its > 0 && k->rnorm >= k->dtol * rnorm0) k->reason = KSP_DIVERGED_DTOL;
 }
 
+// device pointers of the basis vectors V[0..nv) for a dots request
+static PetscErrorCode basis_ptrs(KSP k, PetscInt nv, PCMiniApplyDots* req) {
+  req->nv = nv;
+  req->out = k->dots_dev;
+  for (PetscInt i = 0; i < nv; ++i) {
+    const PetscScalar* a;
+    PetscCall(VecHIPGetArrayRead(k->V[i], &a));
+    req->v[i] = a;
+    PetscCall(VecHIPRestoreArrayRead(k->V[i], &a));
+  }
+  return PETSC_SUCCESS;
+}
+
 // preconditioned residual into z (left: z = B (b - A x); right: z = b - A x).  x = 0: left,
-// z = B b straight from b (no copy of b); right, z = a copy of b.
-static PetscErrorCode residual(KSP k, Vec b, Vec x, bool x_zero, Vec z) {
+// z = B b straight from b (no copy of b); right, z = a copy of b.  *norm = |z| (its square asked
+// from the shell's apply on device bases, else VecNorm).
+static PetscErrorCode residual(KSP k, Vec b, Vec x, bool x_zero, Vec z, PetscReal* norm) {
   Vec r = k->side == PC_LEFT ? k->t : z;
   if (x_zero && k->side == PC_LEFT) {
     r = b;
@@ -255,11 +313,30 @@ static PetscErrorCode residual(KSP k, Vec b, Vec x, bool x_zero, Vec z) {
     PetscCall(MatMult(k->A, x, k->t2));
     PetscCall(VecWAXPY(r, -1.0, k->t2, b));
   }
-  if (k->side == PC_LEFT) PetscCall(pc_apply(k, r, z));
+  PCMiniApplyDots req{};
+  bool asked = false;
+  if (k->side == PC_LEFT) {
+    asked = k->fusion && k->dev_basis && z == k->V[0];
+    if (asked) {
+      req.nv = 1;
+      req.v[0] = nullptr;  // |z|^2
+      req.out = k->dots_dev;
+    }
+    PetscCall(pc_apply(k, r, z, asked ? &req : nullptr));
+  }
+  if (asked && req.done) {
+    double s2[2];
+    PetscCall(PetscMiniDeviceRead(k->dots_dev, 2, s2));
+    *norm = std::sqrt(s2[0]);
+    k->fused_norms += 1;
+  } else {
+    PetscCall(VecNorm(z, NORM_2, norm));
+  }
   return PETSC_SUCCESS;
 }
 
-extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
+// the solve; x_unset: x has not been written yet (a zero initial guess is implied, not stored)
+static PetscErrorCode ksp_solve_impl(KSP k, Vec b, Vec x, bool& x_unset) {
   KCHK(k);
   if (!k->A) return PetscErrorSet(PETSC_ERR_ARG_WRONGSTATE, __func__, "KSPSetOperators has not been called");
   PetscCall(PCSetUp(k->pc));
@@ -270,6 +347,7 @@ extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
   k->pc_calls = 0;
   k->pc_seconds = 0.0;
   k->pc_ev_used = 0;
+  k->fused_dots = k->fused_norms = 0;
   if (k->type == KSPPREONLY) {
     if (b == x) {  // PCApply needs x != y
       PetscCall(VecCopy(b, k->rhs));
@@ -284,10 +362,9 @@ extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
   // until x is first written (the end of the first cycle), and copied only if a restart follows.
   bool b_in_x = b == x;
   // x = 0 initially: not set here; the first solution update overwrites x (VecMiniMAXPYNorm).
-  // Consequence (unlike PETSc, which zeroes x first): if the solve returns early with an error
-  // (a failed PCApply / MatMult, PetscCall), x still holds the caller's old contents -- or b,
-  // when b == x.  x is defined only after a successful return.
-  bool x_zero = !k->guess_nonzero, x_unset = x_zero;
+  // An error return before that update zeroes x (KSPSolve below), as PETSc's zeroed x would be.
+  bool x_zero = !k->guess_nonzero;
+  x_unset = x_zero;
 
   std::vector<C> H((size_t)(m + 1) * m), cc((size_t)m), ss((size_t)m), rs((size_t)m + 1), y((size_t)m);
   auto h = [&](PetscInt i, PetscInt j) -> C& { return H[(size_t)j * (m + 1) + i]; };
@@ -307,10 +384,9 @@ extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
   };
 
   while (true) {
-    PetscCall(residual(k, b, x, x_zero, V[0]));
-    x_zero = false;
     PetscReal beta;
-    PetscCall(VecNorm(V[0], NORM_2, &beta));
+    PetscCall(residual(k, b, x, x_zero, V[0], &beta));
+    x_zero = false;
     k->rnorm = beta;
     if (rnorm0 < 0) rnorm0 = beta;
     converged(k, rnorm0);
@@ -324,9 +400,14 @@ extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
     bool happy = false;
     for (; j < m && k->reason == KSP_CONVERGED_ITERATING && k->its < k->maxits; ++j) {
       // w' = B A u_j (left) or A B u_j (right), written into V[j+1]; w = sg_j w'
+      // left: PCApplyBAorAB (a shell may fuse the MatMult into its apply), with the Gram-Schmidt
+      // dots u_i^H w' asked from the apply on device bases (at most 4 vectors)
+      PCMiniApplyDots req{};
+      bool asked = false;
       if (k->side == PC_LEFT) {
-        PetscCall(MatMult(k->A, V[j], k->t));
-        PetscCall(pc_apply(k, k->t, V[j + 1]));
+        asked = k->fusion && k->dev_basis && j + 1 <= 4;
+        if (asked) PetscCall(basis_ptrs(k, j + 1, &req));
+        PetscCall(pc_apply(k, V[j], V[j + 1], asked ? &req : nullptr, true));
       } else {
         PetscCall(pc_apply(k, V[j], k->t));
         PetscCall(MatMult(k->A, k->t, V[j + 1]));
@@ -337,7 +418,12 @@ extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
       std::vector<PetscReal> negsq((size_t)j + 1);
       for (PetscInt i = 0; i <= j; ++i) negsq[(size_t)i] = -(sg[(size_t)i] * sg[(size_t)i]);
       PetscReal hn;
-      PetscCall(VecMiniMDotMAXPYNorm(V[j + 1], j + 1, negsq.data(), V, hv.data(), &hn));
+      if (asked && req.done) {
+        PetscCall(VecMiniMAXPYNormDeviceDots(V[j + 1], j + 1, negsq.data(), V, k->dots_dev, hv.data(), &hn));
+        k->fused_dots += 1;
+      } else {
+        PetscCall(VecMiniMDotMAXPYNorm(V[j + 1], j + 1, negsq.data(), V, hv.data(), &hn));
+      }
       for (PetscInt i = 0; i <= j; ++i) h(i, j) = sg[(size_t)i] * sg[(size_t)j] * hv[(size_t)i];
       hn *= sg[(size_t)j];  // |w| = sg_j |w''|
       h(j + 1, j) = hn;
@@ -405,6 +491,16 @@ extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
     if (k->reason != KSP_CONVERGED_ITERATING) break;
   }
   if (x_unset) PetscCall(VecSet(x, 0.0));  // converged before any update (b = 0): x = 0
+  x_unset = false;
   return pc_collect(k);
+}
+
+extern "C" PetscErrorCode KSPSolve(KSP k, Vec b, Vec x) {
+  bool x_unset = false;
+  const PetscErrorCode rc = ksp_solve_impl(k, b, x, x_unset);
+  // PETSc zeroes x before a zero-guess solve: after an error before the first update x reads 0
+  // here too (not the caller's old contents, nor b when b == x); the first error is returned
+  if (rc && x_unset) VecSet(x, 0.0);
+  return rc;
 }
 #endif  // CFP_WITH_PETSC

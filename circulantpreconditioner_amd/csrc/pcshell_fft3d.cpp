@@ -351,7 +351,9 @@ extern "C" PetscErrorCode build_diag_mat_vec_3D(Vec Diag, Vec cx, Vec cy, Vec cz
 // persistent buffer (cfp_plan_apply_host), slab plan through the shell's; those applies, and
 // every slab apply (its exchanges are host-driven), return complete.  A single-rank apply on
 // device Vecs is ordered on the Vec stream (cfp_pc::device_stream).
-PetscErrorCode shell_apply(FFTShell* s, Vec X, Vec b, bool own, Vec Diag) {
+// ex (single rank, register symbol, b != X): the fused Krylov step (cfp_plan_apply_ex); ex->fused
+// stays -1 when this apply could not take it.
+PetscErrorCode shell_apply(FFTShell* s, Vec X, Vec b, bool own, Vec Diag, cfp_apply_ex_t* ex = nullptr) {
   const PetscInt n = s->nlocal;
   DevIn din;
   if (!own && !s->dplan) PetscCall(din.get(Diag, n));
@@ -361,8 +363,10 @@ PetscErrorCode shell_apply(FFTShell* s, Vec X, Vec b, bool own, Vec Diag) {
   void* vst = nullptr;
   bool vwait = true;
   cfp_pc::device_stream(&vst, &vwait);
+  if (ex) ex->fused = -1;
   auto dev_apply = [&](const double* in, double* out) -> int {
     if (s->dplan) return cfp_dist_plan_apply(s->dplan, in, out, vst);
+    if (ex && own && in != out) return cfp_plan_apply_ex(s->plan, in, out, vst, ex);
     return own ? cfp_plan_apply(s->plan, in, out, vst) : cfp_plan_apply_with_diag(s->plan, din.ptr(), in, out, vst);
   };
   // device Vecs: wait only where the caller cannot rely on stream order
@@ -415,9 +419,9 @@ PetscErrorCode shell_apply(FFTShell* s, Vec X, Vec b, bool own, Vec Diag) {
 
 // solve_3D, :166-190: X = (1/size) F^T( F(b) ./ Diag ), fused into one 3- or 5-launch apply.
 // b_hat is the reference's scratch vector; the fused apply needs none and leaves it untouched.
-extern "C" PetscErrorCode solve_3D(Mat FFT_MAT, Vec X, Vec Diag, Vec b, Vec b_hat, PetscInt size) {
+// ex: the stand-in KSP's dots of X, computed with the apply where it can (shell_apply).
+PetscErrorCode solve_impl(Mat FFT_MAT, Vec X, Vec Diag, Vec b, PetscInt size, cfp_apply_ex_t* ex) {
   PetscFunctionBeginUser;
-  (void)b_hat;
   FFTShell* s;
   PetscCall(fft_shell(FFT_MAT, &s));
   const PetscInt N = s->dims[0] * s->dims[1] * s->dims[2];
@@ -453,9 +457,28 @@ extern "C" PetscErrorCode solve_3D(Mat FFT_MAT, Vec X, Vec Diag, Vec b, Vec b_ha
     }
   }
   ++(own ? s->solves_own : s->solves_diag);
-  PetscCall(shell_apply(s, X, b, own, Diag));
+  PetscCall(shell_apply(s, X, b, own, Diag, ex));
   PetscFunctionReturn(PETSC_SUCCESS);
 }
+extern "C" PetscErrorCode solve_3D(Mat FFT_MAT, Vec X, Vec Diag, Vec b, Vec b_hat, PetscInt size) {
+  (void)b_hat;
+  return solve_impl(FFT_MAT, X, Diag, b, size, nullptr);
+}
+
+#ifndef CFP_WITH_PETSC
+// The stand-in KSP's pending dots request (PCMiniApplyDots) as the post-op of a plan apply
+cfp_apply_ex_t* take_dots(PC pc, cfp_apply_ex_t* ex, PCMiniApplyDots** req) {
+  *req = nullptr;
+  if (PCMiniGetApplyDots(pc, req) || !*req || (*req)->done || (*req)->nv < 1 || (*req)->nv > 8) {
+    *req = nullptr;
+    return nullptr;
+  }
+  ex->post_nv = (int)(*req)->nv;
+  for (PetscInt j = 0; j < (*req)->nv; ++j) ex->post_v[j] = (const double*)(*req)->v[j];
+  ex->post_out = (*req)->out;
+  return ex;
+}
+#endif
 
 // FftTransportSolver, :218-264.  The reference builds three 1-D FFTs of the transport column
 // and the Kronecker Diag on every call, then destroys the caller's FFT_MAT (App. A item 6).
@@ -533,7 +556,79 @@ extern "C" PetscErrorCode applyFFT3DPrecTransport(PC pc, Vec b, Vec x) {
     PetscCall(MatMult(back, ctx->b_cartesien, x));
     PetscFunctionReturn(PETSC_SUCCESS);
   }
+#ifndef CFP_WITH_PETSC
+  // the stand-in KSP may ask for dots of x with its basis (PCMiniApplyDots): they ride in the apply
+  cfp_apply_ex_t exd{};
+  PCMiniApplyDots* req = nullptr;
+  cfp_apply_ex_t* ex = take_dots(pc, &exd, &req);
+  PetscCall(solve_impl(ctx->FFT_MAT, x, ctx->Diag, src, N, ex));
+  if (req && exd.fused >= 0) req->done = PETSC_TRUE;
+#else
   PetscCall(solve_3D(ctx->FFT_MAT, x, ctx->Diag, src, ctx->b_hat, N));
+#endif
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
+// PCShellSetApplyBA callback (PETSc's PCApplyBAorAB on a shell): y = B A x (left) or A B x
+// (right) with A the PC's operator.  One rank, left, register symbol, no remaps, and A the
+// stand-in AIJ in row-class form: A x is formed inside the apply's first sweep (cfp_apply_ex_t,
+// P1 reads x once) instead of a MatMult sweep into `work` -- config 3's transport operator couples
+// cells along x only, so the whole stencil of a row is in the rows P1 loads.  Anything else:
+// MatMult, then the apply, as PETSc does without an applyBA.
+extern "C" PetscErrorCode applyFFT3DPrecTransportBA(PC pc, PCSide side, Vec x, Vec y, Vec work) {
+  PetscFunctionBeginUser;
+  FFTPrecTransportContext* ctx = nullptr;
+  PetscCall(PCShellGetContext(pc, &ctx));
+  PetscCheck(ctx && ctx->FFT_MAT && ctx->Diag, PETSC_COMM_SELF, PETSC_ERR_ARG_WRONGSTATE,
+             "applyFFT3DPrecTransportBA: setupFFTPrec3D has not run");
+  Mat A = nullptr;
+  PetscCall(PCGetOperators(pc, &A, NULL));
+  PetscCheck(A, PETSC_COMM_SELF, PETSC_ERR_ARG_WRONGSTATE, "applyFFT3DPrecTransportBA: the PC has no operator");
+#ifndef CFP_WITH_PETSC
+  if (side == PC_LEFT && !ctx->intersectionMatrix && !ctx_remap_back(ctx) && x != y) {
+    FFTShell* s;
+    PetscCall(fft_shell(ctx->FFT_MAT, &s));
+    bool own = false;
+    PetscCall(diag_is_own_symbol(s, ctx->Diag, &own));
+    PetscInt am, an;
+    PetscCall(MatGetSize(A, &am, &an));
+    const PetscInt N = ctx->n_x * ctx->n_y * ctx->n_z;
+    if (!s->dplan && own && am == N && an == N) {
+      PetscBool has = PETSC_FALSE, xl = PETSC_FALSE;
+      PetscMiniDia dia;
+      PetscCall(PetscMiniMatAIJGetDia(A, ctx->n_x, &has, &xl, &dia));
+      if (has) {
+        cfp_stencil_t st;
+        std::memset((void*)&st, 0, sizeof(st));
+        st.cls = dia.cls;
+        st.mask = dia.mask;
+        st.tab = (const double*)dia.tab;
+        for (int k = 0; k < 8; ++k) st.off[k] = dia.off[k];
+        st.nd = dia.nd;
+        st.ncls = dia.ncls;
+        st.x_local = xl ? 1 : 0;
+        cfp_apply_ex_t ex{};
+        PCMiniApplyDots* req = nullptr;
+        take_dots(pc, &ex, &req);
+        ex.pre = &st;
+        ++s->solves_own;
+        PetscCall(shell_apply(s, y, x, true, nullptr, &ex));
+        PetscCheck(ex.fused >= 0, PETSC_COMM_SELF, PETSC_ERR_PLIB, "applyFFT3DPrecTransportBA: fused apply not taken");
+        if (req) req->done = PETSC_TRUE;
+        PetscFunctionReturn(PETSC_SUCCESS);
+      }
+    }
+  }
+#endif
+  if (side == PC_LEFT) {
+    PetscCall(MatMult(A, x, work));
+    PetscCall(applyFFT3DPrecTransport(pc, work, y));
+  } else if (side == PC_RIGHT) {
+    PetscCall(applyFFT3DPrecTransport(pc, x, work));
+    PetscCall(MatMult(A, work, y));
+  } else {
+    PetscCheck(false, PETSC_COMM_SELF, PETSC_ERR_SUP, "applyFFT3DPrecTransportBA: left or right preconditioning");
+  }
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
@@ -583,6 +678,19 @@ extern "C" PetscErrorCode setupFFTPrec3D(PC pc) {
   }
   PetscCall(d.put());
   PetscCall(e);
+#ifndef CFP_WITH_PETSC
+  // the operator's row-class form for applyFFT3DPrecTransportBA, built (and its x-locality
+  // checked) now rather than inside the first timed solve
+  Mat A = nullptr;
+  PetscCall(PCGetOperators(pc, &A, NULL));
+  MatType mt = nullptr;
+  if (A && !s->dplan) PetscCall(MatGetType(A, &mt));
+  if (mt && std::strcmp(mt, MATSEQAIJ) == 0) {
+    PetscBool has, xl;
+    PetscMiniDia dia;
+    PetscCall(PetscMiniMatAIJGetDia(A, ctx->n_x, &has, &xl, &dia));
+  }
+#endif
   // remember which object and state hold the symbol (solve_3D's register-symbol fast path)
   PetscCall(PetscObjectGetId((PetscObject)ctx->Diag, &s->diag_id));
   PetscCall(PetscObjectStateGet((PetscObject)ctx->Diag, &s->diag_state));

@@ -532,6 +532,24 @@ extern "C" PetscErrorCode applyFFT3DPrecTransport(PC pc, Vec b, Vec x) {
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
+// PCShellSetApplyBA callback (include/pcshell_fft3d.h): real scalars have no fused form, so this is
+// PETSc's PCApplyBAorAB without an applyBA -- MatMult with the PC's operator, then the apply
+extern "C" PetscErrorCode applyFFT3DPrecTransportBA(PC pc, PCSide side, Vec x, Vec y, Vec work) {
+  PetscFunctionBeginUser;
+  Mat A = nullptr;
+  PetscCall(PCGetOperators(pc, &A, NULL));
+  PetscCheck(A, PETSC_COMM_SELF, PETSC_ERR_ARG_WRONGSTATE, "applyFFT3DPrecTransportBA: the PC has no operator");
+  if (side == PC_LEFT) {
+    PetscCall(MatMult(A, x, work));
+    PetscCall(applyFFT3DPrecTransport(pc, work, y));
+  } else {
+    PetscCheck(side == PC_RIGHT, PETSC_COMM_SELF, PETSC_ERR_SUP, "applyFFT3DPrecTransportBA: left or right preconditioning");
+    PetscCall(applyFFT3DPrecTransport(pc, x, work));
+    PetscCall(MatMult(A, work, y));
+  }
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
 // setupFFTPrec3D, :26-84 (real scalars: Diag and b_hat are half spectra, b_cartesien N reals)
 extern "C" PetscErrorCode setupFFTPrec3D(PC pc) {
   PetscFunctionBeginUser;

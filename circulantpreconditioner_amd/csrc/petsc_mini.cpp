@@ -794,7 +794,7 @@ extern "C" PetscErrorCode VecCopy(Vec x, Vec y) {
       const VS* xd;
       PetscCall(dev_read(x, &xd));
       y->mask = MASK_GPU;
-      HIPK(hipMemcpyAsync(y->d, xd, sizeof(VS) * (size_t)x->n, hipMemcpyDeviceToDevice, g_stream));
+      HIPK(cfp::kprof_copy(y->d, xd, sizeof(VS) * (size_t)x->n, hipMemcpyDeviceToDevice, g_stream));
     } else {
       (void)yd;
       HIPK(hipMemcpyAsync(y->d, x->h, sizeof(VS) * (size_t)x->n, hipMemcpyHostToDevice, g_stream));
@@ -1068,6 +1068,53 @@ extern "C" PetscErrorCode VecMiniMDotMAXPYNorm(Vec w, PetscInt nv, const PetscRe
   return PETSC_SUCCESS;
 }
 
+extern "C" PetscErrorCode VecMiniMAXPYNormDeviceDots(Vec w, PetscInt nv, const PetscReal scale[], Vec V[],
+                                                     const double* dots_dev, PetscScalar dots[], PetscReal* norm) {
+  VCHK(w);
+  if (nv <= 0 || nv > MV_MAX) return ERR(PETSC_ERR_ARG_OUTOFRANGE, "nv must be in 1..32");
+  if (!dots_dev || !dots || !scale) return ERR(PETSC_ERR_ARG_NULL, "NULL argument");
+#ifdef CFP_REAL_SCALAR
+  return ERR(PETSC_ERR_SUP, "VecMiniMAXPYNormDeviceDots: complex scalars only");
+#else
+  if (!w->hip || w->nranks != 1) return ERR(PETSC_ERR_SUP, "VecMiniMAXPYNormDeviceDots: device Vecs of one rank");
+  std::vector<const VS*> ys((size_t)nv);
+  for (PetscInt j = 0; j < nv; ++j) {
+    VCHK(V[j]);
+    PetscCall(same_size(w, V[j]));
+    if (!V[j]->hip) return ERR(PETSC_ERR_SUP, "VecMiniMAXPYNormDeviceDots: device Vecs only");
+    PetscCall(dev_read(V[j], &ys[(size_t)j]));
+  }
+  VS* wd;
+  PetscCall(dev_rw(w, &wd));
+  std::vector<VS> r((size_t)nv);
+  double s2 = 0.0;
+  HIPK(cfp::blas_maxpy_dc_norm(wd, (int)nv, ys.data(), scale, dots_dev, w->n, r.data(), &s2, g_stream));
+  for (PetscInt j = 0; j < nv; ++j) dots[j] = to_scalar(C(r[(size_t)j]).real(), C(r[(size_t)j]).imag());
+  if (norm) *norm = std::sqrt(s2);
+  return PETSC_SUCCESS;
+#endif
+}
+
+extern "C" PetscErrorCode PetscMiniProfileBegin(PetscInt max_records) {
+  if (max_records < 1 || max_records > (1 << 22)) return ERR(PETSC_ERR_ARG_OUTOFRANGE, "max_records out of range");
+  HCHK(cfp::kprof_begin((size_t)max_records));
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode PetscMiniProfileEnd(double ms[4], int64_t launches[4]) {
+  if (!ms || !launches) return ERR(PETSC_ERR_ARG_NULL, "NULL output");
+  long long l[4];
+  HCHK(cfp::kprof_end(ms, l));
+  for (int k = 0; k < 4; ++k) launches[k] = l[k];
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode PetscMiniDeviceRead(const double* dev, PetscInt n, double* host) {
+  if (n <= 0) return PETSC_SUCCESS;
+  if (!dev || !host) return ERR(PETSC_ERR_ARG_NULL, "NULL argument");
+  HCHK(hipMemcpyAsync(host, dev, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, g_stream));
+  HCHK(hipStreamSynchronize(g_stream));
+  return PETSC_SUCCESS;
+}
+
 extern "C" PetscErrorCode VecDuplicateVecs(Vec v, PetscInt m, Vec* V[]) {
   VCHK(v);
   if (!V) return ERR(PETSC_ERR_ARG_NULL, "NULL output");
@@ -1116,6 +1163,9 @@ struct _p_Mat {
   cfp::DiaDesc dia_d{};
   unsigned char *dia_cls = nullptr, *dia_mask = nullptr;
   VS* dia_tab = nullptr;
+  std::vector<unsigned char> h_cls, h_mask;  // host copies of the classes (PetscMiniMatAIJGetDia)
+  i64 xloc_len = -1;                         // row length of the cached x-locality test
+  bool xloc = false;
 };
 
 static PetscErrorCode mcheck(Mat A, const char* f) {
@@ -1233,6 +1283,9 @@ static void aij_free_device(Mat M) {
   M->val = M->dia_tab = nullptr;
   M->dia_cls = M->dia_mask = nullptr;
   M->dia = -1;
+  M->h_cls.clear();
+  M->h_mask.clear();
+  M->xloc_len = -1;
 }
 
 // the device copy: the row-class diagonal form when the matrix has one, else the CSR (once;
@@ -1256,6 +1309,9 @@ static PetscErrorCode aij_upload(Mat M) {
         return ERR(PETSC_ERR_MEM, hipGetErrorString(e));
       }
       M->dia_d = d;
+      M->h_cls.swap(cls);
+      M->h_mask.swap(masks);
+      M->xloc_len = -1;
       return PETSC_SUCCESS;
     }
   }
@@ -1281,6 +1337,46 @@ extern "C" PetscErrorCode PetscMiniMatAIJGetFormat(Mat A, int* format) {
   if (!format) return ERR(PETSC_ERR_ARG_NULL, "NULL output");
   if (A->type != MATSEQAIJ) return ERR(PETSC_ERR_ARG_WRONG, "not a MATSEQAIJ");
   *format = A->dia == 1 ? 1 : (A->rowptr ? 0 : -1);
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode PetscMiniMatAIJGetDia(Mat A, PetscInt rowlen, PetscBool* has, PetscBool* x_local,
+                                                 PetscMiniDia* dia) {
+  MCHK(A);
+  if (!has || !x_local || !dia) return ERR(PETSC_ERR_ARG_NULL, "NULL output");
+  if (rowlen < 1) return ERR(PETSC_ERR_ARG_OUTOFRANGE, "rowlen must be >= 1");
+  *has = PETSC_FALSE;
+  *x_local = PETSC_FALSE;
+  if (A->type != MATSEQAIJ) return PETSC_SUCCESS;
+  PetscCall(aij_upload(A));
+  if (A->dia != 1) return PETSC_SUCCESS;
+  if (A->xloc_len != rowlen) {  // every present entry's column in its row's run of rowlen indices
+    // per class the lowest and highest offset present, then one pass over the rows' positions
+    const int nc = A->dia_d.ncls;
+    std::vector<i64> lo((size_t)nc, 0), hi((size_t)nc, 0);
+    for (int c = 0; c < nc; ++c)
+      for (int k = 0; k < A->dia_d.nd; ++k)
+        if ((A->h_mask[(size_t)c] >> k) & 1u) {
+          lo[(size_t)c] = std::min(lo[(size_t)c], A->dia_d.off[k]);
+          hi[(size_t)c] = std::max(hi[(size_t)c], A->dia_d.off[k]);
+        }
+    bool ok = A->m % rowlen == 0 && A->m == A->n;
+    const unsigned char* cl = A->h_cls.data();
+    for (i64 r0 = 0; ok && r0 < A->m; r0 += rowlen)
+      for (i64 q = 0; q < rowlen; ++q) {
+        const int c = cl[r0 + q];
+        if (q + lo[(size_t)c] < 0 || q + hi[(size_t)c] >= rowlen) { ok = false; break; }
+      }
+    A->xloc = ok;
+    A->xloc_len = rowlen;
+  }
+  *has = PETSC_TRUE;
+  *x_local = A->xloc ? PETSC_TRUE : PETSC_FALSE;
+  dia->cls = A->dia_cls;
+  dia->mask = A->dia_mask;
+  dia->tab = (const PetscScalar*)A->dia_tab;
+  for (int k = 0; k < 8; ++k) dia->off[k] = k < A->dia_d.nd ? A->dia_d.off[k] : 0;
+  dia->nd = A->dia_d.nd;
+  dia->ncls = A->dia_d.ncls;
   return PETSC_SUCCESS;
 }
 extern "C" PetscErrorCode MatGetType(Mat A, MatType* t) {
@@ -1407,9 +1503,12 @@ struct _p_PC {
   std::string name;
   void* ctx = nullptr;
   PetscErrorCode (*apply)(PC, Vec, Vec) = nullptr;
+  PetscErrorCode (*applyBA)(PC, PCSide, Vec, Vec, Vec) = nullptr;
   PetscErrorCode (*setup)(PC) = nullptr;
   PetscErrorCode (*destroy)(PC) = nullptr;
   bool setupcalled = false;
+  Mat A = nullptr, P = nullptr;        // PCSetOperators (not owned)
+  PCMiniApplyDots* dots = nullptr;     // the stand-in KSP's pending dots request
 };
 static PetscErrorCode pcheck(PC pc, const char* f) {
   if (!pc || pc->magic != kPCMagic) return PetscErrorSet(PETSC_ERR_ARG_NULL, f, "invalid PC");
@@ -1454,6 +1553,53 @@ extern "C" PetscErrorCode PCApply(PC pc, Vec x, Vec y) {
   if (pc->type == PCNONE || pc->type.empty()) return VecCopy(x, y);
   if (!pc->apply) return ERR(PETSC_ERR_ARG_WRONGSTATE, "PCSHELL has no apply callback");
   return pc->apply(pc, x, y);
+}
+extern "C" PetscErrorCode PCSetOperators(PC pc, Mat A, Mat P) {
+  PCCHK(pc);
+  pc->A = A;
+  pc->P = P ? P : A;
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode PCGetOperators(PC pc, Mat* A, Mat* P) {
+  PCCHK(pc);
+  if (A) *A = pc->A;
+  if (P) *P = pc->P;
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode PCShellSetApplyBA(PC pc, PetscErrorCode (*f)(PC, PCSide, Vec, Vec, Vec)) {
+  PCCHK(pc);
+  pc->applyBA = f;
+  return PETSC_SUCCESS;
+}
+// PETSc's PCApplyBAorAB: the shell's applyBA, else left y = B (A x), right y = A (B x)
+extern "C" PetscErrorCode PCApplyBAorAB(PC pc, PCSide side, Vec x, Vec y, Vec work) {
+  PCCHK(pc); VCHK(x); VCHK(y); VCHK(work);
+  if (x == y) return ERR(PETSC_ERR_ARG_IDN, "x and y must be different vectors");
+  if (side != PC_LEFT && side != PC_RIGHT) return ERR(PETSC_ERR_SUP, "stand-in PCApplyBAorAB: left or right side");
+  PetscCall(PCSetUp(pc));
+  if (pc->type == PCSHELL && pc->applyBA) return pc->applyBA(pc, side, x, y, work);
+  if (!pc->A) return ERR(PETSC_ERR_ARG_WRONGSTATE, "PCSetOperators has not been called");
+  if (side == PC_LEFT) {
+    PetscCall(MatMult(pc->A, x, work));
+    return PCApply(pc, work, y);
+  }
+  PetscCall(PCApply(pc, x, work));
+  return MatMult(pc->A, work, y);
+}
+extern "C" PetscErrorCode PCMiniSetApplyDots(PC pc, PCMiniApplyDots* req) {
+  PCCHK(pc);
+  if (req) {
+    if (req->nv < 1 || req->nv > 8 || !req->out) return ERR(PETSC_ERR_ARG_OUTOFRANGE, "dots request: 1 <= nv <= 8, out set");
+    req->done = PETSC_FALSE;
+  }
+  pc->dots = req;
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode PCMiniGetApplyDots(PC pc, PCMiniApplyDots** req) {
+  PCCHK(pc);
+  if (!req) return ERR(PETSC_ERR_ARG_NULL, "NULL output");
+  *req = pc->dots;
+  return PETSC_SUCCESS;
 }
 extern "C" PetscErrorCode PCDestroy(PC* ppc) {
   if (!ppc || !*ppc) return PETSC_SUCCESS;

@@ -166,6 +166,8 @@ extern "C" void cfp_transport_config_default(cfp_transport_config* cfg, int64_t 
   cfg->lambda_mode = CFP_LAMBDA_MATCHED;
   cfg->pc_side = PC_LEFT;
   cfg->on_device = 1;
+  cfg->fuse = 1;
+  cfg->profile = 0;
 }
 
 // TransportEquation_impl_mpi (one rank): the time loop of implicit upwind steps
@@ -204,6 +206,7 @@ extern "C" PetscErrorCode TransportEquationGMRES(const cfp_transport_config* cfg
   PetscCall(KSPSetTolerances(ksp, cfg->precision, cfg->precision, PETSC_DEFAULT, cfg->max_its));
   PetscCall(KSPGMRESSetRestart(ksp, cfg->restart > 0 ? cfg->restart : 30));
   PetscCall(KSPSetPCSide(ksp, (PCSide)cfg->pc_side));
+  PetscCall(KSPMiniSetFusion(ksp, cfg->fuse ? PETSC_TRUE : PETSC_FALSE));
   PetscCall(KSPGetPC(ksp, &pc));
   FFTPrecTransportContext ctx;
   std::memset((void*)&ctx, 0, sizeof(ctx));
@@ -224,6 +227,7 @@ extern "C" PetscErrorCode TransportEquationGMRES(const cfp_transport_config* cfg
     PetscCall(PCShellSetContext(pc, &ctx));
     PetscCall(PCShellSetSetUp(pc, setupFFTPrec3D));
     PetscCall(PCShellSetApply(pc, applyFFT3DPrecTransport));
+    if (cfg->fuse) PetscCall(PCShellSetApplyBA(pc, applyFFT3DPrecTransportBA));
     PetscCall(PCShellSetDestroy(pc, destroyFFTPrec3D));
     PetscCall(PCShellSetName(pc, "circulant FFT (HIP)"));
     res->lambda[0] = ctx.lambda_x.real();
@@ -247,6 +251,8 @@ extern "C" PetscErrorCode TransportEquationGMRES(const cfp_transport_config* cfg
   bool stationary = false;
   res->all_converged = 1;
   res->min_step_its = -1;
+  if (cfg->profile) PetscCall(PetscMiniProfileBegin(1 << 16));
+  const double t_loop = wall();
   while (it < cfg->ntmax && time <= cfg->tmax && !stationary) {  // :131
     PetscCall(VecCopy(Un, dUn));
     const double v = wall();
@@ -277,6 +283,16 @@ extern "C" PetscErrorCode TransportEquationGMRES(const cfp_transport_config* cfg
     res->last_residual = residu;
     res->last_norm_dU = norm;
     if (reason != KSP_CONVERGED_RTOL && reason != KSP_CONVERGED_ATOL) res->all_converged = 0;  // :166
+    PetscInt fd, fn;
+    PetscCall(KSPMiniGetFusedCounts(ksp, &fd, &fn));
+    res->fused_dots += fd;
+    res->fused_norms += fn;
+  }
+  res->loop_seconds = wall() - t_loop;
+  if (cfg->profile) {
+    PetscCall(PetscMiniProfileEnd(res->dev_ms, res->dev_launches));
+    res->dev_ms[0] = 1e3 * res->pc_seconds;
+    res->dev_launches[0] = res->pc_calls;
   }
   res->steps = it;
   res->time = time;

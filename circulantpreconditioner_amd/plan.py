@@ -51,6 +51,44 @@ def _lam6(lam: Sequence) -> ctypes.Array:
     return (ctypes.c_double * 6)(*vals)
 
 
+class StencilT(ctypes.Structure):
+    """cfp_stencil_t (include/circulant_fft.h): a row-class diagonal operator on device arrays."""
+    _fields_ = [("cls", ctypes.c_void_p), ("mask", ctypes.c_void_p), ("tab", ctypes.c_void_p),
+                ("off", ctypes.c_int64 * 8), ("nd", ctypes.c_int), ("ncls", ctypes.c_int), ("x_local", ctypes.c_int)]
+
+
+class ApplyExT(ctypes.Structure):
+    """cfp_apply_ex_t (include/circulant_fft.h)."""
+    _fields_ = [("pre", ctypes.POINTER(StencilT)), ("post_nv", ctypes.c_int), ("post_v", ctypes.c_void_p * 8),
+                ("post_out", ctypes.c_void_p), ("fused", ctypes.c_int)]
+
+
+def row_class_form(indptr, indices, data, rowlen: int):
+    """Row-class diagonal form of a CSR matrix (numpy arrays), as the stand-in AIJ builds it
+    (petsc_mini.cpp aij_build_dia): (cls uint8 [n], mask uint8 [ncls], tab complex [ncls, nd],
+    offsets [nd], x_local).  Raises ValueError when the matrix has more than 8 diagonals or 256
+    distinct rows."""
+    n = len(indptr) - 1
+    rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(indptr))
+    off_all = indices.astype(np.int64) - rows
+    offs = np.unique(off_all)
+    if len(offs) > 8:
+        raise ValueError("more than 8 diagonals")
+    k = np.searchsorted(offs, off_all)
+    vals = np.zeros((n, len(offs)), dtype=np.complex128)
+    vals[rows, k] = data
+    present = np.zeros((n, len(offs)), dtype=bool)
+    present[rows, k] = True
+    mask_rows = (present * (1 << np.arange(len(offs)))).sum(1).astype(np.uint8)
+    key = np.concatenate([vals.view(np.float64), mask_rows[:, None].astype(np.float64)], axis=1)
+    uniq, first, cls = np.unique(key, axis=0, return_index=True, return_inverse=True)
+    if len(uniq) > 256:
+        raise ValueError("more than 256 distinct rows")
+    cols = rows + offs[k]
+    x_local = bool(n % rowlen == 0 and np.all(cols // rowlen == rows // rowlen))
+    return (cls.reshape(-1).astype(np.uint8), mask_rows[first], vals[first], offs, x_local)
+
+
 PASS_MODES = {0: "fwd", 1: "inv", 2: "fused_sep", 3: "fused_diag", 4: "fused_wave", 5: "rows_fwd", 6: "mid_fused",
               7: "rows_inv", 8: "sym_divide", 9: "plane_fwd", 10: "plane_inv"}
 PASS_AXES = {-1: "-", 0: "x", 1: "y", 2: "z", 3: "xy", 4: "yz"}
@@ -113,6 +151,34 @@ class CirculantPlan:
         xp = _dev_ptr(out, self.N, "out", self.device)
         check(lib().cfp_plan_apply(self._h, bp, xp, _stream_handle(stream)))
         return out
+
+    def apply_ex(self, b: torch.Tensor, out: torch.Tensor, stencil=None, dots_with=(), stream=None):
+        """The Krylov step around one apply (cfp_plan_apply_ex): x = apply(A b) when `stencil` =
+        (cls, mask, tab, offsets, x_local) on the device (uint8, uint8, complex128 tensors), then
+        dots[j] = v_j^H x for v_j in `dots_with` (None: x itself).  Returns (dots (complex128
+        device tensor or None), fused flag)."""
+        ex = ApplyExT()
+        keep = []
+        if stencil is not None:
+            cls, mask, tab, offs, xl = stencil
+            st = StencilT()
+            st.cls, st.mask, st.tab = cls.data_ptr(), mask.data_ptr(), tab.data_ptr()
+            for i, o in enumerate(offs):
+                st.off[i] = int(o)
+            st.nd, st.ncls, st.x_local = len(offs), int(mask.numel()), 1 if xl else 0
+            keep.append(st)
+            ex.pre = ctypes.pointer(st)
+        dots = None
+        if dots_with:
+            dots = torch.zeros(len(dots_with), dtype=torch.complex128, device=out.device)
+            ex.post_nv = len(dots_with)
+            for j, v in enumerate(dots_with[:8]):  # more than 8: refused by the library
+                ex.post_v[j] = None if v is None else _dev_ptr(v, self.N, "dots_with", self.device)
+            ex.post_out = dots.data_ptr()
+        check(lib().cfp_plan_apply_ex(self._h, _dev_ptr(b, self.N, "b", self.device),
+                                      _dev_ptr(out, self.N, "out", self.device), _stream_handle(stream),
+                                      ctypes.byref(ex)))
+        return dots, int(ex.fused)
 
     def apply_with_diag(self, diag: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
                         stream=None) -> torch.Tensor:

@@ -90,6 +90,38 @@ int cfp_plan_apply_host(cfp_plan_t plan, const double *b_host, double *x_host);
 /* Same with a caller-owned device Diag (solve_3D on host Vecs with an explicit Diag). */
 int cfp_plan_apply_with_diag_host(cfp_plan_t plan, const double *diag_dev, const double *b_host, double *x_host);
 
+/* ---- the Krylov step around a PCApply, fused into the apply's sweeps (not in the reference; the
+ * stand-in GMRES's MatMult -> PCApply -> VecMDot chain of tests/TransportEquation_SphericalExplosion_
+ * impl_mpi.cxx:120-136, PETSc's KSP_PCApplyBAorAB followed by KSPGMRESClassicalGramSchmidt's VecMDot).
+ *
+ * pre: the apply reads y = A b instead of b, A in row-class diagonal form (the stand-in AIJ's
+ *   k_dia_spmv layout): row r has class cls[r] < ncls; class c has the entries tab[c nd + k]
+ *   (complex) on the diagonals off[k] (column - row, ascending) whose bit k is set in mask[c].
+ *   x_local != 0 asserts that every present entry stays inside the row's x-line (column and row
+ *   in one run of n_x consecutive indices).
+ * post: after the apply, out[2 j], out[2 j + 1] = (re, im) of v[j]^H x for j < nv (v[j] == NULL:
+ *   x itself, so out[2 j] = |x|^2); out is a device array of 2 nv doubles, written on `stream`.
+ * fused (output): 1 when both ran inside the apply's own sweeps (the 256^3 3-sweep schedule: P1
+ *   streams b once and forms A b in registers when the stencil is x-local with diagonals in
+ *   {-1, 0, +1} and ncls <= 16; P3 reads the v[j] beside its stores, nv <= 4), 0 when they ran
+ *   as separate kernels around a plain apply (same results up to rounding).  b must not alias x
+ *   when pre is given. */
+typedef struct {
+  const unsigned char *cls;  /* [N] device */
+  const unsigned char *mask; /* [ncls] device */
+  const double *tab;         /* [ncls * nd] complex, device */
+  int64_t off[8];
+  int nd, ncls, x_local;
+} cfp_stencil_t;
+typedef struct {
+  const cfp_stencil_t *pre; /* NULL: none */
+  int post_nv;              /* 0: none; at most 8 */
+  const double *post_v[8];
+  double *post_out;
+  int fused;
+} cfp_apply_ex_t;
+int cfp_plan_apply_ex(cfp_plan_t plan, const double *b_dev, double *x_dev, void *stream, cfp_apply_ex_t *ex);
+
 /* Unnormalised 3-D transforms: forward (e^{-}, MatMult) and backward (e^{+}, MatMultTranspose). */
 int cfp_plan_forward(cfp_plan_t plan, const double *in_dev, double *out_dev, void *stream);
 int cfp_plan_backward(cfp_plan_t plan, const double *in_dev, double *out_dev, void *stream);

@@ -74,6 +74,13 @@ struct StructuredTransportContext {
 PetscErrorCode applyFFT3DPrecTransport(PC pc, Vec b, Vec x);
 PetscErrorCode setupFFTPrec3D(PC pc);
 PetscErrorCode destroyFFTPrec3D(PC pc);
+/* Not in the reference (an addition for its GMRES caller, tests/TransportEquation_SphericalExplosion_
+ * impl_mpi.cxx:120-136): the PCShellSetApplyBA callback, y = B A x (left) / A B x (right) with the
+ * PC's operator.  On one rank with the stand-in AIJ it forms A x inside the apply's first sweep
+ * (no MatMult sweep); otherwise it is MatMult + applyFFT3DPrecTransport, what PETSc's
+ * PCApplyBAorAB does for a shell without one.  Register it with
+ * PCShellSetApplyBA(pc, applyFFT3DPrecTransportBA) beside PCShellSetApply. */
+PetscErrorCode applyFFT3DPrecTransportBA(PC pc, PCSide side, Vec x, Vec y, Vec work);
 /* src/PCSHELLFft_3D.hxx:27-41 (Mesh srcMesh -> FFTPrecTransportContext *ctx, see above):
  * n_d = floor(cbrt(nbCells)) (3-D), floor(sqrt) (2-D), nbCells (1-D);
  * lambda_d = a_d * dt * (max_d - min_d) / n_d (src/PCSHELLFft_3D.cxx:146-148, kept as is) */

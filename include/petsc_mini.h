@@ -163,6 +163,19 @@ PetscErrorCode PetscMiniAllreduce(MPI_Comm comm, double *buf, int64_t count, int
  * form (k_dia_spmv: nonzeros on <= 8 fixed diagonals, <= 256 distinct rows -- Cartesian
  * stencils), 0 = CSR, -1 = not uploaded yet (MatShift resets it). */
 PetscErrorCode PetscMiniMatAIJGetFormat(Mat A, int *format);
+/* The device row-class form of an AIJ (above; uploaded now if it has not been): its class bytes,
+ * class masks and coefficient table as device arrays, in the layout of cfp_stencil_t
+ * (include/circulant_fft.h).  *has = PETSC_FALSE when the matrix is not representable (CSR only).
+ * *x_local = PETSC_TRUE when no entry leaves its row's run of `rowlen` consecutive indices (an
+ * operator coupling cells along x only, on an x-fastest grid with n_x = rowlen). */
+typedef struct {
+  const unsigned char *cls;
+  const unsigned char *mask;
+  const PetscScalar *tab;
+  int64_t off[8];
+  int nd, ncls;
+} PetscMiniDia;
+PetscErrorCode PetscMiniMatAIJGetDia(Mat A, PetscInt rowlen, PetscBool *has, PetscBool *x_local, PetscMiniDia *dia);
 /* the ncclComm_t behind an RCCL communicator (NULL for a callback communicator) */
 PetscErrorCode PetscMiniCommGetNCCL(MPI_Comm comm, void **nccl_comm);
 /* One exchange piece of a slab plan over a communicator (the cfp_dist_exchange_fn contract of
@@ -256,6 +269,21 @@ PetscErrorCode VecMiniMDotMAXPYNorm(Vec w, PetscInt nv, const PetscReal scale[],
                                     PetscReal *norm);
 PetscErrorCode VecMiniMAXPYNorm(Vec y, PetscInt nv, const PetscScalar alpha[], Vec x[], PetscBool overwrite,
                                 PetscReal *norm);
+/* The second half of VecMiniMDotMAXPYNorm for dots already on the device (dots_dev[2 j + re/im] =
+ * V[j]^H w, e.g. from a fused PCApply, PCMiniApplyDots): w += sum_j scale[j] dots_j V[j], *norm =
+ * |w|, the dots copied back into dots[]; one host wait.  Device Vecs of one rank, nv <= 32. */
+PetscErrorCode VecMiniMAXPYNormDeviceDots(Vec w, PetscInt nv, const PetscReal scale[], Vec V[], const double *dots_dev,
+                                          PetscScalar dots[], PetscReal *norm);
+/* Device-time profile of the stand-in's own kernels (not in PETSc; what rocprofv3 --kernel-trace
+ * would sum, from inside the process): between Begin and End every MatMult / vector kernel launch
+ * stamps its own dispatch (hipExtLaunchKernelGGL start / stop events) and every device copy is
+ * bracketed by events.  End waits, then writes the summed ms and launch counts per kind: [0]
+ * unused here (PCApply: KSPMiniGetPCApplyStats), [1] MatMult, [2] vector kernels, [3] copies.
+ * At most max_records launches are stamped (later ones run unstamped). */
+PetscErrorCode PetscMiniProfileBegin(PetscInt max_records);
+PetscErrorCode PetscMiniProfileEnd(double ms[4], int64_t launches[4]);
+/* host copy of n doubles of device memory, ordered on the Vec stream (waits) */
+PetscErrorCode PetscMiniDeviceRead(const double *dev, PetscInt n, double *host);
 
 /* ---- Mat */
 PetscErrorCode MatCreateShell(MPI_Comm comm, PetscInt m, PetscInt n, PetscInt M, PetscInt N, void *ctx, Mat *A);
@@ -292,6 +320,26 @@ PetscErrorCode PCShellSetName(PC pc, const char *name);
 PetscErrorCode PCSetUp(PC pc);
 PetscErrorCode PCApply(PC pc, Vec x, Vec y);
 PetscErrorCode PCDestroy(PC *pc);
+/* the operators the PC was given (KSPSetOperators passes them on, as PETSc's KSP does) */
+typedef enum { PC_LEFT = 0, PC_RIGHT = 1, PC_SYMMETRIC = 2 } PCSide;
+PetscErrorCode PCSetOperators(PC pc, Mat Amat, Mat Pmat);
+PetscErrorCode PCGetOperators(PC pc, Mat *Amat, Mat *Pmat);
+/* y = B A x (left) or A B x (right), work a scratch Vec: the shell's applyBA callback when set
+ * (PCShellSetApplyBA), else MatMult and PCApply with pc's Amat (PETSc's PCApplyBAorAB) */
+PetscErrorCode PCShellSetApplyBA(PC pc, PetscErrorCode (*applyBA)(PC, PCSide, Vec, Vec, Vec));
+PetscErrorCode PCApplyBAorAB(PC pc, PCSide side, Vec x, Vec y, Vec work);
+/* not in PETSc: the stand-in KSP asks the next PCApply / PCApplyBAorAB of a shell for the dots
+ * of its output y with device vectors, out[2 j + re/im] = v[j]^H y (v[j] == NULL: y itself), out a
+ * device array; a shell that computed them (fused into its apply) sets done = PETSC_TRUE.
+ * PCMiniSetApplyDots(pc, NULL) withdraws the request. */
+typedef struct {
+  PetscInt nv;
+  const PetscScalar *v[8];
+  double *out;
+  PetscBool done;
+} PCMiniApplyDots;
+PetscErrorCode PCMiniSetApplyDots(PC pc, PCMiniApplyDots *req);
+PetscErrorCode PCMiniGetApplyDots(PC pc, PCMiniApplyDots **req);
 
 /* ---- KSP: GMRES(restart) with PETSc's defaults (restart 30, left preconditioning,
  * classical Gram-Schmidt without refinement, preconditioned residual norm, convergence when
@@ -300,7 +348,6 @@ typedef struct _p_KSP *KSP;
 typedef const char *KSPType;
 #define KSPGMRES "gmres"
 #define KSPPREONLY "preonly"
-typedef enum { PC_LEFT = 0, PC_RIGHT = 1 } PCSide;
 typedef enum {
   KSP_CONVERGED_ITERATING = 0,
   KSP_CONVERGED_RTOL = 2,
@@ -320,8 +367,8 @@ PetscErrorCode KSPSetInitialGuessNonzero(KSP ksp, PetscBool flg);
 PetscErrorCode KSPGetPC(KSP ksp, PC *pc);
 PetscErrorCode KSPSetOperators(KSP ksp, Mat A, Mat P);
 PetscErrorCode KSPSetUp(KSP ksp);
-/* GMRES with a zero initial guess does not zero x first (the first update overwrites it): after
- * an error return x is undefined (its old contents, or b when b == x), unlike PETSc. */
+/* GMRES with a zero initial guess does not zero x first (the first update overwrites it); an
+ * error return before that update leaves x = 0, as PETSc's zeroed x would be. */
 PetscErrorCode KSPSolve(KSP ksp, Vec b, Vec x);
 PetscErrorCode KSPGetConvergedReason(KSP ksp, KSPConvergedReason *reason);
 PetscErrorCode KSPGetIterationNumber(KSP ksp, PetscInt *its);
@@ -330,6 +377,12 @@ PetscErrorCode KSPDestroy(KSP *ksp);
 /* not in PETSc: the device time of the PCApply calls of the last KSPSolve (HIP events around
  * each call on the Vec stream; a device-Vec PCApply is stream-ordered there), and their count */
 PetscErrorCode KSPMiniGetPCApplyStats(KSP ksp, PetscInt *calls, PetscLogDouble *seconds);
+/* not in PETSc: whether the solver asks a shell PC for the Gram-Schmidt dots and residual norms
+ * of its output (PCMiniApplyDots; default PETSC_TRUE) */
+PetscErrorCode KSPMiniSetFusion(KSP ksp, PetscBool on);
+/* not in PETSc: in the last KSPSolve, how many Gram-Schmidt steps took their dots, and how many
+ * restarts their residual norm, from the shell's apply (PCMiniApplyDots) */
+PetscErrorCode KSPMiniGetFusedCounts(KSP ksp, PetscInt *dots, PetscInt *norms);
 /* not in PETSc: allocate the GMRES work vectors now (duplicates of v) instead of in the first
  * KSPSolve, so a timed solve does not include their allocation */
 PetscErrorCode KSPMiniSetUpWork(KSP ksp, Vec v);

@@ -72,6 +72,10 @@ typedef struct {
   int lambda_mode;    /* CFP_LAMBDA_* */
   int pc_side;        /* PC_LEFT (0) / PC_RIGHT (1) */
   int on_device;      /* 1: HIP Vecs (VecCreateSeqHIP), 0: host Vecs (PCNONE only) */
+  int fuse;           /* 1 (default): the fused Krylov step -- PCShellSetApplyBA(pc,
+                       * applyFFT3DPrecTransportBA) and the KSP's dots asked from the apply;
+                       * 0: MatMult + PCApply + VecMDot as separate sweeps (KSPMiniSetFusion) */
+  int profile;        /* 1: device time of the loop's kernels by kind (res->dev_ms, PetscMiniProfile*) */
 } cfp_transport_config;
 
 typedef struct {
@@ -89,6 +93,14 @@ typedef struct {
   int64_t pc_calls;
   double setup_seconds;   /* assembly + PC setup */
   double lambda[3];
+  double loop_seconds;    /* wall time of the whole time loop (solves + the loop's own Vec work) */
+  /* cfg->profile: device ms over the loop -- [0] PCApply (the KSP's stamps or events; with the
+   * fused applyBA it includes the MatMult), [1] MatMult kernels, [2] vector kernels (BLAS-1 and
+   * reductions), [3] copies */
+  double dev_ms[4];
+  int64_t dev_launches[4];
+  int64_t fused_dots;     /* Gram-Schmidt steps whose dots came from the PC apply (summed) */
+  int64_t fused_norms;    /* residual norms that came from the PC apply (summed) */
 } cfp_transport_result;
 
 /* fill cfg with the reference main's defaults for an n^3 grid on [-0.5,0.5]^3 */
