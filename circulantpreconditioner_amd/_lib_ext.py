@@ -55,7 +55,8 @@ class TransportResult(ctypes.Structure):
                 ("last_norm_dU", ctypes.c_double), ("solve_seconds", ctypes.c_double),
                 ("pc_seconds", ctypes.c_double), ("pc_calls", ctypes.c_int64), ("setup_seconds", ctypes.c_double),
                 ("lambda_", ctypes.c_double * 3), ("loop_seconds", ctypes.c_double), ("dev_ms_", ctypes.c_double * 4),
-                ("dev_launches_", ctypes.c_int64 * 4), ("fused_dots", ctypes.c_int64), ("fused_norms", ctypes.c_int64)]
+                ("dev_launches_", ctypes.c_int64 * 4), ("fused_dots", ctypes.c_int64), ("fused_norms", ctypes.c_int64),
+                ("rstart", ctypes.c_int64), ("nlocal", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if not k.endswith("_")}
@@ -201,6 +202,12 @@ def declare(L) -> None:
         "PetscObjectGetId": ([vp, P(i64)], c_int),
         "MatCreateVecsFFTW": ([vp, P(vp), P(vp), P(vp)], c_int),
         "MatGetSize": ([vp, P(i64), P(i64)], c_int),
+        "MatCreateAIJ": ([c_int, i64, i64, i64, i64, i64, vp, i64, vp, P(vp)], c_int),
+        "MatSetValues": ([vp, i64, P(i64), i64, P(i64), vp, c_int], c_int),
+        "MatAssemblyBegin": ([vp, c_int], c_int),
+        "MatAssemblyEnd": ([vp, c_int], c_int),
+        "MatGetOwnershipRange": ([vp, P(i64), P(i64)], c_int),
+        "PetscMiniMatMPIAIJGetHalo": ([vp, P(i64), P(i64)], c_int),
         "MatMult": ([vp, vp, vp], c_int),
         "MatMultTranspose": ([vp, vp, vp], c_int),
         "MatShift": ([vp, S], c_int),

@@ -41,6 +41,13 @@ hipError_t blas_dia_spmv(i64 m, const DiaDesc& d, const unsigned char* cls, cons
                          const cd* x, cd* y, hipStream_t s);
 hipError_t blas_dia_spmv(i64 m, const DiaDesc& d, const unsigned char* cls, const unsigned char* masks,
                          const double* tab, const double* x, double* y, hipStream_t s);
+// distributed AIJ halo: out[i] = x[idx[i]] (idx < 0: 0); y += B x for a CSR block B
+hipError_t blas_gather(cd* out, const cd* x, const i64* idx, i64 n, hipStream_t s);
+hipError_t blas_gather(double* out, const double* x, const i64* idx, i64 n, hipStream_t s);
+hipError_t blas_csr_spmv_add(i64 m, const i64* rowptr, const i64* col, const cd* val, const cd* x, cd* y,
+                             hipStream_t s);
+hipError_t blas_csr_spmv_add(i64 m, const i64* rowptr, const i64* col, const double* val, const double* x, double* y,
+                             hipStream_t s);
 // synchronous reductions, PETSc conventions: dot = y^H x; norm type 0 = NORM_1 (sum |re|+|im|),
 // 1 = NORM_2, 3 = NORM_INFINITY (max modulus)
 hipError_t blas_dot(const cd* x, const cd* y, i64 n, cd* val, hipStream_t s);

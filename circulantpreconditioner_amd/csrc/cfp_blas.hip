@@ -343,6 +343,25 @@ __global__ void __launch_bounds__(BLAS_THREADS) k_csr_spmv_vec(i64 m, const i64*
   }
 }
 
+// halo of a distributed AIJ (petsc_mini.cpp MATMPIAIJ): out[i] = x[idx[i]] (idx < 0: zero
+// padding), and y += B g for the off-diagonal block B (CSR over the ghost slots)
+template <class T> __global__ void k_gather(T* out, const T* x, const i64* idx, i64 n) {
+  GRID_LOOP(i, n) {
+    const i64 j = idx[i];
+    out[i] = j >= 0 ? x[j] : bzero<T>();
+  }
+}
+template <class T>
+__global__ void k_csr_spmv_add(i64 m, const i64* rowptr, const i64* col, const T* val, const T* x, T* y) {
+  GRID_LOOP(r, m) {
+    const i64 p0 = rowptr[r], p1 = rowptr[r + 1];
+    if (p0 == p1) continue;
+    T acc = y[r];
+    for (i64 p = p0; p < p1; ++p) acc = badd(acc, bmul(val[p], x[col[p]]));
+    y[r] = acc;
+  }
+}
+
 // Row-class diagonal SpMV (r05).  A constant-coefficient stencil on a
 // Cartesian grid -- the transport operator of configs 1 and 3 (transport_cartesian.cpp) -- has
 // its nonzeros on a few fixed diagonals and only a handful of distinct rows (interior, and the
@@ -433,6 +452,29 @@ hipError_t blas_csr_spmv(i64 m, i64 nnz, const i64* rowptr, const i64* col, cons
 hipError_t blas_csr_spmv(i64 m, i64 nnz, const i64* rowptr, const i64* col, const double* val, const double* x,
                          double* y, hipStream_t s) {
   return spmv_t(m, nnz, rowptr, col, val, x, y, s);
+}
+
+template <class T>
+static hipError_t gather_t(T* out, const T* x, const i64* idx, i64 n, hipStream_t s) {
+  if (n > 0) blaunch(1, k_gather<T>, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, out, x, idx, n);
+  return hipGetLastError();
+}
+template <class T>
+static hipError_t spmv_add_t(i64 m, const i64* rowptr, const i64* col, const T* val, const T* x, T* y, hipStream_t s) {
+  if (m > 0) blaunch(1, k_csr_spmv_add<T>, dim3(nblocks(m)), dim3(BLAS_THREADS), 0, s, m, rowptr, col, val, x, y);
+  return hipGetLastError();
+}
+hipError_t blas_gather(cd* out, const cd* x, const i64* idx, i64 n, hipStream_t s) { return gather_t(out, x, idx, n, s); }
+hipError_t blas_gather(double* out, const double* x, const i64* idx, i64 n, hipStream_t s) {
+  return gather_t(out, x, idx, n, s);
+}
+hipError_t blas_csr_spmv_add(i64 m, const i64* rowptr, const i64* col, const cd* val, const cd* x, cd* y,
+                             hipStream_t s) {
+  return spmv_add_t(m, rowptr, col, val, x, y, s);
+}
+hipError_t blas_csr_spmv_add(i64 m, const i64* rowptr, const i64* col, const double* val, const double* x, double* y,
+                             hipStream_t s) {
+  return spmv_add_t(m, rowptr, col, val, x, y, s);
 }
 
 template <class T>

@@ -1166,6 +1166,26 @@ struct _p_Mat {
   std::vector<unsigned char> h_cls, h_mask;  // host copies of the classes (PetscMiniMatAIJGetDia)
   i64 xloc_len = -1;                         // row length of the cached x-locality test
   bool xloc = false;
+  // MatCreateAIJ (r06): entries from MatSetValue(s) wait here until MatAssemblyEnd.  This rank's
+  // rows [rstart, rstart + lm); set_*: its own rows' entries, st_*: other ranks' (the stash).
+  bool building = false;
+  int nranks = 1;
+  i64 rstart = 0;
+  std::vector<i64> set_r, set_c, st_r, st_c;
+  std::vector<VS> set_v, st_v;
+  std::vector<char> set_add, st_add;
+  // MATMPIAIJ after assembly: the diagonal block (local rows x local columns, a MATSEQAIJ with
+  // local indices) and the off-diagonal block over the ghost slots q hM + j (the j-th column this
+  // rank needs from rank q); send_idx[q hM + j] = the local row rank q needs from this rank (-1:
+  // padding).  hM = the largest per-peer halo of any rank (0: no exchange at all).
+  Mat dblk = nullptr;
+  std::vector<i64> o_rowptr, o_col;
+  std::vector<VS> o_val;
+  i64 nghost = 0, hM = 0;
+  std::vector<i64> send_idx;
+  i64 *d_orowptr = nullptr, *d_ocol = nullptr, *d_send_idx = nullptr;
+  VS *d_oval = nullptr, *d_sendbuf = nullptr, *d_recvbuf = nullptr;
+  std::vector<VS> h_sendbuf, h_recvbuf;
 };
 
 static PetscErrorCode mcheck(Mat A, const char* f) {
@@ -1381,7 +1401,332 @@ extern "C" PetscErrorCode PetscMiniMatAIJGetDia(Mat A, PetscInt rowlen, PetscBoo
 }
 extern "C" PetscErrorCode MatGetType(Mat A, MatType* t) {
   MCHK(A);
-  *t = A->type == MATSEQAIJ ? MATSEQAIJ : MATSHELL;
+  *t = A->type == MATSEQAIJ ? MATSEQAIJ : (A->type == MATMPIAIJ ? MATMPIAIJ : MATSHELL);
+  return PETSC_SUCCESS;
+}
+
+// ------------------------------------------------------------------ MatCreateAIJ
+extern "C" PetscErrorCode MatCreateAIJ(MPI_Comm comm, PetscInt m, PetscInt n, PetscInt M, PetscInt N, PetscInt,
+                                       const PetscInt[], PetscInt, const PetscInt[], Mat* A) {
+  if (!A) return ERR(PETSC_ERR_ARG_NULL, "NULL output");
+  comm = comm_resolve(comm);
+  PetscInt lm, gm, rs, ln, gn, cs;
+  PetscCall(mpi_layout(comm, m, M, &lm, &gm, &rs));
+  PetscCall(mpi_layout(comm, n, N, &ln, &gn, &cs));
+  Mat a = new _p_Mat;
+  MPI_Comm_size(comm, &a->nranks);
+  a->type = a->nranks > 1 ? MATMPIAIJ : MATSEQAIJ;
+  a->m = gm;
+  a->n = gn;
+  a->lm = lm;
+  a->ln = ln;
+  a->rstart = rs;
+  a->comm = comm;
+  a->building = true;
+  if (a->nranks > 1 && (gm != gn || rs != cs)) {
+    delete a;
+    return ERR(PETSC_ERR_SUP, "the stand-in MPIAIJ needs a square matrix with the same row and column layout");
+  }
+  *A = a;
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode MatSetValues(Mat A, PetscInt m, const PetscInt idxm[], PetscInt n, const PetscInt idxn[],
+                                       const PetscScalar v[], InsertMode mode) {
+  MCHK(A);
+  if (!A->building) return ERR(PETSC_ERR_ARG_WRONGSTATE, "MatSetValues: only on a MatCreateAIJ matrix before MatAssemblyEnd");
+  for (PetscInt a = 0; a < m; ++a) {
+    const PetscInt i = idxm[a];
+    if (i < 0) continue;
+    if (i >= A->m) return ERR(PETSC_ERR_ARG_OUTOFRANGE, "MatSetValues: row out of range");
+    const bool mine = i >= A->rstart && i < A->rstart + A->lm;
+    for (PetscInt b = 0; b < n; ++b) {
+      const PetscInt j = idxn[b];
+      if (j < 0) continue;
+      if (j >= A->n) return ERR(PETSC_ERR_ARG_OUTOFRANGE, "MatSetValues: column out of range");
+      auto& R = mine ? A->set_r : A->st_r;
+      if (R.size() >= ((size_t)1 << 28)) return ERR(PETSC_ERR_MEM, "MatSetValues: 2^28 entries pending");
+      R.push_back(i);
+      (mine ? A->set_c : A->st_c).push_back(j);
+      (mine ? A->set_v : A->st_v).push_back(tocd(v[a * n + b]));
+      (mine ? A->set_add : A->st_add).push_back(mode == ADD_VALUES);
+    }
+  }
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode MatSetValue(Mat A, PetscInt i, PetscInt j, PetscScalar v, InsertMode mode) {
+  return MatSetValues(A, 1, &i, 1, &j, &v, mode);
+}
+extern "C" PetscErrorCode MatGetOwnershipRange(Mat A, PetscInt* lo, PetscInt* hi) {
+  MCHK(A);
+  const PetscInt rs = A->type == MATMPIAIJ || A->building ? A->rstart : 0;
+  if (lo) *lo = rs;
+  if (hi) *hi = rs + A->lm;
+  return PETSC_SUCCESS;
+}
+extern "C" PetscErrorCode PetscMiniMatMPIAIJGetHalo(Mat A, PetscInt* ghosts, PetscInt* max_per_peer) {
+  MCHK(A);
+  if (ghosts) *ghosts = A->type == MATMPIAIJ ? A->nghost : 0;
+  if (max_per_peer) *max_per_peer = A->type == MATMPIAIJ ? A->hM : 0;
+  return PETSC_SUCCESS;
+}
+// Collective, as PETSc's: the stash travels to the row owners (records [row, col, re, im, add]
+// through one all-to-all, padded to the largest per-peer count); then End builds the matrix.
+extern "C" PetscErrorCode MatAssemblyBegin(Mat A, MatAssemblyType) {
+  MCHK(A);
+  if (!A->building) return PETSC_SUCCESS;  // already assembled (PETSc allows re-assembly)
+  if (A->nranks == 1) {
+    if (!A->st_r.empty()) return ERR(PETSC_ERR_PLIB, "stashed rows on one rank");
+    return PETSC_SUCCESS;
+  }
+  CommRec* r = comm_rec(A->comm);
+  if (!r) return ERR(PETSC_ERR_ARG_WRONG, "unknown communicator");
+  const int P = r->size;
+  std::vector<double> starts((size_t)P, 0.0);
+  starts[(size_t)r->rank] = (double)A->rstart;
+  PetscCall(PetscMiniAllreduce(A->comm, starts.data(), P, PETSCMINI_OP_SUM));
+  const auto owner = [&](PetscInt g) {
+    int q = (int)(std::upper_bound(starts.begin(), starts.end(), (double)g) - starts.begin()) - 1;
+    return q < 0 ? 0 : q;
+  };
+  std::vector<std::vector<size_t>> to((size_t)P);
+  for (size_t k = 0; k < A->st_r.size(); ++k) to[(size_t)owner(A->st_r[k])].push_back(k);
+  double mx = 0.0;
+  for (const auto& t : to) mx = std::max(mx, (double)t.size());
+  PetscCall(PetscMiniAllreduce(A->comm, &mx, 1, PETSCMINI_OP_MAX));
+  const size_t Mx = (size_t)mx;
+  if (Mx) {
+    std::vector<double> send((size_t)P * Mx * 5, -1.0), recv((size_t)P * Mx * 5);
+    for (int q = 0; q < P; ++q)
+      for (size_t j = 0; j < to[(size_t)q].size(); ++j) {
+        const size_t k = to[(size_t)q][j];
+        double* rec = &send[((size_t)q * Mx + j) * 5];
+        rec[0] = (double)A->st_r[k];  // exact: indices < 2^53
+        rec[1] = (double)A->st_c[k];
+        rec[2] = C(A->st_v[k]).real();
+        rec[3] = C(A->st_v[k]).imag();
+        rec[4] = A->st_add[k] ? 1.0 : 0.0;
+      }
+    PetscCall(comm_alltoall_host(r, send.data(), recv.data(), Mx * 5 * sizeof(double)));
+    for (size_t e = 0; e < (size_t)P * Mx; ++e) {
+      const double* rec = &recv[e * 5];
+      if (rec[0] < 0) continue;  // padding
+      const i64 row = (i64)rec[0];
+      if (row < A->rstart || row >= A->rstart + A->lm) return ERR(PETSC_ERR_PLIB, "stashed entry delivered to the wrong rank");
+      A->set_r.push_back(row);
+      A->set_c.push_back((i64)rec[1]);
+      A->set_v.push_back(D(std::complex<double>(rec[2], rec[3])));
+      A->set_add.push_back(rec[4] != 0.0);
+    }
+  }
+  A->st_r.clear(), A->st_c.clear(), A->st_v.clear(), A->st_add.clear();
+  return PETSC_SUCCESS;
+}
+
+static void mpiaij_free(Mat A) {
+  if (A->dblk) MatDestroy(&A->dblk);
+  hipFree(A->d_orowptr);
+  hipFree(A->d_ocol);
+  hipFree(A->d_oval);
+  hipFree(A->d_send_idx);
+  hipFree(A->d_sendbuf);
+  hipFree(A->d_recvbuf);
+  A->d_orowptr = A->d_ocol = A->d_send_idx = nullptr;
+  A->d_oval = A->d_sendbuf = A->d_recvbuf = nullptr;
+}
+
+// the pending entries of the local rows, folded in order (INSERT sets, ADD adds), as CSR with
+// global columns; square matrices get their diagonal stored (MatShift needs it)
+static void fold_rows(Mat A, std::vector<i64>* rowptr, std::vector<i64>* col, std::vector<VS>* val) {
+  const size_t ne = A->set_r.size();
+  std::vector<size_t> ord(ne);
+  for (size_t k = 0; k < ne; ++k) ord[k] = k;
+  std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {
+    return A->set_r[a] != A->set_r[b] ? A->set_r[a] < A->set_r[b] : A->set_c[a] < A->set_c[b];
+  });
+  rowptr->assign((size_t)A->lm + 1, 0);
+  col->clear();
+  val->clear();
+  const bool square = A->m == A->n;
+  size_t k = 0;
+  for (i64 lr = 0; lr < A->lm; ++lr) {
+    const i64 row = A->rstart + lr;
+    bool diag = false;
+    while (k < ne && A->set_r[ord[k]] == row) {
+      const i64 c = A->set_c[ord[k]];
+      if (square && !diag && c > row) {  // the diagonal, absent so far: a stored zero
+        col->push_back(row);
+        val->push_back(D(std::complex<double>(0.0, 0.0)));
+        diag = true;
+      }
+      std::complex<double> acc = 0.0;
+      for (; k < ne && A->set_r[ord[k]] == row && A->set_c[ord[k]] == c; ++k)
+        acc = A->set_add[ord[k]] ? acc + C(A->set_v[ord[k]]) : C(A->set_v[ord[k]]);
+      col->push_back(c);
+      val->push_back(D(acc));
+      diag = diag || c == row;
+    }
+    if (square && !diag) {
+      col->push_back(row);
+      val->push_back(D(std::complex<double>(0.0, 0.0)));
+    }
+    (*rowptr)[(size_t)lr + 1] = (i64)col->size();
+  }
+  A->set_r.clear(), A->set_c.clear(), A->set_v.clear(), A->set_add.clear();
+  A->set_r.shrink_to_fit(), A->set_c.shrink_to_fit(), A->set_v.shrink_to_fit(), A->set_add.shrink_to_fit();
+}
+
+extern "C" PetscErrorCode MatAssemblyEnd(Mat A, MatAssemblyType type) {
+  MCHK(A);
+  if (!A->building || type == MAT_FLUSH_ASSEMBLY) return PETSC_SUCCESS;
+  std::vector<i64> rp, cl;
+  std::vector<VS> vl;
+  fold_rows(A, &rp, &cl, &vl);
+  A->building = false;
+  if (A->nranks == 1) {  // MATSEQAIJ: the CSR is the matrix
+    A->h_rowptr.swap(rp);
+    A->h_col.swap(cl);
+    A->h_val.swap(vl);
+    return PETSC_SUCCESS;
+  }
+  CommRec* r = comm_rec(A->comm);
+  if (!r) return ERR(PETSC_ERR_ARG_WRONG, "unknown communicator");
+  const int P = r->size;
+  // split: own columns -> the diagonal block (local indices), others -> ghosts
+  const i64 c0 = A->rstart, c1 = A->rstart + A->ln;
+  std::vector<i64> drp((size_t)A->lm + 1, 0), dcl, orp((size_t)A->lm + 1, 0), ocl_g;
+  std::vector<VS> dvl, ovl;
+  for (i64 lr = 0; lr < A->lm; ++lr) {
+    for (i64 p = rp[(size_t)lr]; p < rp[(size_t)lr + 1]; ++p) {
+      const i64 c = cl[(size_t)p];
+      if (c >= c0 && c < c1) {
+        dcl.push_back(c - c0);
+        dvl.push_back(vl[(size_t)p]);
+      } else {
+        ocl_g.push_back(c);
+        ovl.push_back(vl[(size_t)p]);
+      }
+    }
+    drp[(size_t)lr + 1] = (i64)dcl.size();
+    orp[(size_t)lr + 1] = (i64)ocl_g.size();
+  }
+  // ghosts grouped by owner (the column layout equals the row layout)
+  std::vector<double> starts((size_t)P, 0.0);
+  starts[(size_t)r->rank] = (double)A->rstart;
+  PetscCall(PetscMiniAllreduce(A->comm, starts.data(), P, PETSCMINI_OP_SUM));
+  const auto owner = [&](i64 g) {
+    int q = (int)(std::upper_bound(starts.begin(), starts.end(), (double)g) - starts.begin()) - 1;
+    return q < 0 ? 0 : q;
+  };
+  std::vector<i64> gh(ocl_g);
+  std::sort(gh.begin(), gh.end());
+  gh.erase(std::unique(gh.begin(), gh.end()), gh.end());
+  std::vector<std::vector<i64>> need((size_t)P);
+  for (i64 g : gh) need[(size_t)owner(g)].push_back(g);
+  double mx = 0.0;
+  for (const auto& t : need) mx = std::max(mx, (double)t.size());
+  PetscCall(PetscMiniAllreduce(A->comm, &mx, 1, PETSCMINI_OP_MAX));
+  const i64 hM = (i64)mx;
+  A->nghost = (i64)gh.size();
+  A->hM = hM;
+  // each owner learns which of its rows every peer needs (one all-to-all of the requests)
+  A->send_idx.assign((size_t)P * (size_t)hM, -1);
+  if (hM) {
+    std::vector<double> rq((size_t)P * hM, -1.0), got((size_t)P * hM);
+    for (int q = 0; q < P; ++q)
+      for (size_t j = 0; j < need[(size_t)q].size(); ++j) rq[(size_t)q * hM + j] = (double)need[(size_t)q][j];
+    PetscCall(comm_alltoall_host(r, rq.data(), got.data(), (size_t)hM * sizeof(double)));
+    for (size_t e = 0; e < got.size(); ++e)
+      if (got[e] >= 0) {
+        const i64 g = (i64)got[e];
+        if (g < c0 || g >= c1) return ERR(PETSC_ERR_PLIB, "halo request for a row this rank does not own");
+        A->send_idx[e] = g - c0;
+      }
+  }
+  // off-block columns -> ghost slots q hM + j
+  std::vector<i64> ocl(ocl_g.size());
+  for (size_t p = 0; p < ocl_g.size(); ++p) {
+    const i64 g = ocl_g[p];
+    const int q = owner(g);
+    const auto& nq = need[(size_t)q];
+    ocl[p] = (i64)q * hM + (i64)(std::lower_bound(nq.begin(), nq.end(), g) - nq.begin());
+  }
+  A->o_rowptr.swap(orp);
+  A->o_col.swap(ocl);
+  A->o_val.swap(ovl);
+  mpiaij_free(A);
+  PetscCall(MatCreateSeqAIJWithArrays(PETSC_COMM_SELF, A->lm, A->ln, reinterpret_cast<PetscInt*>(drp.data()),
+                                      reinterpret_cast<PetscInt*>(dcl.data()),
+                                      reinterpret_cast<PetscScalar*>(dvl.data()), &A->dblk));
+  return PETSC_SUCCESS;
+}
+
+// y = A x on several ranks: the halo (gather the rows peers need, one all-to-all), the diagonal
+// block's SpMV into y, then y += the off-diagonal block on the ghosts
+static PetscErrorCode mpiaij_mult(Mat A, Vec x, Vec y) {
+  if (x->n != A->ln || y->n != A->lm || x->N != A->n || y->N != A->m) return ERR(PETSC_ERR_ARG_SIZ, "MatMult sizes");
+  if (x == y) return ERR(PETSC_ERR_ARG_IDN, "x and y must be different vectors");
+  if (x->rstart != A->rstart || y->rstart != A->rstart) return ERR(PETSC_ERR_ARG_WRONG, "MatMult: Vec layout differs from the matrix");
+  CommRec* r = comm_rec(A->comm);
+  if (!r) return ERR(PETSC_ERR_ARG_WRONG, "unknown communicator");
+  const int P = r->size;
+  const size_t hl = (size_t)P * (size_t)A->hM;
+  const bool dev = x->hip && y->hip;
+  if (dev) {
+    const VS* xd;
+    PetscCall(dev_read(x, &xd));
+    VS* yd;
+    PetscCall(dev_rw(y, &yd));
+    if (hl) {
+      if (!A->d_send_idx) {
+        HCHK(hipMalloc(&A->d_send_idx, sizeof(i64) * hl));
+        HCHK(hipMalloc(&A->d_sendbuf, sizeof(VS) * hl));
+        HCHK(hipMalloc(&A->d_recvbuf, sizeof(VS) * hl));
+        HCHK(hipMemcpy(A->d_send_idx, A->send_idx.data(), sizeof(i64) * hl, hipMemcpyHostToDevice));
+        const size_t no = A->o_col.size();
+        HCHK(hipMalloc(&A->d_orowptr, sizeof(i64) * A->o_rowptr.size()));
+        HCHK(hipMalloc(&A->d_ocol, sizeof(i64) * (no ? no : 1)));
+        HCHK(hipMalloc(&A->d_oval, sizeof(VS) * (no ? no : 1)));
+        HCHK(hipMemcpy(A->d_orowptr, A->o_rowptr.data(), sizeof(i64) * A->o_rowptr.size(), hipMemcpyHostToDevice));
+        if (no) HCHK(hipMemcpy(A->d_ocol, A->o_col.data(), sizeof(i64) * no, hipMemcpyHostToDevice));
+        if (no) HCHK(hipMemcpy(A->d_oval, A->o_val.data(), sizeof(VS) * no, hipMemcpyHostToDevice));
+        A->h_sendbuf.resize(hl);
+        A->h_recvbuf.resize(hl);
+      }
+      HIPK(cfp::blas_gather(A->d_sendbuf, xd, A->d_send_idx, (i64)hl, g_stream));
+      HCHK(cfp::kprof_copy(A->h_sendbuf.data(), A->d_sendbuf, sizeof(VS) * hl, hipMemcpyDeviceToHost, g_stream));
+      HCHK(hipStreamSynchronize(g_stream));
+      PetscCall(comm_alltoall_host(r, A->h_sendbuf.data(), A->h_recvbuf.data(), sizeof(VS) * (size_t)A->hM));
+      HCHK(cfp::kprof_copy(A->d_recvbuf, A->h_recvbuf.data(), sizeof(VS) * hl, hipMemcpyHostToDevice, g_stream));
+    }
+    Mat B = A->dblk;
+    PetscCall(aij_upload(B));
+    if (B->dia == 1)
+      HIPK(cfp::blas_dia_spmv(B->m, B->dia_d, B->dia_cls, B->dia_mask, B->dia_tab, xd, yd, g_stream));
+    else
+      HIPK(cfp::blas_csr_spmv(B->m, (i64)B->h_col.size(), B->rowptr, B->col, B->val, xd, yd, g_stream));
+    if (hl && !A->o_col.empty())
+      HIPK(cfp::blas_csr_spmv_add(A->lm, A->d_orowptr, A->d_ocol, A->d_oval, A->d_recvbuf, yd, g_stream));
+    return PETSC_SUCCESS;
+  }
+  const VS* xh;
+  PetscCall(host_read(x, &xh));
+  std::vector<VS> sendb(hl), recvb(hl);
+  for (size_t e = 0; e < hl; ++e)
+    sendb[e] = A->send_idx[e] >= 0 ? xh[A->send_idx[e]] : D(std::complex<double>(0.0, 0.0));
+  if (hl) PetscCall(comm_alltoall_host(r, sendb.data(), recvb.data(), sizeof(VS) * (size_t)A->hM));
+  VS* yh;
+  PetscCall(host_rw(y, &yh));
+  const Mat B = A->dblk;
+  for (i64 lr = 0; lr < A->lm; ++lr) {
+    std::complex<double> acc = 0.0;
+    for (i64 p = B->h_rowptr[lr]; p < B->h_rowptr[lr + 1]; ++p) acc += C(B->h_val[p]) * C(xh[B->h_col[p]]);
+    for (i64 p = A->o_rowptr[lr]; p < A->o_rowptr[lr + 1]; ++p) acc += C(A->o_val[p]) * C(recvb[A->o_col[p]]);
+    yh[lr] = D(acc);
+  }
+  if (y->hip) {
+    HIPK(hipMemcpyAsync(y->d, y->h, sizeof(VS) * (size_t)y->n, hipMemcpyHostToDevice, g_stream));
+    y->mask = MASK_BOTH;
+  }
   return PETSC_SUCCESS;
 }
 extern "C" PetscErrorCode MatGetSize(Mat A, PetscInt* m, PetscInt* n) {
@@ -1434,7 +1779,9 @@ static PetscErrorCode aij_mult(Mat A, Vec x, Vec y) {
 }
 extern "C" PetscErrorCode MatMult(Mat A, Vec x, Vec y) {
   MCHK(A); VCHK(x); VCHK(y);
+  if (A->building) return ERR(PETSC_ERR_ARG_WRONGSTATE, "MatMult before MatAssemblyEnd");
   if (A->type == MATSEQAIJ) return aij_mult(A, x, y);
+  if (A->type == MATMPIAIJ) return mpiaij_mult(A, x, y);
   if (!A->mult) return ERR(PETSC_ERR_SUP, "MatMult not set on this MATSHELL");
   return A->mult(A, x, y);
 }
@@ -1446,6 +1793,8 @@ extern "C" PetscErrorCode MatMultTranspose(Mat A, Vec x, Vec y) {
 }
 extern "C" PetscErrorCode MatShift(Mat A, PetscScalar a) {
   MCHK(A);
+  if (A->building) return ERR(PETSC_ERR_ARG_WRONGSTATE, "MatShift before MatAssemblyEnd");
+  if (A->type == MATMPIAIJ) return MatShift(A->dblk, a);  // the diagonal lives in the diagonal block
   if (A->type != MATSEQAIJ) return ERR(PETSC_ERR_SUP, "MatShift only for AIJ in the stand-in");
   for (i64 r = 0; r < A->m; ++r) {
     bool found = false;
@@ -1468,6 +1817,7 @@ extern "C" PetscErrorCode MatDestroy(Mat* pA) {
   PetscErrorCode rc = PETSC_SUCCESS;
   if (A->destroy) rc = A->destroy(A);
   aij_free_device(A);
+  mpiaij_free(A);
   A->magic = 0;
   delete A;
   *pA = nullptr;

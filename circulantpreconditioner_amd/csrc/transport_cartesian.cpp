@@ -34,21 +34,21 @@ double wall() {
 // normals; un = n . a.  Interior face: un > 0 adds dt |F|/|C| un to the diagonal (:109-110);
 // otherwise the neighbour column gets -dt |F|/|C| un (reference sign, :111-112) or
 // +dt |F|/|C| un (fixed sign).  Border faces add nothing (Neumann, :114-129).
-extern "C" int cfp_transport_csr(int64_t nx, int64_t ny, int64_t nz, const double h[3], double dt, const double a[3],
-                                 int sign_mode, double shift, int64_t* rowptr, int64_t* col, double* val,
-                                 int64_t* nnz) {
+// rows [r0, r1) of the operator: rowptr[c - r0], global columns
+static int transport_csr_rows(int64_t nx, int64_t ny, int64_t nz, const double h[3], double dt, const double a[3],
+                              int sign_mode, double shift, int64_t r0, int64_t r1, int64_t* rowptr, int64_t* col,
+                              double* val, int64_t* nnz) {
   if (!h || !a || !rowptr || !col || !val || !nnz) return CFP_ERR_ARG_NULL;
   if (nx < 1 || ny < 1 || nz < 1 || h[0] <= 0 || h[1] <= 0 || h[2] <= 0) return CFP_ERR_ARG_OUTOFRANGE;
   if (sign_mode != CFP_UPWIND_REFERENCE && sign_mode != CFP_UPWIND_FIXED) return CFP_ERR_ARG_OUTOFRANGE;
+  if (r0 < 0 || r1 < r0 || r1 > nx * ny * nz) return CFP_ERR_ARG_OUTOFRANGE;
   const int64_t n[3] = {nx, ny, nz};
   const int64_t stride[3] = {1, nx, nx * ny};
   const double sgn = sign_mode == CFP_UPWIND_REFERENCE ? -1.0 : 1.0;
   int64_t p = 0;
   rowptr[0] = 0;
-  for (int64_t k = 0; k < nz; ++k)
-    for (int64_t j = 0; j < ny; ++j)
-      for (int64_t i = 0; i < nx; ++i) {
-        const int64_t c = i + nx * (j + ny * k);
+  for (int64_t c = r0; c < r1; ++c) {
+        const int64_t i = c % nx, j = (c / nx) % ny, k = c / (nx * ny);
         const int64_t idx[3] = {i, j, k};
         double diag = shift;
         double off[6] = {0, 0, 0, 0, 0, 0};  // neighbour coefficients: -x,+x,-y,+y,-z,+z
@@ -91,10 +91,16 @@ extern "C" int cfp_transport_csr(int64_t nx, int64_t ny, int64_t nz, const doubl
             ++p;
           }
         }
-        rowptr[c + 1] = p;
-      }
+        rowptr[c - r0 + 1] = p;
+  }
   *nnz = p;
   return CFP_SUCCESS;
+}
+
+extern "C" int cfp_transport_csr(int64_t nx, int64_t ny, int64_t nz, const double h[3], double dt, const double a[3],
+                                 int sign_mode, double shift, int64_t* rowptr, int64_t* col, double* val,
+                                 int64_t* nnz) {
+  return transport_csr_rows(nx, ny, nz, h, dt, a, sign_mode, shift, 0, nx * ny * nz, rowptr, col, val, nnz);
 }
 
 extern "C" double cfp_cartesian_min_ratio_vol_surf(int dim, const double h[3]) {
@@ -120,28 +126,58 @@ extern "C" PetscErrorCode computeDivergenceMatrixCartesian(PetscInt nx, PetscInt
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
+// computeDivergenceMatrix on a communicator (the reference's MatCreateAIJ on PETSC_COMM_WORLD,
+// tests/TransportEquation_SphericalExplosion_impl_mpi.cxx:82-84): every rank sets its own rows
+// (PETSC_DECIDE blocks = whole z-planes when the size divides n_z) and assembles
+extern "C" PetscErrorCode computeDivergenceMatrixCartesianAIJ(MPI_Comm comm, PetscInt nx, PetscInt ny, PetscInt nz,
+                                                              const PetscReal h[3], PetscReal dt, const PetscReal a[3],
+                                                              PetscInt sign_mode, Mat* A) {
+  PetscFunctionBeginUser;
+  PetscCheck(A && h && a, PETSC_COMM_SELF, PETSC_ERR_ARG_NULL, "computeDivergenceMatrixCartesianAIJ: NULL argument");
+  PetscCheck(nx >= 1 && ny >= 1 && nz >= 1, PETSC_COMM_SELF, PETSC_ERR_ARG_OUTOFRANGE, "grid sizes must be >= 1");
+  const int64_t N = nx * ny * nz;
+  PetscCall(MatCreateAIJ(comm, PETSC_DECIDE, PETSC_DECIDE, N, N, 7, NULL, 6, NULL, A));
+  PetscInt lo, hi;
+  PetscCall(MatGetOwnershipRange(*A, &lo, &hi));
+  const int64_t m = hi - lo;
+  std::vector<int64_t> rowptr((size_t)m + 1), col((size_t)(7 * (m > 0 ? m : 1)));
+  std::vector<PetscScalar> val((size_t)(7 * (m > 0 ? m : 1)));
+  int64_t nnz = 0;
+  const int rc = transport_csr_rows(nx, ny, nz, h, dt, a, (int)sign_mode, 0.0, lo, hi, rowptr.data(), col.data(),
+                                    reinterpret_cast<double*>(val.data()), &nnz);
+  PetscCheck(rc == CFP_SUCCESS, PETSC_COMM_SELF, rc, "computeDivergenceMatrixCartesianAIJ: bad arguments");
+  for (int64_t r = 0; r < m; ++r) {
+    const PetscInt row = lo + r, k = rowptr[(size_t)r + 1] - rowptr[(size_t)r];
+    PetscCall(MatSetValues(*A, 1, &row, k, col.data() + rowptr[(size_t)r], val.data() + rowptr[(size_t)r], ADD_VALUES));
+  }
+  PetscCall(MatAssemblyBegin(*A, MAT_FINAL_ASSEMBLY));
+  PetscCall(MatAssemblyEnd(*A, MAT_FINAL_ASSEMBLY));
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
 extern "C" PetscErrorCode initial_conditions_shock_cartesian(PetscInt nx, PetscInt ny, PetscInt nz,
                                                              const PetscReal xmin[3], const PetscReal xmax[3], Vec U) {
   PetscFunctionBeginUser;
   PetscCheck(xmin && xmax, PETSC_COMM_SELF, PETSC_ERR_ARG_NULL, "NULL domain bounds");
-  PetscInt n;
+  PetscInt n, Ng, lo;
   PetscCall(VecGetLocalSize(U, &n));
-  PetscCheck(n == nx * ny * nz, PETSC_COMM_SELF, PETSC_ERR_ARG_SIZ, "U size differs from nx*ny*nz");
+  PetscCall(VecGetSize(U, &Ng));
+  PetscCall(VecGetOwnershipRange(U, &lo, NULL));
+  PetscCheck(Ng == nx * ny * nz, PETSC_COMM_SELF, PETSC_ERR_ARG_SIZ, "U size differs from nx*ny*nz");
   const double hx = (xmax[0] - xmin[0]) / (double)nx, hy = (xmax[1] - xmin[1]) / (double)ny,
                hz = (xmax[2] - xmin[2]) / (double)nz;
   const double cx = (xmin[0] + xmax[0]) / 2, cy = (xmin[1] + xmax[1]) / 2, cz = (xmin[2] + xmax[2]) / 2;
   const double rmax = 0.3;
   PetscScalar* u;
   PetscCall(VecGetArrayWrite(U, &u));
-  for (PetscInt k = 0; k < nz; ++k)
-    for (PetscInt j = 0; j < ny; ++j)
-      for (PetscInt i = 0; i < nx; ++i) {
-        const double x = xmin[0] + (i + 0.5) * hx, y = xmin[1] + (j + 0.5) * hy, z = xmin[2] + (k + 0.5) * hz;
-        double r2 = (x - cx) * (x - cx);
-        if (ny > 1) r2 += (y - cy) * (y - cy);
-        if (nz > 1) r2 += (z - cz) * (z - cz);
-        u[i + nx * (j + ny * k)] = std::sqrt(r2) < rmax ? 650.0 : 600.0;
-      }
+  for (PetscInt c = lo; c < lo + n; ++c) {  // this rank's cells
+    const PetscInt i = c % nx, j = (c / nx) % ny, k = c / (nx * ny);
+    const double x = xmin[0] + (i + 0.5) * hx, y = xmin[1] + (j + 0.5) * hy, z = xmin[2] + (k + 0.5) * hz;
+    double r2 = (x - cx) * (x - cx);
+    if (ny > 1) r2 += (y - cy) * (y - cy);
+    if (nz > 1) r2 += (z - cz) * (z - cz);
+    u[c - lo] = std::sqrt(r2) < rmax ? 650.0 : 600.0;
+  }
   PetscCall(VecRestoreArrayWrite(U, &u));
   PetscFunctionReturn(PETSC_SUCCESS);
 }
@@ -189,14 +225,26 @@ extern "C" PetscErrorCode TransportEquationGMRES(const cfp_transport_config* cfg
   const double dt = cfg->cfl * cfp_cartesian_min_ratio_vol_surf(dim, h) / anorm;  // :54
   res->dt = dt;
 
+  // one rank: sequential Vecs and AIJ; several (PETSC_COMM_WORLD of PetscMiniSetCommWorld): the
+  // reference's VecCreateMPI / MatCreateAIJ on PETSC_COMM_WORLD with PETSC_DECIDE rows (:59-84)
+  int P = 1;
+  PetscCallMPI(MPI_Comm_size(PETSC_COMM_WORLD, &P));
   Vec Un, dUn;
-  if (cfg->on_device) PetscCall(VecCreateSeqHIP(PETSC_COMM_SELF, N, &Un));
+  if (P > 1 && cfg->on_device) PetscCall(VecCreateMPIHIP(PETSC_COMM_WORLD, PETSC_DECIDE, N, &Un));
+  else if (P > 1) PetscCall(VecCreateMPI(PETSC_COMM_WORLD, PETSC_DECIDE, N, &Un));
+  else if (cfg->on_device) PetscCall(VecCreateSeqHIP(PETSC_COMM_SELF, N, &Un));
   else PetscCall(VecCreateSeq(PETSC_COMM_SELF, N, &Un));
   PetscCall(VecDuplicate(Un, &dUn));
   PetscCall(initial_conditions_shock_cartesian(nx, ny, nz, cfg->xmin, cfg->xmax, Un));
+  PetscInt lo, nloc;
+  PetscCall(VecGetOwnershipRange(Un, &lo, NULL));
+  PetscCall(VecGetLocalSize(Un, &nloc));
+  res->rstart = lo;
+  res->nlocal = nloc;
 
   Mat A;
-  PetscCall(computeDivergenceMatrixCartesian(nx, ny, nz, h, dt, cfg->a, cfg->sign_mode, &A));
+  if (P > 1) PetscCall(computeDivergenceMatrixCartesianAIJ(PETSC_COMM_WORLD, nx, ny, nz, h, dt, cfg->a, cfg->sign_mode, &A));
+  else PetscCall(computeDivergenceMatrixCartesian(nx, ny, nz, h, dt, cfg->a, cfg->sign_mode, &A));
   PetscCall(MatShift(A, 1.0));  // :117
 
   KSP ksp;
@@ -296,10 +344,10 @@ extern "C" PetscErrorCode TransportEquationGMRES(const cfp_transport_config* cfg
   }
   res->steps = it;
   res->time = time;
-  if (U_out) {
+  if (U_out) {  // this rank's rows (all of them on one rank)
     const PetscScalar* u;
     PetscCall(VecGetArrayRead(Un, &u));
-    std::memcpy(U_out, (const void*)u, sizeof(double) * 2 * (size_t)N);
+    std::memcpy(U_out, (const void*)u, sizeof(double) * 2 * (size_t)nloc);
     PetscCall(VecRestoreArrayRead(Un, &u));
   }
   PetscCall(KSPDestroy(&ksp));  // destroys the PC, whose destroy callback frees setup's objects

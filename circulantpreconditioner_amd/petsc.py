@@ -334,6 +334,42 @@ class Mat:
                                                   va.ctypes.data, ctypes.byref(h)))
         return cls(h)
 
+    @classmethod
+    def create_aij(cls, N: int, comm: int = PETSC_COMM_WORLD, nlocal: int = -1) -> "Mat":
+        """MatCreateAIJ(comm, nlocal | PETSC_DECIDE, same, N, N, ...): an N x N matrix to fill with
+        set_values and assemble (the reference's MatCreateAIJ on PETSC_COMM_WORLD)."""
+        h = ctypes.c_void_p()
+        PetscCall(lib().MatCreateAIJ(comm, nlocal, nlocal, N, N, 7, None, 6, None, ctypes.byref(h)))
+        return cls(h)
+
+    def set_values(self, rows, cols, vals, add: bool = False) -> "Mat":
+        """MatSetValues(A, len(rows), rows, len(cols), cols, vals (row-major), mode)."""
+        r = np.ascontiguousarray(rows, dtype=np.int64)
+        c = np.ascontiguousarray(cols, dtype=np.int64)
+        v = np.ascontiguousarray(vals, dtype=np.complex128).reshape(-1)
+        if v.size != r.size * c.size:
+            raise ValueError("vals must hold len(rows) * len(cols) values")
+        PetscCall(lib().MatSetValues(self.h, r.size, r.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), c.size,
+                                     c.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), v.ctypes.data,
+                                     ADD_VALUES if add else INSERT_VALUES))
+        return self
+
+    def assemble(self) -> "Mat":
+        PetscCall(lib().MatAssemblyBegin(self.h, 0))
+        PetscCall(lib().MatAssemblyEnd(self.h, 0))
+        return self
+
+    def ownership_range(self) -> tuple:
+        lo, hi = ctypes.c_int64(), ctypes.c_int64()
+        PetscCall(lib().MatGetOwnershipRange(self.h, ctypes.byref(lo), ctypes.byref(hi)))
+        return lo.value, hi.value
+
+    def halo(self) -> tuple:
+        """(ghost columns of this rank, the largest per-peer halo over the ranks): MATMPIAIJ."""
+        g, m = ctypes.c_int64(), ctypes.c_int64()
+        PetscCall(lib().PetscMiniMatMPIAIJGetHalo(self.h, ctypes.byref(g), ctypes.byref(m)))
+        return g.value, m.value
+
     def create_vecs(self, nvec: int = 1) -> list:
         hs = [ctypes.c_void_p() for _ in range(3)]
         refs = [ctypes.byref(hs[i]) if i < nvec else None for i in range(3)]

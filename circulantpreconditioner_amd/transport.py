@@ -83,13 +83,16 @@ def config(n: int | Sequence[int] = 32, **kw) -> TransportConfig:
 
 def run(cfg: TransportConfig, return_field: bool = False):
     """TransportEquationGMRES: the implicit time loop; returns the result dict (and the final
-    field as a complex128 array when asked)."""
+    field as a complex128 array when asked: this rank's rows res['rstart'] .. + res['nlocal'] when
+    PETSC_COMM_WORLD has several ranks, the whole field on one)."""
     res = TransportResult()
     n = int(cfg.nx * cfg.ny * cfg.nz)
     out = np.empty(n, dtype=np.complex128) if return_field else None
     ptr = out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) if out is not None else None
     PetscCall(lib().TransportEquationGMRES(ctypes.byref(cfg), ctypes.byref(res), ptr))
     d = res.as_dict()
+    if out is not None:
+        out = out[:d["nlocal"]].copy()
     return (d, out) if return_field else d
 
 

@@ -99,6 +99,8 @@ typedef const char *VecType;
 #define VECMPIHIP "mpihip"
 #define MATSHELL "shell"
 #define MATSEQAIJ "seqaij"
+#define MATMPIAIJ "mpiaij"
+#define MATAIJ "aij"
 #define MATFFTW "fftw"
 #define PCSHELL "shell"
 #define PCNONE "none"
@@ -294,6 +296,28 @@ PetscErrorCode MatCreateSeqAIJWithArrays(MPI_Comm comm, PetscInt m, PetscInt n, 
 PetscErrorCode MatGetType(Mat A, MatType *type);
 PetscErrorCode MatGetSize(Mat A, PetscInt *m, PetscInt *n);
 PetscErrorCode MatGetLocalSize(Mat A, PetscInt *m, PetscInt *n);
+/* MatCreateAIJ (the reference's transport / wave drivers, tests/TransportEquation_SphericalExplosion_
+ * impl_mpi.cxx:82-84): m, n local sizes or PETSC_DECIDE (PETSc's row blocks, as VecCreateMPI), M, N
+ * global; the preallocation hints are accepted and not needed.  Entries go in with MatSetValue(s)
+ * -- another rank's rows are stashed and delivered by MatAssemblyBegin/End, which are collective on
+ * the communicator -- and the matrix is usable after MatAssemblyEnd(A, MAT_FINAL_ASSEMBLY).  One
+ * rank: a MATSEQAIJ.  Several (MATMPIAIJ): this rank's rows, split as PETSc does into the diagonal
+ * block (its own columns: row-class form / CSR, device SpMV) and the off-diagonal block over the
+ * ghost columns, whose values MatMult fetches from their owners (one all-to-all per MatMult; none
+ * when no rank has ghosts -- an operator that couples cells inside z-slabs only).  Square
+ * matrices always store their diagonal (MatShift). */
+typedef enum { MAT_FINAL_ASSEMBLY = 0, MAT_FLUSH_ASSEMBLY = 1 } MatAssemblyType;
+PetscErrorCode MatCreateAIJ(MPI_Comm comm, PetscInt m, PetscInt n, PetscInt M, PetscInt N, PetscInt d_nz,
+                            const PetscInt d_nnz[], PetscInt o_nz, const PetscInt o_nnz[], Mat *A);
+PetscErrorCode MatSetValue(Mat A, PetscInt i, PetscInt j, PetscScalar v, InsertMode mode);
+PetscErrorCode MatSetValues(Mat A, PetscInt m, const PetscInt idxm[], PetscInt n, const PetscInt idxn[],
+                            const PetscScalar v[], InsertMode mode);
+PetscErrorCode MatAssemblyBegin(Mat A, MatAssemblyType type);
+PetscErrorCode MatAssemblyEnd(Mat A, MatAssemblyType type);
+PetscErrorCode MatGetOwnershipRange(Mat A, PetscInt *lo, PetscInt *hi);
+/* not in PETSc: ghost columns of this rank's rows and the largest per-peer halo of any rank (0:
+ * MatMult exchanges nothing) -- MATMPIAIJ after assembly; 0, 0 otherwise */
+PetscErrorCode PetscMiniMatMPIAIJGetHalo(Mat A, PetscInt *ghosts, PetscInt *max_per_peer);
 PetscErrorCode MatGetComm(Mat A, MPI_Comm *comm); /* not in PETSc (PetscObjectGetComm) */
 PetscErrorCode MatMult(Mat A, Vec x, Vec y);
 PetscErrorCode MatMultTranspose(Mat A, Vec x, Vec y);

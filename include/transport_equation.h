@@ -51,6 +51,12 @@ PetscErrorCode computeDivergenceMatrixCartesian(PetscInt nx, PetscInt ny, PetscI
 PetscErrorCode initial_conditions_shock_cartesian(PetscInt nx, PetscInt ny, PetscInt nz, const PetscReal xmin[3],
                                                   const PetscReal xmax[3], Vec U);
 
+/* computeDivergenceMatrix on a communicator: MatCreateAIJ(comm, PETSC_DECIDE rows), each rank
+ * setting its own rows with MatSetValues, then MatAssemblyBegin/End (no MatShift) */
+PetscErrorCode computeDivergenceMatrixCartesianAIJ(MPI_Comm comm, PetscInt nx, PetscInt ny, PetscInt nz,
+                                                   const PetscReal h[3], PetscReal dt, const PetscReal a[3],
+                                                   PetscInt sign_mode, Mat *A);
+
 /* ---- the implicit transport time loop with GMRES (TransportEquation_impl_mpi) */
 enum { CFP_TRANSPORT_PC_NONE = 0, CFP_TRANSPORT_PC_FFT = 1 };
 /* lambda of the FFT preconditioner: REFERENCE = getFFTPrec3DContext's a dt (max-min)/n
@@ -101,11 +107,16 @@ typedef struct {
   int64_t dev_launches[4];
   int64_t fused_dots;     /* Gram-Schmidt steps whose dots came from the PC apply (summed) */
   int64_t fused_norms;    /* residual norms that came from the PC apply (summed) */
+  int64_t rstart, nlocal; /* this rank's rows (U_out holds nlocal values): 0, N on one rank */
 } cfp_transport_result;
 
 /* fill cfg with the reference main's defaults for an n^3 grid on [-0.5,0.5]^3 */
 void cfp_transport_config_default(cfp_transport_config *cfg, int64_t n);
-/* run the loop; if U_out != NULL the final field is copied there (interleaved re,im, N values) */
+/* run the loop; if U_out != NULL this rank's part of the final field is copied there (interleaved
+ * re,im, res->nlocal values from row res->rstart; the whole field, N values, on one rank).  With
+ * PETSC_COMM_WORLD of several ranks (PetscMiniSetCommWorld) the loop runs on all of them as the
+ * reference's does (VecCreateMPI, MatCreateAIJ, KSP on PETSC_COMM_WORLD; the FFT PCSHELL on the
+ * z-slab plan): every rank calls it with the same cfg. */
 PetscErrorCode TransportEquationGMRES(const cfp_transport_config *cfg, cfp_transport_result *res, double *U_out);
 
 /* ---- the direct-solver time loop (TransportEquationFFT_impl_mpi,

@@ -1,0 +1,148 @@
+"""The reference's MPI caller shape on CPU: MatCreateAIJ on a communicator of
+several gloo ranks, and the transport GMRES time loop on PETSC_COMM_WORLD.
+
+tests/TransportEquation_SphericalExplosion_impl_mpi.cxx:59-84 creates Un with VecCreateMPI and the
+operator with MatCreateAIJ(PETSC_COMM_WORLD, ...), fills both on rank 0 (VecSetValues /
+computeDivergenceMatrix's MatSetValue, stashed and shipped at assembly) and runs KSPSolve on
+PETSC_COMM_WORLD.  Here:
+- the stand-in MATMPIAIJ against scipy: rank 0 sets every row (the reference's pattern), or each
+  rank its own rows with ADD_VALUES split over two calls; MatMult on host Vecs of the PETSC_DECIDE
+  layout, including the ghost exchange of an operator that couples z-neighbours;
+- TransportEquationGMRES on 2 and 3 ranks (host Vecs, PCNONE): the gathered step equals the
+  one-rank run and the iteration counts agree.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _csr(dims, a, sign="fixed", dt=0.013):
+    from circulantpreconditioner_amd import transport as T
+    h = [1.0 / d for d in dims]
+    rp, col, val = T.transport_csr(dims, h, dt, a, sign, 1.0)
+    n = int(np.prod(dims))
+    return sp.csr_matrix((val, col, rp), shape=(n, n))
+
+
+def _worker(rank, P, port, q, job):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=P)
+    try:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from circulantpreconditioner_amd import petsc as Pm
+        from circulantpreconditioner_amd import transport as T
+        comm = Pm.Comm.torch().set_world()
+        out = {}
+        if job == "matmult":
+            for key, a in (("z", (0.3, -1.2, 0.7)), ("x", (1.0, 0.0, 0.0))):
+                dims = (6, 5, 12)  # P = 2, 3: whole z-planes per rank
+                A = _csr(dims, a)
+                N = A.shape[0]
+                x = np.random.default_rng(3).standard_normal(N) + 1j * np.random.default_rng(4).standard_normal(N)
+                for mode in ("rank0", "own"):
+                    M = Pm.Mat.create_aij(N)
+                    lo, hi = M.ownership_range()
+                    if mode == "rank0":  # the reference: rank 0 sets every global row
+                        if rank == 0:
+                            for r in range(N):
+                                cols = A.indices[A.indptr[r]:A.indptr[r + 1]]
+                                M.set_values([r], cols, A.data[A.indptr[r]:A.indptr[r + 1]])
+                    else:  # own rows, each value added in two halves
+                        for r in range(lo, hi):
+                            cols = A.indices[A.indptr[r]:A.indptr[r + 1]]
+                            v = A.data[A.indptr[r]:A.indptr[r + 1]]
+                            M.set_values([r], cols, 0.25 * v, add=True)
+                            M.set_values([r], cols, 0.75 * v, add=True)
+                    M.assemble()
+                    vx, vy = Pm.Vec.mpi(N), Pm.Vec.mpi(N)
+                    vx.set_array(x[lo:hi])
+                    M.mult(vx, vy)
+                    out[(key, mode)] = {"range": (lo, hi), "y": vy.array(), "halo": M.halo()}
+                    M.shift(0.5)
+                    M.mult(vx, vy)
+                    out[(key, mode, "shift")] = vy.array()
+                    M.destroy()
+        else:
+            dims, sign = job
+            res, U = T.run(T.config(dims, pc="none", sign=sign, device=False, steps=2), return_field=True)
+            out = {"res": res, "U": U}
+        Pm.set_comm_world(Pm.PETSC_COMM_SELF)
+        comm.destroy()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(P, job):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, P, port, q, job)) for r in range(P)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=240) for _ in range(P))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    return res
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_mpiaij_assembly_and_matmult(P):
+    res = _spawn(P, "matmult")
+    for key, a in (("z", (0.3, -1.2, 0.7)), ("x", (1.0, 0.0, 0.0))):
+        A = _csr((6, 5, 12), a)
+        N = A.shape[0]
+        x = np.random.default_rng(3).standard_normal(N) + 1j * np.random.default_rng(4).standard_normal(N)
+        for mode in ("rank0", "own"):
+            y = np.empty(N, dtype=np.complex128)
+            ys = np.empty(N, dtype=np.complex128)
+            for r in range(P):
+                lo, hi = res[r][(key, mode)]["range"]
+                y[lo:hi] = res[r][(key, mode)]["y"]
+                ys[lo:hi] = res[r][(key, mode, "shift")]
+            ref = A @ x
+            assert np.linalg.norm(y - ref) <= 1e-14 * np.linalg.norm(ref)
+            assert np.linalg.norm(ys - (ref + 0.5 * x)) <= 1e-14 * np.linalg.norm(ref)
+            halos = [res[r][(key, mode)]["halo"] for r in range(P)]
+            if key == "x":  # x-coupling only: no rank has ghosts, MatMult exchanges nothing
+                assert all(h == (0, 0) for h in halos)
+            else:  # upwind from below in z (a_z > 0): every rank but 0 needs the plane under its slab
+                assert halos[0][0] == 0 and all(h[0] == 6 * 5 for h in halos[1:])
+                assert all(h[1] == 6 * 5 for h in halos)  # the largest per-peer halo, agreed by all
+
+
+@pytest.mark.parametrize("P,dims,sign", [(2, (12, 10, 8), "fixed"), (2, (12, 10, 8), "reference"),
+                                         (3, (10, 8, 9), "reference")])
+def test_transport_gmres_on_several_ranks(P, dims, sign):
+    """TransportEquationGMRES on PETSC_COMM_WORLD of P gloo ranks (host Vecs, PCNONE: the reference
+    driver's PC): the gathered step equals the one-rank run; the iteration counts agree."""
+    from circulantpreconditioner_amd import transport as T
+    res = _spawn(P, (dims, sign))
+    N = int(np.prod(dims))
+    U = np.empty(N, dtype=np.complex128)
+    for r in range(P):
+        lo, n = res[r]["res"]["rstart"], res[r]["res"]["nlocal"]
+        U[lo:lo + n] = res[r]["U"]
+    r1, U1 = T.run(T.config(dims, pc="none", sign=sign, device=False, steps=2), return_field=True)
+    for r in range(P):
+        assert res[r]["res"]["total_its"] == r1["total_its"]
+        assert res[r]["res"]["all_converged"] == r1["all_converged"]
+    assert np.linalg.norm(U - U1) <= 1e-9 * np.linalg.norm(U1)
