@@ -820,6 +820,21 @@ extern "C" int cfp_plan_apply(cfp_plan_t p, const double* b, double* x, void* st
   return run_apply(p, nullptr, (const cd*)b, (cd*)x, (hipStream_t)stream, nullptr);
 }
 
+// whether cfp_plan_apply_ex runs the stencil and the dots inside the apply's own sweeps
+static bool apply_ex_fusable(const cfp_plan_s* p, const cfp_stencil_t* st, int nv) {
+  bool pre_ok = !st || (st->x_local && st->nd >= 1 && st->nd <= 3 && st->ncls >= 1 && st->ncls <= TP_PRE_MAX_CLS);
+  for (int k = 0; st && k < st->nd; ++k) pre_ok = pre_ok && st->off[k] >= -1 && st->off[k] <= 1;
+  const bool cube = p->n[0] == p->n[1] && p->n[1] == p->n[2];
+  return cube && use_three_pass(p, false) && three_pass_fused_supported((int)p->n[0], p->tp_shape) && pre_ok &&
+         nv >= 0 && nv <= TP_POST_MAX;
+}
+
+extern "C" int cfp_plan_apply_ex_fusable(cfp_plan_t p, const cfp_stencil_t* pre, int post_nv, int* fusable) {
+  if (!p || !fusable) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  *fusable = apply_ex_fusable(p, pre, post_nv) ? 1 : 0;
+  return CFP_SUCCESS;
+}
+
 // The Krylov step around one apply (circulant_fft.h cfp_apply_ex_t): y = A b in P1 and the dots
 // in P3 of the 256^3 3-sweep schedule, or the stencil and the dots as their own kernels around a
 // plain apply wherever that schedule or the stencil's shape does not allow the fusion.
@@ -839,11 +854,7 @@ extern "C" int cfp_plan_apply_ex(cfp_plan_t p, const double* b, double* x, void*
   if (!st && nv == 0) return cfp_plan_apply(p, b, x, stream);
   DeviceGuard dg(p->device);
   hipStream_t s = (hipStream_t)stream;
-  bool pre_ok = !st || (st->x_local && st->nd <= 3 && st->ncls <= TP_PRE_MAX_CLS);
-  for (int k = 0; st && k < st->nd; ++k) pre_ok = pre_ok && st->off[k] >= -1 && st->off[k] <= 1;
-  const bool cube = p->n[0] == p->n[1] && p->n[1] == p->n[2];
-  if (cube && use_three_pass(p, false) && three_pass_fused_supported((int)p->n[0], p->tp_shape) && pre_ok &&
-      nv <= TP_POST_MAX) {
+  if (apply_ex_fusable(p, st, nv)) {
     TPArgs fz;
     if (st) {
       fz.pre_cls = st->cls;

@@ -163,6 +163,7 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
   __shared__ cd pre_tab_l[PRE ? 3 * TP_PRE_MAX_CLS : 1];
   __shared__ unsigned pre_mk_l[PRE ? TP_PRE_MAX_CLS + 1 : 1];  // [ncls]: slot masks, [MAX]: their union
   __shared__ const unsigned char* pre_cls_l[1];
+  __shared__ cd pre_edge_l[PRE ? NT : 1];  // PRE: per wave, the edge neighbours its lanes loaded
   // POST: per wave and value, the running sum of its lanes' dot contributions
   __shared__ double post_l[POST ? 2 * NP * (NT / 64) : 1];
   __shared__ const cd* post_ptr_l[POST ? NP : 1];
@@ -230,13 +231,15 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
     } else if constexpr (PRE) {
       // y = A b on the unit's rows.  With lane pairs (LP) lanes L and L + 1 of a wave hold x and
       // x + 1 of one row for L % 32 < 31, so a point's x-neighbours come from its neighbour lanes
-      // (DPP wave_shr / wave_shl); only the lanes at x % 32 = 0 / 31 load theirs (exec-masked, the
-      // same lines: cache hits).  A neighbour outside the row is never used (its slot is absent
-      // from the row's class), so its address is clamped into the row.
+      // (DPP wave_shr / wave_shl).  The neighbours across a wave's 32-column edge are loaded with
+      // b, one per lane -- lane (ty, j < 16) the x - 1 edge of point j, (ty, 16 + j) the x + 1
+      // edge -- and handed to the edge lanes through the wave's LDS slots: one memory round trip
+      // per unit, as the plain load.  A neighbour outside the row is never used (its slot is
+      // absent from the row's class), so its address is clamped into the row.
       static_assert(LP, "the fused stencil relies on the lane-pair layout");
-      const i64 i0 = (i64)(u / N2) * TN * TN + x + (i64)TN * (u % N2 + N2 * ty);
-      const int xm = x > 0 ? -1 : 0, xp = x < TN - 1 ? 1 : 0;
-      const int l32 = (int)(threadIdx.x & 31);
+      const i64 p0 = (i64)(u / N2) * TN * TN + (i64)TN * (u % N2 + N2 * ty);  // row of point 0
+      const i64 i0 = p0 + x;
+      const int l32 = (int)(threadIdx.x & 31), wv = (int)(threadIdx.x >> 6);
       // the slots any class uses, and the class array, from LDS at each use (kernel-argument
       // values would sit in SGPRs across the FFTs)
       const unsigned slots = ((volatile unsigned*)pre_mk_l)[TP_PRE_MAX_CLS];
@@ -249,18 +252,28 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
         v[m] = gload<FLAGS>(in + i);
         cl[m] = cls[i];
       }
+      cd edge = make_cd(0.0, 0.0);
+      {
+        const bool left = l32 < 16;
+        int xe = left ? x - l32 - 1 : x - l32 + 32;
+        xe = xe < 0 ? 0 : (xe > TN - 1 ? TN - 1 : xe);
+        if ((left && hm) || (!left && hp)) edge = gload<0>(in + p0 + (i64)TN * N2 * TY * (l32 & 15) + xe);
+      }
       __builtin_amdgcn_sched_barrier(0);
+      cd* const el = pre_edge_l + 64 * wv;
+      el[threadIdx.x & 63] = edge;
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS writes are done
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int m = 0; m < PTS; ++m) {
-        const i64 i = i0 + (i64)TN * N2 * TY * m;
         cd bm = make_cd(0.0, 0.0), bp = make_cd(0.0, 0.0);
         if (hm) {
           bm = dpp_c<DPP_WAVE_SHR1>(v[m]);
-          if (l32 == 0) bm = gload<0>(in + i + xm);
+          if (l32 == 0) bm = el[32 * ty + m];
         }
         if (hp) {
           bp = dpp_c<DPP_WAVE_SHL1>(v[m]);
-          if (l32 == 31) bp = gload<0>(in + i + xp);
+          if (l32 == 31) bp = el[32 * ty + 16 + m];
         }
         const unsigned mk = pre_mk_l[cl[m]];
         const cd* t = pre_tab_l + 3 * cl[m];

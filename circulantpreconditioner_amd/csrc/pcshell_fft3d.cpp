@@ -466,10 +466,20 @@ extern "C" PetscErrorCode solve_3D(Mat FFT_MAT, Vec X, Vec Diag, Vec b, Vec b_ha
 }
 
 #ifndef CFP_WITH_PETSC
-// The stand-in KSP's pending dots request (PCMiniApplyDots) as the post-op of a plan apply
-cfp_apply_ex_t* take_dots(PC pc, cfp_apply_ex_t* ex, PCMiniApplyDots** req) {
+// The stand-in KSP's pending dots request (PCMiniApplyDots) as the post-op of a plan apply -- taken
+// only when the plan computes them inside its sweeps (with the stencil `pre`, if any); otherwise
+// the KSP's own multi-dot is the same work
+cfp_apply_ex_t* take_dots(PC pc, cfp_apply_ex_t* ex, PCMiniApplyDots** req, const cfp_stencil_t* pre = nullptr) {
   *req = nullptr;
   if (PCMiniGetApplyDots(pc, req) || !*req || (*req)->done || (*req)->nv < 1 || (*req)->nv > 8) {
+    *req = nullptr;
+    return nullptr;
+  }
+  FFTPrecTransportContext* ctx = nullptr;
+  FFTShell* s = nullptr;
+  int fusable = 0;
+  if (PCShellGetContext(pc, &ctx) || !ctx || !ctx->FFT_MAT || fft_shell(ctx->FFT_MAT, &s) || !s->plan ||
+      cfp_plan_apply_ex_fusable(s->plan, pre, (int)(*req)->nv, &fusable) || !fusable) {
     *req = nullptr;
     return nullptr;
   }
@@ -597,8 +607,9 @@ extern "C" PetscErrorCode applyFFT3DPrecTransportBA(PC pc, PCSide side, Vec x, V
       PetscBool has = PETSC_FALSE, xl = PETSC_FALSE;
       PetscMiniDia dia;
       PetscCall(PetscMiniMatAIJGetDia(A, ctx->n_x, &has, &xl, &dia));
+      cfp_stencil_t st;
+      int fusable = 0;
       if (has) {
-        cfp_stencil_t st;
         std::memset((void*)&st, 0, sizeof(st));
         st.cls = dia.cls;
         st.mask = dia.mask;
@@ -607,9 +618,12 @@ extern "C" PetscErrorCode applyFFT3DPrecTransportBA(PC pc, PCSide side, Vec x, V
         st.nd = dia.nd;
         st.ncls = dia.ncls;
         st.x_local = xl ? 1 : 0;
+        CFPCALL(cfp_plan_apply_ex_fusable(s->plan, &st, 0, &fusable));
+      }
+      if (fusable) {  // A x inside the apply's first sweep (else MatMult below: the same kernels)
         cfp_apply_ex_t ex{};
         PCMiniApplyDots* req = nullptr;
-        take_dots(pc, &ex, &req);
+        take_dots(pc, &ex, &req, &st);
         ex.pre = &st;
         ++s->solves_own;
         PetscCall(shell_apply(s, y, x, true, nullptr, &ex));

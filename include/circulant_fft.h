@@ -121,6 +121,10 @@ typedef struct {
   int fused;
 } cfp_apply_ex_t;
 int cfp_plan_apply_ex(cfp_plan_t plan, const double *b_dev, double *x_dev, void *stream, cfp_apply_ex_t *ex);
+/* *fusable = 1 when cfp_plan_apply_ex with this stencil (NULL: none) and post_nv dots would run
+ * them inside the apply (ex->fused = 1); a caller for which the separate kernels are no gain (they
+ * are what it would launch itself) asks first. */
+int cfp_plan_apply_ex_fusable(cfp_plan_t plan, const cfp_stencil_t *pre, int post_nv, int *fusable);
 
 /* Unnormalised 3-D transforms: forward (e^{-}, MatMult) and backward (e^{+}, MatMultTranspose). */
 int cfp_plan_forward(cfp_plan_t plan, const double *in_dev, double *out_dev, void *stream);
