@@ -442,6 +442,7 @@ int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStr
       hipError_t e;
       if (fz && q.tp == 0 && fz->pre_cls) {
         a.pre_cls = fz->pre_cls;
+        a.pre_cls_x = fz->pre_cls_x;
         a.pre_mask = fz->pre_mask;
         a.pre_tab = fz->pre_tab;
         a.pre_nd = fz->pre_nd;
@@ -858,6 +859,7 @@ extern "C" int cfp_plan_apply_ex(cfp_plan_t p, const double* b, double* x, void*
     TPArgs fz;
     if (st) {
       fz.pre_cls = st->cls;
+      fz.pre_cls_x = st->cls_x;
       fz.pre_mask = st->mask;
       fz.pre_tab = (const cd*)st->tab;
       fz.pre_nd = st->nd;

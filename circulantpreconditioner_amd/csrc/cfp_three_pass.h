@@ -29,6 +29,7 @@ struct TPArgs {
   // sums of post_v[j]^H x (j < post_nv; bit j of post_self: x itself, i.e. |x|^2) to post_partial
   // [blockIdx][2 j + re/im], the k_mdot layout (cfp_blas.hip k_mdot_finish).
   const unsigned char* pre_cls = nullptr;   // [N] row class
+  const unsigned char* pre_cls_x = nullptr; // optional [n]: row r's class is pre_cls_x[r mod n]
   const unsigned char* pre_mask = nullptr;  // [ncls] diagonals present per class (bit k: pre_off[k])
   const cd* pre_tab = nullptr;              // [ncls][pre_nd] coefficients
   int pre_nd = 0, pre_ncls = 0;

@@ -91,10 +91,24 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v + w;
 }
 
+// a byte load with the sweep's load policy (the fused stencil's row classes)
+template <int FLAGS>
+__device__ __forceinline__ unsigned char gload_u8(const unsigned char* p) {
+  if constexpr ((FLAGS & F_NT_LD) != 0) return __builtin_nontemporal_load(p);
+  return *p;
+}
+
 // first radix of an n-point FFT done as r0 x PTS x ... x PTS (n = r0 PTS^k, r0 <= PTS)
 constexpr int r0_of(int n, int pts) { return n > pts ? r0_of(n / pts, pts) : n; }
 
 }  // namespace
+
+// P3's reads of the Krylov basis vectors for the fused dots (FUSE > 0): non-temporal, so the
+// 256 MiB vectors do not push the next P1 output out of the Infinity Cache before P2 reads it
+#ifndef CFP_POST_NT
+#define CFP_POST_NT 1
+#endif
+constexpr int kPostLoadFlags = CFP_POST_NT ? F_NT_LD : 0;
 
 // PROBE != 0 only in tools/kexp (tp_probe.hip, p2_512.hip, rows_512.hip, built with
 // CFP_KEXP): timing probes that drop a
@@ -194,8 +208,8 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
     if (tid == 0) {
       unsigned all = 0;
       for (int k = 0; k < a.pre_nd; ++k) all |= 1u << (a.pre_off[k] + 1);
-      pre_mk_l[TP_PRE_MAX_CLS] = all;
-      pre_cls_l[0] = a.pre_cls;
+      pre_mk_l[TP_PRE_MAX_CLS] = all | (a.pre_cls_x ? 8u : 0u);  // bit 3: classes by x alone
+      pre_cls_l[0] = a.pre_cls_x ? a.pre_cls_x : a.pre_cls;
     }
   }
   if constexpr (LP || PRE || POST) __syncthreads();  // phase A reads tw_l (and the stencil) before any barrier
@@ -245,38 +259,47 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
       const unsigned slots = ((volatile unsigned*)pre_mk_l)[TP_PRE_MAX_CLS];
       const bool hm = (slots & 1u) != 0, hp = (slots & 4u) != 0;
       const unsigned char* const cls = ((const unsigned char* const volatile*)pre_cls_l)[0];
+      // classes by x alone (bit 3): one byte per thread (its column x), else one per point.
+      // Every load here is non-temporal like b's: the edge and class lines must not stay in the
+      // caches in place of this sweep's output, which P2 reads next.
+      const bool by_x = (slots & 8u) != 0;
       int cl[PTS];
+      const int clx = by_x ? (int)gload_u8<FLAGS>(cls + x) : 0;
 #pragma unroll
       for (int m = 0; m < PTS; ++m) {
         const i64 i = i0 + (i64)TN * N2 * TY * m;
         v[m] = gload<FLAGS>(in + i);
-        cl[m] = cls[i];
+        cl[m] = by_x ? clx : (int)gload_u8<FLAGS>(cls + i);
       }
       cd edge = make_cd(0.0, 0.0);
       {
         const bool left = l32 < 16;
         int xe = left ? x - l32 - 1 : x - l32 + 32;
         xe = xe < 0 ? 0 : (xe > TN - 1 ? TN - 1 : xe);
-        if ((left && hm) || (!left && hp)) edge = gload<0>(in + p0 + (i64)TN * N2 * TY * (l32 & 15) + xe);
+        if ((left && hm) || (!left && hp)) edge = gload<FLAGS>(in + p0 + (i64)TN * N2 * TY * (l32 & 15) + xe);
       }
       __builtin_amdgcn_sched_barrier(0);
       cd* const el = pre_edge_l + 64 * wv;
       el[threadIdx.x & 63] = edge;
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS writes are done
       __builtin_amdgcn_wave_barrier();
+      // an absent diagonal has a zero coefficient in the dense table: fma(0, b, acc) = acc, so the
+      // sum is the same as k_dia_spmv's, which skips it (finite b)
+      const auto coefs = [&](int c, cd* t) {
+        t[0] = pre_tab_l[3 * c];
+        t[1] = pre_tab_l[3 * c + 1];
+        t[2] = pre_tab_l[3 * c + 2];
+      };
+      cd tx[3];
+      if (by_x) coefs(clx, tx);
 #pragma unroll
       for (int m = 0; m < PTS; ++m) {
-        cd bm = make_cd(0.0, 0.0), bp = make_cd(0.0, 0.0);
-        if (hm) {
-          bm = dpp_c<DPP_WAVE_SHR1>(v[m]);
-          if (l32 == 0) bm = el[32 * ty + m];
+        cd t[3];
+        if (by_x) {
+          t[0] = tx[0], t[1] = tx[1], t[2] = tx[2];
+        } else {
+          coefs(cl[m], t);
         }
-        if (hp) {
-          bp = dpp_c<DPP_WAVE_SHL1>(v[m]);
-          if (l32 == 31) bp = el[32 * ty + 16 + m];
-        }
-        const unsigned mk = pre_mk_l[cl[m]];
-        const cd* t = pre_tab_l + 3 * cl[m];
         // the same fma sequence, in the same diagonal order, as k_dia_spmv: bit-identical to
         // MatMult on the row-class form
         double ax = 0.0, ay = 0.0;
@@ -284,9 +307,17 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
           ax = fma(q.x, b.x, fma(-q.y, b.y, ax));
           ay = fma(q.x, b.y, fma(q.y, b.x, ay));
         };
-        if (mk & 1u) acc(t[0], bm);
-        if (mk & 2u) acc(t[1], v[m]);
-        if (mk & 4u) acc(t[2], bp);
+        if (hm) {
+          cd bm = dpp_c<DPP_WAVE_SHR1>(v[m]);
+          if (l32 == 0) bm = el[32 * ty + m];
+          acc(t[0], bm);
+        }
+        acc(t[1], v[m]);
+        if (hp) {
+          cd bp = dpp_c<DPP_WAVE_SHL1>(v[m]);
+          if (l32 == 31) bp = el[32 * ty + 16 + m];
+          acc(t[2], bp);
+        }
         v[m] = make_cd(ax, ay);
       }
     } else {
@@ -413,7 +444,7 @@ k_tp_rows(const cd* in, cd* out, TPArgs a, int nunits) {
                 for (int m0 = 0; m0 < PTS; m0 += QB) {
                   cd q[QB];
 #pragma unroll
-                  for (int m = 0; m < QB; ++m) q[m] = gload<0>(pv + TR * (m0 + m));
+                  for (int m = 0; m < QB; ++m) q[m] = gload<kPostLoadFlags>(pv + TR * (m0 + m));
 #pragma unroll
                   for (int m = 0; m < QB; ++m) {
                     const cd w = v[m0 + m];

@@ -618,6 +618,7 @@ extern "C" PetscErrorCode applyFFT3DPrecTransportBA(PC pc, PCSide side, Vec x, V
         st.nd = dia.nd;
         st.ncls = dia.ncls;
         st.x_local = xl ? 1 : 0;
+        st.cls_x = dia.cls_x;
         CFPCALL(cfp_plan_apply_ex_fusable(s->plan, &st, 0, &fusable));
       }
       if (fusable) {  // A x inside the apply's first sweep (else MatMult below: the same kernels)

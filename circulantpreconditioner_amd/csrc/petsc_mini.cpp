@@ -1166,6 +1166,7 @@ struct _p_Mat {
   std::vector<unsigned char> h_cls, h_mask;  // host copies of the classes (PetscMiniMatAIJGetDia)
   i64 xloc_len = -1;                         // row length of the cached x-locality test
   bool xloc = false;
+  unsigned char* dia_cls_x = nullptr;        // [xloc_len] when the classes repeat with the row length
   // MatCreateAIJ (r06): entries from MatSetValue(s) wait here until MatAssemblyEnd.  This rank's
   // rows [rstart, rstart + lm); set_*: its own rows' entries, st_*: other ranks' (the stash).
   bool building = false;
@@ -1299,6 +1300,8 @@ static void aij_free_device(Mat M) {
   if (M->dia_cls) hipFree(M->dia_cls);
   if (M->dia_mask) hipFree(M->dia_mask);
   if (M->dia_tab) hipFree(M->dia_tab);
+  if (M->dia_cls_x) hipFree(M->dia_cls_x);
+  M->dia_cls_x = nullptr;
   M->rowptr = M->col = nullptr;
   M->val = M->dia_tab = nullptr;
   M->dia_cls = M->dia_mask = nullptr;
@@ -1388,6 +1391,18 @@ extern "C" PetscErrorCode PetscMiniMatAIJGetDia(Mat A, PetscInt rowlen, PetscBoo
       }
     A->xloc = ok;
     A->xloc_len = rowlen;
+    // classes set by the position in the row alone: keep the first row's on the device
+    bool per = A->m % rowlen == 0;
+    for (i64 r = rowlen; per && r < A->m; ++r) per = cl[r] == cl[r % rowlen];
+    if (A->dia_cls_x) hipFree(A->dia_cls_x);
+    A->dia_cls_x = nullptr;
+    if (per && (hipMalloc(&A->dia_cls_x, (size_t)rowlen) != hipSuccess ||
+                hipMemcpy(A->dia_cls_x, cl, (size_t)rowlen, hipMemcpyHostToDevice) != hipSuccess)) {
+      if (A->dia_cls_x) hipFree(A->dia_cls_x);
+      A->dia_cls_x = nullptr;
+      A->xloc_len = -1;
+      return ERR(PETSC_ERR_MEM, "row-class table");
+    }
   }
   *has = PETSC_TRUE;
   *x_local = A->xloc ? PETSC_TRUE : PETSC_FALSE;
@@ -1397,6 +1412,7 @@ extern "C" PetscErrorCode PetscMiniMatAIJGetDia(Mat A, PetscInt rowlen, PetscBoo
   for (int k = 0; k < 8; ++k) dia->off[k] = k < A->dia_d.nd ? A->dia_d.off[k] : 0;
   dia->nd = A->dia_d.nd;
   dia->ncls = A->dia_d.ncls;
+  dia->cls_x = A->dia_cls_x;
   return PETSC_SUCCESS;
 }
 extern "C" PetscErrorCode MatGetType(Mat A, MatType* t) {

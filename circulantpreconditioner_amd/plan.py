@@ -54,7 +54,8 @@ def _lam6(lam: Sequence) -> ctypes.Array:
 class StencilT(ctypes.Structure):
     """cfp_stencil_t (include/circulant_fft.h): a row-class diagonal operator on device arrays."""
     _fields_ = [("cls", ctypes.c_void_p), ("mask", ctypes.c_void_p), ("tab", ctypes.c_void_p),
-                ("off", ctypes.c_int64 * 8), ("nd", ctypes.c_int), ("ncls", ctypes.c_int), ("x_local", ctypes.c_int)]
+                ("off", ctypes.c_int64 * 8), ("nd", ctypes.c_int), ("ncls", ctypes.c_int), ("x_local", ctypes.c_int),
+                ("cls_x", ctypes.c_void_p)]
 
 
 class ApplyExT(ctypes.Structure):
@@ -154,15 +155,18 @@ class CirculantPlan:
 
     def apply_ex(self, b: torch.Tensor, out: torch.Tensor, stencil=None, dots_with=(), stream=None):
         """The Krylov step around one apply (cfp_plan_apply_ex): x = apply(A b) when `stencil` =
-        (cls, mask, tab, offsets, x_local) on the device (uint8, uint8, complex128 tensors), then
+        (cls, mask, tab, offsets, x_local[, cls_x]) on the device (uint8, uint8, complex128 tensors;
+        cls_x: the [n_x] classes when they depend on x alone), then
         dots[j] = v_j^H x for v_j in `dots_with` (None: x itself).  Returns (dots (complex128
         device tensor or None), fused flag)."""
         ex = ApplyExT()
         keep = []
         if stencil is not None:
-            cls, mask, tab, offs, xl = stencil
+            cls, mask, tab, offs, xl = stencil[:5]
             st = StencilT()
             st.cls, st.mask, st.tab = cls.data_ptr(), mask.data_ptr(), tab.data_ptr()
+            if len(stencil) > 5 and stencil[5] is not None:  # classes by x alone: [n_x] bytes
+                st.cls_x = stencil[5].data_ptr()
             for i, o in enumerate(offs):
                 st.off[i] = int(o)
             st.nd, st.ncls, st.x_local = len(offs), int(mask.numel()), 1 if xl else 0

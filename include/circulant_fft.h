@@ -107,11 +107,14 @@ int cfp_plan_apply_with_diag_host(cfp_plan_t plan, const double *diag_dev, const
  *   as separate kernels around a plain apply (same results up to rounding).  b must not alias x
  *   when pre is given. */
 typedef struct {
-  const unsigned char *cls;  /* [N] device */
-  const unsigned char *mask; /* [ncls] device */
-  const double *tab;         /* [ncls * nd] complex, device */
+  const unsigned char *cls;   /* [N] device */
+  const unsigned char *mask;  /* [ncls] device */
+  const double *tab;          /* [ncls * nd] complex, device */
   int64_t off[8];
   int nd, ncls, x_local;
+  const unsigned char *cls_x; /* optional [n_x] device: cls[r] = cls_x[r mod n_x] for every row
+                               * (classes set by x alone, as an operator coupling along x only);
+                               * the fused P1 then reads one byte per column instead of N */
 } cfp_stencil_t;
 typedef struct {
   const cfp_stencil_t *pre; /* NULL: none */

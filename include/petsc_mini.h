@@ -176,6 +176,7 @@ typedef struct {
   const PetscScalar *tab;
   int64_t off[8];
   int nd, ncls;
+  const unsigned char *cls_x; /* [rowlen] device when cls[r] = cls_x[r mod rowlen] for all rows, else NULL */
 } PetscMiniDia;
 PetscErrorCode PetscMiniMatAIJGetDia(Mat A, PetscInt rowlen, PetscBool *has, PetscBool *x_local, PetscMiniDia *dia);
 /* the ncclComm_t behind an RCCL communicator (NULL for a callback communicator) */
