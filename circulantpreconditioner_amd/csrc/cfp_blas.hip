@@ -284,7 +284,8 @@ __device__ __forceinline__ cd dcoef(const double* dots, double sc, int j, cd) {
 __device__ __forceinline__ double dcoef(const double* dots, double sc, int j, double) { return sc * dots[2 * j]; }
 template <class T>
 __global__ void __launch_bounds__(BLAS_THREADS) k_maxpy_dc(T* y, int k, MVCoefT<double> scale, const double* dots,
-                                                            MVPtrsT<T> xs, i64 n, double* partial) {
+                                                            MVPtrsT<T> xs, i64 n, double* partial, double* dots_out) {
+  if (blockIdx.x == 0 && threadIdx.x < 2 * k) dots_out[threadIdx.x] = dots[threadIdx.x];  // for the host
   double s2 = 0.0;
   GRID_LOOP(i, n) {
     T acc = y[i];
@@ -495,15 +496,22 @@ hipError_t blas_dia_spmv(i64 m, const DiaDesc& d, const unsigned char* cls, cons
   return dia_t(m, d, cls, masks, tab, x, y, s);
 }
 
-// per-thread device + pinned staging of block partial sums (synchronous reductions)
+// per-thread device + pinned staging of block partial sums (synchronous reductions).  hd is the
+// device address of the pinned host buffer h (coherent, mapped): a kernel whose results only the
+// host reads writes them there directly, with vector stores, and the host reads them after the
+// stream sync -- no device-to-host copy (each one a copy kernel of ~4-5 us on the device, several
+// per GMRES iteration).
 struct Partials {
   double* d = nullptr;
   double* h = nullptr;
+  double* hd = nullptr;
   hipError_t get(size_t count) {
     if (d) return hipSuccess;
     hipError_t e = hipMalloc(&d, sizeof(double) * count);
     if (e != hipSuccess) return e;
-    return hipHostMalloc(&h, sizeof(double) * count);
+    e = hipHostMalloc(&h, sizeof(double) * count, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) return e;
+    return hipHostGetDevicePointer((void**)&hd, h, 0);
   }
 };
 
@@ -525,10 +533,10 @@ static hipError_t maxpy_t(T* y, int k, const T* a, const T* const* xs, i64 n, bo
       for (int j = 0; j < kk; ++j) { c.a[j] = a[j0 + j]; p.p[j] = xs[j0 + j]; }
       const bool ow = overwrite && j0 == 0, nrm = norm2 && j0 + MV_MAX >= k;
       const dim3 g(nb), blk(BLAS_THREADS);
-      if (ow && nrm) blaunch(2, (k_maxpy<T, true, true>), g, blk, 0, s, y, kk, c, p, n, part.d);
-      else if (ow) blaunch(2, (k_maxpy<T, true, false>), g, blk, 0, s, y, kk, c, p, n, part.d);
-      else if (nrm) blaunch(2, (k_maxpy<T, false, true>), g, blk, 0, s, y, kk, c, p, n, part.d);
-      else blaunch(2, (k_maxpy<T, false, false>), g, blk, 0, s, y, kk, c, p, n, part.d);
+      if (ow && nrm) blaunch(2, (k_maxpy<T, true, true>), g, blk, 0, s, y, kk, c, p, n, part.hd);
+      else if (ow) blaunch(2, (k_maxpy<T, true, false>), g, blk, 0, s, y, kk, c, p, n, part.hd);
+      else if (nrm) blaunch(2, (k_maxpy<T, false, true>), g, blk, 0, s, y, kk, c, p, n, part.hd);
+      else blaunch(2, (k_maxpy<T, false, false>), g, blk, 0, s, y, kk, c, p, n, part.hd);
     }
   }
   hipError_t e = hipGetLastError();
@@ -537,9 +545,7 @@ static hipError_t maxpy_t(T* y, int k, const T* a, const T* const* xs, i64 n, bo
     *norm2 = 0.0;
     return hipSuccess;
   }
-  e = kprof_copy(part.h, part.d, sizeof(double) * nb, hipMemcpyDeviceToHost, s);
-  if (e != hipSuccess) return e;
-  e = hipStreamSynchronize(s);
+  e = hipStreamSynchronize(s);  // the partials are in pinned host memory
   if (e != hipSuccess) return e;
   double t = 0.0;
   for (unsigned q = 0; q < nb; ++q) t += part.h[q];
@@ -569,10 +575,8 @@ static hipError_t reduce(const T* x, const T* y, i64 n, int kind, double out[2],
   if (e != hipSuccess) return e;
   unsigned nb = nblocks(n);
   if (nb > RED_BLOCKS) nb = RED_BLOCKS;
-  blaunch(2, k_reduce<T>, dim3(nb), dim3(BLAS_THREADS), 0, s, x, y, n, kind, part.d);
-  e = kprof_copy(part.h, part.d, sizeof(double) * 2 * nb, hipMemcpyDeviceToHost, s);
-  if (e != hipSuccess) return e;
-  e = hipStreamSynchronize(s);
+  blaunch(2, k_reduce<T>, dim3(nb), dim3(BLAS_THREADS), 0, s, x, y, n, kind, part.hd);
+  e = hipStreamSynchronize(s);  // the partials are in pinned host memory
   if (e != hipSuccess) return e;
   double a = 0.0, b = 0.0;
   for (unsigned k = 0; k < nb; ++k) {
@@ -690,11 +694,9 @@ static hipError_t maxpy_dc_norm_t(T* w, int k, const T* const* ys, const double*
   for (int j = 0; j < k; ++j) { sc.a[j] = scale[j]; p.p[j] = ys[j]; }
   unsigned mb = nblocks(n);
   if (mb > MAXPY_BLOCKS) mb = MAXPY_BLOCKS;
-  blaunch(2, k_maxpy_dc<T>, dim3(mb), dim3(BLAS_THREADS), 0, s, w, k, sc, dd, p, n, part.d + dlen);
+  // the norm partials and (block 0) the dots straight into pinned host memory
+  blaunch(2, k_maxpy_dc<T>, dim3(mb), dim3(BLAS_THREADS), 0, s, w, k, sc, dd, p, n, part.hd + dlen, part.hd);
   e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  e = kprof_copy(part.h, dd, sizeof(double) * 2 * (size_t)k, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = kprof_copy(part.h + dlen, part.d + dlen, sizeof(double) * mb, hipMemcpyDeviceToHost, s);
   if (e != hipSuccess) return e;
   e = hipStreamSynchronize(s);
   if (e != hipSuccess) return e;

@@ -71,6 +71,7 @@ struct _p_KSP {
   // the dots a shell PC computes inside its apply (PCMiniApplyDots, r06): device results, and
   // whether the basis lives on the device (requests are made only then)
   double* dots_dev = nullptr;
+  double *norm_h = nullptr, *norm_hd = nullptr;  // |r|^2 from the apply: pinned host memory (mapped)
   bool dev_basis = false;
   bool fusion = true;  // KSPMiniSetFusion
   PetscInt fused_dots = 0, fused_norms = 0;  // how many Gram-Schmidt dots / norms came from the PC
@@ -91,7 +92,9 @@ static void free_events(KSP k) {
 
 static void free_work(KSP k) {
   if (k->dots_dev) hipFree(k->dots_dev);
+  if (k->norm_h) hipHostFree(k->norm_h);
   k->dots_dev = nullptr;
+  k->norm_h = k->norm_hd = nullptr;
   k->dev_basis = false;
   if (k->V) VecDestroyVecs(k->nvec, &k->V);
   VecDestroy(&k->t);
@@ -216,7 +219,10 @@ extern "C" PetscErrorCode KSPMiniSetUpWork(KSP k, Vec v) {
     PetscCall(VecGetComm(v, &comm));
     MPI_Comm_size(comm, &P);
     k->dev_basis = P == 1 && std::strcmp(vt, VECSEQHIP) == 0 &&
-                   hipMalloc(&k->dots_dev, sizeof(double) * 16) == hipSuccess;
+                   hipMalloc(&k->dots_dev, sizeof(double) * 16) == hipSuccess &&
+                   hipHostMalloc(&k->norm_h, sizeof(double) * 16, hipHostMallocMapped | hipHostMallocCoherent) ==
+                       hipSuccess &&
+                   hipHostGetDevicePointer((void**)&k->norm_hd, k->norm_h, 0) == hipSuccess;
     if (!k->dev_basis) hipGetLastError();
 #endif
   }
@@ -319,15 +325,14 @@ static PetscErrorCode residual(KSP k, Vec b, Vec x, bool x_zero, Vec z, PetscRea
     asked = k->fusion && k->dev_basis && z == k->V[0];
     if (asked) {
       req.nv = 1;
-      req.v[0] = nullptr;  // |z|^2
-      req.out = k->dots_dev;
+      req.v[0] = nullptr;  // |z|^2, written straight into pinned host memory
+      req.out = k->norm_hd;
     }
     PetscCall(pc_apply(k, r, z, asked ? &req : nullptr));
   }
   if (asked && req.done) {
-    double s2[2];
-    PetscCall(PetscMiniDeviceRead(k->dots_dev, 2, s2));
-    *norm = std::sqrt(s2[0]);
+    PetscCall(VecMiniSynchronize(z));
+    *norm = std::sqrt(k->norm_h[0]);
     k->fused_norms += 1;
   } else {
     PetscCall(VecNorm(z, NORM_2, norm));
