@@ -83,7 +83,7 @@ class WaveResult(ctypes.Structure):
                 ("last_reason", ctypes.c_int), ("all_converged", ctypes.c_int), ("last_residual", ctypes.c_double),
                 ("last_norm_dU", ctypes.c_double), ("solve_seconds", ctypes.c_double),
                 ("pc_seconds", ctypes.c_double), ("pc_calls", ctypes.c_int64), ("setup_seconds", ctypes.c_double),
-                ("kappa", ctypes.c_double * 3)]
+                ("kappa", ctypes.c_double * 3), ("rstart", ctypes.c_int64), ("nlocal", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if k != "kappa"}

@@ -13,11 +13,15 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/circulant_fft.h"
+#include "../../include/circulant_fft_dist.h"
 #include "../../include/transport_equation.h"
 #include "../../include/wave_system.h"
+#include "cfp_fft_device.h"
 #include "pcshell_common.h"
 
 using namespace cfp_pc;
@@ -160,6 +164,34 @@ extern "C" PetscErrorCode computeDivergenceMatrixWaveCartesianDim(PetscInt nx, P
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
+// the same on a communicator (MatCreateAIJ on PETSC_COMM_WORLD as the reference's MPI wave driver,
+// tests/WaveSystem_SphericalExplosion_impl_mpi.cxx:83-85): every rank sets its own rows
+extern "C" PetscErrorCode computeDivergenceMatrixWaveCartesianAIJ(MPI_Comm comm, PetscInt nx, PetscInt ny, PetscInt nz,
+                                                                  PetscInt dim, const PetscReal h[3], PetscReal dt,
+                                                                  PetscReal c0, PetscInt bc, Mat* A) {
+  PetscFunctionBeginUser;
+  PetscCheck(A && h, PETSC_COMM_SELF, PETSC_ERR_ARG_NULL, "computeDivergenceMatrixWaveCartesianAIJ: NULL argument");
+  PetscCheck(dim >= 1 && dim <= 3, PETSC_COMM_SELF, PETSC_ERR_ARG_OUTOFRANGE, "Dimension should be 1, 2 or 3");
+  const int C = (int)dim + 1;
+  const int64_t M = C * nx * ny * nz;
+  const int64_t room = (int64_t)C * C * (2 * dim + 1);
+  std::vector<int64_t> rowptr((size_t)M + 1), col((size_t)(nx * ny * nz * room));
+  std::vector<PetscScalar> val((size_t)(nx * ny * nz * room));
+  int64_t nnz = 0;
+  const int rc = cfp_wave_csr_dim(nx, ny, nz, (int)dim, h, dt, c0, (int)bc, 0.0, rowptr.data(), col.data(),
+                                  reinterpret_cast<double*>(val.data()), &nnz);
+  PetscCheck(rc == CFP_SUCCESS, PETSC_COMM_SELF, rc, "computeDivergenceMatrixWaveCartesianAIJ: bad arguments");
+  PetscCall(MatCreateAIJ(comm, PETSC_DECIDE, PETSC_DECIDE, M, M, (PetscInt)room, NULL, (PetscInt)room, NULL, A));
+  PetscInt lo, hi;
+  PetscCall(MatGetOwnershipRange(*A, &lo, &hi));
+  for (PetscInt r = lo; r < hi; ++r)
+    PetscCall(MatSetValues(*A, 1, &r, rowptr[(size_t)r + 1] - rowptr[(size_t)r], col.data() + rowptr[(size_t)r],
+                           val.data() + rowptr[(size_t)r], ADD_VALUES));
+  PetscCall(MatAssemblyBegin(*A, MAT_FINAL_ASSEMBLY));
+  PetscCall(MatAssemblyEnd(*A, MAT_FINAL_ASSEMBLY));
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
 extern "C" PetscErrorCode computeDivergenceMatrixWaveCartesian(PetscInt nx, PetscInt ny, PetscInt nz,
                                                                const PetscReal h[3], PetscReal dt, PetscReal c0,
                                                                PetscInt bc, Mat* A) {
@@ -170,35 +202,181 @@ extern "C" PetscErrorCode initial_conditions_shock_wave(PetscInt nx, PetscInt ny
                                                         const PetscReal xmax[3], Vec U) {
   PetscFunctionBeginUser;
   PetscCheck(xmin && xmax, PETSC_COMM_SELF, PETSC_ERR_ARG_NULL, "NULL domain bounds");
-  PetscInt n;
+  PetscInt n, ng, lo;
+  PetscCall(VecGetSize(U, &ng));
   PetscCall(VecGetLocalSize(U, &n));
+  PetscCall(VecGetOwnershipRange(U, &lo, NULL));
   const PetscInt N = nx * ny * nz;
-  PetscCheck(N >= 1 && n % N == 0 && n / N >= 2 && n / N <= kC, PETSC_COMM_SELF, PETSC_ERR_ARG_SIZ,
+  PetscCheck(N >= 1 && ng % N == 0 && ng / N >= 2 && ng / N <= kC, PETSC_COMM_SELF, PETSC_ERR_ARG_SIZ,
              "U size is not (dim+1)*nx*ny*nz with dim = 1, 2 or 3");
-  const int C = (int)(n / N), dim = C - 1;  // nbComp = dim + 1
+  const int C = (int)(ng / N), dim = C - 1;  // nbComp = dim + 1
+  PetscCheck(lo % C == 0 && n % C == 0, PETSC_COMM_SELF, PETSC_ERR_ARG_SIZ, "a rank's rows must hold whole cells");
   const double hx = (xmax[0] - xmin[0]) / (double)nx, hy = (xmax[1] - xmin[1]) / (double)ny,
                hz = (xmax[2] - xmin[2]) / (double)nz;
   const double cx = (xmin[0] + xmax[0]) / 2, cy = (xmin[1] + xmax[1]) / 2, cz = (xmin[2] + xmax[2]) / 2;
   PetscScalar* u;
   PetscCall(VecGetArrayWrite(U, &u));
-  for (PetscInt k = 0; k < nz; ++k)
-    for (PetscInt j = 0; j < ny; ++j)
-      for (PetscInt i = 0; i < nx; ++i) {
-        const double x = xmin[0] + (i + 0.5) * hx, y = xmin[1] + (j + 0.5) * hy, z = xmin[2] + (k + 0.5) * hz;
-        // src/WaveSystem.cxx:48-61: y enters r for dim > 1, z for dim == 3 (a single cell
-        // layer's centre is the domain centre, so a 3-D grid with n = 1 adds 0)
-        double r2 = (x - cx) * (x - cx);
-        if (dim > 1 && ny > 1) r2 += (y - cy) * (y - cy);
-        if (dim == 3 && nz > 1) r2 += (z - cz) * (z - cz);
-        const int64_t c = C * (i + nx * (j + ny * k));
-        u[c] = std::sqrt(r2) < 0.3 ? 155e5 : 70e5;
-        for (int d = 1; d < C; ++d) u[c + d] = 0.0;  // rho0 * velocity, velocity = 0
-      }
+  for (PetscInt cell = lo / C; cell < (lo + n) / C; ++cell) {  // this rank's cells
+    const PetscInt i = cell % nx, j = (cell / nx) % ny, k = cell / (nx * ny);
+    const double x = xmin[0] + (i + 0.5) * hx, y = xmin[1] + (j + 0.5) * hy, z = xmin[2] + (k + 0.5) * hz;
+    // src/WaveSystem.cxx:48-61: y enters r for dim > 1, z for dim == 3 (a single cell
+    // layer's centre is the domain centre, so a 3-D grid with n = 1 adds 0)
+    double r2 = (x - cx) * (x - cx);
+    if (dim > 1 && ny > 1) r2 += (y - cy) * (y - cy);
+    if (dim == 3 && nz > 1) r2 += (z - cz) * (z - cz);
+    const int64_t c = C * cell - lo;
+    u[c] = std::sqrt(r2) < 0.3 ? 155e5 : 70e5;
+    for (int d = 1; d < C; ++d) u[c + d] = 0.0;  // rho0 * velocity, velocity = 0
+  }
   PetscCall(VecRestoreArrayWrite(U, &u));
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
 // ------------------------------------------------------------------ PCSHELL
+// Several ranks (the reference's MPI wave driver, tests/WaveSystem_SphericalExplosion_impl_mpi.cxx:
+// 63,83-85,130: Vecs of PETSC_DECIDE rows on PETSC_COMM_WORLD, (d+1) N rows, i.e. whole z-planes of
+// cells when P | n_z): the block-circulant inverse on the z-slab plan of pcshell_common.h.  Per
+// apply: the interleaved cells split into d+1 component slabs, each one's distributed 3-D DFT
+// (the slab plan's forward transform, two all-to-alls through the communicator), the 4x4 solve
+// per frequency on the local slab of the spectrum (global kz from the rank's first plane), each
+// component's backward transform, and the components interleaved again x 1/N.
+struct WaveDist {
+  SlabBacking slab;
+  int64_t nloc = 0, z0 = 0;  // local cells, first global z-plane
+  cfp::cd* buf = nullptr;    // 2 x 4 component slabs of nloc values
+  double2* tab = nullptr;    // (p, q) per axis: [n_x | n_y | n_z]
+  double c0sq = 0.0;
+};
+std::mutex g_wave_mu;
+std::unordered_map<const void*, WaveDist*> g_wave_dist;
+
+WaveDist* wave_dist(const FFTPrecWaveContext* ctx) {
+  std::lock_guard<std::mutex> g(g_wave_mu);
+  auto it = g_wave_dist.find(ctx);
+  return it == g_wave_dist.end() ? nullptr : it->second;
+}
+void wave_dist_free(const FFTPrecWaveContext* ctx) {
+  WaveDist* w = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_wave_mu);
+    auto it = g_wave_dist.find(ctx);
+    if (it == g_wave_dist.end()) return;
+    w = it->second;
+    g_wave_dist.erase(it);
+  }
+  slab_destroy(&w->slab);
+  if (w->buf) hipFree(w->buf);
+  if (w->tab) hipFree(w->tab);
+  delete w;
+}
+
+__global__ void k_wave_split(const cfp::cd* b, cfp::cd* u, int64_t n) {  // u[c n + i] = b[4 i + c]
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) u[c * n + i] = b[4 * i + c];
+}
+__global__ void k_wave_join(const cfp::cd* u, cfp::cd* x, int64_t n, double sc) {  // x[4 i + c] = sc u[c n + i]
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[4 * i + c] = cfp::make_cd(sc * u[c * n + i].x, sc * u[c * n + i].y);
+}
+// v <- S(k)^-1 v on the local slab of the spectrum (natural layout, kz = z0 + local plane)
+__global__ void k_wave_slab_solve(cfp::cd* v, int64_t n, int64_t nx, int64_t ny, int64_t nz, int64_t z0,
+                                  const double2* tab, double c0sq) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t kx = i % nx, ky = (i / nx) % ny, kz = z0 + i / (nx * ny);
+    const double2 pq[3] = {tab[kx], tab[nx + ky], tab[nx + ny + kz]};
+    cfp::cd r[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) r[c] = v[c * n + i];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c * n + i] = cfp::wave_solve(r, c, pq, c0sq);
+  }
+}
+unsigned grid_for(int64_t n) {
+  int64_t g = (n + 255) / 256;
+  return (unsigned)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+}
+
+PetscErrorCode wave_dist_setup(FFTPrecWaveContext* ctx, int P, int dev) {
+  const int dim = ctx->dim ? (int)ctx->dim : 3;
+  PetscCheck(dim == 3 && ctx->n_z % P == 0, PETSC_COMM_SELF, PETSC_ERR_SUP,
+             "setupFFTPrec3DWave on several ranks: a 3-D grid with the rank count dividing n_z");
+  int rank = 0;
+  PetscCallMPI(MPI_Comm_rank(PETSC_COMM_WORLD, &rank));
+  wave_dist_free(ctx);
+  WaveDist* w = new WaveDist;
+  const PetscInt dims[3] = {ctx->n_x, ctx->n_y, ctx->n_z};
+  PetscErrorCode e = slab_create(PETSC_COMM_WORLD, P, rank, dims, dev, &w->slab);
+  int64_t lay[8] = {0};
+  if (!e) e = cfp_err(cfp_slab_layout(ctx->n_x, ctx->n_y, ctx->n_z, P, rank, lay), "setupFFTPrec3DWave");
+  w->nloc = lay[4];
+  w->z0 = lay[2];
+  // the symbol's per-axis (p, q) = (kappa c0 (1 - cos theta), kappa sin theta), as cfp_wave_plan_set_symbol
+  const int64_t n3[3] = {ctx->n_x, ctx->n_y, ctx->n_z};
+  const double kap[3] = {ctx->kappa_x, ctx->kappa_y, ctx->kappa_z};
+  std::vector<double2> t;
+  for (int a = 0; a < 3; ++a)
+    for (int64_t k = 0; k < n3[a]; ++k) {
+      const long double th = 2.0L * 3.14159265358979323846264338327950288L * (long double)k / (long double)n3[a];
+      t.push_back(make_double2((double)((long double)kap[a] * ctx->c0 * (1.0L - cosl(th))),
+                               (double)((long double)kap[a] * sinl(th))));
+    }
+  if (!e && (hipMalloc(&w->tab, sizeof(double2) * t.size()) != hipSuccess ||
+             hipMemcpy(w->tab, t.data(), sizeof(double2) * t.size(), hipMemcpyHostToDevice) != hipSuccess ||
+             hipMalloc(&w->buf, sizeof(cfp::cd) * 8 * (size_t)(w->nloc > 0 ? w->nloc : 1)) != hipSuccess))
+    e = PetscErrorSet(PETSC_ERR_MEM, "setupFFTPrec3DWave", "slab buffers");
+  w->c0sq = ctx->c0 * ctx->c0;
+  if (e) {
+    slab_destroy(&w->slab);
+    if (w->tab) hipFree(w->tab);
+    if (w->buf) hipFree(w->buf);
+    delete w;
+    return e;
+  }
+  std::lock_guard<std::mutex> g(g_wave_mu);
+  g_wave_dist[ctx] = w;
+  return PETSC_SUCCESS;
+}
+
+PetscErrorCode wave_dist_apply(FFTPrecWaveContext* ctx, WaveDist* w, Vec b, Vec x) {
+  const int64_t n = w->nloc, M = 4 * n;
+  PetscCall(check_size(b, M, "applyFFT3DPrecWave: b has the wrong size for this rank's slab"));
+  PetscCall(check_size(x, M, "applyFFT3DPrecWave: x has the wrong size for this rank's slab"));
+  DevIn in;
+  DevOut out;
+  PetscCall(in.get(b, M));
+  PetscCall(out.get(x, M));
+  void* vst = nullptr;
+  bool wait = true;
+  device_stream(&vst, &wait);
+  hipStream_t st = (hipStream_t)vst;
+  cfp::cd *u = w->buf, *v = w->buf + 4 * n;
+  const unsigned g = grid_for(n);
+  int rc = CFP_SUCCESS;
+  hipLaunchKernelGGL(k_wave_split, dim3(g), dim3(256), 0, st, (const cfp::cd*)in.ptr(), u, n);
+  if (hipGetLastError() != hipSuccess) rc = CFP_ERR_LIB;
+  for (int c = 0; c < 4 && !rc; ++c)
+    rc = cfp_dist_plan_forward(w->slab.plan, (const double*)(u + c * n), (double*)(v + c * n), vst);
+  if (!rc) {
+    hipLaunchKernelGGL(k_wave_slab_solve, dim3(g), dim3(256), 0, st, v, n, (int64_t)ctx->n_x, (int64_t)ctx->n_y,
+                       (int64_t)ctx->n_z, (int64_t)w->z0, (const double2*)w->tab, w->c0sq);
+    if (hipGetLastError() != hipSuccess) rc = CFP_ERR_LIB;
+  }
+  for (int c = 0; c < 4 && !rc; ++c)
+    rc = cfp_dist_plan_backward(w->slab.plan, (const double*)(v + c * n), (double*)(u + c * n), vst);
+  if (!rc) {
+    const double sc = 1.0 / (double)(ctx->n_x * ctx->n_y * ctx->n_z);
+    hipLaunchKernelGGL(k_wave_join, dim3(g), dim3(256), 0, st, (const cfp::cd*)u, (cfp::cd*)out.ptr(), n, sc);
+    if (hipGetLastError() != hipSuccess) rc = CFP_ERR_LIB;
+  }
+  if (!rc) rc = cfp_stream_sync(vst);  // the slab applies are host-driven: complete on return
+  PetscCall(out.put());
+  PetscCall(in.put());
+  CFPCALL(rc);
+  return PETSC_SUCCESS;
+}
+
 extern "C" PetscErrorCode setupFFTPrec3DWave(PC pc) {
   PetscFunctionBeginUser;
   FFTPrecWaveContext* ctx = nullptr;
@@ -210,6 +388,12 @@ extern "C" PetscErrorCode setupFFTPrec3DWave(PC pc) {
   PetscCheck(hipGetDevice(&dev) == hipSuccess, PETSC_COMM_SELF, PETSC_ERR_LIB, "no HIP device");
   if (ctx->plan) CFPCALL(cfp_wave_plan_destroy(ctx->plan));
   ctx->plan = nullptr;
+  int P = 1;
+  PetscCallMPI(MPI_Comm_size(PETSC_COMM_WORLD, &P));
+  if (P > 1) {
+    PetscCall(wave_dist_setup(ctx, P, dev));
+    PetscFunctionReturn(PETSC_SUCCESS);
+  }
   const int dim = ctx->dim ? (int)ctx->dim : 3;
   CFPCALL(cfp_wave_plan_create_dim(&ctx->plan, ctx->n_x, ctx->n_y, ctx->n_z, dim, dev));
   const double kappa[3] = {ctx->kappa_x, ctx->kappa_y, ctx->kappa_z};
@@ -221,6 +405,10 @@ extern "C" PetscErrorCode applyFFT3DPrecWave(PC pc, Vec b, Vec x) {
   PetscFunctionBeginUser;
   FFTPrecWaveContext* ctx = nullptr;
   PetscCall(PCShellGetContext(pc, &ctx));
+  if (WaveDist* w = ctx ? wave_dist(ctx) : nullptr) {  // several ranks: the slab-backed apply
+    PetscCall(wave_dist_apply(ctx, w, b, x));
+    PetscFunctionReturn(PETSC_SUCCESS);
+  }
   PetscCheck(ctx && ctx->plan, PETSC_COMM_SELF, PETSC_ERR_ARG_WRONGSTATE, "applyFFT3DPrecWave: setup has not run");
   const PetscInt M = ((ctx->dim ? ctx->dim : 3) + 1) * ctx->n_x * ctx->n_y * ctx->n_z;
   PetscCall(check_size(b, M, "applyFFT3DPrecWave: b has the wrong size"));
@@ -246,6 +434,7 @@ extern "C" PetscErrorCode destroyFFTPrec3DWave(PC pc) {
   PetscFunctionBeginUser;
   FFTPrecWaveContext* ctx = nullptr;
   PetscCall(PCShellGetContext(pc, &ctx));
+  if (ctx) wave_dist_free(ctx);
   if (ctx && ctx->plan) {
     CFPCALL(cfp_wave_plan_destroy(ctx->plan));
     ctx->plan = nullptr;
@@ -303,13 +492,27 @@ extern "C" PetscErrorCode WaveSystemGMRES(const cfp_wave_config* cfg, cfp_wave_r
   res->dt = dt;
   for (int d = 0; d < 3; ++d) res->kappa[d] = d < dim ? dt / h[d] : 0.0;
 
+  // several ranks (PETSC_COMM_WORLD of PetscMiniSetCommWorld): VecCreateMPI / MatCreateAIJ on
+  // PETSC_COMM_WORLD with PETSC_DECIDE rows, as the reference's MPI driver (:63,83-85)
+  int P = 1;
+  PetscCallMPI(MPI_Comm_size(PETSC_COMM_WORLD, &P));
   Vec Un, dUn;
-  if (cfg->on_device) PetscCall(VecCreateSeqHIP(PETSC_COMM_SELF, M, &Un));
+  if (P > 1 && cfg->on_device) PetscCall(VecCreateMPIHIP(PETSC_COMM_WORLD, PETSC_DECIDE, M, &Un));
+  else if (P > 1) PetscCall(VecCreateMPI(PETSC_COMM_WORLD, PETSC_DECIDE, M, &Un));
+  else if (cfg->on_device) PetscCall(VecCreateSeqHIP(PETSC_COMM_SELF, M, &Un));
   else PetscCall(VecCreateSeq(PETSC_COMM_SELF, M, &Un));
   PetscCall(VecDuplicate(Un, &dUn));
   PetscCall(initial_conditions_shock_wave(nx, ny, nz, cfg->xmin, cfg->xmax, Un));
+  PetscInt lo, nloc;
+  PetscCall(VecGetOwnershipRange(Un, &lo, NULL));
+  PetscCall(VecGetLocalSize(Un, &nloc));
+  res->rstart = lo;
+  res->nlocal = nloc;
   Mat A;
-  PetscCall(computeDivergenceMatrixWaveCartesianDim(nx, ny, nz, dim, h, dt, cfg->c0, cfg->bc, &A));
+  if (P > 1)
+    PetscCall(computeDivergenceMatrixWaveCartesianAIJ(PETSC_COMM_WORLD, nx, ny, nz, dim, h, dt, cfg->c0, cfg->bc, &A));
+  else
+    PetscCall(computeDivergenceMatrixWaveCartesianDim(nx, ny, nz, dim, h, dt, cfg->c0, cfg->bc, &A));
   PetscCall(MatShift(A, 1.0));  // :86
 
   KSP ksp;
@@ -386,10 +589,10 @@ extern "C" PetscErrorCode WaveSystemGMRES(const cfp_wave_config* cfg, cfp_wave_r
   }
   res->steps = it;
   res->time = time;
-  if (U_out) {
+  if (U_out) {  // this rank's rows (all of them on one rank)
     const PetscScalar* u;
     PetscCall(VecGetArrayRead(Un, &u));
-    std::memcpy(U_out, (const void*)u, sizeof(double) * 2 * (size_t)M);
+    std::memcpy(U_out, (const void*)u, sizeof(double) * 2 * (size_t)nloc);
     PetscCall(VecRestoreArrayRead(Un, &u));
   }
   PetscCall(KSPDestroy(&ksp));

@@ -413,6 +413,13 @@ class Mat:
             pass
 
 
+class FFTPrecWaveContext(ctypes.Structure):
+    """struct FFTPrecWaveContext (include/wave_system.h)."""
+    _fields_ = [("n_x", ctypes.c_int64), ("n_y", ctypes.c_int64), ("n_z", ctypes.c_int64),
+                ("kappa_x", ctypes.c_double), ("kappa_y", ctypes.c_double), ("kappa_z", ctypes.c_double),
+                ("c0", ctypes.c_double), ("plan", ctypes.c_void_p), ("dim", ctypes.c_int64)]
+
+
 def _fn(name: str) -> int:
     return ctypes.cast(getattr(lib(), name), ctypes.c_void_p).value
 
@@ -440,6 +447,19 @@ class PC:
         PetscCall(lib().PCShellSetApply(self.h, _fn("applyFFT3DPrecTransport")))
         PetscCall(lib().PCShellSetDestroy(self.h, _fn("destroyFFTPrec3D")))
         return self
+
+    @classmethod
+    def wave_shell(cls, ctx: "FFTPrecWaveContext") -> "PC":
+        """PCSHELL with the block-circulant wave callbacks (include/wave_system.h):
+        setupFFTPrec3DWave / applyFFT3DPrecWave / destroyFFTPrec3DWave."""
+        pc = cls()
+        PetscCall(lib().PCSetType(pc.h, b"shell"))
+        pc.ctx = ctx
+        PetscCall(lib().PCShellSetContext(pc.h, ctypes.addressof(ctx)))
+        PetscCall(lib().PCShellSetSetUp(pc.h, _fn("setupFFTPrec3DWave")))
+        PetscCall(lib().PCShellSetApply(pc.h, _fn("applyFFT3DPrecWave")))
+        PetscCall(lib().PCShellSetDestroy(pc.h, _fn("destroyFFTPrec3DWave")))
+        return pc
 
     @classmethod
     def none(cls) -> "PC":

@@ -159,11 +159,14 @@ def config(n: int | Sequence[int] = 32, dim: int = 3, **kw) -> WaveConfig:
 
 
 def run(cfg: WaveConfig, return_field: bool = False):
-    """WaveSystemGMRES: the implicit time loop; result dict (and the final 4N field)."""
+    """WaveSystemGMRES: the implicit time loop; result dict (and the final (dim+1)N field: this
+    rank's rows res['rstart'] .. + res['nlocal'] when PETSC_COMM_WORLD has several ranks)."""
     res = WaveResult()
     m = int(((cfg.dim or 3) + 1) * cfg.nx * cfg.ny * cfg.nz)
     out = np.empty(m, dtype=np.complex128) if return_field else None
     ptr = out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) if out is not None else None
     PetscCall(lib().WaveSystemGMRES(ctypes.byref(cfg), ctypes.byref(res), ptr))
     d = res.as_dict()
+    if out is not None:  # this rank's rows when PETSC_COMM_WORLD has several ranks
+        out = out[:d["nlocal"]].copy()
     return (d, out) if return_field else d

@@ -72,6 +72,10 @@ PetscErrorCode computeDivergenceMatrixWaveCartesian(PetscInt nx, PetscInt ny, Pe
 PetscErrorCode computeDivergenceMatrixWaveCartesianDim(PetscInt nx, PetscInt ny, PetscInt nz, PetscInt dim,
                                                        const PetscReal h[3], PetscReal dt, PetscReal c0, PetscInt bc,
                                                        Mat *A);
+/* the same as a MatCreateAIJ on comm, each rank setting its own PETSC_DECIDE rows */
+PetscErrorCode computeDivergenceMatrixWaveCartesianAIJ(MPI_Comm comm, PetscInt nx, PetscInt ny, PetscInt nz,
+                                                       PetscInt dim, const PetscReal h[3], PetscReal dt, PetscReal c0,
+                                                       PetscInt bc, Mat *A);
 /* pressure 155e5 where |centre - domain centre| < 0.3 else 70e5, momentum 0.  U holds
  * (dim+1)*N values; dim is read from its size (src/WaveSystem.cxx:25-76). */
 PetscErrorCode initial_conditions_shock_wave(PetscInt nx, PetscInt ny, PetscInt nz, const PetscReal xmin[3],
@@ -122,13 +126,18 @@ typedef struct {
   int64_t pc_calls;
   double setup_seconds;
   double kappa[3];
+  int64_t rstart, nlocal; /* this rank's rows of Un (U_out holds nlocal values): 0, (dim+1)N on one rank */
 } cfp_wave_result;
 
 void cfp_wave_config_default(cfp_wave_config *cfg, int64_t n);
 /* the reference main's defaults for a dim-dimensional square / cube of n cells a side
  * (cfl = 1e3 / dim, tests/WaveSystem_SphericalExplosion_impl_seq.cxx:212) */
 void cfp_wave_config_default_dim(cfp_wave_config *cfg, int64_t n, int dim);
-/* U_out: optional (dim+1)N complex (interleaved re,im) final field */
+/* U_out: optional final field, complex (interleaved re,im): this rank's res->nlocal rows from
+ * res->rstart ((dim+1)N on one rank).  With PETSC_COMM_WORLD of several ranks the loop runs on
+ * all of them (VecCreateMPI, MatCreateAIJ, KSP on PETSC_COMM_WORLD as
+ * tests/WaveSystem_SphericalExplosion_impl_mpi.cxx; the block-circulant PCSHELL on the z-slab
+ * plan: 3-D grids with the rank count dividing n_z) */
 PetscErrorCode WaveSystemGMRES(const cfp_wave_config *cfg, cfp_wave_result *res, double *U_out);
 
 #ifdef __cplusplus

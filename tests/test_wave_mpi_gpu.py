@@ -1,0 +1,101 @@
+"""The block-circulant wave preconditioner on several ranks, on the GPU.
+
+The reference's MPI wave driver (tests/WaveSystem_SphericalExplosion_impl_mpi.cxx:63,83-85,130;
+the ctests run it on 2 and 4 ranks, tests/CMakeLists.txt:71-74) holds Un on PETSC_COMM_WORLD with
+PETSC_DECIDE rows of the interleaved (d+1) N unknowns.  Here 2 and 4 processes share cuda:0 over a
+torch.distributed (gloo) communicator:
+- applyFFT3DPrecWave on each rank's slab (the z-slab plan: each component's distributed DFT, the
+  4x4 solve per frequency, the inverse DFTs) against the oracle's block solve, <= 1e-10;
+- WaveSystemGMRES with that PCSHELL (MatCreateAIJ, KSP on PETSC_COMM_WORLD) against the one-rank
+  run: same iteration count, same step.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+C0 = 700.0
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, dims, kappa, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from circulantpreconditioner_amd import petsc as P
+        from circulantpreconditioner_amd import wave as W
+        torch.cuda.set_device(0)
+        comm = P.Comm.torch().set_world()
+        nx, ny, nz = dims
+        M = 4 * nx * ny * nz
+        rng = np.random.default_rng(9)
+        b = rng.standard_normal(M) + 1j * rng.standard_normal(M)
+        ctx = P.FFTPrecWaveContext(nx, ny, nz, kappa[0], kappa[1], kappa[2], C0, None, 3)
+        pc = P.PC.wave_shell(ctx).setup()
+        vb = P.Vec.mpi_hip(M)
+        lo, hi = vb.ownership_range()
+        vb.set_array(b[lo:hi])
+        vx = P.Vec.mpi_hip(M)
+        pc.apply(vb, vx)
+        out = {"range": (lo, hi), "x": vx.array()}
+        pc.destroy()
+        res, U = W.run(W.config(dims, pc="fft", steps=1), return_field=True)
+        out.update(res=res, U=U)
+        P.set_comm_world(P.PETSC_COMM_SELF)
+        comm.destroy()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dims,world", [((32, 32, 32), 2), ((32, 32, 32), 4), ((32, 24, 16), 4)])
+def test_wave_pcshell_and_gmres_on_several_ranks(dims, world):
+    import torch.multiprocessing as mp
+    from circulantpreconditioner_amd import wave as W
+    from oracle import wave as OW
+    kappa = (0.079, 0.05, 0.11)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, dims, kappa, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        parts = dict(q.get(timeout=240) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    nx, ny, nz = dims
+    M = 4 * nx * ny * nz
+    x = np.empty(M, dtype=np.complex128)
+    U = np.empty(M, dtype=np.complex128)
+    for r in range(world):
+        lo, hi = parts[r]["range"]
+        assert (lo, hi) == (r * M // world, (r + 1) * M // world)  # whole z-planes of cells
+        x[lo:hi] = parts[r]["x"]
+        rs, nl = parts[r]["res"]["rstart"], parts[r]["res"]["nlocal"]
+        U[rs:rs + nl] = parts[r]["U"]
+    rng = np.random.default_rng(9)
+    b = rng.standard_normal(M) + 1j * rng.standard_normal(M)
+    xo = OW.block_solve(dims, kappa, b)
+    assert np.linalg.norm(x - xo) <= 1e-10 * np.linalg.norm(xo)
+    r1, U1 = W.run(W.config(dims, pc="fft", steps=1), return_field=True)
+    for r in range(world):
+        assert parts[r]["res"]["total_its"] == r1["total_its"]
+        assert parts[r]["res"]["all_converged"] == r1["all_converged"] == 1
+    assert np.linalg.norm(U - U1) <= 1e-8 * np.linalg.norm(U1)  # reduction order differs by P
