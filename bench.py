@@ -356,6 +356,20 @@ def moved_bytes(passes, N: int) -> int:
     return int(sum(kernel_alg_bytes(p["mode"], N, p["n"]) for p in passes))
 
 
+def copy_rate(dev, nbytes: int = 256 << 20) -> dict:
+    """This box's copy rate in the same run: torch's out-of-place device copy
+    of a 256 MiB buffer, read + write bytes over the HIP-event mean of 50 copies.  The row passes
+    move the same 2 x 268 MB per launch, so frac_of_copy says how far a pass sits from a copy."""
+    import torch
+    a = torch.empty(nbytes // 8, dtype=torch.float64, device=dev)
+    a.fill_(1.0)
+    c = torch.empty_like(a)
+    ms = event_ms(lambda: c.copy_(a), 50, settle_ms=100.0)
+    del a, c
+    return {"GBps": round(2 * nbytes / (ms * 1e-3) / 1e9, 1), "ms": round(ms, 5), "bytes": nbytes,
+            "what": "torch out-of-place copy of 256 MiB, (read + write) / HIP-event mean of 50"}
+
+
 def event_ms(fn, iters: int, settle_ms: float = 150.0) -> float:
     """Mean ms of fn() over iters back-to-back calls (HIP events on the current stream) after
     settle_ms of untimed ones (the clocks ramp between legs, as before the headline's region)."""
@@ -486,6 +500,10 @@ def main() -> int:
                     help="record per-launch events in every n-th timed apply")
     ap.add_argument("--no-live-events", action="store_true",
                     help="time the passes in separate applies instead of inside the timed region")
+    ap.add_argument("--rccl-blocking", action="store_true",
+                    help="N > 1: the library's RCCL communicator uses the blocking protocol "
+                         "(CFP_RCCL_BLOCKING=1: ncclCommInitRank / ncclCommDestroy, no deadline); "
+                         "the line's rccl.mode says which ran")
     ap.add_argument("--deadline", action="append", default=[], metavar="PHASE=SECONDS",
                     help=f"override a phase deadline of the watchdog (phases: {', '.join(DEADLINES)})")
     ap.add_argument("--selftest-cpu", action="store_true",
@@ -499,6 +517,8 @@ def main() -> int:
     if len(grid) != 3:
         raise SystemExit("--grid takes 1 or 3 integers")
     deadlines = parse_deadlines(args.deadline)
+    if args.rccl_blocking:  # before the library loads; self-launched ranks inherit it
+        os.environ["CFP_RCCL_BLOCKING"] = "1"
 
     # N > 1 without a launcher: start the N ranks before anything touches the GPU; a run never
     # silently measures a different GPU count than --gpus asks for
@@ -703,6 +723,11 @@ def main() -> int:
                 "timing": timing_src}
         if tsrc:
             roof["traffic_source"] = tsrc
+        try:
+            cr = copy_rate(dev)
+            roof.update(copy_GBps=cr["GBps"], frac_of_copy=round(achieved / cr["GBps"], 4), copy=cr)
+        except Exception as e:  # report, never fake
+            roof.update(copy_GBps=None, frac_of_copy=None, copy={"error": str(e)})
         b_alg = 208 * N
         ach_apply = b_alg / (ms_per_step * 1e-3) / 1e9
         moved = moved_bytes(passes_info, N)

@@ -108,6 +108,7 @@ def declare(L) -> None:
         "cfp_dist_plan_rccl_info": ([vp, P(c_int), P(c_int), P(c_int), P(ctypes.c_double), ctypes.c_char_p, c_int],
                                     c_int),
         "cfp_rccl_version": ([P(c_int), ctypes.c_char_p, c_int], c_int),
+        "cfp_rccl_blocking": ([P(c_int)], c_int),
         "cfp_dist_plan_destroy": ([vp], c_int),
         "cfp_dist_plan_create_external": ([P(vp), i64, i64, i64, c_int, c_int, c_int], c_int),
         "cfp_dist_plan_work_buffer": ([vp, P(ctypes.c_void_p)], c_int),

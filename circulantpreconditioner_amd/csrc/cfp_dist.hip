@@ -637,6 +637,14 @@ extern "C" int cfp_dist_plan_rccl_info(cfp_dist_plan_t p, int* nranks, int* rank
   return CFP_SUCCESS;
 }
 
+// Host-only: 1 when the library's communicators use the blocking protocol (CFP_RCCL_BLOCKING),
+// 0 for the default non-blocking creation polled against a deadline.
+extern "C" int cfp_rccl_blocking(int* blocking) {
+  if (!blocking) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  *blocking = rccl_blocking() ? 1 : 0;
+  return CFP_SUCCESS;
+}
+
 // Host-only (no GPU, no communicator): the RCCL version and library this process resolved.
 extern "C" int cfp_rccl_version(int* version, char* lib_path, int path_len) {
   if (!version) return set_error(CFP_ERR_ARG_NULL, "NULL argument");

@@ -14,11 +14,26 @@
 
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <thread>
 
 namespace cfp {
 
 constexpr double kRcclDefaultTimeoutS = 300.0;
+
+// CFP_RCCL_BLOCKING=1 in the environment selects the blocking protocol instead: ncclCommInitRank
+// (no deadline: a missing peer hangs, as with any plain RCCL program) and ncclCommDestroy, with
+// every call returning only when it is done.  It is the known-good fallback for a first run
+// between real peers, where the non-blocking group end and the polled finalize have not run
+// before.  Read once per process, so creation and destruction agree.
+inline bool rccl_blocking() {
+  static const bool b = [] {
+    const char* e = std::getenv("CFP_RCCL_BLOCKING");
+    return e && *e && std::strcmp(e, "0") != 0;
+  }();
+  return b;
+}
 
 // Wait until `c` leaves ncclInProgress; `r` is the result of the call just made on it.  A
 // blocking communicator never reports ncclInProgress, so this is a no-op there.  Returns the
@@ -39,9 +54,17 @@ inline ncclResult_t rccl_settle(ncclComm_t c, ncclResult_t r, double deadline_s)
 }
 
 // ncclCommInitRankConfig with blocking = 0, polled against `timeout_s`.  On failure or timeout
-// the half-made communicator is aborted, *comm is NULL and *timed_out says which.
+// the half-made communicator is aborted, *comm is NULL and *timed_out says which.  Under
+// CFP_RCCL_BLOCKING, ncclCommInitRank without a deadline.
 inline ncclResult_t rccl_init_rank(ncclComm_t* comm, int nranks, const ncclUniqueId& id, int rank, double timeout_s,
                                    bool* timed_out) {
+  *comm = nullptr;
+  *timed_out = false;
+  if (rccl_blocking()) {
+    const ncclResult_t nr = ncclCommInitRank(comm, nranks, id, rank);
+    if (nr != ncclSuccess) *comm = nullptr;
+    return nr;
+  }
   ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
   cfg.blocking = 0;
   *comm = nullptr;
@@ -58,9 +81,13 @@ inline ncclResult_t rccl_init_rank(ncclComm_t* comm, int nranks, const ncclUniqu
 }
 
 // Finalize (flush, polled) and destroy; a communicator that does not quiesce within the deadline
-// is aborted instead.
+// is aborted instead.  A blocking communicator (CFP_RCCL_BLOCKING) is destroyed directly.
 inline void rccl_destroy(ncclComm_t c, double timeout_s) {
   if (!c) return;
+  if (rccl_blocking()) {
+    ncclCommDestroy(c);
+    return;
+  }
   ncclResult_t r = ncclCommFinalize(c);
   if (r == ncclSuccess || r == ncclInProgress) r = rccl_settle(c, ncclInProgress, timeout_s);
   if (r == ncclSuccess)

@@ -79,7 +79,15 @@ def rccl_version() -> dict:
     v = ctypes.c_int()
     path = ctypes.create_string_buffer(512)
     check(lib().cfp_rccl_version(ctypes.byref(v), path, 512))
-    return {"version": v.value, "lib": path.value.decode(errors="replace")}
+    return {"version": v.value, "lib": path.value.decode(errors="replace"), "mode": rccl_mode()}
+
+
+def rccl_mode() -> str:
+    """Host-only: 'blocking' when CFP_RCCL_BLOCKING selects ncclCommInitRank / ncclCommDestroy for
+    the library's communicators, else 'non-blocking' (creation polled against a deadline)."""
+    b = ctypes.c_int()
+    check(lib().cfp_rccl_blocking(ctypes.byref(b)))
+    return "blocking" if b.value else "non-blocking"
 
 
 class SlabPlan:
@@ -138,7 +146,7 @@ class SlabPlan:
         check(lib().cfp_dist_plan_rccl_info(self._h, ctypes.byref(n), ctypes.byref(r), ctypes.byref(v),
                                             ctypes.byref(ms), path, 512))
         return {"ranks": n.value, "rank": r.value, "version": v.value, "init_ms": round(ms.value, 1),
-                "lib": path.value.decode(errors="replace")}
+                "lib": path.value.decode(errors="replace"), "mode": rccl_mode()}
 
     @property
     def local_size(self) -> int:

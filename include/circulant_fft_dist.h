@@ -91,7 +91,7 @@ int cfp_dist_unique_id_bytes(void);
 int cfp_dist_get_unique_id(char *id_out);
 
 /* The plan's own communicator is created non-blocking (ncclCommInitRankConfig, blocking = 0) and
- * polled against a deadline: a rank that never joins returns CFP_ERR_LIB ("timed out") instead
+ * polled against a deadline (unless CFP_RCCL_BLOCKING is set, see cfp_rccl_blocking): a rank that never joins returns CFP_ERR_LIB ("timed out") instead
  * of hanging.  cfp_dist_plan_create uses 300 s; _timeout takes the deadline in seconds.  The
  * same deadline bounds each exchange's enqueue and the finalize in cfp_dist_plan_destroy.
  * Replaces FFTW-MPI's plan creation inside MatCreateFFT(PETSC_COMM_WORLD, ...)
@@ -106,6 +106,10 @@ int cfp_dist_plan_create_timeout(cfp_dist_plan_t *plan, int64_t nx, int64_t ny, 
  * NULL; lib_path gets at most path_len bytes). */
 int cfp_dist_plan_rccl_info(cfp_dist_plan_t plan, int *nranks, int *rank, int *version, double *init_ms,
                             char *lib_path, int path_len);
+/* Host-only, no GPU: 1 when CFP_RCCL_BLOCKING (environment, read once per process) selects the
+ * blocking protocol for the library's communicators (ncclCommInitRank with no deadline,
+ * ncclCommDestroy), 0 for the default non-blocking creation polled against the deadline. */
+int cfp_rccl_blocking(int *blocking);
 /* Host-only, no GPU: the RCCL version and library this process resolved. */
 int cfp_rccl_version(int *version, char *lib_path, int path_len);
 /* Same on the caller's RCCL communicator (an ncclComm_t of nranks ranks; it stays the caller's). */

@@ -148,8 +148,11 @@ typedef struct {
   void *user;
 } PetscMiniCommOps;
 PetscErrorCode PetscMiniCommCreate(int size, int rank, const PetscMiniCommOps *ops, MPI_Comm *comm);
-/* an RCCL communicator (ncclCommInitRank on the current HIP device; unique_id = the 128 bytes
- * of cfp_dist_get_unique_id, created on rank 0 and broadcast by the caller) */
+/* an RCCL communicator on the current HIP device (unique_id = the 128 bytes of
+ * cfp_dist_get_unique_id, created on rank 0 and broadcast by the caller).  It is created
+ * NON-BLOCKING (ncclCommInitRankConfig, blocking = 0), polled against a 300 s deadline; a rank
+ * that never joins is an error, not a hang.  CFP_RCCL_BLOCKING=1 in the environment selects
+ * ncclCommInitRank (blocking, no deadline) instead; cfp_rccl_blocking reports which. */
 PetscErrorCode PetscMiniCommCreateRCCL(int size, int rank, const char *unique_id, MPI_Comm *comm);
 /* refused (PETSC_ERR_ARG_WRONGSTATE) while FFT matrices built on the communicator still exist */
 PetscErrorCode PetscMiniCommDestroy(MPI_Comm *comm);
@@ -179,7 +182,11 @@ typedef struct {
   const unsigned char *cls_x; /* [rowlen] device when cls[r] = cls_x[r mod rowlen] for all rows, else NULL */
 } PetscMiniDia;
 PetscErrorCode PetscMiniMatAIJGetDia(Mat A, PetscInt rowlen, PetscBool *has, PetscBool *x_local, PetscMiniDia *dia);
-/* the ncclComm_t behind an RCCL communicator (NULL for a callback communicator) */
+/* the ncclComm_t behind an RCCL communicator (NULL for a callback communicator).  Unless
+ * CFP_RCCL_BLOCKING is set it is a non-blocking communicator: an RCCL call the caller makes on it
+ * (ncclGroupEnd, a collective, ncclCommFinalize) may return ncclInProgress, and the caller must
+ * poll ncclCommGetAsyncError until the state leaves ncclInProgress before relying on it.  The
+ * communicator stays the library's: do not destroy it. */
 PetscErrorCode PetscMiniCommGetNCCL(MPI_Comm comm, void **nccl_comm);
 /* One exchange piece of a slab plan over a communicator (the cfp_dist_exchange_fn contract of
  * include/circulant_fft_dist.h; user = (void *)(intptr_t)comm): device buffers, staged through

@@ -236,3 +236,17 @@ def test_rccl_library_is_reported_host_only():
     from circulantpreconditioner_amd.distributed import rccl_version
     v = rccl_version()
     assert v["version"] >= 21400 and "rccl" in v["lib"]
+
+
+def test_rccl_blocking_switch_is_reported():
+    """CFP_RCCL_BLOCKING=1 (bench.py --rccl-blocking) selects the blocking RCCL protocol
+    for the library's communicators, read once per process; rccl_version() / rccl_info() say which."""
+    code = "from circulantpreconditioner_amd.distributed import rccl_mode; print(rccl_mode())"
+    for env, want in (({"CFP_RCCL_BLOCKING": "1"}, "blocking"), ({"CFP_RCCL_BLOCKING": "0"}, "non-blocking"),
+                      ({}, "non-blocking")):
+        e = {k: v for k, v in os.environ.items() if k != "CFP_RCCL_BLOCKING"}
+        e.update(env)
+        out = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True, timeout=120,
+                             cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        assert out.returncode == 0, out.stderr
+        assert out.stdout.strip() == want

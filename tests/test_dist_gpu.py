@@ -6,7 +6,9 @@
 * SlabPlan runs in fresh child processes, one per rank, sharing cuda:0: each rank runs the
   library's kernel segments and the two all-to-alls go through torch.distributed (gloo,
   staged through host memory), so the per-rank plan is exercised across processes.
-* The RCCL executor with world = 1; with more ranks it is exercised by bench.py --gpus N.
+* The RCCL executor with world = 1 only.  With more ranks it runs only in the driver's
+  multi-GPU bench (bench.py --gpus N on an 8-GPU node); this suite never starts it.  The
+  per-rank plan it drives is the one the gloo multi-process tests check.
 * At 256^3 and 512^3 (AUTO for every P | 32 up to 16 since r05)
   every rank runs the 3-sweep schedule (x + y1 into the per-peer chunks | y2 + z + symbol +
   inverses on its k1 rows | inverse), checked against the oracle and against the 5-pass slab
