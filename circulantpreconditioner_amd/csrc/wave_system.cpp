@@ -210,13 +210,13 @@ extern "C" PetscErrorCode initial_conditions_shock_wave(PetscInt nx, PetscInt ny
   PetscCheck(N >= 1 && ng % N == 0 && ng / N >= 2 && ng / N <= kC, PETSC_COMM_SELF, PETSC_ERR_ARG_SIZ,
              "U size is not (dim+1)*nx*ny*nz with dim = 1, 2 or 3");
   const int C = (int)(ng / N), dim = C - 1;  // nbComp = dim + 1
-  PetscCheck(lo % C == 0 && n % C == 0, PETSC_COMM_SELF, PETSC_ERR_ARG_SIZ, "a rank's rows must hold whole cells");
   const double hx = (xmax[0] - xmin[0]) / (double)nx, hy = (xmax[1] - xmin[1]) / (double)ny,
                hz = (xmax[2] - xmin[2]) / (double)nz;
   const double cx = (xmin[0] + xmax[0]) / 2, cy = (xmin[1] + xmax[1]) / 2, cz = (xmin[2] + xmax[2]) / 2;
   PetscScalar* u;
   PetscCall(VecGetArrayWrite(U, &u));
-  for (PetscInt cell = lo / C; cell < (lo + n) / C; ++cell) {  // this rank's cells
+  // this rank's rows; PETSC_DECIDE may split a cell's d+1 unknowns between two ranks
+  for (PetscInt cell = lo / C; cell * C < lo + n; ++cell) {
     const PetscInt i = cell % nx, j = (cell / nx) % ny, k = cell / (nx * ny);
     const double x = xmin[0] + (i + 0.5) * hx, y = xmin[1] + (j + 0.5) * hy, z = xmin[2] + (k + 0.5) * hz;
     // src/WaveSystem.cxx:48-61: y enters r for dim > 1, z for dim == 3 (a single cell
@@ -224,9 +224,10 @@ extern "C" PetscErrorCode initial_conditions_shock_wave(PetscInt nx, PetscInt ny
     double r2 = (x - cx) * (x - cx);
     if (dim > 1 && ny > 1) r2 += (y - cy) * (y - cy);
     if (dim == 3 && nz > 1) r2 += (z - cz) * (z - cz);
-    const int64_t c = C * cell - lo;
-    u[c] = std::sqrt(r2) < 0.3 ? 155e5 : 70e5;
-    for (int d = 1; d < C; ++d) u[c + d] = 0.0;  // rho0 * velocity, velocity = 0
+    for (int d = 0; d < C; ++d) {  // pressure, then rho0 * velocity (velocity = 0)
+      const int64_t row = C * cell + d;
+      if (row >= lo && row < lo + n) u[row - lo] = d == 0 ? (std::sqrt(r2) < 0.3 ? 155e5 : 70e5) : 0.0;
+    }
   }
   PetscCall(VecRestoreArrayWrite(U, &u));
   PetscFunctionReturn(PETSC_SUCCESS);
@@ -235,16 +236,20 @@ extern "C" PetscErrorCode initial_conditions_shock_wave(PetscInt nx, PetscInt ny
 // ------------------------------------------------------------------ PCSHELL
 // Several ranks (the reference's MPI wave driver, tests/WaveSystem_SphericalExplosion_impl_mpi.cxx:
 // 63,83-85,130: Vecs of PETSC_DECIDE rows on PETSC_COMM_WORLD, (d+1) N rows, i.e. whole z-planes of
-// cells when P | n_z): the block-circulant inverse on the z-slab plan of pcshell_common.h.  Per
-// apply: the interleaved cells split into d+1 component slabs, each one's distributed 3-D DFT
-// (the slab plan's forward transform, two all-to-alls through the communicator), the 4x4 solve
-// per frequency on the local slab of the spectrum (global kz from the rank's first plane), each
-// component's backward transform, and the components interleaved again x 1/N.
+// cells when P | n_z; whole rows of cells of a 2-D grid when P | n_y): the block-circulant inverse
+// on the z-slab plan of pcshell_common.h.  Per apply: the interleaved cells split into d+1
+// component slabs, each one's distributed DFT (the slab plan's forward transform, two all-to-alls
+// through the communicator), the (d+1)x(d+1) solve per frequency on the local slab of the
+// spectrum (global frequency from the rank's first plane), each component's backward transform,
+// and the components interleaved again x 1/N.  A 2-D grid (n_x, n_y) runs as the plan grid
+// (1, n_x, n_y): the same memory order, its rows split over the ranks.
 struct WaveDist {
   SlabBacking slab;
-  int64_t nloc = 0, z0 = 0;  // local cells, first global z-plane
-  cfp::cd* buf = nullptr;    // 2 x 4 component slabs of nloc values
-  double2* tab = nullptr;    // (p, q) per axis: [n_x | n_y | n_z]
+  int ncomp = 4;               // d + 1 interleaved unknowns per cell
+  int64_t pd[3] = {0, 0, 0};   // the slab plan's grid: (n_x, n_y, n_z), or (1, n_x, n_y) for d = 2
+  int64_t nloc = 0, z0 = 0;    // local cells, first global plane of the plan's slowest axis
+  cfp::cd* buf = nullptr;      // 2 x (d + 1) component slabs of nloc values
+  double2* tab = nullptr;      // (p, q) per physical axis: [n_x | n_y | n_z]
   double c0sq = 0.0;
 };
 std::mutex g_wave_mu;
@@ -270,27 +275,35 @@ void wave_dist_free(const FFTPrecWaveContext* ctx) {
   delete w;
 }
 
-__global__ void k_wave_split(const cfp::cd* b, cfp::cd* u, int64_t n) {  // u[c n + i] = b[4 i + c]
+template <int C>
+__global__ void k_wave_split(const cfp::cd* b, cfp::cd* u, int64_t n) {  // u[c n + i] = b[C i + c]
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) u[c * n + i] = b[4 * i + c];
+    for (int c = 0; c < C; ++c) u[c * n + i] = b[C * i + c];
 }
-__global__ void k_wave_join(const cfp::cd* u, cfp::cd* x, int64_t n, double sc) {  // x[4 i + c] = sc u[c n + i]
+template <int C>
+__global__ void k_wave_join(const cfp::cd* u, cfp::cd* x, int64_t n, double sc) {  // x[C i + c] = sc u[c n + i]
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) x[4 * i + c] = cfp::make_cd(sc * u[c * n + i].x, sc * u[c * n + i].y);
+    for (int c = 0; c < C; ++c) x[C * i + c] = cfp::make_cd(sc * u[c * n + i].x, sc * u[c * n + i].y);
 }
-// v <- S(k)^-1 v on the local slab of the spectrum (natural layout, kz = z0 + local plane)
-__global__ void k_wave_slab_solve(cfp::cd* v, int64_t n, int64_t nx, int64_t ny, int64_t nz, int64_t z0,
-                                  const double2* tab, double c0sq) {
+// v <- S(k)^-1 v on the local slab of the spectrum.  Point i of the slab is (i0, i1, z0 + i2) on
+// the plan's grid pd; its physical frequency is that for d = 3, and (i1, z0 + i2, 0) for d = 2
+// (the 2-D grid runs as the plan grid (1, n_x, n_y), the same memory order).  A 2-D cell has no
+// z velocity: r[3] = 0 and n_z = 1 gives (p, q) = (0, 0) on that axis, so wave_solve's 4x4 algebra
+// reduces to the 3x3 block.
+template <int C>
+__global__ void k_wave_slab_solve(cfp::cd* v, int64_t n, int64_t pd0, int64_t pd1, int64_t z0, int64_t nx,
+                                  int64_t ny, const double2* tab, double c0sq) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t kx = i % nx, ky = (i / nx) % ny, kz = z0 + i / (nx * ny);
+    const int64_t i0 = i % pd0, i1 = (i / pd0) % pd1, i2 = z0 + i / (pd0 * pd1);
+    const int64_t kx = C == 4 ? i0 : i1, ky = C == 4 ? i1 : i2, kz = C == 4 ? i2 : 0;
     const double2 pq[3] = {tab[kx], tab[nx + ky], tab[nx + ny + kz]};
     cfp::cd r[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) r[c] = v[c * n + i];
+    for (int c = 0; c < 4; ++c) r[c] = c < C ? v[c * n + i] : cfp::make_cd(0.0, 0.0);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) v[c * n + i] = cfp::wave_solve(r, c, pq, c0sq);
+    for (int c = 0; c < C; ++c) v[c * n + i] = cfp::wave_solve(r, c, pq, c0sq);
   }
 }
 unsigned grid_for(int64_t n) {
@@ -300,16 +313,26 @@ unsigned grid_for(int64_t n) {
 
 PetscErrorCode wave_dist_setup(FFTPrecWaveContext* ctx, int P, int dev) {
   const int dim = ctx->dim ? (int)ctx->dim : 3;
-  PetscCheck(dim == 3 && ctx->n_z % P == 0, PETSC_COMM_SELF, PETSC_ERR_SUP,
-             "setupFFTPrec3DWave on several ranks: a 3-D grid with the rank count dividing n_z");
+  // PETSC_DECIDE rows are whole planes of cells of the slowest axis when P divides it; the slab
+  // plan splits that axis the same way, so no redistribution is needed
+  PetscCheck((dim == 3 && ctx->n_z % P == 0) || (dim == 2 && ctx->n_z == 1 && ctx->n_y % P == 0), PETSC_COMM_SELF,
+             PETSC_ERR_SUP,
+             "setupFFTPrec3DWave on several ranks: a 3-D grid with the rank count dividing n_z, or a 2-D grid "
+             "with it dividing n_y");
   int rank = 0;
   PetscCallMPI(MPI_Comm_rank(PETSC_COMM_WORLD, &rank));
   wave_dist_free(ctx);
   WaveDist* w = new WaveDist;
-  const PetscInt dims[3] = {ctx->n_x, ctx->n_y, ctx->n_z};
+  w->ncomp = dim + 1;
+  if (dim == 3) {
+    w->pd[0] = ctx->n_x, w->pd[1] = ctx->n_y, w->pd[2] = ctx->n_z;
+  } else {
+    w->pd[0] = 1, w->pd[1] = ctx->n_x, w->pd[2] = ctx->n_y;
+  }
+  const PetscInt dims[3] = {w->pd[0], w->pd[1], w->pd[2]};
   PetscErrorCode e = slab_create(PETSC_COMM_WORLD, P, rank, dims, dev, &w->slab);
   int64_t lay[8] = {0};
-  if (!e) e = cfp_err(cfp_slab_layout(ctx->n_x, ctx->n_y, ctx->n_z, P, rank, lay), "setupFFTPrec3DWave");
+  if (!e) e = cfp_err(cfp_slab_layout(w->pd[0], w->pd[1], w->pd[2], P, rank, lay), "setupFFTPrec3DWave");
   w->nloc = lay[4];
   w->z0 = lay[2];
   // the symbol's per-axis (p, q) = (kappa c0 (1 - cos theta), kappa sin theta), as cfp_wave_plan_set_symbol
@@ -324,7 +347,7 @@ PetscErrorCode wave_dist_setup(FFTPrecWaveContext* ctx, int P, int dev) {
     }
   if (!e && (hipMalloc(&w->tab, sizeof(double2) * t.size()) != hipSuccess ||
              hipMemcpy(w->tab, t.data(), sizeof(double2) * t.size(), hipMemcpyHostToDevice) != hipSuccess ||
-             hipMalloc(&w->buf, sizeof(cfp::cd) * 8 * (size_t)(w->nloc > 0 ? w->nloc : 1)) != hipSuccess))
+             hipMalloc(&w->buf, sizeof(cfp::cd) * 2 * w->ncomp * (size_t)(w->nloc > 0 ? w->nloc : 1)) != hipSuccess))
     e = PetscErrorSet(PETSC_ERR_MEM, "setupFFTPrec3DWave", "slab buffers");
   w->c0sq = ctx->c0 * ctx->c0;
   if (e) {
@@ -339,8 +362,35 @@ PetscErrorCode wave_dist_setup(FFTPrecWaveContext* ctx, int P, int dev) {
   return PETSC_SUCCESS;
 }
 
+template <int C>
+int wave_dist_run(const FFTPrecWaveContext* ctx, const WaveDist* w, const cfp::cd* b, cfp::cd* x, void* vst) {
+  const int64_t n = w->nloc;
+  hipStream_t st = (hipStream_t)vst;
+  cfp::cd *u = w->buf, *v = w->buf + C * n;
+  const unsigned g = grid_for(n);
+  int rc = CFP_SUCCESS;
+  hipLaunchKernelGGL(k_wave_split<C>, dim3(g), dim3(256), 0, st, b, u, n);
+  if (hipGetLastError() != hipSuccess) rc = CFP_ERR_LIB;
+  for (int c = 0; c < C && !rc; ++c)
+    rc = cfp_dist_plan_forward(w->slab.plan, (const double*)(u + c * n), (double*)(v + c * n), vst);
+  if (!rc) {
+    hipLaunchKernelGGL(k_wave_slab_solve<C>, dim3(g), dim3(256), 0, st, v, n, w->pd[0], w->pd[1], w->z0,
+                       (int64_t)ctx->n_x, (int64_t)ctx->n_y, (const double2*)w->tab, w->c0sq);
+    if (hipGetLastError() != hipSuccess) rc = CFP_ERR_LIB;
+  }
+  for (int c = 0; c < C && !rc; ++c)
+    rc = cfp_dist_plan_backward(w->slab.plan, (const double*)(v + c * n), (double*)(u + c * n), vst);
+  if (!rc) {
+    const double sc = 1.0 / (double)(ctx->n_x * ctx->n_y * ctx->n_z);
+    hipLaunchKernelGGL(k_wave_join<C>, dim3(g), dim3(256), 0, st, (const cfp::cd*)u, x, n, sc);
+    if (hipGetLastError() != hipSuccess) rc = CFP_ERR_LIB;
+  }
+  if (!rc) rc = cfp_stream_sync(vst);  // the slab applies are host-driven: complete on return
+  return rc;
+}
+
 PetscErrorCode wave_dist_apply(FFTPrecWaveContext* ctx, WaveDist* w, Vec b, Vec x) {
-  const int64_t n = w->nloc, M = 4 * n;
+  const int64_t M = w->ncomp * w->nloc;
   PetscCall(check_size(b, M, "applyFFT3DPrecWave: b has the wrong size for this rank's slab"));
   PetscCall(check_size(x, M, "applyFFT3DPrecWave: x has the wrong size for this rank's slab"));
   DevIn in;
@@ -350,27 +400,9 @@ PetscErrorCode wave_dist_apply(FFTPrecWaveContext* ctx, WaveDist* w, Vec b, Vec 
   void* vst = nullptr;
   bool wait = true;
   device_stream(&vst, &wait);
-  hipStream_t st = (hipStream_t)vst;
-  cfp::cd *u = w->buf, *v = w->buf + 4 * n;
-  const unsigned g = grid_for(n);
-  int rc = CFP_SUCCESS;
-  hipLaunchKernelGGL(k_wave_split, dim3(g), dim3(256), 0, st, (const cfp::cd*)in.ptr(), u, n);
-  if (hipGetLastError() != hipSuccess) rc = CFP_ERR_LIB;
-  for (int c = 0; c < 4 && !rc; ++c)
-    rc = cfp_dist_plan_forward(w->slab.plan, (const double*)(u + c * n), (double*)(v + c * n), vst);
-  if (!rc) {
-    hipLaunchKernelGGL(k_wave_slab_solve, dim3(g), dim3(256), 0, st, v, n, (int64_t)ctx->n_x, (int64_t)ctx->n_y,
-                       (int64_t)ctx->n_z, (int64_t)w->z0, (const double2*)w->tab, w->c0sq);
-    if (hipGetLastError() != hipSuccess) rc = CFP_ERR_LIB;
-  }
-  for (int c = 0; c < 4 && !rc; ++c)
-    rc = cfp_dist_plan_backward(w->slab.plan, (const double*)(v + c * n), (double*)(u + c * n), vst);
-  if (!rc) {
-    const double sc = 1.0 / (double)(ctx->n_x * ctx->n_y * ctx->n_z);
-    hipLaunchKernelGGL(k_wave_join, dim3(g), dim3(256), 0, st, (const cfp::cd*)u, (cfp::cd*)out.ptr(), n, sc);
-    if (hipGetLastError() != hipSuccess) rc = CFP_ERR_LIB;
-  }
-  if (!rc) rc = cfp_stream_sync(vst);  // the slab applies are host-driven: complete on return
+  const cfp::cd* bp = (const cfp::cd*)in.ptr();
+  cfp::cd* xp = (cfp::cd*)out.ptr();
+  const int rc = w->ncomp == 4 ? wave_dist_run<4>(ctx, w, bp, xp, vst) : wave_dist_run<3>(ctx, w, bp, xp, vst);
   PetscCall(out.put());
   PetscCall(in.put());
   CFPCALL(rc);

@@ -82,7 +82,10 @@ PetscErrorCode initial_conditions_shock_wave(PetscInt nx, PetscInt ny, PetscInt 
                                              const PetscReal xmax[3], Vec U);
 
 /* PCSHELL of the block-circulant preconditioner (new capability; same registration pattern
- * as applyFFT3DPrecTransport: PCShellSetContext(pc, &ctx), SetSetUp/SetApply/SetDestroy) */
+ * as applyFFT3DPrecTransport: PCShellSetContext(pc, &ctx), SetSetUp/SetApply/SetDestroy).
+ * With PETSC_COMM_WORLD of P > 1 ranks, setup builds the z-slab plan instead of `plan` and b / x
+ * are this rank's PETSC_DECIDE rows: a 3-D grid needs P | n_z, a 2-D grid (n_z = 1) P | n_y
+ * (whole planes / rows of cells per rank); other shapes return PETSC_ERR_SUP. */
 struct FFTPrecWaveContext {
   PetscInt n_x, n_y, n_z;
   PetscReal kappa_x, kappa_y, kappa_z; /* dt / h_d */
@@ -137,7 +140,7 @@ void cfp_wave_config_default_dim(cfp_wave_config *cfg, int64_t n, int dim);
  * res->rstart ((dim+1)N on one rank).  With PETSC_COMM_WORLD of several ranks the loop runs on
  * all of them (VecCreateMPI, MatCreateAIJ, KSP on PETSC_COMM_WORLD as
  * tests/WaveSystem_SphericalExplosion_impl_mpi.cxx; the block-circulant PCSHELL on the z-slab
- * plan: 3-D grids with the rank count dividing n_z) */
+ * plan: 3-D grids with the rank count dividing n_z, 2-D grids with it dividing n_y) */
 PetscErrorCode WaveSystemGMRES(const cfp_wave_config *cfg, cfp_wave_result *res, double *U_out);
 
 #ifdef __cplusplus

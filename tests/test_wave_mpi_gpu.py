@@ -5,7 +5,9 @@ the ctests run it on 2 and 4 ranks, tests/CMakeLists.txt:71-74) holds Un on PETS
 PETSC_DECIDE rows of the interleaved (d+1) N unknowns.  Here 2 and 4 processes share cuda:0 over a
 torch.distributed (gloo) communicator:
 - applyFFT3DPrecWave on each rank's slab (the z-slab plan: each component's distributed DFT, the
-  4x4 solve per frequency, the inverse DFTs) against the oracle's block solve, <= 1e-10;
+  (d+1)x(d+1) solve per frequency, the inverse DFTs) against the oracle's block solve, <= 1e-10,
+  on 3-D grids and on 2-D ones (the reference's MPI ctests run the 2-D 50 x 50 square on 2 and 4
+  ranks; 50 x 50 on 4 ranks does not give whole rows per rank, so 52 x 48 stands in for it);
 - WaveSystemGMRES with that PCSHELL (MatCreateAIJ, KSP on PETSC_COMM_WORLD) against the one-rank
   run: same iteration count, same step.
 """
@@ -27,7 +29,7 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port, dims, kappa, q):
+def _rank(rank, world, port, dims, kappa, q, dim=3):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
@@ -40,11 +42,11 @@ def _rank(rank, world, port, dims, kappa, q):
         from circulantpreconditioner_amd import wave as W
         torch.cuda.set_device(0)
         comm = P.Comm.torch().set_world()
-        nx, ny, nz = dims
-        M = 4 * nx * ny * nz
+        nx, ny, nz = (tuple(dims) + (1,))[:3]
+        M = (dim + 1) * nx * ny * nz
         rng = np.random.default_rng(9)
         b = rng.standard_normal(M) + 1j * rng.standard_normal(M)
-        ctx = P.FFTPrecWaveContext(nx, ny, nz, kappa[0], kappa[1], kappa[2], C0, None, 3)
+        ctx = P.FFTPrecWaveContext(nx, ny, nz, kappa[0], kappa[1], kappa[2] if dim == 3 else 0.0, C0, None, dim)
         pc = P.PC.wave_shell(ctx).setup()
         vb = P.Vec.mpi_hip(M)
         lo, hi = vb.ownership_range()
@@ -53,7 +55,7 @@ def _rank(rank, world, port, dims, kappa, q):
         pc.apply(vb, vx)
         out = {"range": (lo, hi), "x": vx.array()}
         pc.destroy()
-        res, U = W.run(W.config(dims, pc="fft", steps=1), return_field=True)
+        res, U = W.run(W.config(dims, dim=dim, pc="fft", steps=1), return_field=True)
         out.update(res=res, U=U)
         P.set_comm_world(P.PETSC_COMM_SELF)
         comm.destroy()
@@ -62,7 +64,9 @@ def _rank(rank, world, port, dims, kappa, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dims,world", [((32, 32, 32), 2), ((32, 32, 32), 4), ((32, 24, 16), 4)])
+@pytest.mark.parametrize("dims,world", [((32, 32, 32), 2), ((32, 32, 32), 4), ((32, 24, 16), 4),
+                                        ((50, 50), 2),   # the reference's MPI ctest mesh (CMakeLists.txt:71-72)
+                                        ((52, 48), 4)])  # 2-D: whole rows of cells per rank (4 | n_y)
 def test_wave_pcshell_and_gmres_on_several_ranks(dims, world):
     import torch.multiprocessing as mp
     from circulantpreconditioner_amd import wave as W
@@ -71,7 +75,8 @@ def test_wave_pcshell_and_gmres_on_several_ranks(dims, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, dims, kappa, q)) for r in range(world)]
+    dim = len(dims)
+    procs = [ctx.Process(target=_rank, args=(r, world, port, dims, kappa, q, dim)) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -80,8 +85,8 @@ def test_wave_pcshell_and_gmres_on_several_ranks(dims, world):
         for p in procs:
             p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)
-    nx, ny, nz = dims
-    M = 4 * nx * ny * nz
+    nx, ny, nz = (tuple(dims) + (1,))[:3]
+    M = (dim + 1) * nx * ny * nz
     x = np.empty(M, dtype=np.complex128)
     U = np.empty(M, dtype=np.complex128)
     for r in range(world):
@@ -92,9 +97,9 @@ def test_wave_pcshell_and_gmres_on_several_ranks(dims, world):
         U[rs:rs + nl] = parts[r]["U"]
     rng = np.random.default_rng(9)
     b = rng.standard_normal(M) + 1j * rng.standard_normal(M)
-    xo = OW.block_solve(dims, kappa, b)
+    xo = OW.block_solve(dims, kappa, b, dim=dim)
     assert np.linalg.norm(x - xo) <= 1e-10 * np.linalg.norm(xo)
-    r1, U1 = W.run(W.config(dims, pc="fft", steps=1), return_field=True)
+    r1, U1 = W.run(W.config(dims, dim=dim, pc="fft", steps=1), return_field=True)
     for r in range(world):
         assert parts[r]["res"]["total_its"] == r1["total_its"]
         assert parts[r]["res"]["all_converged"] == r1["all_converged"] == 1
