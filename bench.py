@@ -357,17 +357,26 @@ def moved_bytes(passes, N: int) -> int:
 
 
 def copy_rate(dev, nbytes: int = 256 << 20) -> dict:
-    """This box's copy rate in the same run: torch's out-of-place device copy
-    of a 256 MiB buffer, read + write bytes over the HIP-event mean of 50 copies.  The row passes
-    move the same 2 x 268 MB per launch, so frac_of_copy says how far a pass sits from a copy."""
+    """This box's copy rate in the same run: out-of-place device copies of a
+    256 MiB buffer, read + write bytes over the HIP-event mean of 50 copies, with the library's
+    copy kernel (cfp_device_copy: 16-byte lanes, non-temporal stores) and with torch's.  The
+    faster one is the bar: the 3-sweep passes move the same 2 x 268 MB per launch, so
+    frac_of_copy says how far the dominant pass sits from a plain copy of its bytes."""
     import torch
+    from circulantpreconditioner_amd._lib import check, lib
     a = torch.empty(nbytes // 8, dtype=torch.float64, device=dev)
     a.fill_(1.0)
     c = torch.empty_like(a)
-    ms = event_ms(lambda: c.copy_(a), 50, settle_ms=100.0)
+    s = torch.cuda.current_stream().cuda_stream
+    ms_t = event_ms(lambda: c.copy_(a), 50, settle_ms=100.0)
+    ms_l = event_ms(lambda: check(lib().cfp_device_copy(c.data_ptr(), a.data_ptr(), nbytes, s)), 50, settle_ms=100.0)
+    ok = bool(torch.equal(a, c))
     del a, c
-    return {"GBps": round(2 * nbytes / (ms * 1e-3) / 1e9, 1), "ms": round(ms, 5), "bytes": nbytes,
-            "what": "torch out-of-place copy of 256 MiB, (read + write) / HIP-event mean of 50"}
+    gb = lambda ms: round(2 * nbytes / (ms * 1e-3) / 1e9, 1)  # noqa: E731
+    return {"GBps": max(gb(ms_l), gb(ms_t)), "library_GBps": gb(ms_l), "torch_GBps": gb(ms_t),
+            "library_ms": round(ms_l, 5), "torch_ms": round(ms_t, 5), "bytes": nbytes, "library_copy_ok": ok,
+            "what": "256 MiB out-of-place device copy, (read + write) / HIP-event mean of 50; GBps = the "
+                    "faster of the library's copy kernel and torch's"}
 
 
 def event_ms(fn, iters: int, settle_ms: float = 150.0) -> float:

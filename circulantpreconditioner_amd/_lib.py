@@ -34,6 +34,7 @@ def _declare(L) -> None:
         "cfp_last_error": ([], ctypes.c_char_p),
         "cfp_device_count": ([P(c_int)], c_int),
         "cfp_stream_sync": ([vp], c_int),
+        "cfp_device_copy": ([vp, vp, ctypes.c_size_t, vp], c_int),
         "cfp_plan_create": ([P(vp), i64, i64, i64, c_int], c_int),
         "cfp_plan_destroy": ([vp], c_int),
         "cfp_plan_set_symbol_transport": ([vp, dp], c_int),

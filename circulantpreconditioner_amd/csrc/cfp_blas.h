@@ -97,4 +97,7 @@ hipError_t kprof_end(double ms[4], long long launches[4]);
 void kprof_reset();
 bool kprof_take(int kind, hipEvent_t* e0, hipEvent_t* e1);
 hipError_t kprof_copy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s);
+// device-to-device copy on the library's tuned kernel (16-byte lanes, NT stores; kprof kind 3);
+// unaligned or odd sizes go through hipMemcpyAsync
+hipError_t blas_copy_bytes(void* dst, const void* src, size_t bytes, hipStream_t s);
 }  // namespace cfp

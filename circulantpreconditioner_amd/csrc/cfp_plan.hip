@@ -65,6 +65,12 @@ extern "C" int cfp_stream_sync(void* stream) {
   return CFP_SUCCESS;
 }
 
+extern "C" int cfp_device_copy(void* dst, const void* src, size_t bytes, void* stream) {
+  if ((!dst || !src) && bytes) return set_error(CFP_ERR_ARG_NULL, "cfp_device_copy: NULL pointer");
+  HIPCHK(cfp::blas_copy_bytes(dst, src, bytes, (hipStream_t)stream));
+  return CFP_SUCCESS;
+}
+
 // ------------------------------------------------------------------ twiddles
 namespace cfp {
 

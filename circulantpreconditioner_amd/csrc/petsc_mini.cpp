@@ -794,7 +794,7 @@ extern "C" PetscErrorCode VecCopy(Vec x, Vec y) {
       const VS* xd;
       PetscCall(dev_read(x, &xd));
       y->mask = MASK_GPU;
-      HIPK(cfp::kprof_copy(y->d, xd, sizeof(VS) * (size_t)x->n, hipMemcpyDeviceToDevice, g_stream));
+      HIPK(cfp::blas_copy_bytes(y->d, xd, sizeof(VS) * (size_t)x->n, g_stream));
     } else {
       (void)yd;
       HIPK(hipMemcpyAsync(y->d, x->h, sizeof(VS) * (size_t)x->n, hipMemcpyHostToDevice, g_stream));

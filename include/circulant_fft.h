@@ -28,6 +28,7 @@
 #ifndef CIRCULANT_FFT_H
 #define CIRCULANT_FFT_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -52,6 +53,10 @@ const char *cfp_version(void);
 const char *cfp_last_error(void);
 int cfp_device_count(int *count);
 int cfp_stream_sync(void *stream);
+/* Device-to-device copy of `bytes` on `stream` with the library's copy kernel (16-byte lanes,
+ * non-temporal stores; the stand-in VecCopy uses it).  Unaligned or non-multiple-of-16 sizes go
+ * through hipMemcpyAsync.  bench.py times it as the box's copy rate beside the roofline. */
+int cfp_device_copy(void *dst, const void *src, size_t bytes, void *stream);
 
 /* ---- single-GPU plan: n_x, n_y, n_z >= 1; `device` = HIP ordinal.  Axes up to 4096 take one
  * pass each (powers of two 16..1024 register-resident, others LDS mixed-radix); a longer axis

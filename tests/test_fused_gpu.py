@@ -113,3 +113,17 @@ def test_config1_dots_fall_back():
     ru, Uu = T.run(T.config(32, pc="fft", sign="fixed", device=True, steps=2, fuse=0), return_field=True)
     assert rf["total_its"] == ru["total_its"]
     assert np.linalg.norm(Uf - Uu) <= 1e-11 * np.linalg.norm(Uu)
+
+
+def test_device_copy():
+    """cfp_device_copy (the stand-in VecCopy's kernel): aligned sizes on the 16-byte-lane kernel,
+    odd sizes and offsets through hipMemcpyAsync, zero bytes a no-op; bit-exact."""
+    from circulantpreconditioner_amd._lib import check, lib
+    g = torch.Generator(device="cuda").manual_seed(5)
+    a = torch.randint(0, 256, (1 << 22,), dtype=torch.uint8, device="cuda", generator=g)
+    for off, nb in ((0, 1 << 22), (0, 16 * 12345), (16, 16 * 777), (3, 1001), (0, 7), (0, 0)):
+        c = torch.zeros_like(a)
+        check(lib().cfp_device_copy(c.data_ptr() + off, a.data_ptr() + off, nb, None))
+        torch.cuda.synchronize()
+        assert torch.equal(c[off:off + nb], a[off:off + nb])
+        assert int(c[:off].sum()) == 0 and int(c[off + nb:].sum()) == 0
