@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/pcshell_fft3d.h"
@@ -1167,6 +1168,12 @@ struct _p_Mat {
   i64 xloc_len = -1;                         // row length of the cached x-locality test
   bool xloc = false;
   unsigned char* dia_cls_x = nullptr;        // [xloc_len] when the classes repeat with the row length
+  // AIJ in block row-class form (aij_build_bdia) when the row-class form does not fit: B x B blocks
+  int bdia = -1;  // -1: not tried yet, 0: not representable, 1: built
+  cfp::BDiaDesc bdia_d{};
+  unsigned char* bdia_cls = nullptr;
+  unsigned short* bdia_mask = nullptr;
+  VS* bdia_tab = nullptr;
   // MatCreateAIJ (r06): entries from MatSetValue(s) wait here until MatAssemblyEnd.  This rank's
   // rows [rstart, rstart + lm); set_*: its own rows' entries, st_*: other ranks' (the stash).
   bool building = false;
@@ -1293,6 +1300,98 @@ static bool aij_build_dia(Mat M, cfp::DiaDesc* d, std::vector<unsigned char>* cl
   return true;
 }
 
+// Block row-class form of the host CSR (cfp_blas.h, k_bdia_spmv), tried when the row-class form
+// does not fit: the matrix cut into B x B blocks (B = 2, 3, 4), every nonzero block on one of at
+// most BDIA_MAX block diagonals (a 3-D periodic stencil has 13), at most 256 distinct block rows, their table within the LDS
+// budget.  The interleaved wave operator (wave_system.cpp: d + 1 unknowns per cell, a 2d + 1 cell
+// stencil) qualifies with B = d + 1.  Among the block sizes that fit, the one with the fewest
+// multiply-adds per row (nd B) wins; the product is the same up to summation order.
+static bool aij_build_bdia_b(Mat M, int B, cfp::BDiaDesc* d, std::vector<unsigned char>* cls,
+                             std::vector<unsigned short>* masks, std::vector<VS>* tab) {
+  const i64 m = M->m;
+  if (m <= 0 || m % B || M->n != m || M->h_col.empty()) return false;
+  const i64 mb = m / B;
+  std::vector<i64> offs;
+  for (i64 r = 0; r < m; ++r)
+    for (i64 p = M->h_rowptr[r]; p < M->h_rowptr[r + 1]; ++p) {
+      const i64 o = M->h_col[p] / B - r / B;
+      if (std::find(offs.begin(), offs.end(), o) == offs.end()) {
+        if ((int)offs.size() == BDIA_MAX) return false;
+        offs.push_back(o);
+      }
+    }
+  std::sort(offs.begin(), offs.end());
+  const int nd = (int)offs.size(), bs = nd * B * B;
+  const size_t per_cls = sizeof(VS) * (size_t)bs;
+  cls->assign((size_t)mb, 0);
+  masks->clear();
+  tab->clear();
+  std::vector<VS> row((size_t)bs);
+  std::unordered_map<uint64_t, std::vector<int>> seen;  // hash of (mask, values) -> classes
+  int last = -1;
+  for (i64 R = 0; R < mb; ++R) {
+    unsigned mk = 0;
+    for (int q = 0; q < bs; ++q) row[(size_t)q] = D(std::complex<double>(0.0, 0.0));
+    for (int i = 0; i < B; ++i) {
+      const i64 r = R * B + i;
+      for (i64 p = M->h_rowptr[r]; p < M->h_rowptr[r + 1]; ++p) {
+        const i64 c = M->h_col[p];
+        const int k = (int)(std::lower_bound(offs.begin(), offs.end(), c / B - R) - offs.begin());
+        mk |= 1u << k;
+        VS& v = row[(size_t)((k * B + i) * B + (int)(c % B))];
+        v = D(C(v) + C(M->h_val[(size_t)p]));  // duplicates add, as the CSR product does
+      }
+    }
+    const auto same = [&](int c) {
+      return (*masks)[(size_t)c] == mk && std::memcmp(&(*tab)[(size_t)c * bs], row.data(), per_cls) == 0;
+    };
+    int c = (last >= 0 && same(last)) ? last : -1;  // consecutive cells mostly share a class
+    uint64_t h = 1469598103934665603ull ^ mk;
+    if (c < 0) {
+      const unsigned char* b = reinterpret_cast<const unsigned char*>(row.data());
+      for (size_t q = 0; q < per_cls; ++q) h = (h ^ b[q]) * 1099511628211ull;
+      for (int q : seen[h])
+        if (same(q)) {
+          c = q;
+          break;
+        }
+    }
+    if (c < 0) {
+      if (masks->size() == 256 || (masks->size() + 1) * per_cls > BDIA_LDS_MAX) return false;
+      c = (int)masks->size();
+      masks->push_back((unsigned short)mk);
+      tab->insert(tab->end(), row.begin(), row.end());
+      seen[h].push_back(c);
+    }
+    (*cls)[(size_t)R] = (unsigned char)c;
+    last = c;
+  }
+  for (int k = 0; k < nd; ++k) d->off[k] = offs[(size_t)k];
+  d->nd = nd;
+  d->ncls = (int)masks->size();
+  d->B = B;
+  return true;
+}
+static bool aij_build_bdia(Mat M, cfp::BDiaDesc* d, std::vector<unsigned char>* cls, std::vector<unsigned short>* masks,
+                           std::vector<VS>* tab) {
+  bool any = false;
+  for (int B = 4; B >= 2; --B) {
+    cfp::BDiaDesc dd{};
+    std::vector<unsigned char> cc;
+    std::vector<unsigned short> mm;
+    std::vector<VS> tt;
+    if (!aij_build_bdia_b(M, B, &dd, &cc, &mm, &tt)) continue;
+    if (!any || dd.nd * dd.B < d->nd * d->B) {
+      *d = dd;
+      cls->swap(cc);
+      masks->swap(mm);
+      tab->swap(tt);
+      any = true;
+    }
+  }
+  return any;
+}
+
 static void aij_free_device(Mat M) {
   if (M->rowptr) hipFree(M->rowptr);
   if (M->col) hipFree(M->col);
@@ -1301,6 +1400,13 @@ static void aij_free_device(Mat M) {
   if (M->dia_mask) hipFree(M->dia_mask);
   if (M->dia_tab) hipFree(M->dia_tab);
   if (M->dia_cls_x) hipFree(M->dia_cls_x);
+  if (M->bdia_cls) hipFree(M->bdia_cls);
+  if (M->bdia_mask) hipFree(M->bdia_mask);
+  if (M->bdia_tab) hipFree(M->bdia_tab);
+  M->bdia_cls = nullptr;
+  M->bdia_mask = nullptr;
+  M->bdia_tab = nullptr;
+  M->bdia = -1;
   M->dia_cls_x = nullptr;
   M->rowptr = M->col = nullptr;
   M->val = M->dia_tab = nullptr;
@@ -1314,7 +1420,7 @@ static void aij_free_device(Mat M) {
 // the device copy: the row-class diagonal form when the matrix has one, else the CSR (once;
 // MatShift rebuilds it)
 static PetscErrorCode aij_upload(Mat M) {
-  if (M->rowptr || M->dia == 1) return PETSC_SUCCESS;
+  if (M->rowptr || M->dia == 1 || M->bdia == 1) return PETSC_SUCCESS;
   if (M->dia < 0) {
     std::vector<unsigned char> cls, masks;
     std::vector<VS> tab;
@@ -1335,6 +1441,28 @@ static PetscErrorCode aij_upload(Mat M) {
       M->h_cls.swap(cls);
       M->h_mask.swap(masks);
       M->xloc_len = -1;
+      return PETSC_SUCCESS;
+    }
+  }
+  if (M->bdia < 0) {
+    std::vector<unsigned char> cls;
+    std::vector<unsigned short> masks;
+    std::vector<VS> tab;
+    cfp::BDiaDesc d{};
+    M->bdia = aij_build_bdia(M, &d, &cls, &masks, &tab) ? 1 : 0;
+    if (M->bdia == 1) {
+      const size_t mb = sizeof(unsigned short) * masks.size();
+      hipError_t e = hipMalloc(&M->bdia_cls, cls.size());
+      if (e == hipSuccess) e = hipMalloc(&M->bdia_mask, mb);
+      if (e == hipSuccess) e = hipMalloc(&M->bdia_tab, sizeof(VS) * tab.size());
+      if (e == hipSuccess) e = hipMemcpy(M->bdia_cls, cls.data(), cls.size(), hipMemcpyHostToDevice);
+      if (e == hipSuccess) e = hipMemcpy(M->bdia_mask, masks.data(), mb, hipMemcpyHostToDevice);
+      if (e == hipSuccess) e = hipMemcpy(M->bdia_tab, tab.data(), sizeof(VS) * tab.size(), hipMemcpyHostToDevice);
+      if (e != hipSuccess) {
+        aij_free_device(M);
+        return ERR(PETSC_ERR_MEM, hipGetErrorString(e));
+      }
+      M->bdia_d = d;
       return PETSC_SUCCESS;
     }
   }
@@ -1359,7 +1487,7 @@ extern "C" PetscErrorCode PetscMiniMatAIJGetFormat(Mat A, int* format) {
   MCHK(A);
   if (!format) return ERR(PETSC_ERR_ARG_NULL, "NULL output");
   if (A->type != MATSEQAIJ) return ERR(PETSC_ERR_ARG_WRONG, "not a MATSEQAIJ");
-  *format = A->dia == 1 ? 1 : (A->rowptr ? 0 : -1);
+  *format = A->dia == 1 ? 1 : A->bdia == 1 ? 2 : (A->rowptr ? 0 : -1);
   return PETSC_SUCCESS;
 }
 extern "C" PetscErrorCode PetscMiniMatAIJGetDia(Mat A, PetscInt rowlen, PetscBool* has, PetscBool* x_local,
@@ -1678,6 +1806,17 @@ extern "C" PetscErrorCode MatAssemblyEnd(Mat A, MatAssemblyType type) {
 
 // y = A x on several ranks: the halo (gather the rows peers need, one all-to-all), the diagonal
 // block's SpMV into y, then y += the off-diagonal block on the ghosts
+// y = B x on the device in the form aij_upload chose
+static PetscErrorCode aij_spmv_dev(Mat B, const VS* xd, VS* yd) {
+  if (B->dia == 1)
+    HIPK(cfp::blas_dia_spmv(B->m, B->dia_d, B->dia_cls, B->dia_mask, B->dia_tab, xd, yd, g_stream));
+  else if (B->bdia == 1)
+    HIPK(cfp::blas_bdia_spmv(B->m / B->bdia_d.B, B->bdia_d, B->bdia_cls, B->bdia_mask, B->bdia_tab, xd, yd, g_stream));
+  else
+    HIPK(cfp::blas_csr_spmv(B->m, (i64)B->h_col.size(), B->rowptr, B->col, B->val, xd, yd, g_stream));
+  return PETSC_SUCCESS;
+}
+
 static PetscErrorCode mpiaij_mult(Mat A, Vec x, Vec y) {
   if (x->n != A->ln || y->n != A->lm || x->N != A->n || y->N != A->m) return ERR(PETSC_ERR_ARG_SIZ, "MatMult sizes");
   if (x == y) return ERR(PETSC_ERR_ARG_IDN, "x and y must be different vectors");
@@ -1716,10 +1855,7 @@ static PetscErrorCode mpiaij_mult(Mat A, Vec x, Vec y) {
     }
     Mat B = A->dblk;
     PetscCall(aij_upload(B));
-    if (B->dia == 1)
-      HIPK(cfp::blas_dia_spmv(B->m, B->dia_d, B->dia_cls, B->dia_mask, B->dia_tab, xd, yd, g_stream));
-    else
-      HIPK(cfp::blas_csr_spmv(B->m, (i64)B->h_col.size(), B->rowptr, B->col, B->val, xd, yd, g_stream));
+    PetscCall(aij_spmv_dev(B, xd, yd));
     if (hl && !A->o_col.empty())
       HIPK(cfp::blas_csr_spmv_add(A->lm, A->d_orowptr, A->d_ocol, A->d_oval, A->d_recvbuf, yd, g_stream));
     return PETSC_SUCCESS;
@@ -1772,10 +1908,7 @@ static PetscErrorCode aij_mult(Mat A, Vec x, Vec y) {
     PetscCall(dev_read(x, &xd));
     VS* yd;
     PetscCall(dev_rw(y, &yd));
-    if (A->dia == 1)
-      HIPK(cfp::blas_dia_spmv(A->m, A->dia_d, A->dia_cls, A->dia_mask, A->dia_tab, xd, yd, g_stream));
-    else
-      HIPK(cfp::blas_csr_spmv(A->m, (i64)A->h_col.size(), A->rowptr, A->col, A->val, xd, yd, g_stream));
+    PetscCall(aij_spmv_dev(A, xd, yd));
   } else {
     const VS* xh;
     PetscCall(host_read(x, &xh));
@@ -1818,7 +1951,7 @@ extern "C" PetscErrorCode MatShift(Mat A, PetscScalar a) {
       if (A->h_col[p] == r) { A->h_val[p] = D(C(A->h_val[p]) + a); found = true; }
     if (!found) return ERR(PETSC_ERR_ARG_WRONGSTATE, "MatShift needs an allocated diagonal");
   }
-  if (A->dia == 1) {  // the classes change with the diagonal: rebuild at the next device MatMult
+  if (A->dia == 1 || A->bdia == 1) {  // the classes change with the diagonal: rebuild at the next device MatMult
     HCHK(hipDeviceSynchronize());
     aij_free_device(A);
   } else if (A->val && !A->h_val.empty()) {

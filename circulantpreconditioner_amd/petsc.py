@@ -391,11 +391,12 @@ class Mat:
         return y
 
     def aij_format(self) -> str:
-        """The stand-in AIJ's device storage: 'dia' (row-class diagonal form), 'csr', or 'none'
-        before the first device MatMult."""
+        """The stand-in AIJ's device storage: 'dia' (row-class diagonal form), 'bdia' (block
+        row-class form, e.g. the interleaved wave operator), 'csr', or 'none' before the first
+        device MatMult."""
         f = ctypes.c_int()
         PetscCall(lib().PetscMiniMatAIJGetFormat(self.h, ctypes.byref(f)))
-        return {1: "dia", 0: "csr"}.get(f.value, "none")
+        return {1: "dia", 2: "bdia", 0: "csr"}.get(f.value, "none")
 
     def shift(self, a) -> "Mat":
         PetscCall(lib().MatShift(self.h, _S(a)))

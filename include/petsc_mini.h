@@ -166,7 +166,9 @@ PetscErrorCode PetscMiniCommResolve(MPI_Comm comm, MPI_Comm *resolved);
 PetscErrorCode PetscMiniAllreduce(MPI_Comm comm, double *buf, int64_t count, int op);
 /* Device storage the stand-in AIJ picked at its first device MatMult: 1 = row-class diagonal
  * form (k_dia_spmv: nonzeros on <= 8 fixed diagonals, <= 256 distinct rows -- Cartesian
- * stencils), 0 = CSR, -1 = not uploaded yet (MatShift resets it). */
+ * stencils), 2 = block row-class form (k_bdia_spmv: B x B blocks, B = 2..4, on <= 8 block
+ * diagonals, <= 256 distinct block rows -- the interleaved wave operator), 0 = CSR, -1 = not
+ * uploaded yet (MatShift resets it). */
 PetscErrorCode PetscMiniMatAIJGetFormat(Mat A, int *format);
 /* The device row-class form of an AIJ (above; uploaded now if it has not been): its class bytes,
  * class masks and coefficient table as device arrays, in the layout of cfp_stencil_t

@@ -394,3 +394,31 @@ def test_wave_reference_default_2d_50x50():
     assert r_fft["steps"] == r_none["steps"] > 0
     assert r_fft["all_converged"] == 1
     assert r_none["all_converged"] == 0 or r_fft["total_its"] * 3 <= r_none["total_its"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims,dim,bc", [((20, 16, 12), 3, "wall"), ((12, 10, 8), 3, "periodic"),
+                                         ((9, 7, 5), 3, "neumann"), ((2, 2, 2), 3, "periodic"),
+                                         ((50, 50), 2, "wall"), ((24, 18), 2, "periodic"), ((40,), 1, "wall")])
+def test_wave_operator_block_row_class_spmv(dims, dim, bc):
+    """The stand-in AIJ stores the interleaved wave operator in block row-class form (B = d + 1
+    blocks on <= 16 block diagonals, one class byte per cell) and its device MatMult equals
+    scipy's CSR product; MatShift rebuilds it."""
+    d3 = tuple(dims) + (1,) * (3 - len(dims))
+    h = [1.0 / v for v in d3]
+    A = _csr(d3, h, 3e-4, bc, shift=1.0, dim=dim)
+    m = A.shape[0]
+    M = P.Mat.aij(A.indptr.astype(np.int64), A.indices.astype(np.int64), A.data, A.shape)
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal(m) + 1j * rng.standard_normal(m)
+    xv, yv = P.Vec.seq_hip(m).set_array(x), P.Vec.seq_hip(m)
+    M.mult(xv, yv)
+    assert M.aij_format() == "bdia"
+    ref = A @ x
+    assert np.linalg.norm(yv.array() - ref) <= 1e-14 * np.linalg.norm(ref)
+    M.shift(0.25 + 0.5j)
+    assert M.aij_format() == "none"
+    M.mult(xv, yv)
+    assert M.aij_format() == "bdia"
+    ref = ref + (0.25 + 0.5j) * x
+    assert np.linalg.norm(yv.array() - ref) <= 1e-14 * np.linalg.norm(ref)
