@@ -73,7 +73,7 @@ class WaveConfig(ctypes.Structure):
                 ("cfl", ctypes.c_double), ("tmax", ctypes.c_double), ("ntmax", ctypes.c_int64),
                 ("precision", ctypes.c_double), ("max_its", ctypes.c_int64), ("restart", ctypes.c_int64),
                 ("pc", ctypes.c_int), ("bc", ctypes.c_int), ("pc_side", ctypes.c_int), ("on_device", ctypes.c_int),
-                ("dim", ctypes.c_int)]
+                ("dim", ctypes.c_int), ("profile", ctypes.c_int)]
 
 
 class WaveResult(ctypes.Structure):
@@ -83,11 +83,15 @@ class WaveResult(ctypes.Structure):
                 ("last_reason", ctypes.c_int), ("all_converged", ctypes.c_int), ("last_residual", ctypes.c_double),
                 ("last_norm_dU", ctypes.c_double), ("solve_seconds", ctypes.c_double),
                 ("pc_seconds", ctypes.c_double), ("pc_calls", ctypes.c_int64), ("setup_seconds", ctypes.c_double),
-                ("kappa", ctypes.c_double * 3), ("rstart", ctypes.c_int64), ("nlocal", ctypes.c_int64)]
+                ("kappa", ctypes.c_double * 3), ("rstart", ctypes.c_int64), ("nlocal", ctypes.c_int64),
+                ("loop_seconds", ctypes.c_double), ("dev_ms_", ctypes.c_double * 4),
+                ("dev_launches_", ctypes.c_int64 * 4)]
 
     def as_dict(self) -> dict:
-        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "kappa"}
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "kappa" and not k.endswith("_")}
         d["kappa"] = list(self.kappa)
+        d["dev_ms"] = dict(zip(("pcapply", "matmult", "vector", "copy"), self.dev_ms_))
+        d["dev_launches"] = dict(zip(("pcapply", "matmult", "vector", "copy"), self.dev_launches_))
         return d
 
 

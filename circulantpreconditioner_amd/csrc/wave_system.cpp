@@ -588,6 +588,8 @@ extern "C" PetscErrorCode WaveSystemGMRES(const cfp_wave_config* cfg, cfp_wave_r
   bool stationary = false;
   res->all_converged = 1;
   res->min_step_its = -1;
+  if (cfg->profile) PetscCall(PetscMiniProfileBegin(1 << 16));
+  const double t_loop = wall();
   while (it < cfg->ntmax && time <= cfg->tmax && !stationary) {  // :95
     PetscCall(VecCopy(Un, dUn));
     const double v = wall();
@@ -618,6 +620,12 @@ extern "C" PetscErrorCode WaveSystemGMRES(const cfp_wave_config* cfg, cfp_wave_r
     res->last_residual = residu;
     res->last_norm_dU = norm;
     if (reason != KSP_CONVERGED_RTOL && reason != KSP_CONVERGED_ATOL) res->all_converged = 0;
+  }
+  res->loop_seconds = wall() - t_loop;
+  if (cfg->profile) {
+    PetscCall(PetscMiniProfileEnd(res->dev_ms, res->dev_launches));
+    res->dev_ms[0] = 1e3 * res->pc_seconds;
+    res->dev_launches[0] = res->pc_calls;
   }
   res->steps = it;
   res->time = time;

@@ -115,6 +115,7 @@ typedef struct {
   int pc_side;        /* PC_LEFT / PC_RIGHT */
   int on_device;
   int dim;            /* mesh dimension 1, 2 or 3 (nbComp = dim + 1); 0 = 3 */
+  int profile;        /* 1: stamp every kernel of the time loop (PetscMiniProfileBegin): dev_ms below */
 } cfp_wave_config;
 
 /* same layout as cfp_transport_result (transport_equation.h); lambda[] holds kappa */
@@ -130,6 +131,9 @@ typedef struct {
   double setup_seconds;
   double kappa[3];
   int64_t rstart, nlocal; /* this rank's rows of Un (U_out holds nlocal values): 0, (dim+1)N on one rank */
+  double loop_seconds;    /* wall time of the time loop */
+  double dev_ms[4];       /* profile = 1: device ms of the loop by kind: PCApply, MatMult, vector kernels, copies */
+  int64_t dev_launches[4];
 } cfp_wave_result;
 
 void cfp_wave_config_default(cfp_wave_config *cfg, int64_t n);
