@@ -44,18 +44,19 @@ hipError_t blas_dia_spmv(i64 m, const DiaDesc& d, const unsigned char* cls, cons
 // Block row-class form (k_bdia_spmv): the matrix in B x B blocks (B = 2..4, e.g. the d + 1
 // interleaved unknowns of a wave-system cell), every nonzero in a block on one of nd <= BDIA_MAX
 // block diagonals (block column - block row = off[k], ascending), each block row one of
-// ncls <= 256 classes; class c holds the dense block tab[((c nd + k) B + i) B + j] (row i, column
-// j) on the diagonals whose bit k of masks[c] is set.  y[R B + i] = sum_k,j tab[..] x[(R + off[k]) B + j].
+// ncls <= 256 classes; class c has a block on the diagonals whose bit k of masks[c] is set, stored
+// densely (row i, column j) in ascending k from block cbase[c] of tab: the q-th present block of
+// class c is tab[((cbase[c] + q) B + i) B + j].  y[R B + i] = sum_k,j block(k)[i][j] x[(R + off[k]) B + j].
 #define BDIA_MAX 16
 struct BDiaDesc {
   i64 off[BDIA_MAX];
-  int nd = 0, ncls = 0, B = 0;
+  int nd = 0, ncls = 0, B = 0, nblk = 0;  // nblk: blocks in tab
 };
 #define BDIA_LDS_MAX (60 * 1024)
 hipError_t blas_bdia_spmv(i64 mb, const BDiaDesc& d, const unsigned char* cls, const unsigned short* masks,
-                          const cd* tab, const cd* x, cd* y, hipStream_t s);
+                          const unsigned short* cbase, const cd* tab, const cd* x, cd* y, hipStream_t s);
 hipError_t blas_bdia_spmv(i64 mb, const BDiaDesc& d, const unsigned char* cls, const unsigned short* masks,
-                          const double* tab, const double* x, double* y, hipStream_t s);
+                          const unsigned short* cbase, const double* tab, const double* x, double* y, hipStream_t s);
 // distributed AIJ halo: out[i] = x[idx[i]] (idx < 0: 0); y += B x for a CSR block B
 hipError_t blas_gather(cd* out, const cd* x, const i64* idx, i64 n, hipStream_t s);
 hipError_t blas_gather(double* out, const double* x, const i64* idx, i64 n, hipStream_t s);

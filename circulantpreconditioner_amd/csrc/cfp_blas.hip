@@ -439,19 +439,23 @@ __global__ void __launch_bounds__(BLAS_THREADS) k_dia_spmv(i64 m, DiaDesc d, con
 // nonzeros per 3-D cell).
 template <class T, int B>
 __global__ void __launch_bounds__(BLAS_THREADS) k_bdia_spmv(i64 mb, BDiaDesc d, const unsigned char* cls,
-                                                            const unsigned short* masks, const T* tab, const T* x,
-                                                            T* y) {
+                                                            const unsigned short* masks, const unsigned short* cbase,
+                                                            const T* tab, const T* x, T* y) {
   extern __shared__ __attribute__((aligned(16))) unsigned char bdia_lds[];
   T* st = reinterpret_cast<T*>(bdia_lds);
-  const int nt = d.ncls * d.nd * B * B;
+  const int nt = d.nblk * B * B;
   unsigned short* sm = reinterpret_cast<unsigned short*>(bdia_lds + sizeof(T) * (size_t)nt);
+  unsigned short* sb = sm + d.ncls;
   for (int i = threadIdx.x; i < nt; i += blockDim.x) st[i] = tab[i];
-  for (int i = threadIdx.x; i < d.ncls; i += blockDim.x) sm[i] = masks[i];
+  for (int i = threadIdx.x; i < d.ncls; i += blockDim.x) {
+    sm[i] = masks[i];
+    sb[i] = cbase[i];
+  }
   __syncthreads();
   GRID_LOOP(r, mb) {
     const int c = cls[r];
     const unsigned mk = sm[c];
-    const T* blk = st + c * d.nd * B * B;
+    const T* blk = st + (int)sb[c] * B * B;
     double ax[B], ay[B];
 #pragma unroll
     for (int i = 0; i < B; ++i) ax[i] = ay[i] = 0.0;
@@ -465,7 +469,8 @@ __global__ void __launch_bounds__(BLAS_THREADS) k_bdia_spmv(i64 mb, BDiaDesc d, 
 #pragma unroll
         for (int i = 0; i < B; ++i)
 #pragma unroll
-          for (int j = 0; j < B; ++j) spmv_acc(blk[(k * B + i) * B + j], xv[j], ax[i], ay[i]);
+          for (int j = 0; j < B; ++j) spmv_acc(blk[i * B + j], xv[j], ax[i], ay[i]);
+        blk += B * B;
       }
     }
 #pragma unroll
@@ -577,27 +582,28 @@ hipError_t blas_dia_spmv(i64 m, const DiaDesc& d, const unsigned char* cls, cons
 }
 
 template <class T>
-static hipError_t bdia_t(i64 mb, const BDiaDesc& d, const unsigned char* cls, const unsigned short* masks, const T* tab,
-                         const T* x, T* y, hipStream_t s) {
+static hipError_t bdia_t(i64 mb, const BDiaDesc& d, const unsigned char* cls, const unsigned short* masks,
+                         const unsigned short* cbase, const T* tab, const T* x, T* y, hipStream_t s) {
   if (mb <= 0) return hipSuccess;
-  if (d.nd < 1 || d.nd > BDIA_MAX || d.ncls < 1 || d.ncls > 256 || d.B < 2 || d.B > 4) return hipErrorInvalidValue;
-  const size_t lds = sizeof(T) * (size_t)(d.ncls * d.nd * d.B * d.B) + 512;
-  if (lds > BDIA_LDS_MAX + 512) return hipErrorInvalidValue;
+  if (d.nd < 1 || d.nd > BDIA_MAX || d.ncls < 1 || d.ncls > 256 || d.B < 2 || d.B > 4 || d.nblk < 1)
+    return hipErrorInvalidValue;
+  const size_t lds = sizeof(T) * (size_t)(d.nblk * d.B * d.B) + 2 * sizeof(unsigned short) * 256;
+  if (lds > BDIA_LDS_MAX + 1024) return hipErrorInvalidValue;
   const dim3 g(nblocks(mb)), b(BLAS_THREADS);
   switch (d.B) {
-    case 2: blaunch(1, (k_bdia_spmv<T, 2>), g, b, (unsigned)lds, s, mb, d, cls, masks, tab, x, y); break;
-    case 3: blaunch(1, (k_bdia_spmv<T, 3>), g, b, (unsigned)lds, s, mb, d, cls, masks, tab, x, y); break;
-    default: blaunch(1, (k_bdia_spmv<T, 4>), g, b, (unsigned)lds, s, mb, d, cls, masks, tab, x, y);
+    case 2: blaunch(1, (k_bdia_spmv<T, 2>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, tab, x, y); break;
+    case 3: blaunch(1, (k_bdia_spmv<T, 3>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, tab, x, y); break;
+    default: blaunch(1, (k_bdia_spmv<T, 4>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, tab, x, y);
   }
   return hipGetLastError();
 }
 hipError_t blas_bdia_spmv(i64 mb, const BDiaDesc& d, const unsigned char* cls, const unsigned short* masks,
-                          const cd* tab, const cd* x, cd* y, hipStream_t s) {
-  return bdia_t(mb, d, cls, masks, tab, x, y, s);
+                          const unsigned short* cbase, const cd* tab, const cd* x, cd* y, hipStream_t s) {
+  return bdia_t(mb, d, cls, masks, cbase, tab, x, y, s);
 }
 hipError_t blas_bdia_spmv(i64 mb, const BDiaDesc& d, const unsigned char* cls, const unsigned short* masks,
-                          const double* tab, const double* x, double* y, hipStream_t s) {
-  return bdia_t(mb, d, cls, masks, tab, x, y, s);
+                          const unsigned short* cbase, const double* tab, const double* x, double* y, hipStream_t s) {
+  return bdia_t(mb, d, cls, masks, cbase, tab, x, y, s);
 }
 
 // per-thread device + pinned staging of block partial sums (synchronous reductions).  hd is the

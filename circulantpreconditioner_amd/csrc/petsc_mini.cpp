@@ -1172,7 +1172,7 @@ struct _p_Mat {
   int bdia = -1;  // -1: not tried yet, 0: not representable, 1: built
   cfp::BDiaDesc bdia_d{};
   unsigned char* bdia_cls = nullptr;
-  unsigned short* bdia_mask = nullptr;
+  unsigned short *bdia_mask = nullptr, *bdia_cbase = nullptr;
   VS* bdia_tab = nullptr;
   // MatCreateAIJ (r06): entries from MatSetValue(s) wait here until MatAssemblyEnd.  This rank's
   // rows [rstart, rstart + lm); set_*: its own rows' entries, st_*: other ranks' (the stash).
@@ -1302,12 +1302,13 @@ static bool aij_build_dia(Mat M, cfp::DiaDesc* d, std::vector<unsigned char>* cl
 
 // Block row-class form of the host CSR (cfp_blas.h, k_bdia_spmv), tried when the row-class form
 // does not fit: the matrix cut into B x B blocks (B = 2, 3, 4), every nonzero block on one of at
-// most BDIA_MAX block diagonals (a 3-D periodic stencil has 13), at most 256 distinct block rows, their table within the LDS
-// budget.  The interleaved wave operator (wave_system.cpp: d + 1 unknowns per cell, a 2d + 1 cell
-// stencil) qualifies with B = d + 1.  Among the block sizes that fit, the one with the fewest
+// most BDIA_MAX block diagonals (a 3-D periodic stencil has 13), at most 256 distinct block
+// rows, their present blocks within the LDS budget.  The interleaved wave operator
+// (wave_system.cpp: d + 1 unknowns per cell, a 2d + 1 cell stencil) qualifies with B = d + 1.  Among the block sizes that fit, the one with the fewest
 // multiply-adds per row (nd B) wins; the product is the same up to summation order.
 static bool aij_build_bdia_b(Mat M, int B, cfp::BDiaDesc* d, std::vector<unsigned char>* cls,
-                             std::vector<unsigned short>* masks, std::vector<VS>* tab) {
+                             std::vector<unsigned short>* masks, std::vector<unsigned short>* cbase,
+                             std::vector<VS>* tab) {
   const i64 m = M->m;
   if (m <= 0 || m % B || M->n != m || M->h_col.empty()) return false;
   const i64 mb = m / B;
@@ -1323,11 +1324,13 @@ static bool aij_build_bdia_b(Mat M, int B, cfp::BDiaDesc* d, std::vector<unsigne
   std::sort(offs.begin(), offs.end());
   const int nd = (int)offs.size(), bs = nd * B * B;
   const size_t per_cls = sizeof(VS) * (size_t)bs;
+  const size_t blk_bytes = sizeof(VS) * (size_t)(B * B);
   cls->assign((size_t)mb, 0);
   masks->clear();
-  tab->clear();
+  std::vector<VS> dense;  // classes' rows, dense over all nd diagonals (for the comparison)
   std::vector<VS> row((size_t)bs);
   std::unordered_map<uint64_t, std::vector<int>> seen;  // hash of (mask, values) -> classes
+  size_t nblk = 0;
   int last = -1;
   for (i64 R = 0; R < mb; ++R) {
     unsigned mk = 0;
@@ -1343,7 +1346,7 @@ static bool aij_build_bdia_b(Mat M, int B, cfp::BDiaDesc* d, std::vector<unsigne
       }
     }
     const auto same = [&](int c) {
-      return (*masks)[(size_t)c] == mk && std::memcmp(&(*tab)[(size_t)c * bs], row.data(), per_cls) == 0;
+      return (*masks)[(size_t)c] == mk && std::memcmp(&dense[(size_t)c * bs], row.data(), per_cls) == 0;
     };
     int c = (last >= 0 && same(last)) ? last : -1;  // consecutive cells mostly share a class
     uint64_t h = 1469598103934665603ull ^ mk;
@@ -1357,34 +1360,48 @@ static bool aij_build_bdia_b(Mat M, int B, cfp::BDiaDesc* d, std::vector<unsigne
         }
     }
     if (c < 0) {
-      if (masks->size() == 256 || (masks->size() + 1) * per_cls > BDIA_LDS_MAX) return false;
+      nblk += (size_t)__builtin_popcount(mk);
+      if (masks->size() == 256 || nblk * blk_bytes > BDIA_LDS_MAX) return false;
       c = (int)masks->size();
       masks->push_back((unsigned short)mk);
-      tab->insert(tab->end(), row.begin(), row.end());
+      dense.insert(dense.end(), row.begin(), row.end());
       seen[h].push_back(c);
     }
     (*cls)[(size_t)R] = (unsigned char)c;
     last = c;
   }
+  // the table: each class's present blocks in ascending k
+  cbase->clear();
+  tab->clear();
+  for (size_t c = 0; c < masks->size(); ++c) {
+    cbase->push_back((unsigned short)(tab->size() / (size_t)(B * B)));
+    for (int k = 0; k < nd; ++k)
+      if (((*masks)[c] >> k) & 1u) {
+        const VS* b0 = &dense[c * (size_t)bs + (size_t)k * B * B];
+        tab->insert(tab->end(), b0, b0 + B * B);
+      }
+  }
   for (int k = 0; k < nd; ++k) d->off[k] = offs[(size_t)k];
   d->nd = nd;
   d->ncls = (int)masks->size();
   d->B = B;
+  d->nblk = (int)(tab->size() / (size_t)(B * B));
   return true;
 }
 static bool aij_build_bdia(Mat M, cfp::BDiaDesc* d, std::vector<unsigned char>* cls, std::vector<unsigned short>* masks,
-                           std::vector<VS>* tab) {
+                           std::vector<unsigned short>* cbase, std::vector<VS>* tab) {
   bool any = false;
   for (int B = 4; B >= 2; --B) {
     cfp::BDiaDesc dd{};
     std::vector<unsigned char> cc;
-    std::vector<unsigned short> mm;
+    std::vector<unsigned short> mm, bb;
     std::vector<VS> tt;
-    if (!aij_build_bdia_b(M, B, &dd, &cc, &mm, &tt)) continue;
+    if (!aij_build_bdia_b(M, B, &dd, &cc, &mm, &bb, &tt)) continue;
     if (!any || dd.nd * dd.B < d->nd * d->B) {
       *d = dd;
       cls->swap(cc);
       masks->swap(mm);
+      cbase->swap(bb);
       tab->swap(tt);
       any = true;
     }
@@ -1403,8 +1420,9 @@ static void aij_free_device(Mat M) {
   if (M->bdia_cls) hipFree(M->bdia_cls);
   if (M->bdia_mask) hipFree(M->bdia_mask);
   if (M->bdia_tab) hipFree(M->bdia_tab);
+  if (M->bdia_cbase) hipFree(M->bdia_cbase);
   M->bdia_cls = nullptr;
-  M->bdia_mask = nullptr;
+  M->bdia_mask = M->bdia_cbase = nullptr;
   M->bdia_tab = nullptr;
   M->bdia = -1;
   M->dia_cls_x = nullptr;
@@ -1446,17 +1464,19 @@ static PetscErrorCode aij_upload(Mat M) {
   }
   if (M->bdia < 0) {
     std::vector<unsigned char> cls;
-    std::vector<unsigned short> masks;
+    std::vector<unsigned short> masks, cbase;
     std::vector<VS> tab;
     cfp::BDiaDesc d{};
-    M->bdia = aij_build_bdia(M, &d, &cls, &masks, &tab) ? 1 : 0;
+    M->bdia = aij_build_bdia(M, &d, &cls, &masks, &cbase, &tab) ? 1 : 0;
     if (M->bdia == 1) {
       const size_t mb = sizeof(unsigned short) * masks.size();
       hipError_t e = hipMalloc(&M->bdia_cls, cls.size());
       if (e == hipSuccess) e = hipMalloc(&M->bdia_mask, mb);
+      if (e == hipSuccess) e = hipMalloc(&M->bdia_cbase, mb);
       if (e == hipSuccess) e = hipMalloc(&M->bdia_tab, sizeof(VS) * tab.size());
       if (e == hipSuccess) e = hipMemcpy(M->bdia_cls, cls.data(), cls.size(), hipMemcpyHostToDevice);
       if (e == hipSuccess) e = hipMemcpy(M->bdia_mask, masks.data(), mb, hipMemcpyHostToDevice);
+      if (e == hipSuccess) e = hipMemcpy(M->bdia_cbase, cbase.data(), mb, hipMemcpyHostToDevice);
       if (e == hipSuccess) e = hipMemcpy(M->bdia_tab, tab.data(), sizeof(VS) * tab.size(), hipMemcpyHostToDevice);
       if (e != hipSuccess) {
         aij_free_device(M);
@@ -1811,7 +1831,8 @@ static PetscErrorCode aij_spmv_dev(Mat B, const VS* xd, VS* yd) {
   if (B->dia == 1)
     HIPK(cfp::blas_dia_spmv(B->m, B->dia_d, B->dia_cls, B->dia_mask, B->dia_tab, xd, yd, g_stream));
   else if (B->bdia == 1)
-    HIPK(cfp::blas_bdia_spmv(B->m / B->bdia_d.B, B->bdia_d, B->bdia_cls, B->bdia_mask, B->bdia_tab, xd, yd, g_stream));
+    HIPK(cfp::blas_bdia_spmv(B->m / B->bdia_d.B, B->bdia_d, B->bdia_cls, B->bdia_mask, B->bdia_cbase, B->bdia_tab, xd,
+                             yd, g_stream));
   else
     HIPK(cfp::blas_csr_spmv(B->m, (i64)B->h_col.size(), B->rowptr, B->col, B->val, xd, yd, g_stream));
   return PETSC_SUCCESS;
