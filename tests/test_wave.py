@@ -413,12 +413,14 @@ def test_wave_operator_block_row_class_spmv(dims, dim, bc):
     x = rng.standard_normal(m) + 1j * rng.standard_normal(m)
     xv, yv = P.Vec.seq_hip(m).set_array(x), P.Vec.seq_hip(m)
     M.mult(xv, yv)
-    assert M.aij_format() == "bdia"
+    # a 2 x 2 x 2 periodic grid has so few distinct diagonals that the scalar row-class form fits
+    want = "dia" if max(d3) <= 2 else "bdia"
+    assert M.aij_format() == want
     ref = A @ x
     assert np.linalg.norm(yv.array() - ref) <= 1e-14 * np.linalg.norm(ref)
     M.shift(0.25 + 0.5j)
     assert M.aij_format() == "none"
     M.mult(xv, yv)
-    assert M.aij_format() == "bdia"
+    assert M.aij_format() == want
     ref = ref + (0.25 + 0.5j) * x
     assert np.linalg.norm(yv.array() - ref) <= 1e-14 * np.linalg.norm(ref)
