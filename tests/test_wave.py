@@ -413,8 +413,9 @@ def test_wave_operator_block_row_class_spmv(dims, dim, bc):
     x = rng.standard_normal(m) + 1j * rng.standard_normal(m)
     xv, yv = P.Vec.seq_hip(m).set_array(x), P.Vec.seq_hip(m)
     M.mult(xv, yv)
-    # a 2 x 2 x 2 periodic grid has so few distinct diagonals that the scalar row-class form fits
-    want = "dia" if max(d3) <= 2 else "bdia"
+    # 1-D (2 unknowns, 3 cells) and a 2 x 2 x 2 periodic grid have few enough distinct diagonals
+    # (<= 8) that the scalar row-class form fits and is preferred
+    want = "dia" if dim == 1 or max(d3) <= 2 else "bdia"
     assert M.aij_format() == want
     ref = A @ x
     assert np.linalg.norm(yv.array() - ref) <= 1e-14 * np.linalg.norm(ref)
