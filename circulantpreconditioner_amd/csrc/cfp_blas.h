@@ -46,7 +46,9 @@ hipError_t blas_dia_spmv(i64 m, const DiaDesc& d, const unsigned char* cls, cons
 // block diagonals (block column - block row = off[k], ascending), each block row one of
 // ncls <= 256 classes; class c has a block on the diagonals whose bit k of masks[c] is set, stored
 // densely (row i, column j) in ascending k from block cbase[c] of tab: the q-th present block of
-// class c is tab[((cbase[c] + q) B + i) B + j].  y[R B + i] = sum_k,j block(k)[i][j] x[(R + off[k]) B + j].
+// class c is tab[((cbase[c] + q) B + i) B + j], and bnz[cbase[c] + q] marks its nonzero entries
+// (bit i B + j) and, in bits 16.., the columns that have any.
+// y[R B + i] = sum_k,j block(k)[i][j] x[(R + off[k]) B + j].
 #define BDIA_MAX 16
 struct BDiaDesc {
   i64 off[BDIA_MAX];
@@ -54,9 +56,11 @@ struct BDiaDesc {
 };
 #define BDIA_LDS_MAX (60 * 1024)
 hipError_t blas_bdia_spmv(i64 mb, const BDiaDesc& d, const unsigned char* cls, const unsigned short* masks,
-                          const unsigned short* cbase, const cd* tab, const cd* x, cd* y, hipStream_t s);
+                          const unsigned short* cbase, const unsigned* bnz, const cd* tab, const cd* x, cd* y,
+                          hipStream_t s);
 hipError_t blas_bdia_spmv(i64 mb, const BDiaDesc& d, const unsigned char* cls, const unsigned short* masks,
-                          const unsigned short* cbase, const double* tab, const double* x, double* y, hipStream_t s);
+                          const unsigned short* cbase, const unsigned* bnz, const double* tab, const double* x,
+                          double* y, hipStream_t s);
 // distributed AIJ halo: out[i] = x[idx[i]] (idx < 0: 0); y += B x for a CSR block B
 hipError_t blas_gather(cd* out, const cd* x, const i64* idx, i64 n, hipStream_t s);
 hipError_t blas_gather(double* out, const double* x, const i64* idx, i64 n, hipStream_t s);

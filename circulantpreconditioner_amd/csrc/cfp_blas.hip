@@ -431,22 +431,24 @@ __global__ void __launch_bounds__(BLAS_THREADS) k_dia_spmv(i64 m, DiaDesc d, con
 }
 
 // Block row-class form (cfp_blas.h): one thread per block row.  The class table sits in LDS; the
-// threads of a wave mostly share a class (interior cells), so its reads are broadcasts.  Per
-// present block diagonal the thread loads the neighbour's B contiguous values and does the dense
-// B x B product (the absent entries of a block are zeros in the table: a few wasted FMAs, no
-// divergence).  The interleaved wave operator on a Cartesian grid: x read once through the caches,
-// y written once, one class byte per cell -- against CSR's 24 bytes per nonzero (about 34
-// nonzeros per 3-D cell).
+// threads of a wave mostly share a class (interior cells), so its reads are broadcasts and the
+// per-entry tests below are uniform branches.  Per present block diagonal the thread loads the
+// neighbour's values in the columns the block uses and multiplies by the block's nonzeros only
+// (the wave operator: 4 of 16 entries in a neighbour block, 2 of 4 columns).  The interleaved wave
+// operator on a Cartesian grid: x read once through the caches, y written once, one class byte per
+// cell -- against CSR's 24 bytes per nonzero (about 28 nonzeros per 3-D cell).
 template <class T, int B>
 __global__ void __launch_bounds__(BLAS_THREADS) k_bdia_spmv(i64 mb, BDiaDesc d, const unsigned char* cls,
                                                             const unsigned short* masks, const unsigned short* cbase,
-                                                            const T* tab, const T* x, T* y) {
+                                                            const unsigned* bnz, const T* tab, const T* x, T* y) {
   extern __shared__ __attribute__((aligned(16))) unsigned char bdia_lds[];
   T* st = reinterpret_cast<T*>(bdia_lds);
   const int nt = d.nblk * B * B;
-  unsigned short* sm = reinterpret_cast<unsigned short*>(bdia_lds + sizeof(T) * (size_t)nt);
+  unsigned* sz = reinterpret_cast<unsigned*>(bdia_lds + sizeof(T) * (size_t)nt);
+  unsigned short* sm = reinterpret_cast<unsigned short*>(sz + d.nblk);
   unsigned short* sb = sm + d.ncls;
   for (int i = threadIdx.x; i < nt; i += blockDim.x) st[i] = tab[i];
+  for (int i = threadIdx.x; i < d.nblk; i += blockDim.x) sz[i] = bnz[i];
   for (int i = threadIdx.x; i < d.ncls; i += blockDim.x) {
     sm[i] = masks[i];
     sb[i] = cbase[i];
@@ -455,7 +457,7 @@ __global__ void __launch_bounds__(BLAS_THREADS) k_bdia_spmv(i64 mb, BDiaDesc d, 
   GRID_LOOP(r, mb) {
     const int c = cls[r];
     const unsigned mk = sm[c];
-    const T* blk = st + (int)sb[c] * B * B;
+    int q = sb[c];
     double ax[B], ay[B];
 #pragma unroll
     for (int i = 0; i < B; ++i) ax[i] = ay[i] = 0.0;
@@ -463,14 +465,17 @@ __global__ void __launch_bounds__(BLAS_THREADS) k_bdia_spmv(i64 mb, BDiaDesc d, 
     for (int k = 0; k < BDIA_MAX; ++k) {
       if (k < d.nd && ((mk >> k) & 1u)) {
         const T* xb = x + (r + d.off[k]) * B;
+        const T* blk = st + q * B * B;
+        const unsigned nz = sz[q];
         T xv[B];
 #pragma unroll
-        for (int j = 0; j < B; ++j) xv[j] = xb[j];
+        for (int j = 0; j < B; ++j) xv[j] = ((nz >> (16 + j)) & 1u) ? xb[j] : T{};
 #pragma unroll
         for (int i = 0; i < B; ++i)
 #pragma unroll
-          for (int j = 0; j < B; ++j) spmv_acc(blk[i * B + j], xv[j], ax[i], ay[i]);
-        blk += B * B;
+          for (int j = 0; j < B; ++j)
+            if ((nz >> (i * B + j)) & 1u) spmv_acc(blk[i * B + j], xv[j], ax[i], ay[i]);
+        ++q;
       }
     }
 #pragma unroll
@@ -583,27 +588,30 @@ hipError_t blas_dia_spmv(i64 m, const DiaDesc& d, const unsigned char* cls, cons
 
 template <class T>
 static hipError_t bdia_t(i64 mb, const BDiaDesc& d, const unsigned char* cls, const unsigned short* masks,
-                         const unsigned short* cbase, const T* tab, const T* x, T* y, hipStream_t s) {
+                         const unsigned short* cbase, const unsigned* bnz, const T* tab, const T* x, T* y,
+                         hipStream_t s) {
   if (mb <= 0) return hipSuccess;
   if (d.nd < 1 || d.nd > BDIA_MAX || d.ncls < 1 || d.ncls > 256 || d.B < 2 || d.B > 4 || d.nblk < 1)
     return hipErrorInvalidValue;
-  const size_t lds = sizeof(T) * (size_t)(d.nblk * d.B * d.B) + 2 * sizeof(unsigned short) * 256;
-  if (lds > BDIA_LDS_MAX + 1024) return hipErrorInvalidValue;
+  const size_t lds = (sizeof(T) * d.B * d.B + sizeof(unsigned)) * (size_t)d.nblk + 2 * sizeof(unsigned short) * 256;
+  if (lds > BDIA_LDS_MAX + 2048) return hipErrorInvalidValue;
   const dim3 g(nblocks(mb)), b(BLAS_THREADS);
   switch (d.B) {
-    case 2: blaunch(1, (k_bdia_spmv<T, 2>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, tab, x, y); break;
-    case 3: blaunch(1, (k_bdia_spmv<T, 3>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, tab, x, y); break;
-    default: blaunch(1, (k_bdia_spmv<T, 4>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, tab, x, y);
+    case 2: blaunch(1, (k_bdia_spmv<T, 2>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, bnz, tab, x, y); break;
+    case 3: blaunch(1, (k_bdia_spmv<T, 3>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, bnz, tab, x, y); break;
+    default: blaunch(1, (k_bdia_spmv<T, 4>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, bnz, tab, x, y);
   }
   return hipGetLastError();
 }
 hipError_t blas_bdia_spmv(i64 mb, const BDiaDesc& d, const unsigned char* cls, const unsigned short* masks,
-                          const unsigned short* cbase, const cd* tab, const cd* x, cd* y, hipStream_t s) {
-  return bdia_t(mb, d, cls, masks, cbase, tab, x, y, s);
+                          const unsigned short* cbase, const unsigned* bnz, const cd* tab, const cd* x, cd* y,
+                          hipStream_t s) {
+  return bdia_t(mb, d, cls, masks, cbase, bnz, tab, x, y, s);
 }
 hipError_t blas_bdia_spmv(i64 mb, const BDiaDesc& d, const unsigned char* cls, const unsigned short* masks,
-                          const unsigned short* cbase, const double* tab, const double* x, double* y, hipStream_t s) {
-  return bdia_t(mb, d, cls, masks, cbase, tab, x, y, s);
+                          const unsigned short* cbase, const unsigned* bnz, const double* tab, const double* x,
+                          double* y, hipStream_t s) {
+  return bdia_t(mb, d, cls, masks, cbase, bnz, tab, x, y, s);
 }
 
 // per-thread device + pinned staging of block partial sums (synchronous reductions).  hd is the

@@ -1173,6 +1173,7 @@ struct _p_Mat {
   cfp::BDiaDesc bdia_d{};
   unsigned char* bdia_cls = nullptr;
   unsigned short *bdia_mask = nullptr, *bdia_cbase = nullptr;
+  unsigned* bdia_bnz = nullptr;
   VS* bdia_tab = nullptr;
   // MatCreateAIJ (r06): entries from MatSetValue(s) wait here until MatAssemblyEnd.  This rank's
   // rows [rstart, rstart + lm); set_*: its own rows' entries, st_*: other ranks' (the stash).
@@ -1308,7 +1309,7 @@ static bool aij_build_dia(Mat M, cfp::DiaDesc* d, std::vector<unsigned char>* cl
 // multiply-adds per row (nd B) wins; the product is the same up to summation order.
 static bool aij_build_bdia_b(Mat M, int B, cfp::BDiaDesc* d, std::vector<unsigned char>* cls,
                              std::vector<unsigned short>* masks, std::vector<unsigned short>* cbase,
-                             std::vector<VS>* tab) {
+                             std::vector<unsigned>* bnz, std::vector<VS>* tab) {
   const i64 m = M->m;
   if (m <= 0 || m % B || M->n != m || M->h_col.empty()) return false;
   const i64 mb = m / B;
@@ -1370,14 +1371,20 @@ static bool aij_build_bdia_b(Mat M, int B, cfp::BDiaDesc* d, std::vector<unsigne
     (*cls)[(size_t)R] = (unsigned char)c;
     last = c;
   }
-  // the table: each class's present blocks in ascending k
+  // the table: each class's present blocks in ascending k, with their nonzero and column masks
   cbase->clear();
+  bnz->clear();
   tab->clear();
+  const VS zero = D(std::complex<double>(0.0, 0.0));
   for (size_t c = 0; c < masks->size(); ++c) {
     cbase->push_back((unsigned short)(tab->size() / (size_t)(B * B)));
     for (int k = 0; k < nd; ++k)
       if (((*masks)[c] >> k) & 1u) {
         const VS* b0 = &dense[c * (size_t)bs + (size_t)k * B * B];
+        unsigned nz = 0;
+        for (int e = 0; e < B * B; ++e)
+          if (std::memcmp(&b0[e], &zero, sizeof(VS)) != 0) nz |= (1u << e) | (1u << (16 + e % B));
+        bnz->push_back(nz);
         tab->insert(tab->end(), b0, b0 + B * B);
       }
   }
@@ -1389,19 +1396,21 @@ static bool aij_build_bdia_b(Mat M, int B, cfp::BDiaDesc* d, std::vector<unsigne
   return true;
 }
 static bool aij_build_bdia(Mat M, cfp::BDiaDesc* d, std::vector<unsigned char>* cls, std::vector<unsigned short>* masks,
-                           std::vector<unsigned short>* cbase, std::vector<VS>* tab) {
+                           std::vector<unsigned short>* cbase, std::vector<unsigned>* bnz, std::vector<VS>* tab) {
   bool any = false;
   for (int B = 4; B >= 2; --B) {
     cfp::BDiaDesc dd{};
     std::vector<unsigned char> cc;
     std::vector<unsigned short> mm, bb;
+    std::vector<unsigned> zz;
     std::vector<VS> tt;
-    if (!aij_build_bdia_b(M, B, &dd, &cc, &mm, &bb, &tt)) continue;
+    if (!aij_build_bdia_b(M, B, &dd, &cc, &mm, &bb, &zz, &tt)) continue;
     if (!any || dd.nd * dd.B < d->nd * d->B) {
       *d = dd;
       cls->swap(cc);
       masks->swap(mm);
       cbase->swap(bb);
+      bnz->swap(zz);
       tab->swap(tt);
       any = true;
     }
@@ -1421,6 +1430,8 @@ static void aij_free_device(Mat M) {
   if (M->bdia_mask) hipFree(M->bdia_mask);
   if (M->bdia_tab) hipFree(M->bdia_tab);
   if (M->bdia_cbase) hipFree(M->bdia_cbase);
+  if (M->bdia_bnz) hipFree(M->bdia_bnz);
+  M->bdia_bnz = nullptr;
   M->bdia_cls = nullptr;
   M->bdia_mask = M->bdia_cbase = nullptr;
   M->bdia_tab = nullptr;
@@ -1465,14 +1476,18 @@ static PetscErrorCode aij_upload(Mat M) {
   if (M->bdia < 0) {
     std::vector<unsigned char> cls;
     std::vector<unsigned short> masks, cbase;
+    std::vector<unsigned> bnz;
     std::vector<VS> tab;
     cfp::BDiaDesc d{};
-    M->bdia = aij_build_bdia(M, &d, &cls, &masks, &cbase, &tab) ? 1 : 0;
+    M->bdia = aij_build_bdia(M, &d, &cls, &masks, &cbase, &bnz, &tab) ? 1 : 0;
     if (M->bdia == 1) {
       const size_t mb = sizeof(unsigned short) * masks.size();
       hipError_t e = hipMalloc(&M->bdia_cls, cls.size());
       if (e == hipSuccess) e = hipMalloc(&M->bdia_mask, mb);
       if (e == hipSuccess) e = hipMalloc(&M->bdia_cbase, mb);
+      if (e == hipSuccess) e = hipMalloc(&M->bdia_bnz, sizeof(unsigned) * bnz.size());
+      if (e == hipSuccess)
+        e = hipMemcpy(M->bdia_bnz, bnz.data(), sizeof(unsigned) * bnz.size(), hipMemcpyHostToDevice);
       if (e == hipSuccess) e = hipMalloc(&M->bdia_tab, sizeof(VS) * tab.size());
       if (e == hipSuccess) e = hipMemcpy(M->bdia_cls, cls.data(), cls.size(), hipMemcpyHostToDevice);
       if (e == hipSuccess) e = hipMemcpy(M->bdia_mask, masks.data(), mb, hipMemcpyHostToDevice);
@@ -1831,8 +1846,8 @@ static PetscErrorCode aij_spmv_dev(Mat B, const VS* xd, VS* yd) {
   if (B->dia == 1)
     HIPK(cfp::blas_dia_spmv(B->m, B->dia_d, B->dia_cls, B->dia_mask, B->dia_tab, xd, yd, g_stream));
   else if (B->bdia == 1)
-    HIPK(cfp::blas_bdia_spmv(B->m / B->bdia_d.B, B->bdia_d, B->bdia_cls, B->bdia_mask, B->bdia_cbase, B->bdia_tab, xd,
-                             yd, g_stream));
+    HIPK(cfp::blas_bdia_spmv(B->m / B->bdia_d.B, B->bdia_d, B->bdia_cls, B->bdia_mask, B->bdia_cbase, B->bdia_bnz,
+                             B->bdia_tab, xd, yd, g_stream));
   else
     HIPK(cfp::blas_csr_spmv(B->m, (i64)B->h_col.size(), B->rowptr, B->col, B->val, xd, yd, g_stream));
   return PETSC_SUCCESS;
