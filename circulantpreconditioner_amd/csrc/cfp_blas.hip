@@ -595,7 +595,12 @@ static hipError_t bdia_t(i64 mb, const BDiaDesc& d, const unsigned char* cls, co
     return hipErrorInvalidValue;
   const size_t lds = (sizeof(T) * d.B * d.B + sizeof(unsigned)) * (size_t)d.nblk + 2 * sizeof(unsigned short) * 256;
   if (lds > BDIA_LDS_MAX + 2048) return hipErrorInvalidValue;
-  const dim3 g(nblocks(mb)), b(BLAS_THREADS);
+  // persistent grid: each workgroup stages the class table into LDS once (tens of KB), so a
+  // workgroup per 256 cells would re-read it ~8,000 times at 128^3; 4 per CU then walk the cells
+  i64 nb = nblocks(mb);
+  const i64 cap = 4 * (i64)blas_cu_count();
+  if (nb > cap) nb = cap;
+  const dim3 g((unsigned)nb), b(BLAS_THREADS);
   switch (d.B) {
     case 2: blaunch(1, (k_bdia_spmv<T, 2>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, bnz, tab, x, y); break;
     case 3: blaunch(1, (k_bdia_spmv<T, 3>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, bnz, tab, x, y); break;
