@@ -16,7 +16,10 @@
 //   P3w k_wtp_rows<inv>: P1w on the conjugate, x 1/N.
 //
 // An apply moves 3 x (read + write) x 64 bytes per cell instead of the 5-sweep schedule's 5 x.
+#include <hip/hip_ext.h>
+
 #include "cfp_fft_device.h"
+#include "cfp_internal.h"
 #include "cfp_lane.h"
 #include "cfp_three_pass.h"
 
@@ -864,6 +867,16 @@ static int wcu_count() {
   return cus;
 }
 
+// a launch that stamps its own dispatch while the stand-in KSP times the apply (g_stamp set by
+// run_wave from g_apply_stamp, cfp_internal.h): the apply's device time without event packets
+#define WTP_LAUNCH(K, G, B, S, ...)                                                                   \
+  do {                                                                                                \
+    if (g_stamp.start || g_stamp.stop)                                                                \
+      hipExtLaunchKernelGGL(K, G, B, 0, S, g_stamp.start, g_stamp.stop, 0, __VA_ARGS__);              \
+    else                                                                                              \
+      hipLaunchKernelGGL(K, G, B, 0, S, __VA_ARGS__);                                                 \
+  } while (0)
+
 hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArgs& a, hipStream_t s) {
   // persistent grids, two 512-thread workgroups per CU (70 / 64 KiB of LDS each)
   const int g = 2 * wcu_count();
@@ -874,11 +887,11 @@ hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArg
     // P2w 64.9-65.0 against 65.5-66.2 us; the whole apply within the noise); -DCFP_WAVE_MID_XCD=0: A/B
     const unsigned gm = units < g ? units : g;
     if (((uintptr_t)out & 15) == 0 && CFP_WAVE_MID_XCD && gm % 8 == 0)
-      hipLaunchKernelGGL((k_wtp_mid_ct2<true, 0, true, true>), dim3(gm), dim3(512), 0, s, out, a, units);
+      WTP_LAUNCH((k_wtp_mid_ct2<true, 0, true, true>), dim3(gm), dim3(512), s, out, a, units);
     else if (((uintptr_t)out & 15) == 0)
-      hipLaunchKernelGGL((k_wtp_mid_ct2<true, 0, true>), dim3(units < g ? units : g), dim3(512), 0, s, out, a, units);
+      WTP_LAUNCH((k_wtp_mid_ct2<true, 0, true>), dim3(units < g ? units : g), dim3(512), s, out, a, units);
     else
-      hipLaunchKernelGGL((k_wtp_mid_ct2<true>), dim3(units < g ? units : g), dim3(512), 0, s, out, a, units);
+      WTP_LAUNCH((k_wtp_mid_ct2<true>), dim3(units < g ? units : g), dim3(512), s, out, a, units);
   } else {
     const int units = WNX * WN2;  // z-planes x y2
     // P1w out of place: non-temporal loads keep b out of the 256 MB Infinity Cache, which then
@@ -887,15 +900,15 @@ hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArg
     // units in XCD order (CFP_ROWS_XCD) when the grid is a multiple of 8 workgroups
     const bool xo = CFP_ROWS_XCD != 0 && gg.x % 8 == 0;
     if (stage == 0 && in != out && xo)
-      hipLaunchKernelGGL((k_wtp_rows<false, F_NT_LD, true>), gg, dim3(512), 0, s, in, out, a, units);
+      WTP_LAUNCH((k_wtp_rows<false, F_NT_LD, true>), gg, dim3(512), s, in, out, a, units);
     else if (stage == 0 && in != out)
-      hipLaunchKernelGGL((k_wtp_rows<false, F_NT_LD>), gg, dim3(512), 0, s, in, out, a, units);
+      WTP_LAUNCH((k_wtp_rows<false, F_NT_LD>), gg, dim3(512), s, in, out, a, units);
     else if (stage == 0)
-      hipLaunchKernelGGL((k_wtp_rows<false, 0>), gg, dim3(512), 0, s, in, out, a, units);
+      WTP_LAUNCH((k_wtp_rows<false, 0>), gg, dim3(512), s, in, out, a, units);
     else if (xo)
-      hipLaunchKernelGGL((k_wtp_rows<true, F_NT_ST, true>), gg, dim3(512), 0, s, in, out, a, units);
+      WTP_LAUNCH((k_wtp_rows<true, F_NT_ST, true>), gg, dim3(512), s, in, out, a, units);
     else
-      hipLaunchKernelGGL((k_wtp_rows<true, F_NT_ST>), gg, dim3(512), 0, s, in, out, a, units);
+      WTP_LAUNCH((k_wtp_rows<true, F_NT_ST>), gg, dim3(512), s, in, out, a, units);
   }
   return hipGetLastError();
 }
