@@ -437,7 +437,7 @@ __global__ void __launch_bounds__(BLAS_THREADS) k_dia_spmv(i64 m, DiaDesc d, con
 // (the wave operator: 4 of 16 entries in a neighbour block, 2 of 4 columns).  The interleaved wave
 // operator on a Cartesian grid: x read once through the caches, y written once, one class byte per
 // cell -- against CSR's 24 bytes per nonzero (about 28 nonzeros per 3-D cell).
-template <class T, int B, int NDC>
+template <class T, int B>
 __global__ void __launch_bounds__(BLAS_THREADS) k_bdia_spmv(i64 mb, BDiaDesc d, const unsigned char* cls,
                                                             const unsigned short* masks, const unsigned short* cbase,
                                                             const unsigned* bnz, const T* tab, const T* x, T* y) {
@@ -454,36 +454,31 @@ __global__ void __launch_bounds__(BLAS_THREADS) k_bdia_spmv(i64 mb, BDiaDesc d, 
     sb[i] = cbase[i];
   }
   __syncthreads();
-  GRID_LOOP(r, mb) {
-    // the neighbours' loads do not wait for the class: every diagonal's block is loaded at a
-    // clamped (always valid) cell and an absent one is selected to zero afterwards, so the
-    // compiler can issue the loads of all NDC diagonals together (diagonals nd..NDC-1 have
-    // offset 0 and are never present)
-    const int c = cls[r];
-    T xv[NDC][B];
-#pragma unroll
-    for (int k = 0; k < NDC; ++k) {
-      i64 j = r + d.off[k];
-      j = j < 0 ? 0 : (j >= mb ? mb - 1 : j);
-      const T* xb = x + j * B;
-#pragma unroll
-      for (int t = 0; t < B; ++t) xv[k][t] = xb[t];
-    }
+  const i64 stride = (i64)gridDim.x * blockDim.x;
+  i64 r = (i64)blockIdx.x * blockDim.x + threadIdx.x;
+  int cn = r < mb ? cls[r] : 0;  // the class byte of the next cell is loaded one iteration ahead
+  for (; r < mb; r += stride) {
+    const int c = cn;
+    if (r + stride < mb) cn = cls[r + stride];
     const unsigned mk = sm[c];
     int q = sb[c];
     double ax[B], ay[B];
 #pragma unroll
     for (int i = 0; i < B; ++i) ax[i] = ay[i] = 0.0;
 #pragma unroll
-    for (int k = 0; k < NDC; ++k) {
-      if ((mk >> k) & 1u) {
+    for (int k = 0; k < BDIA_MAX; ++k) {
+      if (k < d.nd && ((mk >> k) & 1u)) {
+        const T* xb = x + (r + d.off[k]) * B;
         const T* blk = st + q * B * B;
         const unsigned nz = sz[q];
+        T xv[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) xv[j] = ((nz >> (16 + j)) & 1u) ? xb[j] : T{};
 #pragma unroll
         for (int i = 0; i < B; ++i)
 #pragma unroll
-          for (int t = 0; t < B; ++t)
-            if ((nz >> (i * B + t)) & 1u) spmv_acc(blk[i * B + t], xv[k][t], ax[i], ay[i]);
+          for (int j = 0; j < B; ++j)
+            if ((nz >> (i * B + j)) & 1u) spmv_acc(blk[i * B + j], xv[j], ax[i], ay[i]);
         ++q;
       }
     }
@@ -610,14 +605,11 @@ static hipError_t bdia_t(i64 mb, const BDiaDesc& d, const unsigned char* cls, co
   const i64 cap = 4 * (i64)blas_cu_count();
   if (nb > cap) nb = cap;
   const dim3 g((unsigned)nb), b(BLAS_THREADS);
-  BDiaDesc dd = d;
-  const int ndc = d.nd <= 8 ? 8 : 16;
-  for (int k = d.nd; k < BDIA_MAX; ++k) dd.off[k] = 0;  // padding diagonals: never present
-#define BDL(BB, NN) blaunch(1, (k_bdia_spmv<T, BB, NN>), g, b, (unsigned)lds, s, mb, dd, cls, masks, cbase, bnz, tab, x, y)
-  if (d.B == 2) ndc == 8 ? BDL(2, 8) : BDL(2, 16);
-  else if (d.B == 3) ndc == 8 ? BDL(3, 8) : BDL(3, 16);
-  else ndc == 8 ? BDL(4, 8) : BDL(4, 16);
-#undef BDL
+  switch (d.B) {
+    case 2: blaunch(1, (k_bdia_spmv<T, 2>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, bnz, tab, x, y); break;
+    case 3: blaunch(1, (k_bdia_spmv<T, 3>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, bnz, tab, x, y); break;
+    default: blaunch(1, (k_bdia_spmv<T, 4>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, bnz, tab, x, y);
+  }
   return hipGetLastError();
 }
 hipError_t blas_bdia_spmv(i64 mb, const BDiaDesc& d, const unsigned char* cls, const unsigned short* masks,
