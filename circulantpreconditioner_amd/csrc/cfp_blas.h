@@ -120,4 +120,6 @@ hipError_t kprof_copy(void* dst, const void* src, size_t bytes, hipMemcpyKind ki
 // device-to-device copy on the library's tuned kernel (16-byte lanes, NT stores; kprof kind 3);
 // unaligned or odd sizes go through hipMemcpyAsync
 hipError_t blas_copy_bytes(void* dst, const void* src, size_t bytes, hipStream_t s);
+// wait on the host for the work queued on s so far (an event polled; see cfp_blas.hip)
+hipError_t host_wait(hipStream_t s);
 }  // namespace cfp

@@ -86,6 +86,25 @@ hipError_t kprof_copy(void* dst, const void* src, size_t bytes, hipMemcpyKind ki
   return r;
 }
 
+// The host's wait for a reduction result (the Krylov loop waits once per iteration): an event
+// recorded on the stream and polled, instead of hipStreamSynchronize.  The result itself is
+// already in pinned host memory when the event completes; polling returns a few microseconds
+// sooner than the blocking wait, and the next launches follow at once.
+hipError_t host_wait(hipStream_t s) {
+  static thread_local hipEvent_t ev = nullptr;
+  if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+    ev = nullptr;
+    return hipStreamSynchronize(s);
+  }
+  hipError_t e = hipEventRecord(ev, s);
+  if (e != hipSuccess) return e;
+  for (;;) {
+    e = hipEventQuery(ev);
+    if (e != hipErrorNotReady) return e;
+    __builtin_ia32_pause();
+  }
+}
+
 // Device-to-device copy (VecCopy, cfp_device_copy): 16-byte lanes, four 256-thread workgroups per
 // CU striding the vector, non-temporal stores (the copy's destination is not read back soon; the
 // source keeps its Infinity Cache lines).  tools/kexp/copy_probe.hip measured this shape at
@@ -672,7 +691,7 @@ static hipError_t maxpy_t(T* y, int k, const T* a, const T* const* xs, i64 n, bo
     *norm2 = 0.0;
     return hipSuccess;
   }
-  e = hipStreamSynchronize(s);  // the partials are in pinned host memory
+  e = host_wait(s);  // the partials are in pinned host memory
   if (e != hipSuccess) return e;
   double t = 0.0;
   for (unsigned q = 0; q < nb; ++q) t += part.h[q];
@@ -703,7 +722,7 @@ static hipError_t reduce(const T* x, const T* y, i64 n, int kind, double out[2],
   unsigned nb = nblocks(n);
   if (nb > RED_BLOCKS) nb = RED_BLOCKS;
   blaunch(2, k_reduce<T>, dim3(nb), dim3(BLAS_THREADS), 0, s, x, y, n, kind, part.hd);
-  e = hipStreamSynchronize(s);  // the partials are in pinned host memory
+  e = host_wait(s);  // the partials are in pinned host memory
   if (e != hipSuccess) return e;
   double a = 0.0, b = 0.0;
   for (unsigned k = 0; k < nb; ++k) {
@@ -754,7 +773,7 @@ static hipError_t mdot_t(const T* x, int k, const T* const* ys, i64 n, double* v
     blaunch(2, k_mdot<T>, dim3(nb), dim3(BLAS_THREADS), 0, s, x, kk, p, n, part.d);
     e = kprof_copy(part.h, part.d, sizeof(double) * 2 * MDOT_K * nb, hipMemcpyDeviceToHost, s);
     if (e != hipSuccess) return e;
-    e = hipStreamSynchronize(s);
+    e = host_wait(s);
     if (e != hipSuccess) return e;
     for (int j = 0; j < kk; ++j) {
       double ra = 0.0, rb = 0.0;
@@ -825,7 +844,7 @@ static hipError_t maxpy_dc_norm_t(T* w, int k, const T* const* ys, const double*
   blaunch(2, k_maxpy_dc<T>, dim3(mb), dim3(BLAS_THREADS), 0, s, w, k, sc, dd, p, n, part.hd + dlen, part.hd);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  e = hipStreamSynchronize(s);
+  e = host_wait(s);
   if (e != hipSuccess) return e;
   for (int o = 0; o < 2 * k; ++o) dots[o] = part.h[o];
   double t = 0.0;

@@ -363,7 +363,7 @@ static PetscErrorCode vcheck(Vec v, const char* f) {
 // host-timed region that starts here does not include earlier asynchronous work
 extern "C" PetscErrorCode VecMiniSynchronize(Vec v) {
   VCHK(v);
-  if (v->hip) HCHK(hipStreamSynchronize(g_stream));
+  if (v->hip) HCHK(cfp::host_wait(g_stream));
   return PETSC_SUCCESS;
 }
 
