@@ -443,7 +443,8 @@ def wave_gmres_leg(n: int, steps: int) -> dict:
     rtol = abstol = 1e-5, restart 30) on an n^3 grid, with the (d+1)-block-circulant PCSHELL
     (applyFFT3DPrecWave) on one GPU, `steps` implicit steps after a 1-step warm-up run.  Device time
     per step from the library's dispatch stamps, split by kind (the MatMult runs the block
-    row-class SpMV of the interleaved operator)."""
+    row-class SpMV of the interleaved operator; the Gram-Schmidt dot and the residual norm ride
+    in the block apply's last sweep, fused_dots / fused_norms)."""
     from circulantpreconditioner_amd import wave as W
     W.run(W.config(n, pc="fft", steps=1))  # warm-up (plan, operator upload)
     r = W.run(W.config(n, pc="fft", steps=steps, profile=1))
@@ -458,6 +459,7 @@ def wave_gmres_leg(n: int, steps: int) -> dict:
             "pcapply_us": round(1e6 * r["pc_seconds"] / max(1, r["pc_calls"]), 1),
             "wall_ms_per_step": round(1e3 * r["loop_seconds"] / k, 4),
             "wall_ms_per_solve": round(1e3 * r["solve_seconds"] / k, 4),
+            "fused_dots": r["fused_dots"], "fused_norms": r["fused_norms"],
             "check": {"what": "every solve converged (KSP reason 2/3)", "ok": ok}}
 
 

@@ -73,7 +73,7 @@ class WaveConfig(ctypes.Structure):
                 ("cfl", ctypes.c_double), ("tmax", ctypes.c_double), ("ntmax", ctypes.c_int64),
                 ("precision", ctypes.c_double), ("max_its", ctypes.c_int64), ("restart", ctypes.c_int64),
                 ("pc", ctypes.c_int), ("bc", ctypes.c_int), ("pc_side", ctypes.c_int), ("on_device", ctypes.c_int),
-                ("dim", ctypes.c_int), ("profile", ctypes.c_int)]
+                ("dim", ctypes.c_int), ("profile", ctypes.c_int), ("fuse", ctypes.c_int)]
 
 
 class WaveResult(ctypes.Structure):
@@ -85,7 +85,7 @@ class WaveResult(ctypes.Structure):
                 ("pc_seconds", ctypes.c_double), ("pc_calls", ctypes.c_int64), ("setup_seconds", ctypes.c_double),
                 ("kappa", ctypes.c_double * 3), ("rstart", ctypes.c_int64), ("nlocal", ctypes.c_int64),
                 ("loop_seconds", ctypes.c_double), ("dev_ms_", ctypes.c_double * 4),
-                ("dev_launches_", ctypes.c_int64 * 4)]
+                ("dev_launches_", ctypes.c_int64 * 4), ("fused_dots", ctypes.c_int64), ("fused_norms", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if k != "kappa" and not k.endswith("_")}
@@ -278,6 +278,7 @@ def declare(L) -> None:
         "cfp_wave_plan_destroy": ([vp], c_int),
         "cfp_wave_plan_set_symbol": ([vp, P(ctypes.c_double), ctypes.c_double], c_int),
         "cfp_wave_plan_apply": ([vp, dp, dp, vp], c_int),
+        "cfp_wave_plan_apply_dots": ([vp, dp, dp, vp, c_int, ctypes.POINTER(ctypes.c_void_p), dp, P(c_int)], c_int),
         "cfp_wave_plan_set_schedule": ([vp, c_int], c_int),
         "cfp_wave_plan_forward": ([vp, dp, dp, vp], c_int),
         "cfp_wave_plan_backward": ([vp, dp, dp, vp], c_int),

@@ -98,8 +98,16 @@ struct WTPArgs {
   const cd* tw;
   WaveSym wave;
   double scale;
+  // P3w with the Gram-Schmidt dots (r06, as the scalar P3's post_*): post_v[j]^H x over the
+  // stored points for j < post_nv <= TP_POST_MAX (bit j of post_self: x itself), one partial per
+  // workgroup and value into post_partial[block][16] (k_mdot's layout)
+  const cd* post_v[4] = {nullptr, nullptr, nullptr, nullptr};
+  int post_nv = 0, post_self = 0;
+  double* post_partial = nullptr;
 };
 bool wave_three_pass_supported(const i64 n[3], int ncomp);
-hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArgs& a, hipStream_t s);
+// grid_out (optional): the workgroups of the launch (the dots' partial count for stage 2)
+hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArgs& a, hipStream_t s,
+                                  unsigned* grid_out = nullptr);
 
 }  // namespace cfp

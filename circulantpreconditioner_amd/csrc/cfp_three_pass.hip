@@ -79,18 +79,6 @@ __device__ __forceinline__ int xcd_unit(int it, int G) {
   return it - b + (b & 7) * (G >> 3) + (b >> 3);
 }
 
-// sum over the wave's 64 lanes (every lane gets it): DPP within rows, swizzle across 16, permlane32
-__device__ __forceinline__ double wave_sum_d(double v) {
-  v += dpp_d<DPP_XOR1>(v);
-  v += dpp_d<DPP_XOR2>(v);
-  v += dpp_d<DPP_XOR3>(dpp_d<DPP_HALF_MIRROR>(v));  // lane ^ 4
-  v += dpp_d<DPP_ROW_ROR8>(v);
-  v += swz_xor16(v);
-  double w = v;
-  swap_d<5>(v, w);  // lanes < 32 get (v, v[L + 32]) pairs' partner in w
-  return v + w;
-}
-
 // a byte load with the sweep's load policy (the fused stencil's row classes)
 template <int FLAGS>
 __device__ __forceinline__ unsigned char gload_u8(const unsigned char* p) {

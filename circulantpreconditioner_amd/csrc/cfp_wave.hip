@@ -23,6 +23,7 @@
 
 #include "../../include/circulant_fft.h"
 #include "../../include/wave_system.h"
+#include "cfp_blas.h"
 #include "cfp_host.h"
 #include "cfp_internal.h"
 #include "cfp_three_pass.h"
@@ -48,6 +49,7 @@ struct cfp_wave_plan_s {
   std::vector<int> axes;
   int fused = 0;
   int schedule = CFP_SCHEDULE_AUTO;  // AUTO: 3 sweeps where cfp_wave_three.hip serves the grid
+  double* post_partial = nullptr;    // P3w's dot partials (cfp_wave_plan_apply_dots)
 };
 
 namespace {
@@ -142,7 +144,8 @@ std::vector<WStep> wave_steps(const cfp_wave_plan_s* p) {
   return st;
 }
 
-int run_wave(cfp_wave_plan_s* p, const cd* b, cd* x, hipStream_t s, std::vector<hipEvent_t>* ev) {
+int run_wave(cfp_wave_plan_s* p, const cd* b, cd* x, hipStream_t s, std::vector<hipEvent_t>* ev,
+             const WTPArgs* post = nullptr, unsigned* p3grid = nullptr) {
   if (!p->has_sym) return set_error(CFP_ERR_ARG_WRONGSTATE, "no symbol set (call cfp_wave_plan_set_symbol)");
   std::vector<WStep> st = wave_steps(p);
   const double invN = 1.0 / (double)p->N;
@@ -155,6 +158,12 @@ int run_wave(cfp_wave_plan_s* p, const cd* b, cd* x, hipStream_t s, std::vector<
       a.wave = wave_pass(p, 2, PASS_FUSED_WAVE, 1.0).wave;
       a.wave.fused = 2;
       a.scale = q.scale ? invN : 1.0;
+      if (post && q.tp == 2) {
+        for (int j = 0; j < 4; ++j) a.post_v[j] = post->post_v[j];
+        a.post_nv = post->post_nv;
+        a.post_self = post->post_self;
+        a.post_partial = post->post_partial;
+      }
       if (!ev && g_apply_stamp.start) {  // the caller times the whole apply (stand-in KSP)
         if (i == 0) {
           g_stamp.start = g_apply_stamp.start;
@@ -165,7 +174,7 @@ int run_wave(cfp_wave_plan_s* p, const cd* b, cd* x, hipStream_t s, std::vector<
           ++g_apply_stamp.hits;
         }
       }
-      hipError_t e = launch_wave_three_pass(q.tp, q.from_b ? b : x, x, a, s);
+      hipError_t e = launch_wave_three_pass(q.tp, q.from_b ? b : x, x, a, s, q.tp == 2 ? p3grid : nullptr);
       g_stamp = LaunchStamp{};
       if (e != hipSuccess) return hip_error(e, "wave 3-sweep launch");
       continue;
@@ -235,6 +244,7 @@ extern "C" int cfp_wave_plan_destroy(cfp_wave_plan_t p) {
   for (auto& kv : p->tw) hipFree(kv.second);
   for (int a = 0; a < 3; ++a)
     if (p->tab[a]) hipFree(p->tab[a]);
+  if (p->post_partial) hipFree(p->post_partial);
   delete p;
   return CFP_SUCCESS;
 }
@@ -266,6 +276,44 @@ extern "C" int cfp_wave_plan_apply(cfp_wave_plan_t p, const double* b, double* x
   if (!p || !b || !x) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
   Guard g(p->device);
   return run_wave(p, (const cd*)b, (cd*)x, (hipStream_t)stream, nullptr);
+}
+
+// x = S^{-1} b and dots[2 j + re/im] = v[j]^H x (v[j] NULL or x: |x|^2), dots a device array.
+// On the 3-sweep schedule the dots ride in P3w's stores (*fused = 1, at most 4 vectors);
+// otherwise the apply runs, then one multi-dot sweep (*fused = 0).
+extern "C" int cfp_wave_plan_apply_dots(cfp_wave_plan_t p, const double* b, double* x, void* stream, int nv,
+                                        const double* const* v, double* dots, int* fused) {
+  if (!p || !b || !x || (nv > 0 && (!v || !dots))) return set_error(CFP_ERR_ARG_NULL, "NULL argument");
+  if (nv < 0 || nv > 8) return set_error(CFP_ERR_ARG_OUTOFRANGE, "nv must be in 0..8");
+  if (fused) *fused = 0;
+  Guard g(p->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (nv == 0) return run_wave(p, (const cd*)b, (cd*)x, s, nullptr);
+  if (use_three(p) && nv <= 4) {
+    if (!p->post_partial) HIPCHK(hipMalloc(&p->post_partial, sizeof(double) * 16 * 1024));
+    WTPArgs post;
+    for (int j = 0; j < nv; ++j) {
+      post.post_v[j] = (const cd*)v[j];
+      if (!v[j] || v[j] == x) post.post_self |= 1 << j;
+    }
+    post.post_nv = nv;
+    post.post_partial = p->post_partial;
+    unsigned gp = 0;
+    int rc = run_wave(p, (const cd*)b, (cd*)x, s, nullptr, &post, &gp);
+    if (rc) return rc;
+    if (gp < 1 || gp > 1024) return set_error(CFP_ERR_LIB, "P3w grid out of range");
+    hipError_t e = blas_mdot_finish(p->post_partial, (int)gp, nv, dots, s);
+    if (e != hipSuccess) return hip_error(e, "dots finish");
+    if (fused) *fused = 1;
+    return CFP_SUCCESS;
+  }
+  int rc = run_wave(p, (const cd*)b, (cd*)x, s, nullptr);
+  if (rc) return rc;
+  const cd* ys[8];
+  for (int j = 0; j < nv; ++j) ys[j] = (const cd*)v[j] == (const cd*)x ? nullptr : (const cd*)v[j];
+  hipError_t e = blas_mdot_dev((const cd*)x, nv, ys, p->N * p->ncomp, dots, s);
+  if (e != hipSuccess) return hip_error(e, "dots");
+  return CFP_SUCCESS;
 }
 
 extern "C" int cfp_wave_plan_forward(cfp_wave_plan_t p, const double* in, double* out, void* stream) {

@@ -54,9 +54,27 @@ constexpr int wr0_of(int n, int pts) { return n > pts ? wr0_of(n / pts, pts) : n
 // P1w / P3w.  512 threads, 16 points each; one unit = (z, y2); persistent over the units.
 // FLAGS: the global load / store policy (F_NT_LD, F_NT_ST).  XCD: units in xcd_round_unit order
 // (the grid a multiple of 8 workgroups).
-template <bool INV, int FLAGS, bool XCD = false>
+// NP > 0 (P3w only): the Gram-Schmidt dots post_v[j]^H x of the stored points ride in the sweep
+// (WTPArgs post_*), as in the scalar P3 (cfp_three_pass.hip): per unit the lanes' sums are wave
+// reductions added to the wave's LDS slot, one partial per workgroup and value at the end.
+template <bool INV, int FLAGS, bool XCD = false, int NP = 0>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 k_wtp_rows(const cd* in, cd* out, WTPArgs a, int nunits) {
+  constexpr bool POST = INV && NP > 0;
+  constexpr int NPP = POST ? NP : 1;
+  constexpr int NW = 512 / 64;
+  __shared__ double post_l[POST ? 2 * NPP * NW : 1];
+  __shared__ const cd* post_ptr_l[NPP];
+  __shared__ int post_n_l[2];  // post_nv, post_self
+  if constexpr (POST) {
+    for (int i = threadIdx.x; i < 2 * NPP * NW; i += 512) post_l[i] = 0.0;
+    if (threadIdx.x < NPP) post_ptr_l[threadIdx.x] = a.post_v[threadIdx.x];
+    if (threadIdx.x == 0) {
+      post_n_l[0] = a.post_nv;
+      post_n_l[1] = a.post_self;
+    }
+    __syncthreads();
+  }
   constexpr int PTS = 16, TR = WNX / PTS;  // row mode: 8 threads per (row, comp)
   constexpr int NROW = WN1 * WNC;          // 64 row-mode rows (k1, comp)
   constexpr int CS = WW + WW / 16;         // padded stride of the column-mode transpose rows
@@ -121,10 +139,59 @@ k_wtp_rows(const cd* in, cd* out, WTPArgs a, int nunits) {
         for (int t = 0; t < PTS; ++t) gstore<FLAGS>(dst + WNC * TR * t, cmul(v[t], w));
       } else {
 #pragma unroll
-        for (int t = 0; t < PTS; ++t) gstore<FLAGS>(dst + WNC * TR * t, make_cd(v[t].x * sc, v[t].y * sy));
+        for (int t = 0; t < PTS; ++t) {
+          v[t] = make_cd(v[t].x * sc, v[t].y * sy);
+          gstore<FLAGS>(dst + WNC * TR * t, v[t]);
+        }
+      }
+      if constexpr (POST) {
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        const int pnv = ((volatile int*)post_n_l)[0], pself = ((volatile int*)post_n_l)[1];
+        const i64 e0 = dst - out;
+        constexpr int QB = 4;
+#pragma unroll
+        for (int j = 0; j < NPP; ++j) {
+          if (j < pnv) {
+            double sr = 0.0, si = 0.0;
+            if ((pself >> j) & 1) {
+#pragma unroll
+              for (int t = 0; t < PTS; ++t) sr += v[t].x * v[t].x + v[t].y * v[t].y;
+            } else {
+              const cd* pv = ((const cd* volatile*)post_ptr_l)[j] + e0;
+#pragma unroll
+              for (int t0 = 0; t0 < PTS; t0 += QB) {
+                cd q[QB];
+#pragma unroll
+                for (int t = 0; t < QB; ++t) q[t] = gload<F_NT_LD>(pv + WNC * TR * (t0 + t));
+#pragma unroll
+                for (int t = 0; t < QB; ++t) {
+                  const cd w = v[t0 + t];
+                  sr += q[t].x * w.x + q[t].y * w.y;
+                  si += q[t].x * w.y - q[t].y * w.x;
+                }
+              }
+            }
+            sr = wave_sum_d(sr);
+            si = wave_sum_d(si);
+            if (lane == 0) {
+              post_l[(2 * j) * NW + wv] += sr;
+              post_l[(2 * j + 1) * NW + wv] += si;
+            }
+          }
+        }
       }
     }
     lds_barrier();  // the next unit's first exchange overwrites LDS
+  }
+  if constexpr (POST) {
+    // one partial per workgroup and value: the waves' sums in a fixed order
+    __syncthreads();
+    if (threadIdx.x < 2 * NPP) {
+      double t = 0.0;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) t += post_l[threadIdx.x * NW + q];
+      a.post_partial[(size_t)blockIdx.x * 16 + threadIdx.x] = t;
+    }
   }
 }
 
@@ -877,7 +944,8 @@ static int wcu_count() {
       hipLaunchKernelGGL(K, G, B, 0, S, __VA_ARGS__);                                                 \
   } while (0)
 
-hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArgs& a, hipStream_t s) {
+hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArgs& a, hipStream_t s,
+                                  unsigned* grid_out) {
   // persistent grids, two 512-thread workgroups per CU (70 / 64 KiB of LDS each)
   const int g = 2 * wcu_count();
   if (stage == 1) {
@@ -905,10 +973,17 @@ hipError_t launch_wave_three_pass(int stage, const cd* in, cd* out, const WTPArg
       WTP_LAUNCH((k_wtp_rows<false, F_NT_LD>), gg, dim3(512), s, in, out, a, units);
     else if (stage == 0)
       WTP_LAUNCH((k_wtp_rows<false, 0>), gg, dim3(512), s, in, out, a, units);
-    else if (xo)
+    else if (a.post_nv > 0) {  // P3w with the dots
+      if (a.post_nv > 4 || !a.post_partial || gg.x > 1024) return hipErrorInvalidValue;
+      if (xo)
+        WTP_LAUNCH((k_wtp_rows<true, F_NT_ST, true, 4>), gg, dim3(512), s, in, out, a, units);
+      else
+        WTP_LAUNCH((k_wtp_rows<true, F_NT_ST, false, 4>), gg, dim3(512), s, in, out, a, units);
+    } else if (xo)
       WTP_LAUNCH((k_wtp_rows<true, F_NT_ST, true>), gg, dim3(512), s, in, out, a, units);
     else
       WTP_LAUNCH((k_wtp_rows<true, F_NT_ST>), gg, dim3(512), s, in, out, a, units);
+    if (grid_out) *grid_out = gg.x;
   }
   return hipGetLastError();
 }

@@ -454,6 +454,23 @@ extern "C" PetscErrorCode applyFFT3DPrecWave(PC pc, Vec b, Vec x) {
   void* st = nullptr;
   bool wait = true;
   if (!in.tmp && !out.tmp) device_stream(&st, &wait);
+  // the stand-in KSP may ask for dots of x with its basis (PCMiniApplyDots): on the 3-sweep
+  // schedule they ride in the last sweep's stores (cfp_wave_plan_apply_dots); otherwise the
+  // request stays open and the KSP runs its own multi-dot
+  PCMiniApplyDots* req = nullptr;
+  int npass = 0;
+  if (!in.tmp && !out.tmp && PCMiniGetApplyDots(pc, &req) == PETSC_SUCCESS && req && !req->done && req->nv >= 1 &&
+      req->nv <= 4 && cfp_wave_plan_num_passes(ctx->plan, &npass) == CFP_SUCCESS && npass == 3) {
+    int fused = 0;
+    int rc = cfp_wave_plan_apply_dots(ctx->plan, in.ptr(), out.ptr(), st, (int)req->nv,
+                                      reinterpret_cast<const double* const*>(req->v), req->out, &fused);
+    if (rc == CFP_SUCCESS && fused) req->done = PETSC_TRUE;
+    if (rc == CFP_SUCCESS && wait) rc = cfp_stream_sync(st);
+    PetscCall(out.put());
+    PetscCall(in.put());
+    CFPCALL(rc);
+    PetscFunctionReturn(PETSC_SUCCESS);
+  }
   int rc = cfp_wave_plan_apply(ctx->plan, in.ptr(), out.ptr(), st);
   if (rc == CFP_SUCCESS && (wait || in.tmp || out.tmp)) rc = cfp_stream_sync(st);
   PetscCall(out.put());
@@ -495,6 +512,7 @@ extern "C" void cfp_wave_config_default(cfp_wave_config* cfg, int64_t n) {
   cfg->pc_side = PC_LEFT;
   cfg->on_device = 1;
   cfg->dim = 3;
+  cfg->fuse = 1;
 }
 
 extern "C" void cfp_wave_config_default_dim(cfp_wave_config* cfg, int64_t n, int dim) {
@@ -554,6 +572,7 @@ extern "C" PetscErrorCode WaveSystemGMRES(const cfp_wave_config* cfg, cfp_wave_r
   PetscCall(KSPSetTolerances(ksp, cfg->precision, cfg->precision, PETSC_DEFAULT, cfg->max_its));
   PetscCall(KSPGMRESSetRestart(ksp, cfg->restart > 0 ? cfg->restart : 30));
   PetscCall(KSPSetPCSide(ksp, (PCSide)cfg->pc_side));
+  PetscCall(KSPMiniSetFusion(ksp, cfg->fuse ? PETSC_TRUE : PETSC_FALSE));
   PetscCall(KSPGetPC(ksp, &pc));
   FFTPrecWaveContext ctx;
   std::memset((void*)&ctx, 0, sizeof(ctx));
@@ -620,6 +639,10 @@ extern "C" PetscErrorCode WaveSystemGMRES(const cfp_wave_config* cfg, cfp_wave_r
     res->last_residual = residu;
     res->last_norm_dU = norm;
     if (reason != KSP_CONVERGED_RTOL && reason != KSP_CONVERGED_ATOL) res->all_converged = 0;
+    PetscInt fd, fn;
+    PetscCall(KSPMiniGetFusedCounts(ksp, &fd, &fn));
+    res->fused_dots += fd;
+    res->fused_norms += fn;
   }
   res->loop_seconds = wall() - t_loop;
   if (cfg->profile) {

@@ -69,6 +69,20 @@ class WavePlan:
                                         _stream_handle(stream)))
         return out
 
+    def apply_dots(self, b: torch.Tensor, out: torch.Tensor | None = None, dots_with=(), stream=None):
+        """x = S^{-1} b and the dots v^H x for each v in dots_with (None: x itself), at most 8,
+        computed inside the last sweep on the 3-sweep schedule (cfp_wave_plan_apply_dots).
+        Returns (x, dots as a complex128 tensor on the device, fused)."""
+        if out is None:
+            out = torch.empty_like(b)
+        nv = len(dots_with)
+        dots = torch.zeros(max(1, nv), dtype=torch.complex128, device=b.device)
+        ptrs = (ctypes.c_void_p * max(1, nv))(*[None if v is None else _dev_ptr(v, self.size, "v") for v in dots_with])
+        fused = ctypes.c_int()
+        check(lib().cfp_wave_plan_apply_dots(self._h, _dev_ptr(b, self.size, "b"), _dev_ptr(out, self.size, "out"),
+                                             _stream_handle(stream), nv, ptrs, dots.data_ptr(), ctypes.byref(fused)))
+        return out, dots[:nv], fused.value
+
     def forward(self, x: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
         if out is None:
             out = torch.empty_like(x)

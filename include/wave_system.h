@@ -42,6 +42,13 @@ int cfp_wave_plan_destroy(cfp_wave_plan_t plan);
 int cfp_wave_plan_set_symbol(cfp_wave_plan_t plan, const double kappa[3], double c0);
 /* x = S^{-1} b on the periodic grid (b, x: (dim+1)*nx*ny*nz complex doubles; x may alias b) */
 int cfp_wave_plan_apply(cfp_wave_plan_t plan, const double *b, double *x, void *stream);
+/* x = S^{-1} b and dots[2 j], dots[2 j + 1] = Re, Im of v[j]^H x for j < nv <= 8 (v[j] NULL or x:
+ * |x|^2); dots is a device array of 2 nv doubles, written on `stream`.  On the 3-sweep schedule
+ * (3-D 128^3) and nv <= 4 the dots ride in the last sweep's stores (*fused = 1: the Gram-Schmidt
+ * dots of the stand-in GMRES, PCMiniApplyDots); otherwise one multi-dot sweep follows the apply
+ * (*fused = 0). */
+int cfp_wave_plan_apply_dots(cfp_wave_plan_t plan, const double *b, double *x, void *stream, int nv,
+                             const double *const *v, double *dots, int *fused);
 /* unnormalised forward / backward 3-D DFT of each component (tests and tools) */
 int cfp_wave_plan_forward(cfp_wave_plan_t plan, const double *in, double *out, void *stream);
 int cfp_wave_plan_backward(cfp_wave_plan_t plan, const double *in, double *out, void *stream);
@@ -116,6 +123,8 @@ typedef struct {
   int on_device;
   int dim;            /* mesh dimension 1, 2 or 3 (nbComp = dim + 1); 0 = 3 */
   int profile;        /* 1: stamp every kernel of the time loop (PetscMiniProfileBegin): dev_ms below */
+  int fuse;           /* 1 (default): the KSP asks the block PCSHELL for the Gram-Schmidt dots
+                         (KSPMiniSetFusion; they ride in the 3-sweep apply); 0: separate sweeps */
 } cfp_wave_config;
 
 /* same layout as cfp_transport_result (transport_equation.h); lambda[] holds kappa */
@@ -134,6 +143,7 @@ typedef struct {
   double loop_seconds;    /* wall time of the time loop */
   double dev_ms[4];       /* profile = 1: device ms of the loop by kind: PCApply, MatMult, vector kernels, copies */
   int64_t dev_launches[4];
+  int64_t fused_dots, fused_norms; /* Gram-Schmidt dots / residual norms computed inside the PCSHELL apply */
 } cfp_wave_result;
 
 void cfp_wave_config_default(cfp_wave_config *cfg, int64_t n);

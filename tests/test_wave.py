@@ -425,3 +425,47 @@ def test_wave_operator_block_row_class_spmv(dims, dim, bc):
     assert M.aij_format() == want
     ref = ref + (0.25 + 0.5j) * x
     assert np.linalg.norm(yv.array() - ref) <= 1e-14 * np.linalg.norm(ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grid,want_fused", [((128, 128, 128), 1), ((32, 24, 16), 0)])
+def test_wave_apply_dots_match_separate_steps(grid, want_fused):
+    """cfp_wave_plan_apply_dots: x = S^{-1} b and the Gram-Schmidt dots v_j^H x.  On the 128^3
+    3-sweep schedule they ride in P3w's stores; elsewhere one multi-dot sweep follows.  Either way
+    the same numbers as the plain apply and torch's dots."""
+    import torch
+    from circulantpreconditioner_amd.plan import fill_uniform
+    wp = W.WavePlan(grid).set_symbol((0.079, 0.05, 0.11))
+    n = 4 * int(np.prod(grid))
+    b = torch.empty(n, dtype=torch.complex128, device="cuda")
+    fill_uniform(b, 11)
+    vs = [torch.empty_like(b) for _ in range(3)]
+    for i, v in enumerate(vs):
+        fill_uniform(v, 100 + i)
+    xr = wp.apply(b)
+    for dots_with in ([None], [vs[0]], [vs[0], vs[1]], [vs[0], vs[1], vs[2], None]):
+        x, dots, fused = wp.apply_dots(b, dots_with=dots_with)
+        assert fused == want_fused
+        assert float(torch.linalg.vector_norm(x - xr) / torch.linalg.vector_norm(xr)) < 1e-15
+        ref = torch.stack([torch.vdot(v if v is not None else xr, xr) for v in dots_with])
+        assert float(torch.linalg.vector_norm(dots - ref) / torch.linalg.vector_norm(ref)) < 1e-12
+    # more than 4 vectors: the separate sweep, same numbers
+    x, dots, fused = wp.apply_dots(b, dots_with=[vs[0], vs[1], vs[2], None, vs[0]])
+    assert fused == 0
+    ref = torch.stack([torch.vdot(v if v is not None else xr, xr) for v in [vs[0], vs[1], vs[2], xr, vs[0]]])
+    assert float(torch.linalg.vector_norm(dots - ref) / torch.linalg.vector_norm(ref)) < 1e-12
+    wp.close()
+
+
+@pytest.mark.gpu
+def test_wave_gmres_fused_dots_equal_unfused():
+    """Config 4's implicit step with the Gram-Schmidt dots and the residual norm computed inside
+    the block PCSHELL's 3-sweep apply, against the same loop with separate sweeps: same
+    iterations, same iterate to rounding."""
+    rf, Uf = W.run(W.config(128, pc="fft", steps=2, fuse=1), return_field=True)
+    ru, Uu = W.run(W.config(128, pc="fft", steps=2, fuse=0), return_field=True)
+    assert rf["all_converged"] == ru["all_converged"] == 1
+    assert rf["total_its"] == ru["total_its"]
+    assert rf["fused_dots"] == rf["total_its"] and rf["fused_norms"] == rf["steps"]
+    assert ru["fused_dots"] == 0 and ru["fused_norms"] == 0
+    assert np.linalg.norm(Uf - Uu) <= 1e-11 * np.linalg.norm(Uu)
