@@ -73,7 +73,6 @@ struct _p_KSP {
   double* dots_dev = nullptr;
   double *norm_h = nullptr, *norm_hd = nullptr;  // |r|^2 from the apply: pinned host memory (mapped)
   bool dev_basis = false;
-  hipEvent_t norm_ev = nullptr;  // recorded after an apply whose |z|^2 lands in norm_h
   bool fusion = true;  // KSPMiniSetFusion
   PetscInt fused_dots = 0, fused_norms = 0;  // how many Gram-Schmidt dots / norms came from the PC
 };
@@ -96,8 +95,6 @@ static void free_work(KSP k) {
   if (k->norm_h) hipHostFree(k->norm_h);
   k->dots_dev = nullptr;
   k->norm_h = k->norm_hd = nullptr;
-  if (k->norm_ev) hipEventDestroy(k->norm_ev);
-  k->norm_ev = nullptr;
   k->dev_basis = false;
   if (k->V) VecDestroyVecs(k->nvec, &k->V);
   VecDestroy(&k->t);
@@ -225,8 +222,7 @@ extern "C" PetscErrorCode KSPMiniSetUpWork(KSP k, Vec v) {
                    hipMalloc(&k->dots_dev, sizeof(double) * 16) == hipSuccess &&
                    hipHostMalloc(&k->norm_h, sizeof(double) * 16, hipHostMallocMapped | hipHostMallocCoherent) ==
                        hipSuccess &&
-                   hipHostGetDevicePointer((void**)&k->norm_hd, k->norm_h, 0) == hipSuccess &&
-                   hipEventCreateWithFlags(&k->norm_ev, hipEventDisableTiming) == hipSuccess;
+                   hipHostGetDevicePointer((void**)&k->norm_hd, k->norm_h, 0) == hipSuccess;
     if (!k->dev_basis) hipGetLastError();
 #endif
   }
@@ -312,11 +308,8 @@ static PetscErrorCode basis_ptrs(KSP k, PetscInt nv, PCMiniApplyDots* req) {
 
 // preconditioned residual into z (left: z = B (b - A x); right: z = b - A x).  x = 0: left,
 // z = B b straight from b (no copy of b); right, z = a copy of b.  *norm = |z| (its square asked
-// from the shell's apply on device bases, else VecNorm).  With `pending` set and the square
-// computed by the apply, the host does not wait here: *pending = true, and the caller reads it
-// with residual_norm() after queueing more work (the first iteration's apply).
-static PetscErrorCode residual(KSP k, Vec b, Vec x, bool x_zero, Vec z, PetscReal* norm, bool* pending = nullptr) {
-  if (pending) *pending = false;
+// from the shell's apply on device bases, else VecNorm).
+static PetscErrorCode residual(KSP k, Vec b, Vec x, bool x_zero, Vec z, PetscReal* norm) {
   Vec r = k->side == PC_LEFT ? k->t : z;
   if (x_zero && k->side == PC_LEFT) {
     r = b;
@@ -337,30 +330,13 @@ static PetscErrorCode residual(KSP k, Vec b, Vec x, bool x_zero, Vec z, PetscRea
     }
     PetscCall(pc_apply(k, r, z, asked ? &req : nullptr));
   }
-  if (asked && req.done && pending && k->norm_ev) {
-    void* st = nullptr;
-    PetscCall(VecMiniGetStream(&st));
-    if (hipEventRecord(k->norm_ev, (hipStream_t)st) != hipSuccess)
-      return PetscErrorSet(PETSC_ERR_LIB, __func__, "hipEventRecord");
-    *pending = true;
-    k->fused_norms += 1;
-  } else if (asked && req.done) {
+  if (asked && req.done) {
     PetscCall(VecMiniSynchronize(z));
     *norm = std::sqrt(k->norm_h[0]);
     k->fused_norms += 1;
   } else {
     PetscCall(VecNorm(z, NORM_2, norm));
   }
-  return PETSC_SUCCESS;
-}
-
-// |z| of a pending residual(): waits for the event recorded after its apply (later work keeps
-// running), then reads the square from pinned host memory
-static PetscErrorCode residual_norm(KSP k, PetscReal* norm) {
-  hipError_t e;
-  while ((e = hipEventQuery(k->norm_ev)) == hipErrorNotReady) __builtin_ia32_pause();
-  if (e != hipSuccess) return PetscErrorSet(PETSC_ERR_LIB, __func__, "hipEventQuery");
-  *norm = std::sqrt(k->norm_h[0]);
   return PETSC_SUCCESS;
 }
 
@@ -412,32 +388,9 @@ static PetscErrorCode ksp_solve_impl(KSP k, Vec b, Vec x, bool& x_unset) {
     return PETSC_SUCCESS;
   };
 
-  // the first iteration's w' = B A u_0 (left, fused): queued before the host reads |r_0|, so the
-  // device runs it while the host waits (u_0 is kept unnormalised; sg_0 = 1 / |r_0| is applied
-  // after).  If the cycle ends at |r_0| (converged or out of iterations) it is simply not used.
-  const auto apply_iter = [&](PetscInt j, PCMiniApplyDots* req, bool* asked) -> PetscErrorCode {
-    *asked = false;
-    if (k->side == PC_LEFT) {
-      *asked = k->fusion && k->dev_basis && j + 1 <= 4;
-      if (*asked) PetscCall(basis_ptrs(k, j + 1, req));
-      PetscCall(pc_apply(k, V[j], V[j + 1], *asked ? req : nullptr, true));
-    } else {
-      PetscCall(pc_apply(k, V[j], k->t));
-      PetscCall(MatMult(k->A, k->t, V[j + 1]));
-    }
-    return PETSC_SUCCESS;
-  };
   while (true) {
-    PetscReal beta = 0.0;
-    bool pending = false;
-    PetscCall(residual(k, b, x, x_zero, V[0], &beta, k->side == PC_LEFT && m > 0 ? &pending : nullptr));
-    PCMiniApplyDots req0{};
-    bool asked0 = false, pre0 = false;
-    if (pending) {
-      PetscCall(apply_iter(0, &req0, &asked0));
-      pre0 = true;
-      PetscCall(residual_norm(k, &beta));
-    }
+    PetscReal beta;
+    PetscCall(residual(k, b, x, x_zero, V[0], &beta));
     x_zero = false;
     k->rnorm = beta;
     if (rnorm0 < 0) rnorm0 = beta;
@@ -445,7 +398,6 @@ static PetscErrorCode ksp_solve_impl(KSP k, Vec b, Vec x, bool& x_unset) {
     if (k->reason != KSP_CONVERGED_ITERATING) break;
     if (k->its >= k->maxits) { k->reason = KSP_DIVERGED_ITS; break; }
     sg[0] = 1.0 / beta;
-    if (!(sg[0] > 1e-150 && sg[0] < 1e150)) pre0 = false;  // u_0 is rescaled: apply it again
     PetscCall(renormalise(0));
     std::fill(rs.begin(), rs.end(), C(0.0));
     rs[0] = beta;
@@ -457,11 +409,13 @@ static PetscErrorCode ksp_solve_impl(KSP k, Vec b, Vec x, bool& x_unset) {
       // dots u_i^H w' asked from the apply on device bases (at most 4 vectors)
       PCMiniApplyDots req{};
       bool asked = false;
-      if (j == 0 && pre0) {  // queued before |r_0| was read
-        req = req0;
-        asked = asked0;
+      if (k->side == PC_LEFT) {
+        asked = k->fusion && k->dev_basis && j + 1 <= 4;
+        if (asked) PetscCall(basis_ptrs(k, j + 1, &req));
+        PetscCall(pc_apply(k, V[j], V[j + 1], asked ? &req : nullptr, true));
       } else {
-        PetscCall(apply_iter(j, &req, &asked));
+        PetscCall(pc_apply(k, V[j], k->t));
+        PetscCall(MatMult(k->A, k->t, V[j + 1]));
       }
       // classical Gram-Schmidt: h_ij = v_i^H w, w -= sum h_ij v_i, and |w|, in two sweeps and
       // one host wait (the MAXPY coefficients -sg_i^2 u_i^H w' are formed on the device)
