@@ -861,8 +861,12 @@ def main() -> int:
                     x3 = torch.empty_like(b3)
                     ms3 = event_ms(lambda: p3.apply(b3, out=x3), 2000)
                     r3 = transport_residual(b3, x3, g3, LAM, 0, 1, dev)
+                    n3 = g3[0] * g3[1] * g3[2]
+                    mv3 = moved_bytes(p3.passes(), n3)
                     other_configs[key] = {"value": round(1e3 / ms3, 1), "unit": "PCApply/s",
                                           "ms_per_apply": round(ms3, 5),
+                                          "moved_bytes": mv3, "moved_GBps": round(mv3 / (ms3 * 1e-3) / 1e9, 1),
+                                          "B_alg_GBps": round(208 * n3 / (ms3 * 1e-3) / 1e9, 1),
                                           "schedule": " | ".join(f"{q['axis']}:{q['mode']}" for q in p3.passes()),
                                           "check": {"residual": r3, "tol": RES_TOL, "ok": r3 < RES_TOL}}
                     if not r3 < RES_TOL:
@@ -882,9 +886,14 @@ def main() -> int:
             wp.set_schedule("five")
             x5 = wp.apply(bw)
             dw = float(torch.linalg.vector_norm(x5 - xw) / torch.linalg.vector_norm(x5))
+            nw = 128 ** 3
+            mvw = (2 * sweeps) * 64 * nw  # each sweep reads and writes the 4-component field
             other_configs["config4_wave128"] = {
                 "value": round(1e3 / msw, 1), "unit": "block PCApply/s", "ms_per_apply": round(msw, 5),
                 "sweeps": sweeps, "dtype": "c128, 4 interleaved unknowns per cell",
+                "moved_bytes": mvw, "moved_GBps": round(mvw / (msw * 1e-3) / 1e9, 1),
+                "B_alg_GBps": round(1024 * nw / (msw * 1e-3) / 1e9, 1),
+                "note": "moved = 2 x 64 B per cell per sweep; B_alg = SURVEY 8(d)'s 1024 N for the block config",
                 "check": {"what": "rel. difference to the 5-sweep schedule", "value": dw, "ok": dw < 1e-12}}
             if not dw < 1e-12:
                 check["ok"] = False
