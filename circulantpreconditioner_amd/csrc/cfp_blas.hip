@@ -457,7 +457,7 @@ __global__ void __launch_bounds__(BLAS_THREADS) k_dia_spmv(i64 m, DiaDesc d, con
 // operator on a Cartesian grid: x read once through the caches, y written once, one class byte per
 // cell -- against CSR's 24 bytes per nonzero (about 28 nonzeros per 3-D cell).
 template <class T, int B>
-__global__ void __launch_bounds__(BLAS_THREADS) k_bdia_spmv(i64 mb, BDiaDesc d, const unsigned char* cls,
+__global__ void __launch_bounds__(512) k_bdia_spmv(i64 mb, BDiaDesc d, const unsigned char* cls,
                                                             const unsigned short* masks, const unsigned short* cbase,
                                                             const unsigned* bnz, const T* tab, const T* x, T* y) {
   extern __shared__ __attribute__((aligned(16))) unsigned char bdia_lds[];
@@ -466,6 +466,8 @@ __global__ void __launch_bounds__(BLAS_THREADS) k_bdia_spmv(i64 mb, BDiaDesc d, 
   unsigned* sz = reinterpret_cast<unsigned*>(bdia_lds + sizeof(T) * (size_t)nt);
   unsigned short* sm = reinterpret_cast<unsigned short*>(sz + d.nblk);
   unsigned short* sb = sm + d.ncls;
+  __shared__ i64 so[BDIA_MAX];
+  if (threadIdx.x < BDIA_MAX) so[threadIdx.x] = threadIdx.x < d.nd ? d.off[threadIdx.x] : 0;
   for (int i = threadIdx.x; i < nt; i += blockDim.x) st[i] = tab[i];
   for (int i = threadIdx.x; i < d.nblk; i += blockDim.x) sz[i] = bnz[i];
   for (int i = threadIdx.x; i < d.ncls; i += blockDim.x) {
@@ -479,26 +481,46 @@ __global__ void __launch_bounds__(BLAS_THREADS) k_bdia_spmv(i64 mb, BDiaDesc d, 
   for (; r < mb; r += stride) {
     const int c = cn;
     if (r + stride < mb) cn = cls[r + stride];
-    const unsigned mk = sm[c];
+    // the present blocks in ascending k, software-pipelined: the next block's neighbour values
+    // are loaded before the current block's products, so one load latency per cell instead of
+    // one per block (the offsets come from LDS: a per-lane index into the kernel arguments
+    // would go through scratch)
+    unsigned rem = sm[c];
     int q = sb[c];
     double ax[B], ay[B];
 #pragma unroll
     for (int i = 0; i < B; ++i) ax[i] = ay[i] = 0.0;
+    T xc[B], xn[B];
+    unsigned nzc = 0;
+    if (rem) {
+      const int k = __builtin_ctz(rem);
+      rem &= rem - 1;
+      nzc = sz[q];
+      const T* xb = x + (r + so[k]) * B;
 #pragma unroll
-    for (int k = 0; k < BDIA_MAX; ++k) {
-      if (k < d.nd && ((mk >> k) & 1u)) {
-        const T* xb = x + (r + d.off[k]) * B;
+      for (int j = 0; j < B; ++j) xc[j] = ((nzc >> (16 + j)) & 1u) ? xb[j] : T{};
+      for (;;) {
+        const bool more = rem != 0;
+        unsigned nzn = 0;
+        if (more) {
+          const int k2 = __builtin_ctz(rem);
+          rem &= rem - 1;
+          nzn = sz[q + 1];
+          const T* xb2 = x + (r + so[k2]) * B;
+#pragma unroll
+          for (int j = 0; j < B; ++j) xn[j] = ((nzn >> (16 + j)) & 1u) ? xb2[j] : T{};
+        }
         const T* blk = st + q * B * B;
-        const unsigned nz = sz[q];
-        T xv[B];
-#pragma unroll
-        for (int j = 0; j < B; ++j) xv[j] = ((nz >> (16 + j)) & 1u) ? xb[j] : T{};
 #pragma unroll
         for (int i = 0; i < B; ++i)
 #pragma unroll
           for (int j = 0; j < B; ++j)
-            if ((nz >> (i * B + j)) & 1u) spmv_acc(blk[i * B + j], xv[j], ax[i], ay[i]);
+            if ((nzc >> (i * B + j)) & 1u) spmv_acc(blk[i * B + j], xc[j], ax[i], ay[i]);
+        if (!more) break;
         ++q;
+        nzc = nzn;
+#pragma unroll
+        for (int j = 0; j < B; ++j) xc[j] = xn[j];
       }
     }
 #pragma unroll
@@ -619,11 +641,13 @@ static hipError_t bdia_t(i64 mb, const BDiaDesc& d, const unsigned char* cls, co
   const size_t lds = (sizeof(T) * d.B * d.B + sizeof(unsigned)) * (size_t)d.nblk + 2 * sizeof(unsigned short) * 256;
   if (lds > BDIA_LDS_MAX + 2048) return hipErrorInvalidValue;
   // persistent grid: each workgroup stages the class table into LDS once (tens of KB), so a
-  // workgroup per 256 cells would re-read it ~8,000 times at 128^3; 4 per CU then walk the cells
-  i64 nb = nblocks(mb);
-  const i64 cap = 4 * (i64)blas_cu_count();
+  // workgroup per 256 cells would re-read it ~8,000 times at 128^3.  512-thread workgroups, as
+  // many per CU as the table's LDS allows (at most 3: 24 waves, the kernel's ~70 VGPRs allow 28)
+  i64 nb = (mb + 511) / 512;
+  const i64 per_cu = lds <= 48 * 1024 ? 3 : (lds <= 75 * 1024 ? 2 : 1);
+  const i64 cap = per_cu * (i64)blas_cu_count();
   if (nb > cap) nb = cap;
-  const dim3 g((unsigned)nb), b(BLAS_THREADS);
+  const dim3 g((unsigned)(nb < 1 ? 1 : nb)), b(512);
   switch (d.B) {
     case 2: blaunch(1, (k_bdia_spmv<T, 2>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, bnz, tab, x, y); break;
     case 3: blaunch(1, (k_bdia_spmv<T, 3>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, bnz, tab, x, y); break;
