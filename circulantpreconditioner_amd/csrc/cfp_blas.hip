@@ -528,6 +528,67 @@ __global__ void __launch_bounds__(512) k_bdia_spmv(i64 mb, BDiaDesc d, const uns
   }
 }
 
+// B = 4 (the 3-D wave system's cells): one thread per row, 4 lanes of a quad per cell.  Each lane
+// loads only its own column of a neighbour cell -- consecutive lanes read consecutive 16 bytes, so
+// a wave instruction reads whole lines -- and takes the other columns from its quad through DPP
+// broadcasts (the quad shares a class, so it is active together).  All present blocks' values
+// are loaded before the products: one load latency per cell.
+template <int J>
+__device__ __forceinline__ double quad_bc(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffll), J * 0x55, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), J * 0x55, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int J>
+__device__ __forceinline__ cd quad_bc(cd v) { return make_cd(quad_bc<J>(v.x), quad_bc<J>(v.y)); }
+
+template <class T, int NDC>
+__global__ void __launch_bounds__(512) k_bdia4_spmv(i64 m, BDiaDesc d, const unsigned char* cls,
+                                                    const unsigned short* masks, const unsigned short* cbase,
+                                                    const unsigned* bnz, const T* tab, const T* x, T* y) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char bdia_lds[];
+  T* st = reinterpret_cast<T*>(bdia_lds);
+  const int nt = d.nblk * 16;
+  unsigned* sz = reinterpret_cast<unsigned*>(bdia_lds + sizeof(T) * (size_t)nt);
+  unsigned short* sm = reinterpret_cast<unsigned short*>(sz + d.nblk);
+  unsigned short* sb = sm + d.ncls;
+  __shared__ i64 so[BDIA_MAX];
+  if (threadIdx.x < BDIA_MAX) so[threadIdx.x] = threadIdx.x < d.nd ? d.off[threadIdx.x] : 0;
+  for (int i = threadIdx.x; i < nt; i += blockDim.x) st[i] = tab[i];
+  for (int i = threadIdx.x; i < d.nblk; i += blockDim.x) sz[i] = bnz[i];
+  for (int i = threadIdx.x; i < d.ncls; i += blockDim.x) {
+    sm[i] = masks[i];
+    sb[i] = cbase[i];
+  }
+  __syncthreads();
+  GRID_LOOP(rr, m) {
+    const i64 R = rr >> 2;
+    const int i = (int)(rr & 3);
+    const int c = cls[R];
+    const unsigned mk = sm[c];
+    T xk[NDC];
+#pragma unroll
+    for (int k = 0; k < NDC; ++k)
+      if (k < d.nd && ((mk >> k) & 1u)) xk[k] = x[(R + so[k]) * 4 + i];
+    int q = sb[c];
+    double ax = 0.0, ay = 0.0;
+#pragma unroll
+    for (int k = 0; k < NDC; ++k) {
+      if (k < d.nd && ((mk >> k) & 1u)) {
+        const unsigned nz = sz[q];
+        const T* row = st + q * 16 + i * 4;
+        if ((nz >> 16) & 1u) spmv_acc(row[0], quad_bc<0>(xk[k]), ax, ay);
+        if ((nz >> 17) & 1u) spmv_acc(row[1], quad_bc<1>(xk[k]), ax, ay);
+        if ((nz >> 18) & 1u) spmv_acc(row[2], quad_bc<2>(xk[k]), ax, ay);
+        if ((nz >> 19) & 1u) spmv_acc(row[3], quad_bc<3>(xk[k]), ax, ay);
+        ++q;
+      }
+    }
+    spmv_store(y + rr, ax, ay);
+  }
+}
+
 // ------------------------------------------------------------------ host launchers
 #define L1(K, ...) \
   do { if (n > 0) blaunch(2, K, dim3(nblocks(n)), dim3(BLAS_THREADS), 0, s, __VA_ARGS__); return hipGetLastError(); } while (0)
@@ -648,6 +709,16 @@ static hipError_t bdia_t(i64 mb, const BDiaDesc& d, const unsigned char* cls, co
   const i64 cap = per_cu * (i64)blas_cu_count();
   if (nb > cap) nb = cap;
   const dim3 g((unsigned)(nb < 1 ? 1 : nb)), b(512);
+  if (d.B == 4) {  // one thread per row (k_bdia4_spmv): 4 times the threads
+    i64 nb4 = (4 * mb + 511) / 512;
+    if (nb4 > cap) nb4 = cap;
+    const dim3 g4((unsigned)(nb4 < 1 ? 1 : nb4));
+    if (d.nd <= 8)
+      blaunch(1, (k_bdia4_spmv<T, 8>), g4, b, (unsigned)lds, s, 4 * mb, d, cls, masks, cbase, bnz, tab, x, y);
+    else
+      blaunch(1, (k_bdia4_spmv<T, 16>), g4, b, (unsigned)lds, s, 4 * mb, d, cls, masks, cbase, bnz, tab, x, y);
+    return hipGetLastError();
+  }
   switch (d.B) {
     case 2: blaunch(1, (k_bdia_spmv<T, 2>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, bnz, tab, x, y); break;
     case 3: blaunch(1, (k_bdia_spmv<T, 3>), g, b, (unsigned)lds, s, mb, d, cls, masks, cbase, bnz, tab, x, y); break;
