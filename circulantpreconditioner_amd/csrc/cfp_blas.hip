@@ -238,38 +238,15 @@ __device__ __forceinline__ double wave_max(double v) {
 
 // y = (OW ? 0 : y) + sum_j a_j x_j (the GMRES basis update, up to MV_MAX vectors per launch),
 // with NRM: per-block sums of |y|^2 of the result (one sweep)
-// Four elements per thread and pass (grid-stride apart, so every load instruction stays
-// contiguous across the wave): each vector's four loads issue together.
-#define MAXPY_U 4
 template <class T, bool OW, bool NRM>
 __global__ void __launch_bounds__(BLAS_THREADS) k_maxpy(T* y, int k, MVCoefT<T> a, MVPtrsT<T> xs, i64 n,
                                                          double* partial) {
   double s2 = 0.0;
-  const i64 stride = (i64)gridDim.x * blockDim.x;
-  for (i64 i0 = (i64)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += MAXPY_U * stride) {
-    T acc[MAXPY_U];
-#pragma unroll
-    for (int u = 0; u < MAXPY_U; ++u) {
-      const i64 i = i0 + u * stride;
-      acc[u] = (OW || i >= n) ? bzero<T>() : y[i];
-    }
-    for (int j = 0; j < k; ++j) {
-      const T c = a.a[j];
-      const T* xp = xs.p[j];
-#pragma unroll
-      for (int u = 0; u < MAXPY_U; ++u) {
-        const i64 i = i0 + u * stride;
-        if (i < n) acc[u] = badd(acc[u], bmul(c, xp[i]));
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < MAXPY_U; ++u) {
-      const i64 i = i0 + u * stride;
-      if (i < n) {
-        bstore<(CFP_BLAS_NT & 2) != 0>(y + i, acc[u]);
-        if (NRM) s2 += babs2(acc[u]);
-      }
-    }
+  GRID_LOOP(i, n) {
+    T acc = OW ? bzero<T>() : y[i];
+    for (int j = 0; j < k; ++j) acc = badd(acc, bmul(a.a[j], xs.p[j][i]));
+    bstore<(CFP_BLAS_NT & 2) != 0>(y + i, acc);
+    if (NRM) s2 += babs2(acc);
   }
   if constexpr (NRM) {
     __shared__ double sm[BLAS_THREADS / 64];
@@ -365,36 +342,12 @@ template <class T>
 __global__ void __launch_bounds__(BLAS_THREADS) k_maxpy_dc(T* y, int k, MVCoefT<double> scale, const double* dots,
                                                             MVPtrsT<T> xs, i64 n, double* partial, double* dots_out) {
   if (blockIdx.x == 0 && threadIdx.x < 2 * k) dots_out[threadIdx.x] = dots[threadIdx.x];  // for the host
-  // the coefficients once per workgroup (not re-read from global memory per element)
-  __shared__ T cf[MV_MAX];
-  for (int j = threadIdx.x; j < k; j += blockDim.x) cf[j] = dcoef(dots, scale.a[j], j, T{});
-  __syncthreads();
   double s2 = 0.0;
-  const i64 stride = (i64)gridDim.x * blockDim.x;
-  for (i64 i0 = (i64)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += MAXPY_U * stride) {
-    T acc[MAXPY_U];
-#pragma unroll
-    for (int u = 0; u < MAXPY_U; ++u) {
-      const i64 i = i0 + u * stride;
-      acc[u] = i < n ? y[i] : bzero<T>();
-    }
-    for (int j = 0; j < k; ++j) {
-      const T c = cf[j];
-      const T* xp = xs.p[j];
-#pragma unroll
-      for (int u = 0; u < MAXPY_U; ++u) {
-        const i64 i = i0 + u * stride;
-        if (i < n) acc[u] = badd(acc[u], bmul(c, xp[i]));
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < MAXPY_U; ++u) {
-      const i64 i = i0 + u * stride;
-      if (i < n) {
-        bstore<(CFP_BLAS_NT & 2) != 0>(y + i, acc[u]);
-        s2 += babs2(acc[u]);
-      }
-    }
+  GRID_LOOP(i, n) {
+    T acc = y[i];
+    for (int j = 0; j < k; ++j) acc = badd(acc, bmul(dcoef(dots, scale.a[j], j, acc), xs.p[j][i]));
+    bstore<(CFP_BLAS_NT & 2) != 0>(y + i, acc);
+    s2 += babs2(acc);
   }
   __shared__ double sm[BLAS_THREADS / 64];
   s2 = wave_sum(s2);
