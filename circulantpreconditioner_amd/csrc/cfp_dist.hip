@@ -607,7 +607,8 @@ extern "C" int cfp_dist_plan_create_timeout(cfp_dist_plan_t* plan, int64_t nx, i
     p->R.release();
     if (timed_out)
       return set_error(CFP_ERR_LIB, "ncclCommInitRankConfig: timed out after %.1f s (rank %d of %d)", p->timeout_s, r, P);
-    return set_error(CFP_ERR_LIB, "ncclCommInitRankConfig: %s (rank %d of %d)", ncclGetErrorString(nr), r, P);
+    return set_error(CFP_ERR_LIB, "%s: %s (rank %d of %d)", rccl_blocking() ? "ncclCommInitRank" : "ncclCommInitRankConfig",
+                     ncclGetErrorString(nr), r, P);
   }
   *plan = p.release();
   return CFP_SUCCESS;
