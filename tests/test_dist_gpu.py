@@ -441,3 +441,46 @@ def test_rccl_single_rank_transforms_and_diag(oracle):
     finally:
         if created:
             dist.destroy_process_group()
+
+
+_BLOCKING_CHILD = r"""
+import os, sys, json
+import numpy as np
+sys.path.insert(0, os.getcwd())
+import torch
+import torch.distributed as dist
+from circulantpreconditioner_amd.distributed import SlabPlan, rccl_mode
+dist.init_process_group("gloo", rank=0, world_size=1, init_method="tcp://127.0.0.1:%s" % sys.argv[1])
+dims, lam = (32, 16, 8), (0.6, 0.15, 0.02)
+b = torch.randn(int(np.prod(dims)), dtype=torch.complex128).cuda()
+plan = SlabPlan(dims, rank=0, world=1, device=0, timeout_s=60.0)
+plan.set_transport_symbol(lam)
+x = plan.apply(b)
+ref = SlabPlan(dims, rank=0, world=1, device=0, exchange="torch").set_transport_symbol(lam).apply(b)
+print(json.dumps({"mode": rccl_mode(), "ranks": plan.rccl_info()["ranks"],
+                  "rel": float(torch.linalg.vector_norm(x - ref) / torch.linalg.vector_norm(ref))}))
+plan.close()
+dist.destroy_process_group()
+"""
+
+
+def test_rccl_blocking_protocol_single_rank():
+    """CFP_RCCL_BLOCKING=1 (bench.py --rccl-blocking): the plan's communicator is made
+    by ncclCommInitRank and destroyed by ncclCommDestroy; world = 1 through RCCL equals the torch
+    exchange.  In a child process: the switch is read once per process."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, CFP_RCCL_BLOCKING="1")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", _BLOCKING_CHILD, str(port)], env=env, cwd=root, capture_output=True,
+                         text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["mode"] == "blocking" and r["ranks"] == 1
+    assert r["rel"] < 1e-14
