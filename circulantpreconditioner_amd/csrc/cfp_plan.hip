@@ -462,6 +462,7 @@ int run_apply(cfp_plan_s* p, const cd* diag_override, const cd* b, cd* x, hipStr
         a.post_partial = fz->post_partial;
         e = launch_three_pass_fused(2, tn, tin, tout, a, s, p3grid);
       } else {
+        a.krylov = fz != nullptr || g_apply_stamp.start != nullptr;  // an apply inside the stand-in KSP
         e = launch_three_pass(q.tp, tn, tin, tout, a, p->tp_shape, s);
       }
       g_stamp = LaunchStamp{};

@@ -38,6 +38,11 @@ struct TPArgs {
   int post_nv = 0;
   int post_self = 0;  // bit j: post_v[j] is x itself (NULL)
   double* post_partial = nullptr;
+  // 1: this apply runs inside the stand-in KSP (a fused Krylov step, cfp_plan_apply_ex, or a
+  // PCApply the KSP times).  Its P2 is the same kernel under a second instantiation, so that a
+  // kernel trace lists the in-solver P2 apart from the bare apply's (the two run at different
+  // clocks); no effect on the work.
+  int krylov = 0;
 };
 
 

@@ -667,7 +667,7 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 // XCD (r04): units in xcd_unit order (whole rounds), so x tiles that share 128-byte lines run
 // under one L2 (T = 32 natural layout: 64-byte tiles).
 template <int T, int N2, int TN, int PROBE = 0, bool PF = false, int NX = TN, int ST = 0, int LD = 0, bool BL = false,
-          bool XCD = false>
+          bool XCD = false, int TAG = 0>
 __global__ void __launch_bounds__(T * (TN / 16)) __attribute__((amdgpu_waves_per_eu(4)))
 k_tp_mid_sw(cd* data, TPArgs a, int nunits) {
 #ifndef CFP_KEXP
@@ -1335,7 +1335,10 @@ hipError_t launch_three_pass_slab(int stage, int n, const cd* in, cd* out, const
   if (stage == 1) {
     const int nk1 = a.lnyl ? (1 << a.lnyl) / 8 : 32;  // local k1 values: nyl / N2
     const int units = 32 * nk1;                        // x tiles x local k1
-    if (((uintptr_t)out & 15) == 0)  // the LDS-DMA prefetch needs 16-byte addresses
+    if (((uintptr_t)out & 15) == 0 && a.krylov)  // TAG 1: the fused Krylov step's P2 (TPArgs::krylov)
+      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true, 256, 0, kP2LoadFlags, false, false, 1>),
+                         dim3(grid_of(units, 1)), dim3(1024), 0, s, out, a, units);
+    else if (((uintptr_t)out & 15) == 0)  // the LDS-DMA prefetch needs 16-byte addresses
       hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true, 256, 0, kP2LoadFlags>), dim3(grid_of(units, 1)), dim3(1024), 0, s,
                          out, a, units);
     else
