@@ -1288,6 +1288,13 @@ static void launch_mid(cd* data, const TPArgs& a, hipStream_t s) {
 template <int N2, int TN, bool PF = false, bool BL = false, int T = 64>
 static void launch_mid_sw(cd* data, const TPArgs& a, hipStream_t s) {
   constexpr int units = (TN / (T / N2)) * (TN / N2);
+  if constexpr (T == 64 && N2 == 8 && TN == 256 && PF && !BL) {
+    if (a.krylov) {  // the default 256^3 P2 inside the stand-in KSP: same kernel, TAG 1 (TPArgs::krylov)
+      TP_LAUNCH((k_tp_mid_sw<T, N2, TN, 0, PF, TN, 0, kP2LoadFlags, BL, false, 1>), dim3(grid_of(units, 64 / T)),
+                dim3(T * (TN / 16)), s, data, a, units);
+      return;
+    }
+  }
   TP_LAUNCH((k_tp_mid_sw<T, N2, TN, 0, PF, TN, 0, kP2LoadFlags, BL>), dim3(grid_of(units, 64 / T)),
             dim3(T * (TN / 16)), s, data, a, units);
 }
@@ -1335,10 +1342,7 @@ hipError_t launch_three_pass_slab(int stage, int n, const cd* in, cd* out, const
   if (stage == 1) {
     const int nk1 = a.lnyl ? (1 << a.lnyl) / 8 : 32;  // local k1 values: nyl / N2
     const int units = 32 * nk1;                        // x tiles x local k1
-    if (((uintptr_t)out & 15) == 0 && a.krylov)  // TAG 1: the fused Krylov step's P2 (TPArgs::krylov)
-      hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true, 256, 0, kP2LoadFlags, false, false, 1>),
-                         dim3(grid_of(units, 1)), dim3(1024), 0, s, out, a, units);
-    else if (((uintptr_t)out & 15) == 0)  // the LDS-DMA prefetch needs 16-byte addresses
+    if (((uintptr_t)out & 15) == 0)  // the LDS-DMA prefetch needs 16-byte addresses
       hipLaunchKernelGGL((k_tp_mid_sw<64, 8, 256, 0, true, 256, 0, kP2LoadFlags>), dim3(grid_of(units, 1)), dim3(1024), 0, s,
                          out, a, units);
     else
