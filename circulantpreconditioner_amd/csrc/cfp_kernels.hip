@@ -677,6 +677,7 @@ hipError_t launch_axis_pass(const PassDesc& p, const cd* in, cd* out, const cd* 
 // SPLIT: the plane moves through LDS in real / imaginary halves (n (n + n/16) doubles), else
 // whole complex values with rows padded by one element (n (n + 1) complex: 158 KiB at n = 100)
 template <int N> struct PlaneCfg;
+template <> struct PlaneCfg<32> { static constexpr int PTS = 8, R0 = 4; static constexpr bool SPLIT = false; };
 template <> struct PlaneCfg<64> { static constexpr int PTS = 8, R0 = 8; static constexpr bool SPLIT = false; };
 template <> struct PlaneCfg<100> { static constexpr int PTS = 10, R0 = 10; static constexpr bool SPLIT = false; };
 template <> struct PlaneCfg<128> { static constexpr int PTS = 16, R0 = 8; static constexpr bool SPLIT = true; };
@@ -690,6 +691,7 @@ constexpr size_t plane_lds_bytes() {
          sizeof(cd) * N;
 }
 constexpr size_t kGfx950LdsBytes = 160 * 1024;
+static_assert(plane_lds_bytes<32>() <= kGfx950LdsBytes, "k_plane<32> exceeds the CU's LDS");
 static_assert(plane_lds_bytes<64>() <= kGfx950LdsBytes, "k_plane<64> exceeds the CU's LDS");
 static_assert(plane_lds_bytes<100>() <= kGfx950LdsBytes, "k_plane<100> exceeds the CU's LDS");
 static_assert(plane_lds_bytes<128>() <= kGfx950LdsBytes, "k_plane<128> exceeds the CU's LDS");
@@ -764,7 +766,7 @@ __global__ void __launch_bounds__(N*(N / PlaneCfg<N>::PTS)) k_plane(const cd* in
 }
 
 // gated on the static_asserts above (the kernels are only built when they fit gfx950's LDS)
-bool plane_supported(i64 n) { return n == 64 || n == 100 || n == 128; }
+bool plane_supported(i64 n) { return n == 32 || n == 64 || n == 100 || n == 128; }
 
 template <int N>
 static hipError_t launch_plane_t(bool inverse, i64 planes, const cd* in, cd* out, const cd* tw, double scale,
@@ -779,6 +781,7 @@ hipError_t launch_plane_pass(bool inverse, int n, i64 planes, const cd* in, cd* 
                              hipStream_t s) {
   if (planes <= 0) return hipSuccess;
   switch (n) {
+    case 32: return launch_plane_t<32>(inverse, planes, in, out, tw, scale, s);
     case 64: return launch_plane_t<64>(inverse, planes, in, out, tw, scale, s);
     case 100: return launch_plane_t<100>(inverse, planes, in, out, tw, scale, s);
     case 128: return launch_plane_t<128>(inverse, planes, in, out, tw, scale, s);

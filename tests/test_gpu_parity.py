@@ -502,7 +502,7 @@ def test_three_pass_100_vs_oracle(cp, oracle, mid):
 
 # ------------------------------------------------------------------ plane schedule (n_x = n_y)
 @pytest.mark.parametrize("n", [(100, 100, 100), (64, 64, 64), (128, 128, 128), (100, 100, 7), (64, 64, 2),
-                               (128, 128, 10)], ids=lambda n: "x".join(map(str, n)))
+                               (128, 128, 10), (32, 32, 32), (32, 32, 5)], ids=lambda n: "x".join(map(str, n)))
 def test_plane_vs_oracle(cp, oracle, n):
     """x + y DFTs of whole z-planes | fused z | inverse planes: against the oracle (separable
     symbol and explicit Diag), in place, and against the 5-pass schedule."""
