@@ -230,15 +230,17 @@ bool use_three_pass(const cfp_plan_s* p, bool diag_override) {
   return three_pass_supported(p->n) || three_pass_sq_supported(p->n);
 }
 
-// the plane schedule (n_x = n_y in {64, 100, 128}, n_z > 1): plane forward (x + y DFTs of
-// whole z-planes), the fused z pass, plane inverse -- on request, and by default for 100^2 and
-// 64^2 planes, where the five passes are launch-cost bound
+// the plane schedule (n_x = n_y in {32, 64, 100, 128}, n_z > 1): plane forward (x + y DFTs of
+// whole z-planes), the fused z pass, plane inverse -- on request, and by default for 100^2, 64^2
+// and 32^2 planes, where the five passes are launch-cost bound
 bool use_plane(const cfp_plan_s* p) {
   if (p->external_x || p->long_axes() || p->n[0] != p->n[1] || !plane_supported(p->n[0]) || p->n[2] < 2)
     return false;
   if (p->schedule == CFP_SCHEDULE_PLANE) return true;
-  // (128^2 planes lose to the 5 passes: 15,400 vs 17,100 PCApply/s, profiles/r02t_plane_schedule.md)
-  return p->schedule == CFP_SCHEDULE_AUTO && p->chunk_planes == 0 && (p->n[0] == 100 || p->n[0] == 64);
+  // (128^2 planes lose to the 5 passes: 15,400 vs 17,100 PCApply/s, profiles/r02t_plane_schedule.md;
+  // 32^2 planes win: 32^3 at 65,300-71,500 against 39,400-43,000, profiles/r06z2_plane32_ab.txt)
+  return p->schedule == CFP_SCHEDULE_AUTO && p->chunk_planes == 0 &&
+         (p->n[0] == 100 || p->n[0] == 64 || p->n[0] == 32);
 }
 
 // axis order of the 5-pass schedule: the last one is fused with the symbol

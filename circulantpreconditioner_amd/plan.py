@@ -236,7 +236,7 @@ class CirculantPlan:
 
     def set_schedule(self, schedule: str | int) -> "CirculantPlan":
         """'auto'/'five' (z fused), 'five_y' (y fused), 'three' (256^3: 3 sweeps) or 'plane'
-        (n_x = n_y in {64, 100, 128}: x + y DFTs of whole z-planes | fused z | inverse planes)."""
+        (n_x = n_y in {32, 64, 100, 128}: x + y DFTs of whole z-planes | fused z | inverse planes)."""
         v = self.SCHEDULES[schedule] if isinstance(schedule, str) else int(schedule)
         check(lib().cfp_plan_set_schedule(self._h, v))
         return self

@@ -159,8 +159,8 @@ int cfp_plan_set_graph(cfp_plan_t plan, int on);
  * (128^3 and 256^3 plans only, CFP_ERR_SUP
  * otherwise; an explicit Diag still takes 5 passes): x + first y stage | last y stage + z +
  * symbol + inverses | inverse of the first, 96 N bytes instead of 160 N.
- * PLANE (n_x = n_y in {64, 100, 128}, n_z > 1; CFP_ERR_SUP otherwise; AUTO picks it for
- * n_x = n_y = 100 -- the reference's default mesh -- and 64): x + y DFTs of whole z-planes | z fused with
+ * PLANE (n_x = n_y in {32, 64, 100, 128}, n_z > 1; CFP_ERR_SUP otherwise; AUTO picks it for
+ * n_x = n_y = 100 when THREE_PASS does not apply, 64 and 32): x + y DFTs of whole z-planes | z fused with
  * the symbol | inverse planes, 3 launches instead of 5 (any symbol, explicit Diag included). */
 #define CFP_SCHEDULE_AUTO 0
 #define CFP_SCHEDULE_FIVE_PASS 1

@@ -543,6 +543,9 @@ def test_plane_schedule_rules(cp):
     with cp.CirculantPlan((64, 64, 64)) as plan:  # AUTO: planes for 64^2 too
         plan.set_transport_symbol((0.5, 0.5, 0.5))
         assert len(plan.passes()) == 3
+    with cp.CirculantPlan((32, 32, 32)) as plan:  # ... and for 32^2 (BASELINE config 1; r06z2)
+        plan.set_transport_symbol((0.5, 0.5, 0.5))
+        assert [p["mode"] for p in plan.passes()] == ["plane_fwd", "fused_sep", "plane_inv"]
     with cp.CirculantPlan((128, 128, 128)) as plan:  # ... but not for 128^3: 3 sweeps there (r03m)
         plan.set_transport_symbol((0.5, 0.5, 0.5))
         assert [p["mode"] for p in plan.passes()] == ["rows_fwd", "mid_fused", "rows_inv"]
