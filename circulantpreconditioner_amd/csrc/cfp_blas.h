@@ -53,6 +53,7 @@ hipError_t blas_dia_spmv(i64 m, const DiaDesc& d, const unsigned char* cls, cons
 struct BDiaDesc {
   i64 off[BDIA_MAX];
   int nd = 0, ncls = 0, B = 0, nblk = 0;  // nblk: blocks in tab
+  int re = 0;  // 1: every table entry has a zero imaginary part (the wave operator): real x complex products
 };
 #define BDIA_LDS_MAX (60 * 1024)
 hipError_t blas_bdia_spmv(i64 mb, const BDiaDesc& d, const unsigned char* cls, const unsigned short* masks,

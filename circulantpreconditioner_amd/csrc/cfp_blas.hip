@@ -543,7 +543,20 @@ __device__ __forceinline__ double quad_bc(double v) {
 template <int J>
 __device__ __forceinline__ cd quad_bc(cd v) { return make_cd(quad_bc<J>(v.x), quad_bc<J>(v.y)); }
 
-template <class T, int NDC>
+#ifndef CFP_BDIA_XCD
+#define CFP_BDIA_XCD 0
+#endif
+#ifndef CFP_BDIA_RE
+#define CFP_BDIA_RE 1
+#endif
+// RE (complex fields, d.re): the table's entries are real, so each product is two FMAs on the
+// real part instead of a complex multiply-add's four
+__device__ __forceinline__ void spmv_acc_re(cd a, cd b, double& ax, double& ay) {
+  ax = fma(a.x, b.x, ax);
+  ay = fma(a.x, b.y, ay);
+}
+__device__ __forceinline__ void spmv_acc_re(double a, double b, double& ax, double&) { ax = fma(a, b, ax); }
+template <class T, int NDC, bool RE>
 __global__ void __launch_bounds__(512) k_bdia4_spmv(i64 m, BDiaDesc d, const unsigned char* cls,
                                                     const unsigned short* masks, const unsigned short* cbase,
                                                     const unsigned* bnz, const T* tab, const T* x, T* y) {
@@ -562,7 +575,20 @@ __global__ void __launch_bounds__(512) k_bdia4_spmv(i64 m, BDiaDesc d, const uns
     sb[i] = cbase[i];
   }
   __syncthreads();
-  GRID_LOOP(rr, m) {
+  // XCD-contiguous cells (-DCFP_BDIA_XCD=1, A/B only): with the grid a multiple of 8, workgroup b
+  // runs on XCD b mod 8, and each XCD walks its own eighth of the rows in order, so the y / z
+  // neighbours a wave reads were pulled into that XCD's L2 by its own earlier waves.  Measured
+  // 2 us slower per MatMult than the plain grid-stride order (profiles/r06z4_wave_spmv_ab.txt).
+  i64 r0 = (i64)blockIdx.x * blockDim.x + threadIdx.x, r1 = m, rs = (i64)gridDim.x * blockDim.x;
+#if CFP_BDIA_XCD
+  if ((gridDim.x & 7) == 0) {
+    const i64 xcd = blockIdx.x & 7, mb = m >> 2;
+    r0 = ((xcd * mb) >> 3) * 4 + (i64)(blockIdx.x >> 3) * blockDim.x + threadIdx.x;
+    r1 = (((xcd + 1) * mb) >> 3) * 4;
+    rs = (i64)(gridDim.x >> 3) * blockDim.x;
+  }
+#endif
+  for (i64 rr = r0; rr < r1; rr += rs) {
     const i64 R = rr >> 2;
     const int i = (int)(rr & 3);
     const int c = cls[R];
@@ -578,10 +604,17 @@ __global__ void __launch_bounds__(512) k_bdia4_spmv(i64 m, BDiaDesc d, const uns
       if (k < d.nd && ((mk >> k) & 1u)) {
         const unsigned nz = sz[q];
         const T* row = st + q * 16 + i * 4;
-        if ((nz >> 16) & 1u) spmv_acc(row[0], quad_bc<0>(xk[k]), ax, ay);
-        if ((nz >> 17) & 1u) spmv_acc(row[1], quad_bc<1>(xk[k]), ax, ay);
-        if ((nz >> 18) & 1u) spmv_acc(row[2], quad_bc<2>(xk[k]), ax, ay);
-        if ((nz >> 19) & 1u) spmv_acc(row[3], quad_bc<3>(xk[k]), ax, ay);
+        if constexpr (RE) {
+          if ((nz >> 16) & 1u) spmv_acc_re(row[0], quad_bc<0>(xk[k]), ax, ay);
+          if ((nz >> 17) & 1u) spmv_acc_re(row[1], quad_bc<1>(xk[k]), ax, ay);
+          if ((nz >> 18) & 1u) spmv_acc_re(row[2], quad_bc<2>(xk[k]), ax, ay);
+          if ((nz >> 19) & 1u) spmv_acc_re(row[3], quad_bc<3>(xk[k]), ax, ay);
+        } else {
+          if ((nz >> 16) & 1u) spmv_acc(row[0], quad_bc<0>(xk[k]), ax, ay);
+          if ((nz >> 17) & 1u) spmv_acc(row[1], quad_bc<1>(xk[k]), ax, ay);
+          if ((nz >> 18) & 1u) spmv_acc(row[2], quad_bc<2>(xk[k]), ax, ay);
+          if ((nz >> 19) & 1u) spmv_acc(row[3], quad_bc<3>(xk[k]), ax, ay);
+        }
         ++q;
       }
     }
@@ -713,10 +746,13 @@ static hipError_t bdia_t(i64 mb, const BDiaDesc& d, const unsigned char* cls, co
     i64 nb4 = (4 * mb + 511) / 512;
     if (nb4 > cap) nb4 = cap;
     const dim3 g4((unsigned)(nb4 < 1 ? 1 : nb4));
-    if (d.nd <= 8)
-      blaunch(1, (k_bdia4_spmv<T, 8>), g4, b, (unsigned)lds, s, 4 * mb, d, cls, masks, cbase, bnz, tab, x, y);
+    constexpr bool CX = std::is_same<T, cd>::value;
+    if (d.nd <= 8 && CX && d.re && CFP_BDIA_RE)
+      blaunch(1, (k_bdia4_spmv<T, 8, CX>), g4, b, (unsigned)lds, s, 4 * mb, d, cls, masks, cbase, bnz, tab, x, y);
+    else if (d.nd <= 8)
+      blaunch(1, (k_bdia4_spmv<T, 8, false>), g4, b, (unsigned)lds, s, 4 * mb, d, cls, masks, cbase, bnz, tab, x, y);
     else
-      blaunch(1, (k_bdia4_spmv<T, 16>), g4, b, (unsigned)lds, s, 4 * mb, d, cls, masks, cbase, bnz, tab, x, y);
+      blaunch(1, (k_bdia4_spmv<T, 16, false>), g4, b, (unsigned)lds, s, 4 * mb, d, cls, masks, cbase, bnz, tab, x, y);
     return hipGetLastError();
   }
   switch (d.B) {

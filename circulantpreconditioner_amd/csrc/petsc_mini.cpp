@@ -1393,6 +1393,9 @@ static bool aij_build_bdia_b(Mat M, int B, cfp::BDiaDesc* d, std::vector<unsigne
   d->ncls = (int)masks->size();
   d->B = B;
   d->nblk = (int)(tab->size() / (size_t)(B * B));
+  d->re = 1;
+  for (const VS& v : *tab)
+    if (C(v).imag() != 0.0) d->re = 0;
   return true;
 }
 static bool aij_build_bdia(Mat M, cfp::BDiaDesc* d, std::vector<unsigned char>* cls, std::vector<unsigned short>* masks,
