@@ -24,6 +24,13 @@ hipError_t blas_pmult(cd* w, const cd* x, const cd* y, i64 n, hipStream_t s);
 hipError_t blas_maxpy(cd* y, int k, const cd* a, const cd* const* xs, i64 n, hipStream_t s);
 // y = (overwrite ? 0 : y) + sum_j a[j] xs[j]; norm2 != nullptr: also sum |y|^2 of the result,
 // accumulated in the same sweep (synchronous then, like the reductions below)
+// y += a x with the |y|^2 per-workgroup partials of the result written to partial (a device
+// address, e.g. of mapped pinned memory; at most BLAS_NORM_PARTIALS), no wait: *nb = the partial
+// count (0 for n = 0).  The stand-in VecAXPY keeps them for a following VecNorm (petsc_mini.cpp).
+#define BLAS_NORM_PARTIALS 1024
+hipError_t blas_axpy_partials(cd* y, cd a, const cd* x, i64 n, double* partial, unsigned* nb, hipStream_t s);
+hipError_t blas_axpy_partials(double* y, double a, const double* x, i64 n, double* partial, unsigned* nb,
+                              hipStream_t s);
 hipError_t blas_maxpy_norm(cd* y, int k, const cd* a, const cd* const* xs, i64 n, bool overwrite, double* norm2,
                            hipStream_t s);
 // y = A x for a CSR matrix of m rows and nnz nonzeros (nnz picks the lanes per row)

@@ -829,6 +829,27 @@ static hipError_t maxpy_t(T* y, int k, const T* a, const T* const* xs, i64 n, bo
   *norm2 = t;
   return hipSuccess;
 }
+template <class T>
+static hipError_t axpy_partials_t(T* y, T a, const T* x, i64 n, double* partial, unsigned* nb_out, hipStream_t s) {
+  static_assert(BLAS_NORM_PARTIALS <= MAXPY_BLOCKS, "partials");
+  unsigned nb = nblocks(n);
+  if (nb > BLAS_NORM_PARTIALS) nb = BLAS_NORM_PARTIALS;
+  *nb_out = n > 0 ? nb : 0;
+  if (n <= 0) return hipSuccess;
+  MVCoefT<T> c;
+  MVPtrsT<T> p;
+  c.a[0] = a;
+  p.p[0] = x;
+  blaunch(2, (k_maxpy<T, false, true>), dim3(nb), dim3(BLAS_THREADS), 0, s, y, 1, c, p, n, partial);
+  return hipGetLastError();
+}
+hipError_t blas_axpy_partials(cd* y, cd a, const cd* x, i64 n, double* partial, unsigned* nb, hipStream_t s) {
+  return axpy_partials_t(y, a, x, n, partial, nb, s);
+}
+hipError_t blas_axpy_partials(double* y, double a, const double* x, i64 n, double* partial, unsigned* nb,
+                              hipStream_t s) {
+  return axpy_partials_t(y, a, x, n, partial, nb, s);
+}
 hipError_t blas_maxpy(cd* y, int k, const cd* a, const cd* const* xs, i64 n, hipStream_t s) {
   return maxpy_t(y, k, a, xs, n, false, nullptr, s);
 }

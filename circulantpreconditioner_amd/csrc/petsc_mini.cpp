@@ -344,6 +344,12 @@ struct _p_Vec {
   int device = 0;
   PetscObjectId id = 0;
   PetscObjectState state = 0;  // bumped by every write access (PetscObjectStateGet)
+  // |x|^2 partials of the last device VecAXPY into this vector (mapped pinned memory), valid while
+  // state == nrm_state: a VecNorm(NORM_2) right after it sums them instead of re-reading the
+  // vector (PETSc likewise caches norms against the object state)
+  double *nrm_h = nullptr, *nrm_hd = nullptr;
+  unsigned nrm_nb = 0;
+  PetscObjectState nrm_state = -1;
   // VecSetValues entries of rows owned by other ranks, delivered by VecAssemblyBegin/End
   std::vector<PetscInt> st_idx;
   std::vector<VS> st_val;
@@ -508,6 +514,7 @@ extern "C" PetscErrorCode VecDestroy(Vec* pv) {
   VCHK(v);
   if (v->own_d && v->d) hipFree(v->d);
   if (v->own_h && v->h) free(v->h);
+  if (v->nrm_h) hipHostFree(v->nrm_h);
   v->magic = 0;
   delete v;
   *pv = nullptr;
@@ -869,9 +876,29 @@ static PetscErrorCode binop(Vec out, Vec a, Vec b, DevOp dop, HostOp hop) {
 
 extern "C" PetscErrorCode VecAXPY(Vec y, PetscScalar a, Vec x) {  // y += a x
   const i64 n = y ? y->n : 0;
-  return binop(y, x, nullptr,
-               [&](VS* o, const VS* xa, const VS*) { return cfp::blas_axpy(o, tocd(a), xa, n, g_stream); },
-               [&](VS* o, const VS* xa, const VS*) { for (i64 i = 0; i < n; ++i) o[i] = D(C(o[i]) + a * C(xa[i])); });
+  // on the device the sweep also leaves |y|^2 partials for a following VecNorm (the time loops'
+  // VecAXPY(dU, -1, U); VecNorm(dU): one sweep of dU fewer per step)
+  if (y && y->magic == kVecMagic && y->hip && !y->nrm_h) {
+    if (hipHostMalloc(&y->nrm_h, sizeof(double) * BLAS_NORM_PARTIALS, hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer((void**)&y->nrm_hd, y->nrm_h, 0) != hipSuccess) {
+      if (y->nrm_h) hipHostFree(y->nrm_h);
+      y->nrm_h = y->nrm_hd = nullptr;
+      (void)hipGetLastError();
+    }
+  }
+  unsigned nb = 0;
+  bool dev = false;
+  PetscCall(binop(y, x, nullptr,
+                  [&](VS* o, const VS* xa, const VS*) {
+                    dev = true;
+                    if (y->nrm_hd) return cfp::blas_axpy_partials(o, tocd(a), xa, n, y->nrm_hd, &nb, g_stream);
+                    return cfp::blas_axpy(o, tocd(a), xa, n, g_stream);
+                  },
+                  [&](VS* o, const VS* xa, const VS*) { for (i64 i = 0; i < n; ++i) o[i] = D(C(o[i]) + a * C(xa[i])); }));
+  y->nrm_nb = dev ? nb : 0;
+  y->nrm_state = y->state;
+  return PETSC_SUCCESS;
 }
 extern "C" PetscErrorCode VecAYPX(Vec y, PetscScalar b, Vec x) {  // y = x + b y
   const i64 n = y ? y->n : 0;
@@ -926,7 +953,12 @@ extern "C" PetscErrorCode VecDot(Vec x, Vec y, PetscScalar* val) {  // y^H x
 extern "C" PetscErrorCode VecNorm(Vec x, NormType t, PetscReal* val) {
   VCHK(x);
   if (t == NORM_FROBENIUS) t = NORM_2;
-  if (x->hip) {
+  if (x->hip && t == NORM_2 && x->nrm_nb > 0 && x->nrm_state == x->state) {  // VecAXPY's partials
+    HIPK(cfp::host_wait(g_stream));
+    double s = 0.0;
+    for (unsigned q = 0; q < x->nrm_nb; ++q) s += x->nrm_h[q];
+    *val = std::sqrt(s);
+  } else if (x->hip) {
     const VS* xd;
     PetscCall(dev_read(x, &xd));
     HIPK(cfp::blas_norm(xd, x->n, (int)t, val, g_stream));

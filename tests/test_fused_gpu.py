@@ -127,3 +127,46 @@ def test_device_copy():
         torch.cuda.synchronize()
         assert torch.equal(c[off:off + nb], a[off:off + nb])
         assert int(c[:off].sum()) == 0 and int(c[off + nb:].sum()) == 0
+
+
+@pytest.mark.parametrize("n", [1, 1000, 256 * 1024 + 3, 0])
+def test_axpy_norm_partials_follow_the_vector_state(n):
+    """VecAXPY on a device Vec leaves the |y|^2 partials of its result; VecNorm(NORM_2) sums them
+    while the vector is unchanged (the time loops' VecAXPY(dU, -1, U); VecNorm(dU)), and any later
+    write -- VecScale, VecSet, another AXPY, a VecHIPGetArray write, a host-side set -- is seen.
+    Norms agree with numpy to 1e-12; NORM_1 / NORM_INFINITY never take the partials."""
+    from circulantpreconditioner_amd import petsc as P
+    rng = np.random.default_rng(7)
+    a = rng.standard_normal(n) + 1j * rng.standard_normal(n)
+    b = rng.standard_normal(n) + 1j * rng.standard_normal(n)
+    y, x = P.Vec.seq_hip(n).set_array(a), P.Vec.seq_hip(n).set_array(b)
+
+    def close(v, want):
+        assert abs(v - want) <= 1e-12 * max(want, 1e-300)
+
+    y.axpy(-0.5 + 0.25j, x)
+    ref = a + (-0.5 + 0.25j) * b
+    close(y.norm(), np.linalg.norm(ref))
+    close(y.norm(), np.linalg.norm(ref))  # twice: still unchanged
+    close(y.norm(P.NORM_1), np.abs(ref.real).sum() + np.abs(ref.imag).sum())
+    close(y.norm(P.NORM_INFINITY), np.abs(ref).max(initial=0.0))
+    y.scale(3.0)
+    ref = 3.0 * ref
+    close(y.norm(), np.linalg.norm(ref))
+    y.axpy(1.0, x)
+    ref = ref + b
+    close(y.norm(), np.linalg.norm(ref))
+    if n:
+        from circulantpreconditioner_amd._lib import check, lib
+        t = torch.full((n,), 2.0 + 0j, dtype=torch.complex128, device="cuda")
+        with y.hip_array() as p:  # a raw device write between the AXPY and the norm
+            torch.cuda.synchronize()
+            check(lib().cfp_device_copy(p, t.data_ptr(), 16 * n, None))
+            torch.cuda.synchronize()
+        close(y.norm(), 2.0 * np.sqrt(n))
+    y.axpy(1.0, x)
+    y.set_array(a)  # host-side write after the AXPY
+    close(y.norm(), np.linalg.norm(a))
+    y.axpy(2.0, x)
+    y.set(1.0)
+    close(y.norm(), np.sqrt(n))
