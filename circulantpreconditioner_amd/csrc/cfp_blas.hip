@@ -549,6 +549,9 @@ __device__ __forceinline__ cd quad_bc(cd v) { return make_cd(quad_bc<J>(v.x), qu
 #ifndef CFP_BDIA_RE
 #define CFP_BDIA_RE 1
 #endif
+#ifndef CFP_BDIA_PF
+#define CFP_BDIA_PF 0
+#endif
 // RE (complex fields, d.re): the table's entries are real, so each product is two FMAs on the
 // real part instead of a complex multiply-add's four
 __device__ __forceinline__ void spmv_acc_re(cd a, cd b, double& ax, double& ay) {
@@ -588,15 +591,17 @@ __global__ void __launch_bounds__(512) k_bdia4_spmv(i64 m, BDiaDesc d, const uns
     rs = (i64)(gridDim.x >> 3) * blockDim.x;
   }
 #endif
-  for (i64 rr = r0; rr < r1; rr += rs) {
+  const auto load = [&](i64 rr, int c, T* xk) {
     const i64 R = rr >> 2;
     const int i = (int)(rr & 3);
-    const int c = cls[R];
     const unsigned mk = sm[c];
-    T xk[NDC];
 #pragma unroll
     for (int k = 0; k < NDC; ++k)
       if (k < d.nd && ((mk >> k) & 1u)) xk[k] = x[(R + so[k]) * 4 + i];
+  };
+  const auto product = [&](i64 rr, int c, const T* xk) {
+    const int i = (int)(rr & 3);
+    const unsigned mk = sm[c];
     int q = sb[c];
     double ax = 0.0, ay = 0.0;
 #pragma unroll
@@ -619,7 +624,36 @@ __global__ void __launch_bounds__(512) k_bdia4_spmv(i64 m, BDiaDesc d, const uns
       }
     }
     spmv_store(y + rr, ax, ay);
+  };
+#if CFP_BDIA_PF
+  // software-pipelined over the grid-stride iterations (-DCFP_BDIA_PF=1, A/B only): the next
+  // row's neighbour values are in flight while this row's products run, and the class byte is
+  // read two rows ahead.  124 VGPRs against 80, so 2 workgroups per CU instead of 3: 103-107
+  // against 91-95 us per MatMult (profiles/r06z6_wave_spmv_pf_ab.txt)
+  i64 rr = r0;
+  int c = rr < r1 ? cls[rr >> 2] : 0;
+  int cn = rr + rs < r1 ? cls[(rr + rs) >> 2] : 0;
+  T xk[NDC];
+  if (rr < r1) load(rr, c, xk);
+  for (; rr < r1; rr += rs) {
+    const i64 rn = rr + rs;
+    T xn[NDC];
+    if (rn < r1) load(rn, cn, xn);
+    const int cnn = rn + rs < r1 ? cls[(rn + rs) >> 2] : 0;
+    product(rr, c, xk);
+#pragma unroll
+    for (int k = 0; k < NDC; ++k) xk[k] = xn[k];
+    c = cn;
+    cn = cnn;
   }
+#else
+  for (i64 rr = r0; rr < r1; rr += rs) {
+    const int c = cls[rr >> 2];
+    T xk[NDC];
+    load(rr, c, xk);
+    product(rr, c, xk);
+  }
+#endif
 }
 
 // ------------------------------------------------------------------ host launchers
@@ -744,7 +778,9 @@ static hipError_t bdia_t(i64 mb, const BDiaDesc& d, const unsigned char* cls, co
   const dim3 g((unsigned)(nb < 1 ? 1 : nb)), b(512);
   if (d.B == 4) {  // one thread per row (k_bdia4_spmv): 4 times the threads
     i64 nb4 = (4 * mb + 511) / 512;
-    if (nb4 > cap) nb4 = cap;
+    // the pipelined kernel holds two rows' values (~124 VGPRs): 4 waves per SIMD, 2 workgroups per CU
+    const i64 cap4 = CFP_BDIA_PF ? (per_cu < 2 ? per_cu : 2) * (i64)blas_cu_count() : cap;
+    if (nb4 > cap4) nb4 = cap4;
     const dim3 g4((unsigned)(nb4 < 1 ? 1 : nb4));
     constexpr bool CX = std::is_same<T, cd>::value;
     if (d.nd <= 8 && CX && d.re && CFP_BDIA_RE)
