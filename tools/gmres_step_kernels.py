@@ -6,7 +6,10 @@ leading copies; the number of implicit steps comes from --steps (the run's own c
 per-kernel calls, median and total microseconds, and the device busy time per step, split into
 KSPSolve's own kernels and the reference time loop's vector operations around it
 (TransportEquation_impl_mpi.cxx:131-166: VecCopy(Un, dUn) -- a copy of more than 20 us --,
-VecAXPY(dUn, -1, Un) and VecNorm(dUn) -- a k_axpy followed by a k_reduce).
+VecAXPY(dUn, -1, Un) and VecNorm(dUn) -- a k_axpy followed by a k_reduce).  Since r06 the
+copy is k_copy16, and since r06z5 the AXPY writes the norm partials itself (one k_maxpy<T, false,
+true> with no k_reduce after it, the same kernel as the unfused Gram-Schmidt MAXPY), so on later
+traces the split below counts that AXPY as KSPSolve's; the device time per step is unaffected.
 
     python tools/gmres_step_kernels.py gpurun_out/r04a_gmres256_trace [--steps 6]
 """
@@ -49,7 +52,7 @@ def main():
           f"({a.steps} steps), span {(sol[-1][1] - sol[0][0]) / 1e3 / a.steps:.1f} us per step")
     loop = set()
     for i, (s, e, n) in enumerate(sol):
-        if "copyBuffer" in n and (e - s) / 1e3 > 20.0:
+        if ("copyBuffer" in n or "k_copy16" in n) and (e - s) / 1e3 > 20.0:
             loop.add(i)
         if "k_axpy" in n and i + 1 < len(sol) and "k_reduce" in sol[i + 1][2]:
             loop.update((i, i + 1))
